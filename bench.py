@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mpaths/s of the hair path tracer on MI355X.
+
+Workload (BASELINE.json configs[2], the metric's config): models/furball with
+the Marschner BSDF, 512x512 @ 256 spp, maxDepth 65, synthetic furball hair
+(40,000 strands, ~3.2e5 segments, seed 1), sunsky stand-in lighting.
+One step = one full frame: every sample of every pixel traced to
+termination (MIPathTracer::Li, path.cpp:119-294) and splatted into the film.
+With N GPUs the frame's 32x32 blocks are dealt block-cyclically to ranks and
+the RGBW films are summed on rank 0 with one RCCL reduce (strong scaling).
+
+Launch:  python bench.py [--gpus 1 --steps 3 --warmup 1]
+         python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "cs184-final-project-mitsuba0.5_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (import first: one HIP runtime per process)
+import torch.distributed as dist  # noqa: E402
+
+from mitsuba_amd import native, scenes  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+# algorithmic bytes of k_trace (DESIGN.md "Byte model"):
+#   closest ray: queue id 4 + ray 32 + hit record 32 = 68 B
+#   shadow ray:  queue id 4 + origin 16 + direction/maxt 16 = 36 B, +48 B (contribution + radiance RMW)
+#                when unoccluded
+#   node visit 8 B, primitive test 4 B leaf index + 128 B segment record
+BYTES_CLOSEST, BYTES_SHADOW, BYTES_UNOCC, BYTES_NODE, BYTES_PRIM = 68, 36, 48, 8, 132
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="furball_marschner")
+    ap.add_argument("--strands", type=int, default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--max-depth", type=int, default=None)
+    ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--cpu-spp", type=int, default=2, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--workdir", default=os.path.join(tempfile.gettempdir(), "hpt_bench"))
+    return ap.parse_args()
+
+
+def cpu_baseline(args, cfg, xml_defines, hair_file, env_rgb, nodes, idx):
+    """Oracle built with the reference's flags (liboracle_ref.so), bounded sample on host cores."""
+    import oracle_lib
+    import scene_util
+
+    _, cam, bsdf = scene_util.config_params(args.config)
+    o = oracle_lib.Oracle(variant="ref")
+    W, H = xml_defines["width"], xml_defines["height"]
+    o.setup(cam, 35.0, W, H, hair_file, float(cfg["radius"]), bsdf, env_rgb, xml_defines["maxDepth"])
+    o.set_kdtree(nodes, idx)
+    o.prepare()
+    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    o.render(0, args.cpu_spp, threads=threads, width=W, height=H)
+    dt = time.perf_counter() - t0
+    paths = W * H * args.cpu_spp
+    return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
+            "sample": "%dx%d @ %d spp of the same scene (%d paths), %.2f s, liboracle_ref.so "
+                      "(-O3 -march=nocona -msse2 -funsafe-math-optimizations, config-ubuntu-20.04.py:8)"
+                      % (W, H, args.cpu_spp, paths, dt)}
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        dist.init_process_group("nccl")  # RCCL over xGMI on ROCm
+    torch.cuda.set_device(local)
+    cfg = scenes.CONFIGS[args.config]
+    n = args.strands or cfg["n"]
+    W = args.width or cfg["width"]
+    H = args.height or cfg["height"]
+    spp = args.spp or cfg["spp"]
+    max_depth = args.max_depth if args.max_depth is not None else cfg["max_depth"]
+    defines = {"width": W, "height": H, "spp": spp, "maxDepth": max_depth}
+    workdir = os.path.join(args.workdir, "r%d" % rank)
+    xml = scenes.make_scene(args.config, workdir, n_strands=n)
+    hair_file = os.path.join(workdir, "%s_%d.mitshair" % (cfg["geom"], n))
+
+    r = native.Renderer(device=local)
+    r.load_scene_xml(xml, defines)
+    t0 = time.perf_counter()
+    r.prepare()
+    t_prep = time.perf_counter() - t0
+    info = r.info()
+    film = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:%d" % local)
+
+    def step():
+        film.zero_()
+        torch.cuda.synchronize()
+        r.render_device(film.data_ptr(), 0, spp, shard=rank, n_shards=world, collect_stats=True)
+        if world > 1:
+            dist.reduce(film, 0)
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ms_trace = 0.0
+    launches = 0
+    tot = dict(nodes=0, prims=0, closest=0, shadow=0, unocc=0, bounces=0)
+    for _ in range(args.steps):
+        step()
+        s = r.stats()
+        ms_trace += s.ms_trace
+        launches += s.trace_launches
+        tot["nodes"] += s.nodes
+        tot["prims"] += s.prims
+        tot["closest"] += s.closest_rays
+        tot["shadow"] += s.shadow_rays
+        tot["unocc"] += s.shadow_unoccluded
+        tot["bounces"] += s.bounces
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device="cuda:%d" % local)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+
+    paths_total = W * H * spp * args.steps
+    value = paths_total / dt / 1e6
+    bytes_alg = (BYTES_CLOSEST * tot["closest"] + BYTES_SHADOW * tot["shadow"] + BYTES_UNOCC * tot["unocc"]
+                 + BYTES_NODE * tot["nodes"] + BYTES_PRIM * tot["prims"])
+    achieved = bytes_alg / (ms_trace * 1e-3) / 1e9 if ms_trace > 0 else 0.0
+    out = None
+    if rank == 0:
+        cpu = None
+        if args.cpu_baseline == "auto" and world == 1:
+            nodes, idx, _ = r.kdtree()
+            cpu = cpu_baseline(args, cfg, defines, hair_file, r.envmap(), nodes, idx)
+        img = native.develop(film.cpu().numpy())
+        out = {
+            "metric": "Mpaths/sec + achieved HBM GB/s, furball Marschner 512² @ 256spp",
+            "value": round(value, 3),
+            "unit": "Mpaths/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32 (f64 cylinder tests)",
+            "data": "synthetic hair (seeded, BINARY_HAIR) + sunsky stand-in envmap; reference blobs absent",
+            "config": {"workload": "%s %dx%d @ %d spp, maxDepth %d, %d strands / %d segments"
+                                   % (args.config, W, H, spp, max_depth, n, info.segments),
+                       "paths_per_step": W * H * spp, "parallelism": "tiles%d" % world,
+                       "kd_nodes": int(info.kd_nodes), "kd_depth": int(info.kd_depth),
+                       "prepare_s": round(t_prep, 3)},
+            "roofline": {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "avg_launch_ms": round(ms_trace / max(1, launches), 4), "launches": int(launches),
+                         "bytes_per_step": int(bytes_alg // args.steps),
+                         "rank0_trace_ms_per_step": round(ms_trace / args.steps, 3)},
+            "cpu_baseline": cpu,
+            "stats": {"bounces_per_path": round(tot["bounces"] / max(1, paths_total / world), 4),
+                      "nodes_per_ray": round(tot["nodes"] / max(1, tot["closest"] + tot["shadow"]), 2),
+                      "prims_per_ray": round(tot["prims"] / max(1, tot["closest"] + tot["shadow"]), 2),
+                      "image_mean": float(img.mean())},
+        }
+        print(json.dumps(out), flush=True)
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,198 @@
+/*
+ * mitsuba_cli.cpp -- `mitsuba`-compatible command line front end.
+ *
+ * Mirrors src/mitsuba/mitsuba.cpp:52-400 for the hair path: parse options,
+ * load each scene XML, render, develop the film and write it next to the
+ * scene (or to -o).  Rendering runs on MI355X devices through libhairpt.so;
+ * with --gpus N the 32x32 blocks are dealt block-cyclically over N devices
+ * (one host thread + one hpt_context each) and the per-device films are
+ * summed -- the single-node analogue of the reference's -c remote workers.
+ *
+ *   mitsuba [options] <scene.xml> [<scene2.xml> ...]
+ *     -D key=val   define $key for the XML        -o fname   output file
+ *     -p count     (accepted; GPU render)          -q         quiet
+ *     -x           skip scenes whose output exists -b/-r/-z/-v (accepted)
+ *     --spp N --width W --height H --max-depth D   overrides
+ *     --device i   first device                    --gpus N   devices to use
+ *     --stats      print timing / traversal statistics
+ */
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "hairpt.h"
+#include "host/host_scene.h"
+
+namespace {
+
+void usage() {
+    std::printf(
+        "Mitsuba-compatible hair path tracer for AMD Instinct MI355X\n"
+        "Usage: mitsuba [options] <scene.xml>...\n"
+        "Options:\n"
+        "   -h          Display this help text\n"
+        "   -D key=val  Define a constant, which can referenced as \"$key\" in the scene\n"
+        "   -o fname    Write the output image to the file denoted by \"fname\"\n"
+        "   -p count    Override the detected number of processors (ignored: GPU render)\n"
+        "   -q          Quiet mode - do not print any log messages to stdout\n"
+        "   -x          Skip rendering of files where output already exists\n"
+        "   --spp N --width W --height H --max-depth D   override scene parameters\n"
+        "   --device I --gpus N   render on N devices starting at I\n"
+        "   --stats     print per-kernel timing and traversal counters\n");
+}
+
+struct Opts {
+    std::vector<std::pair<std::string, std::string>> defines;
+    std::string out;
+    bool quiet = false, skipExisting = false, stats = false;
+    int spp = 0, width = 0, height = 0, maxDepth = -2, device = 0, gpus = 1;
+    std::vector<std::string> scenes;
+};
+
+bool exists(const std::string &p) {
+    std::ifstream f(p);
+    return (bool) f;
+}
+
+} // namespace
+
+int main(int argc, char **argv) {
+    Opts o;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto next = [&](const char *what) -> std::string {
+            if (i + 1 >= argc) {
+                std::fprintf(stderr, "missing argument for %s\n", what);
+                std::exit(1);
+            }
+            return argv[++i];
+        };
+        if (a == "-h" || a == "--help") { usage(); return 0; }
+        else if (a == "-D") {
+            std::string kv = next("-D");
+            size_t eq = kv.find('=');
+            if (eq == std::string::npos) { std::fprintf(stderr, "-D expects key=value\n"); return 1; }
+            o.defines.push_back({kv.substr(0, eq), kv.substr(eq + 1)});
+        } else if (a == "-o") o.out = next("-o");
+        else if (a == "-p" || a == "-b" || a == "-r" || a == "-L" || a == "-a") (void) next(a.c_str());
+        else if (a == "-q") o.quiet = true;
+        else if (a == "-x") o.skipExisting = true;
+        else if (a == "-v" || a == "-z" || a == "-t" || a == "-w") {}
+        else if (a == "-c" || a == "-s") {
+            std::fprintf(stderr, "network rendering (-c/-s) is replaced by --gpus on one MI355X node\n");
+            return 1;
+        } else if (a == "--spp") o.spp = std::atoi(next("--spp").c_str());
+        else if (a == "--width") o.width = std::atoi(next("--width").c_str());
+        else if (a == "--height") o.height = std::atoi(next("--height").c_str());
+        else if (a == "--max-depth") o.maxDepth = std::atoi(next("--max-depth").c_str());
+        else if (a == "--device") o.device = std::atoi(next("--device").c_str());
+        else if (a == "--gpus") o.gpus = std::max(1, std::atoi(next("--gpus").c_str()));
+        else if (a == "--stats") o.stats = true;
+        else if (!a.empty() && a[0] == '-') { std::fprintf(stderr, "unknown option %s\n", a.c_str()); usage(); return 1; }
+        else o.scenes.push_back(a);
+    }
+    if (o.scenes.empty()) { usage(); return 1; }
+    for (const std::string &scene : o.scenes) {
+        std::vector<const char *> keys, vals;
+        for (auto &kv : o.defines) { keys.push_back(kv.first.c_str()); vals.push_back(kv.second.c_str()); }
+        hpt::SceneDesc desc;
+        try {
+            std::map<std::string, std::string> defs(o.defines.begin(), o.defines.end());
+            desc = hpt::parseSceneXML(scene, defs);
+        } catch (const std::exception &e) {
+            std::fprintf(stderr, "Error while parsing \"%s\": %s\n", scene.c_str(), e.what());
+            return 2;
+        }
+        bool ldr = desc.film == "ldrfilm" || desc.fileFormat == "png";
+        std::string out = o.out;
+        if (out.empty()) {
+            size_t dot = scene.find_last_of('.');
+            out = (dot == std::string::npos ? scene : scene.substr(0, dot)) + (ldr ? ".png" : ".pfm");
+        }
+        if (o.skipExisting && exists(out)) {
+            if (!o.quiet) std::printf("Skipping \"%s\": output exists\n", scene.c_str());
+            continue;
+        }
+        const int G = o.gpus;
+        std::vector<hpt_context *> ctx(G, nullptr);
+        int W = 0, H = 0, spp = 0;
+        for (int g = 0; g < G; ++g) {
+            int rc = hpt_context_create(o.device + g, &ctx[g]);
+            if (rc) { std::fprintf(stderr, "cannot create a gfx950 context on device %d (%d)\n", o.device + g, rc); return 3; }
+            rc = hpt_load_scene_xml(ctx[g], scene.c_str(), (int) keys.size(), keys.data(), vals.data());
+            if (rc) { std::fprintf(stderr, "%s\n", hpt_last_error(ctx[g])); return 2; }
+            hpt_scene_info info;
+            hpt_get_scene_info(ctx[g], &info);
+            if (o.width || o.height || o.maxDepth != -2) {
+                /* re-issue the camera / integrator with overrides */
+                W = o.width ? o.width : info.width;
+                H = o.height ? o.height : info.height;
+                hpt_set_camera(ctx[g], desc.toWorld, desc.fov, W, H, desc.nearClip, desc.farClip);
+                hpt_set_integrator(ctx[g], o.maxDepth != -2 ? o.maxDepth : info.max_depth, info.rr_depth,
+                                   info.strict_normals, info.hide_emitters);
+            }
+            if (o.spp) hpt_set_sampler(ctx[g], o.spp);
+            rc = hpt_prepare(ctx[g]);
+            if (rc) { std::fprintf(stderr, "%s\n", hpt_last_error(ctx[g])); return 2; }
+            hpt_get_scene_info(ctx[g], &info);
+            W = info.width;
+            H = info.height;
+            spp = info.spp;
+            if (g == 0 && !o.quiet)
+                std::printf("Scene \"%s\": %dx%d @ %d spp, %llu hair segments, kd-tree %llu nodes (depth %d, %.2f s)\n",
+                            scene.c_str(), W, H, spp, (unsigned long long) info.segments,
+                            (unsigned long long) info.kd_nodes, info.kd_depth, info.kd_build_seconds);
+        }
+        std::vector<std::vector<float>> films(G, std::vector<float>((size_t) W * H * 4, 0.0f));
+        std::vector<int> rcs(G, 0);
+        auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> th;
+        for (int g = 0; g < G; ++g)
+            th.emplace_back([&, g] {
+                hpt_render_params p;
+                std::memset(&p, 0, sizeof(p));
+                p.spp_begin = 0;
+                p.spp_end = spp;
+                p.shard = g;
+                p.n_shards = G;
+                p.collect_stats = o.stats ? 1 : 0;
+                rcs[g] = hpt_render(ctx[g], &p, films[g].data());
+            });
+        for (auto &t : th) t.join();
+        double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        for (int g = 0; g < G; ++g)
+            if (rcs[g]) { std::fprintf(stderr, "render failed on device %d: %s\n", o.device + g, hpt_last_error(ctx[g])); return 4; }
+        /* film combine (renderproc.cpp:142-145) + develop (ldrfilm.cpp:300-330) */
+        std::vector<float> rgb((size_t) W * H * 3, 0.0f);
+        for (size_t i = 0; i < (size_t) W * H; ++i) {
+            float acc[4] = {0, 0, 0, 0};
+            for (int g = 0; g < G; ++g)
+                for (int k = 0; k < 4; ++k) acc[k] += films[g][4 * i + k];
+            float inv = acc[3] != 0 ? 1.0f / acc[3] : 0.0f;
+            for (int k = 0; k < 3; ++k) rgb[3 * i + k] = acc[k] * inv;
+        }
+        bool ok = ldr ? hpt::writePNG8(out, rgb.data(), W, H, desc.gamma) : hpt::writePFM(out, rgb.data(), W, H);
+        if (!ok) { std::fprintf(stderr, "cannot write %s\n", out.c_str()); return 5; }
+        if (!o.quiet) {
+            double paths = (double) W * H * spp;
+            std::printf("Rendering finished (took %.3f s, %.2f Mpaths/s on %d GPU%s) -> %s\n", sec, paths / sec * 1e-6, G,
+                        G > 1 ? "s" : "", out.c_str());
+            if (o.stats) {
+                hpt_stats s;
+                hpt_get_stats(ctx[0], &s);
+                std::printf("device 0: trace %.2f ms (%llu launches) shade %.2f post %.2f camera %.2f gather %.2f; "
+                            "nodes %llu prims %llu bounces %llu max bounce %d\n",
+                            s.ms_trace, (unsigned long long) s.trace_launches, s.ms_shade, s.ms_post, s.ms_camera,
+                            s.ms_gather, (unsigned long long) s.nodes, (unsigned long long) s.prims,
+                            (unsigned long long) s.bounces, s.max_bounces);
+            }
+        }
+        for (auto c : ctx) hpt_context_destroy(c);
+    }
+    return 0;
+}

@@ -1,0 +1,155 @@
+/*
+ * host_scene.h -- host-side scene model of the MI355X hair path tracer.
+ *
+ * The host owns everything that is built once per scene: the parsed scene
+ * description, the hair vertices (hair.cpp:609-785 loader semantics), the SAH
+ * kd-tree over hair segments, the Marschner / Kajiya-Kay precomputations and
+ * the environment-map sampling tables.  hpt_capi.cpp uploads the result to
+ * HBM as an HptScene (hpt_device.h).
+ */
+#ifndef HPT_HOST_SCENE_H
+#define HPT_HOST_SCENE_H
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../hpt_device.h"
+
+namespace hpt {
+
+struct Vec3f {
+    float x = 0, y = 0, z = 0;
+};
+
+/* ---- parsed scene description (subset of the Mitsuba 0.5 scene schema) ---- */
+struct SceneDesc {
+    /* integrator (integrator.cpp:190-203, path.cpp) */
+    std::string integrator = "path";
+    int maxDepth = -1, rrDepth = 5;
+    bool strictNormals = false, hideEmitters = false;
+    /* sensor (perspective.cpp) */
+    float toWorld[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    float fov = 45.0f, nearClip = 1e-2f, farClip = 1e4f;
+    std::string fovAxis = "x";
+    /* sampler */
+    std::string sampler = "sobol";
+    int spp = 4;
+    /* film */
+    std::string film = "hdrfilm";
+    int width = 768, height = 576;
+    float gamma = -1.0f;
+    std::string fileFormat;
+    std::string rfilter = "tent";
+    /* hair shape (hair.cpp:609-640) */
+    std::string hairFile;
+    float radius = 0.025f, angleThreshold = 1.0f, reduction = 0.0f;
+    float hairToWorld[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    bool hairHasToWorld = false;
+    /* bsdf */
+    std::string bsdf = "";
+    float intIOR = 1.5046f, extIOR = 1.000277f;   /* ior.h: bk7 / air defaults */
+    std::string distribution = "beckmann";
+    float alpha = 0.1f;                            /* microfacet.h:99-140 defaults */
+    float diffuse[3] = {0.5f, 0.5f, 0.5f};
+    float specular[3] = {0.5f, 0.5f, 0.5f};        /* marschner default 0.5 */
+    bool specularGiven = false;
+    float exponent = 30.0f;
+    bool nonlinear = false;
+    /* emitter */
+    std::string emitter = "";
+    std::string envFile;
+    float envScale = 1.0f;
+    float turbidity = 3.0f, skyScale = 1.0f, sunScale = 1.0f, sunRadiusScale = 1.0f;
+    float sunDirection[3] = {0, 1, 0};
+    bool sunDirectionGiven = false;
+    int skyResolution = 512;
+    float emitterToWorld[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    std::string sceneDir;
+};
+
+/* Parse a Mitsuba scene XML (scenehandler.cpp semantics for the subset used by
+ * models/ scenes: <default>, $-substitution, <ref>, nested objects, typed
+ * properties, <transform> with matrix/lookat/translate/rotate/scale).
+ * Throws std::runtime_error with a message on failure. */
+SceneDesc parseSceneXML(const std::string &path, const std::map<std::string, std::string> &defines);
+
+/* ---- hair geometry ---- */
+struct HairData {
+    std::vector<float> xyz;         /* 3 per vertex */
+    std::vector<uint8_t> starts;    /* n + 1 entries, last = 1 */
+    float radius = 0.025f;
+    size_t nDegenerate = 0, nSkipped = 0;
+    size_t vertexCount() const { return xyz.size() / 3; }
+};
+
+/* hair.cpp:609-785 (binary + ASCII).  to_world may be null. */
+HairData loadHair(const std::string &path, float radius, float angleThresholdDeg, float reduction,
+                  const float *toWorld);
+
+/* ---- kd-tree ---- */
+struct KDTreeHost {
+    std::vector<HptNode> nodes;
+    std::vector<uint32_t> prims;          /* segment index per leaf entry */
+    std::vector<HptSegment> segs;         /* per segment (index = segment id) */
+    std::vector<uint32_t> segFirstVertex; /* segment id -> first vertex index */
+    float aabbMin[3], aabbMax[3];
+    int maxDepthUsed = 0;
+    size_t leaves = 0, emptyLeaves = 0;
+    double buildSeconds = 0;
+};
+
+struct KDBuildParams {
+    float traversalCost = 10.0f;   /* hair.cpp:130-136 */
+    float queryCost = 15.0f;
+    float emptySpaceBonus = 0.9f;
+    int stopPrims = 1;
+    int maxBadRefines = 3;         /* gkdtree.h:731-746 */
+    int bins = 128;                /* min-max bins */
+    bool clip = true;              /* perfect splits via getClippedAABB */
+    int threads = 0;               /* 0 = hardware concurrency */
+};
+
+KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params);
+
+/* ---- precomputation ---- */
+struct MarschnerHost {
+    std::vector<HptF4> table[3];
+    std::vector<float> cdf[3], sums[3];
+    std::vector<float> trans;      /* 1D slice */
+    float fdr = 0, invEta2 = 0, specularSamplingWeight = 0;
+    float vR = 0, vTT = 0, vTRT = 0, scaleAngleRad = 0;
+    float diffuse[3];
+};
+
+bool precomputeMarschner(const SceneDesc &d, const std::string &dataDir, MarschnerHost &out,
+                         std::string &err);
+void configureKajiyaKay(const SceneDesc &d, HptKajiyaKay &out);
+
+struct EnvHost {
+    int w = 0, h = 0;
+    std::vector<float> rgb;        /* input bitmap (linear RGB) */
+    std::vector<HptF4> texel;      /* half-rounded */
+    std::vector<float> cdfRows, cdfCols, rowWeights;
+    float normalization = 0, scale = 1, pixelSizeX = 0, pixelSizeY = 0;
+    float toWorld[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+};
+
+void buildEnvMap(EnvHost &env);                           /* envmap.cpp:244-314 */
+void rasterizeSunSkyStandIn(const SceneDesc &d, EnvHost &env); /* see DESIGN.md */
+bool loadEnvFile(const std::string &path, EnvHost &env, std::string &err); /* .hdr / .pfm */
+
+void setupCamera(const SceneDesc &d, HptCamera &cam);      /* perspective.cpp:125-165 */
+void setupTent(float *lut, float &scale);                 /* rfilter.cpp:38-56 */
+
+/* float <-> IEEE half (round to nearest even) */
+uint16_t floatToHalf(float f);
+float halfToFloat(uint16_t h);
+
+/* image output (ldrfilm.cpp:300-330 / hdrfilm.cpp:214-227) */
+bool writePFM(const std::string &path, const float *rgb, int w, int h);
+bool writePNG8(const std::string &path, const float *rgb, int w, int h, float gamma);
+
+} // namespace hpt
+#endif

@@ -1,0 +1,488 @@
+/*
+ * kdtree_build.cpp -- SAH kd-tree over hair segments (host, multithreaded).
+ *
+ * Cost model and parameters follow HairKDTree (src/shapes/hair.cpp:108-159):
+ * traversal cost 10, query cost 15, empty-space bonus 0.9, stop at 1
+ * primitive, clipping ("perfect splits") on, retraction after 3 bad
+ * refinements, depth cap 8 + 1.3 log2(N) limited to 48 (gkdtree.h:986-988).
+ * Split search is min-max binning (128 bins) for large nodes and an exact
+ * event sweep for small ones -- the same two-tier strategy as
+ * GenericKDTree::buildTreeMinMax / buildTreeSAH, implemented independently.
+ *
+ * Primitive bounds use the reference's geometry:
+ *   getAABB        -- ellipses cut by the two miter planes, radius*(1-1e-4)
+ *                     (hair.cpp:349-378)
+ *   getClippedAABB -- infinite cylinder (radius*(1+1e-4)) against the six
+ *                     faces of the clipped box (hair.cpp:246-343)
+ * in single precision like the reference.  The tree's AABB is the union of
+ * getAABB over all segments, which the traversal uses for its entry clip
+ * (hair.cpp:200-217, skdtree.cpp:124).
+ *
+ * Output layout (hpt_device.h HptNode): depth-first with sibling pairs, so
+ * an inner node's children are nodes[left] and nodes[left+1].
+ */
+#include <algorithm>
+#include <array>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <future>
+#include <limits>
+#include <stdexcept>
+#include <thread>
+
+#include "host_scene.h"
+
+namespace hpt {
+namespace {
+
+const float kEps = 1e-4f;
+const float kInf = std::numeric_limits<float>::infinity();
+
+struct V {
+    float x, y, z;
+    float operator[](int i) const { return i == 0 ? x : (i == 1 ? y : z); }
+    float &operator[](int i) { return i == 0 ? x : (i == 1 ? y : z); }
+};
+inline V operator+(V a, V b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline V operator-(V a, V b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline V operator*(V a, float f) { return {a.x * f, a.y * f, a.z * f}; }
+inline V operator*(float f, V a) { return a * f; }
+inline float dot(V a, V b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+inline float len(V a) { return std::sqrt(dot(a, a)); }
+inline V cross(V a, V b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x}; }
+inline V normalize(V a) { float r = 1.0f / len(a); return a * r; }
+inline bool eq(V a, V b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
+
+struct Box {
+    V mn{kInf, kInf, kInf}, mx{-kInf, -kInf, -kInf};
+    bool valid() const { return mx.x >= mn.x && mx.y >= mn.y && mx.z >= mn.z; }
+    void expand(V p) {
+        for (int i = 0; i < 3; ++i) {
+            mn[i] = std::min(mn[i], p[i]);
+            mx[i] = std::max(mx[i], p[i]);
+        }
+    }
+    void expand(const Box &b) {
+        for (int i = 0; i < 3; ++i) {
+            mn[i] = std::min(mn[i], b.mn[i]);
+            mx[i] = std::max(mx[i], b.mx[i]);
+        }
+    }
+    void clip(const Box &b) {
+        for (int i = 0; i < 3; ++i) {
+            mn[i] = std::max(mn[i], b.mn[i]);
+            mx[i] = std::min(mx[i], b.mx[i]);
+        }
+    }
+    bool contains(V p) const {
+        for (int i = 0; i < 3; ++i)
+            if (p[i] < mn[i] || p[i] > mx[i]) return false;
+        return true;
+    }
+    float area() const {
+        V d = mx - mn;
+        return 2.0f * (d.x * d.y + d.y * d.z + d.z * d.x);
+    }
+};
+
+void coordSystem(V a, V &b, V &c) { /* util.cpp:592-601 */
+    if (std::abs(a.x) > std::abs(a.y)) {
+        float inv = 1.0f / std::sqrt(a.x * a.x + a.z * a.z);
+        c = {a.z * inv, 0.0f, -a.x * inv};
+    } else {
+        float inv = 1.0f / std::sqrt(a.y * a.y + a.z * a.z);
+        c = {0.0f, a.z * inv, -a.y * inv};
+    }
+    b = cross(c, a);
+}
+
+bool solveQuadF(float a, float b, float c, float &x0, float &x1) {
+    if (a == 0) {
+        if (b != 0) { x0 = x1 = -c / b; return true; }
+        return false;
+    }
+    float disc = b * b - 4.0f * a * c;
+    if (disc < 0) return false;
+    float sq = std::sqrt(disc), temp = (b < 0) ? -0.5f * (b - sq) : -0.5f * (b + sq);
+    x0 = temp / a;
+    x1 = c / temp;
+    if (x0 > x1) std::swap(x0, x1);
+    return true;
+}
+
+struct SegGeom {
+    const HairData &h;
+    explicit SegGeom(const HairData &hd) : h(hd) {}
+    V vtx(uint32_t i) const { return {h.xyz[3 * i], h.xyz[3 * i + 1], h.xyz[3 * i + 2]}; }
+    V tangent(uint32_t iv) const { return normalize(vtx(iv + 1) - vtx(iv)); }
+    V firstMiter(uint32_t iv) const {
+        return !h.starts[iv] ? normalize(normalize(vtx(iv) - vtx(iv - 1)) + tangent(iv)) : tangent(iv);
+    }
+    V secondMiter(uint32_t iv) const {
+        return !h.starts[iv + 2] ? normalize(tangent(iv) + normalize(vtx(iv + 2) - vtx(iv + 1))) : tangent(iv);
+    }
+
+    /* ellipse from cutting an infinite cylinder with a plane (hair.cpp:246-286) */
+    static bool cylPlane(V planePt, V planeN, V cylPt, V cylD, float radius, V &center, V *axes, float *lengths) {
+        if (std::abs(dot(planeN, cylD)) < kEps) return false;
+        V B, A = cylD - dot(cylD, planeN) * planeN;
+        float l = len(A);
+        if (l > kEps && !eq(planeN, cylD)) {
+            A = A * (1.0f / l);
+            B = cross(planeN, A);
+        } else {
+            coordSystem(planeN, A, B);
+        }
+        V delta = planePt - cylPt, deltaProj = delta - cylD * dot(delta, cylD);
+        float aDotD = dot(A, cylD), bDotD = dot(B, cylD);
+        float c0 = 1 - aDotD * aDotD, c1 = 1 - bDotD * bDotD;
+        float c2 = 2 * dot(A, deltaProj), c3 = 2 * dot(B, deltaProj);
+        float c4 = dot(delta, deltaProj) - radius * radius;
+        float lambda = (c2 * c2 / (4 * c0) + c3 * c3 / (4 * c1) - c4) / (c0 * c1);
+        float alpha0 = -c2 / (2 * c0), beta0 = -c3 / (2 * c1);
+        lengths[0] = std::sqrt(c1 * lambda);
+        lengths[1] = std::sqrt(c0 * lambda);
+        center = planePt + alpha0 * A + beta0 * B;
+        axes[0] = A;
+        axes[1] = B;
+        return true;
+    }
+
+    /* hair.cpp:349-378 */
+    Box aabb(uint32_t iv) const {
+        Box r;
+        V c, ax[2];
+        float l[2] = {0, 0};
+        for (int end = 0; end < 2; ++end) {
+            V p = end == 0 ? vtx(iv) : vtx(iv + 1);
+            V n = end == 0 ? firstMiter(iv) : secondMiter(iv);
+            if (!cylPlane(p, n, p, tangent(iv), h.radius * (1 - kEps), c, ax, l)) {
+                l[0] = l[1] = 0;
+                c = p;
+            }
+            ax[0] = ax[0] * l[0];
+            ax[1] = ax[1] * l[1];
+            for (int i = 0; i < 3; ++i) {
+                float range = std::sqrt(ax[0][i] * ax[0][i] + ax[1][i] * ax[1][i]);
+                r.mn[i] = std::min(r.mn[i], c[i] - range);
+                r.mx[i] = std::max(r.mx[i], c[i] + range);
+            }
+        }
+        return r;
+    }
+
+    /* hair.cpp:289-343 */
+    Box cylFace(int axis, V mn, V mx, V cylPt, V cylD) const {
+        int a1 = (axis + 1) % 3, a2 = (axis + 2) % 3;
+        V n{0, 0, 0};
+        n[axis] = 1;
+        V c, ax[2];
+        float l[2];
+        Box out;
+        if (!cylPlane(mn, n, cylPt, cylD, h.radius * (1 + kEps), c, ax, l)) return out;
+        for (int i = 0; i < 4; ++i) {
+            V p1, p2;
+            p1[axis] = p2[axis] = mn[axis];
+            p1[a1] = ((i + 1) & 2) ? mn[a1] : mx[a1];
+            p1[a2] = ((i + 0) & 2) ? mn[a2] : mx[a2];
+            p2[a1] = ((i + 2) & 2) ? mn[a1] : mx[a1];
+            p2[a2] = ((i + 1) & 2) ? mn[a2] : mx[a2];
+            float p1x = dot(p1 - c, ax[0]) / l[0], p1y = dot(p1 - c, ax[1]) / l[1];
+            float p2x = dot(p2 - c, ax[0]) / l[0], p2y = dot(p2 - c, ax[1]) / l[1];
+            float rx = p2x - p1x, ry = p2y - p1y;
+            float A = rx * rx + ry * ry, B = 2 * (p1x * rx + p1y * ry), C = p1x * p1x + p1y * p1y - 1;
+            float x0, x1;
+            if (solveQuadF(A, B, C, x0, x1)) {
+                if (x0 >= 0 && x0 <= 1) out.expand(p1 + (p2 - p1) * x0);
+                if (x1 >= 0 && x1 <= 1) out.expand(p1 + (p2 - p1) * x1);
+            }
+        }
+        ax[0] = ax[0] * l[0];
+        ax[1] = ax[1] * l[1];
+        Box face;
+        face.mn = mn;
+        face.mx = mx;
+        for (int i = 0; i < 2; ++i) {
+            int j = (i == 0) ? a1 : a2;
+            float alpha = ax[0][j], beta = ax[1][j];
+            float tmp = 1 / std::sqrt(alpha * alpha + beta * beta);
+            float cosT = alpha * tmp, sinT = beta * tmp;
+            V q1 = c + cosT * ax[0] + sinT * ax[1];
+            V q2 = c - cosT * ax[0] - sinT * ax[1];
+            if (face.contains(q1)) out.expand(q1);
+            if (face.contains(q2)) out.expand(q2);
+        }
+        return out;
+    }
+
+    Box clipped(uint32_t iv, const Box &box) const {
+        Box base = aabb(iv);
+        base.clip(box);
+        if (!base.valid()) return base;
+        V cp = vtx(iv), cd = tangent(iv);
+        Box r;
+        const V &a = base.mn, &b = base.mx;
+        r.expand(cylFace(0, {a.x, a.y, a.z}, {a.x, b.y, b.z}, cp, cd));
+        r.expand(cylFace(0, {b.x, a.y, a.z}, {b.x, b.y, b.z}, cp, cd));
+        r.expand(cylFace(1, {a.x, a.y, a.z}, {b.x, a.y, b.z}, cp, cd));
+        r.expand(cylFace(1, {a.x, b.y, a.z}, {b.x, b.y, b.z}, cp, cd));
+        r.expand(cylFace(2, {a.x, a.y, a.z}, {b.x, b.y, a.z}, cp, cd));
+        r.expand(cylFace(2, {a.x, a.y, b.z}, {b.x, b.y, b.z}, cp, cd));
+        r.clip(base);
+        return r;
+    }
+};
+
+struct Ref {
+    uint32_t seg;
+    Box b;
+};
+
+struct BNode {
+    int axis = -1;
+    float split = 0;
+    std::unique_ptr<BNode> kid[2];
+    std::vector<uint32_t> prims;
+};
+
+struct Builder {
+    const SegGeom &g;
+    const std::vector<uint32_t> &segIv;
+    KDBuildParams P;
+    int maxDepth;
+
+    struct Split {
+        float cost = kInf;
+        int axis = -1;
+        float pos = 0;
+        size_t nl = 0, nr = 0;
+    };
+
+    Split findSplit(const std::vector<Ref> &refs, const Box &bounds) const {
+        Split best;
+        const size_t N = refs.size();
+        const float invSA = 1.0f / bounds.area();
+        for (int axis = 0; axis < 3; ++axis) {
+            float lo = bounds.mn[axis], hi = bounds.mx[axis], ext = hi - lo;
+            if (!(ext > 0)) continue;
+            auto evalCost = [&](float pos, size_t nl, size_t nr) {
+                Box L = bounds, R = bounds;
+                L.mx[axis] = pos;
+                R.mn[axis] = pos;
+                float c = P.traversalCost + P.queryCost * (L.area() * nl + R.area() * nr) * invSA;
+                if (nl == 0 || nr == 0) c *= P.emptySpaceBonus;
+                return c;
+            };
+            if (N <= 256) {
+                /* exact sweep over primitive bound events */
+                std::vector<std::pair<float, int>> ev;
+                ev.reserve(2 * N);
+                for (auto &r : refs) {
+                    ev.push_back({r.b.mn[axis], 1}); /* start */
+                    ev.push_back({r.b.mx[axis], 0}); /* end */
+                }
+                std::sort(ev.begin(), ev.end());
+                size_t nl = 0, nr = N;
+                for (size_t i = 0; i < ev.size();) {
+                    float pos = ev[i].first;
+                    size_t ends = 0, starts = 0;
+                    while (i < ev.size() && ev[i].first == pos) {
+                        if (ev[i].second == 0) ends++;
+                        else starts++;
+                        ++i;
+                    }
+                    nr -= ends;
+                    if (pos > lo && pos < hi) {
+                        float c = evalCost(pos, nl, nr);
+                        if (c < best.cost) best = {c, axis, pos, nl, nr};
+                    }
+                    nl += starts;
+                }
+            } else {
+                const int B = P.bins;
+                std::vector<uint32_t> minB(B, 0), maxB(B, 0);
+                float scale = B / ext;
+                for (auto &r : refs) {
+                    int a = (int) ((r.b.mn[axis] - lo) * scale), b = (int) ((r.b.mx[axis] - lo) * scale);
+                    a = std::min(std::max(a, 0), B - 1);
+                    b = std::min(std::max(b, 0), B - 1);
+                    minB[a]++;
+                    maxB[b]++;
+                }
+                size_t nl = 0, nEndedLeft = 0;
+                for (int i = 0; i < B - 1; ++i) {
+                    nl += minB[i];
+                    nEndedLeft += maxB[i];
+                    size_t nr = N - nEndedLeft;
+                    float pos = lo + (float) (i + 1) * (ext / B);
+                    if (!(pos > lo && pos < hi)) continue;
+                    float c = evalCost(pos, nl, nr);
+                    if (c < best.cost) best = {c, axis, pos, nl, nr};
+                }
+            }
+        }
+        return best;
+    }
+
+    std::unique_ptr<BNode> build(std::vector<Ref> refs, Box bounds, int depth, int badRefines) {
+        std::unique_ptr<BNode> node(new BNode());
+        const size_t N = refs.size();
+        auto makeLeaf = [&]() {
+            node->prims.reserve(N);
+            for (auto &r : refs) node->prims.push_back(r.seg);
+            return std::move(node);
+        };
+        if ((int) N <= P.stopPrims || depth >= maxDepth) return makeLeaf();
+        float leafCost = P.queryCost * (float) N;
+        Split s = findSplit(refs, bounds);
+        if (s.axis < 0) return makeLeaf();
+        if (s.cost >= leafCost) {
+            if ((s.cost > 4 * leafCost && N < 16) || badRefines >= P.maxBadRefines) return makeLeaf();
+            ++badRefines;
+        }
+        Box lb = bounds, rb = bounds;
+        lb.mx[s.axis] = s.pos;
+        rb.mn[s.axis] = s.pos;
+        std::vector<Ref> L, R;
+        L.reserve(s.nl);
+        R.reserve(s.nr);
+        for (auto &r : refs) {
+            float a = r.b.mn[s.axis], b = r.b.mx[s.axis];
+            if (b <= s.pos && !(a == b && b == s.pos)) {
+                L.push_back(r);
+            } else if (a >= s.pos) {
+                R.push_back(r);
+            } else {
+                Box cl = r.b, cr = r.b;
+                if (P.clip) {
+                    cl = g.clipped(segIv[r.seg], lb);
+                    cr = g.clipped(segIv[r.seg], rb);
+                } else {
+                    cl.clip(lb);
+                    cr.clip(rb);
+                }
+                if (cl.valid()) L.push_back({r.seg, cl});
+                if (cr.valid()) R.push_back({r.seg, cr});
+            }
+        }
+        std::vector<Ref>().swap(refs);
+        node->axis = s.axis;
+        node->split = s.pos;
+        if (N > 20000 && depth < 6) {
+            auto fut = std::async(std::launch::async, [&, lb, badRefines]() {
+                return build(std::move(L), lb, depth + 1, badRefines);
+            });
+            node->kid[1] = build(std::move(R), rb, depth + 1, badRefines);
+            node->kid[0] = fut.get();
+        } else {
+            node->kid[0] = build(std::move(L), lb, depth + 1, badRefines);
+            node->kid[1] = build(std::move(R), rb, depth + 1, badRefines);
+        }
+        return node;
+    }
+};
+
+void flatten(const BNode *n, uint32_t idx, int depth, KDTreeHost &t) {
+    t.maxDepthUsed = std::max(t.maxDepthUsed, depth);
+    if (n->axis < 0) {
+        uint32_t start = (uint32_t) t.prims.size();
+        for (uint32_t p : n->prims) t.prims.push_back(p);
+        t.nodes[idx].w0 = 0x80000000u | start;
+        t.nodes[idx].w1 = (uint32_t) t.prims.size();
+        t.leaves++;
+        if (n->prims.empty()) t.emptyLeaves++;
+        return;
+    }
+    uint32_t left = (uint32_t) t.nodes.size();
+    if (left >= (1u << 29)) throw std::runtime_error("kd-tree too large");
+    t.nodes.push_back({0, 0});
+    t.nodes.push_back({0, 0});
+    uint32_t sb;
+    std::memcpy(&sb, &n->split, 4);
+    t.nodes[idx].w0 = (left << 2) | (uint32_t) n->axis;
+    t.nodes[idx].w1 = sb;
+    flatten(n->kid[0].get(), left, depth + 1, t);
+    flatten(n->kid[1].get(), left + 1, depth + 1, t);
+}
+
+} // namespace
+
+KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
+    auto t0 = std::chrono::steady_clock::now();
+    KDTreeHost t;
+    SegGeom g(hair);
+    const size_t nv = hair.vertexCount();
+    /* segment index list (hair.cpp:117-123) */
+    std::vector<uint32_t> segIv;
+    segIv.reserve(nv);
+    for (size_t i = 0; i + 1 < nv; ++i)
+        if (!hair.starts[i + 1]) segIv.push_back((uint32_t) i);
+    const size_t S = segIv.size();
+    t.segFirstVertex = segIv;
+
+    /* double-precision per-segment records (hair.cpp:551-596) */
+    t.segs.resize(S);
+    for (size_t s = 0; s < S; ++s) {
+        uint32_t iv = segIv[s];
+        auto vd = [&](uint32_t i) {
+            return std::array<double, 3>{(double) hair.xyz[3 * i], (double) hair.xyz[3 * i + 1],
+                                         (double) hair.xyz[3 * i + 2]};
+        };
+        auto nrmd = [](std::array<double, 3> v) {
+            double l = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+            double r = 1.0 / l;
+            return std::array<double, 3>{v[0] * r, v[1] * r, v[2] * r};
+        };
+        auto subd = [](std::array<double, 3> a, std::array<double, 3> b) {
+            return std::array<double, 3>{a[0] - b[0], a[1] - b[1], a[2] - b[2]};
+        };
+        auto addd = [](std::array<double, 3> a, std::array<double, 3> b) {
+            return std::array<double, 3>{a[0] + b[0], a[1] + b[1], a[2] + b[2]};
+        };
+        auto v1 = vd(iv), v2 = vd(iv + 1);
+        auto axis = nrmd(subd(v2, v1));
+        std::array<double, 3> n1 = axis, n2 = axis;
+        if (!hair.starts[iv]) n1 = nrmd(addd(nrmd(subd(v1, vd(iv - 1))), axis));
+        if (!hair.starts[iv + 2]) n2 = nrmd(addd(axis, nrmd(subd(vd(iv + 2), v2))));
+        HptSegment &r = t.segs[s];
+        for (int k = 0; k < 3; ++k) {
+            r.v1[k] = v1[k];
+            r.axis[k] = axis[k];
+            r.n1[k] = n1[k];
+            r.n2[k] = n2[k];
+            r.v2[k] = v2[k];
+        }
+        r.iv = iv;
+        r.pad = 0;
+    }
+
+    /* primitive bounds + tree AABB (gkdtree.h:990-994) */
+    std::vector<Ref> refs(S);
+    Box root;
+    for (size_t s = 0; s < S; ++s) {
+        refs[s].seg = (uint32_t) s;
+        refs[s].b = g.aabb(segIv[s]);
+        root.expand(refs[s].b);
+    }
+    for (int i = 0; i < 3; ++i) {
+        t.aabbMin[i] = root.mn[i];
+        t.aabbMax[i] = root.mx[i];
+    }
+    if (S == 0) {
+        t.nodes.push_back({0x80000000u, 0});
+        t.leaves = 1;
+        return t;
+    }
+    int lg = 0;
+    while ((S >> (lg + 1)) != 0) lg++;
+    Builder b{g, segIv, params, std::min((int) (8 + 1.3f * lg), 48)};
+    std::unique_ptr<BNode> tree = b.build(std::move(refs), root, 0, 0);
+    t.nodes.reserve(2 * S);
+    t.nodes.push_back({0, 0});
+    flatten(tree.get(), 0, 0, t);
+    t.buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return t;
+}
+
+} // namespace hpt

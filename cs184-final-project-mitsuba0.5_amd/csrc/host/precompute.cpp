@@ -1,0 +1,709 @@
+/*
+ * precompute.cpp -- per-scene host precomputation for the hair path tracer.
+ *
+ *   Marschner ("marschner" plugin = src/bsdfs/marschner_diffuse.cpp):
+ *     azimuthal scattering tables N_R, N_TT, N_TRT (64x64, :751-847) by a
+ *     140-point Gauss-Legendre quadrature (gausssexylingerie.hpp) over a
+ *     wrapped-Gaussian detector table; per-lobe sampling CDFs
+ *     (Azimuthal ctor :41-62 -> InterpolatedDistribution1D ctor); the rough
+ *     dielectric transmittance reduced to a 1-D slice (rtrans.h:292-377) and
+ *     the diffuse Fresnel term Fdr (configure :222-238).
+ *   Kajiya-Kay (kajiyakay.cpp:80-107): energy conservation + sampling weight.
+ *   Environment map (envmap.cpp:244-314): fp16 texels, luminance*sin(theta)
+ *     marginal/conditional CDFs, normalisation.
+ *   Camera (perspective.cpp:125-165, sobol.cpp:147-158), tent filter LUT
+ *     (rfilter.cpp:38-56).
+ *
+ * All arithmetic is single precision in the reference's operation order,
+ * compiled without FMA contraction, so the device consumes the same table
+ * bits the reference's constructor would produce.
+ */
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+
+#include "host_scene.h"
+
+namespace hpt {
+namespace {
+
+const float kPi = 3.14159265358979323846f;
+const float kEps = 1e-4f;
+
+inline float clampf(float v, float lo, float hi) { return std::min(hi, std::max(lo, v)); }
+inline int clampi(int v, int lo, int hi) { return std::min(hi, std::max(lo, v)); }
+
+/* ---------------- cubic interpolation (libcore/spline.cpp) ---------------- */
+float cubic1D(float x, const float *values, size_t size, float min, float max) {
+    if (!(x >= min && x <= max)) return 0.0f;
+    float t = ((x - min) * (size - 1)) / (max - min);
+    size_t k = std::max((size_t) 0, std::min((size_t) t, size - 2));
+    float f0 = values[k], f1 = values[k + 1], d0, d1;
+    d0 = (k > 0) ? 0.5f * (values[k + 1] - values[k - 1]) : values[k + 1] - values[k];
+    d1 = (k + 2 < size) ? 0.5f * (values[k + 2] - values[k]) : values[k + 1] - values[k];
+    t = t - (float) k;
+    float t2 = t * t, t3 = t2 * t;
+    return (2 * t3 - 3 * t2 + 1) * f0 + (-2 * t3 + 3 * t2) * f1 + (t3 - 2 * t2 + t) * d0 + (t3 - t2) * d1;
+}
+
+bool knotW(float p, size_t size, float *w, size_t &knot) {
+    if (!(p >= 0.0f && p <= 1.0f)) return false;
+    float t = ((p - 0.0f) * (size - 1)) / (1.0f - 0.0f);
+    knot = std::min((size_t) t, size - 2);
+    t = t - (float) knot;
+    float t2 = t * t, t3 = t2 * t;
+    w[0] = 0.0f;
+    w[1] = 2 * t3 - 3 * t2 + 1;
+    w[2] = -2 * t3 + 3 * t2;
+    w[3] = 0.0f;
+    float d0 = t3 - 2 * t2 + t, d1 = t3 - t2;
+    if (knot > 0) { w[2] += 0.5f * d0; w[0] -= 0.5f * d0; }
+    else { w[2] += d0; w[1] -= d0; }
+    if (knot + 2 < size) { w[3] += 0.5f * d1; w[1] -= 0.5f * d1; }
+    else { w[2] += d1; w[1] -= d1; }
+    return true;
+}
+
+float cubic2D(float px, float py, const float *v, size_t sx, size_t sy) {
+    float kw[2][4];
+    size_t kn[2];
+    if (!knotW(px, sx, kw[0], kn[0]) || !knotW(py, sy, kw[1], kn[1])) return 0.0f;
+    float r = 0.0f;
+    for (int y = -1; y <= 2; ++y) {
+        float wy = kw[1][y + 1];
+        for (int x = -1; x <= 2; ++x) {
+            float w = kw[0][x + 1] * wy;
+            if (w == 0) continue;
+            r += v[(kn[1] + y) * sx + kn[0] + x] * w;
+        }
+    }
+    return r;
+}
+
+float cubic3D(float px, float py, float pz, const float *v, size_t sx, size_t sy, size_t sz) {
+    float kw[3][4];
+    size_t kn[3];
+    if (!knotW(px, sx, kw[0], kn[0]) || !knotW(py, sy, kw[1], kn[1]) || !knotW(pz, sz, kw[2], kn[2]))
+        return 0.0f;
+    float r = 0.0f;
+    for (int z = -1; z <= 2; ++z) {
+        float wz = kw[2][z + 1];
+        for (int y = -1; y <= 2; ++y) {
+            float wyz = kw[1][y + 1] * wz;
+            for (int x = -1; x <= 2; ++x) {
+                float w = kw[0][x + 1] * wyz;
+                if (w == 0) continue;
+                r += v[((kn[2] + z) * sy + (kn[1] + y)) * sx + kn[0] + x] * w;
+            }
+        }
+    }
+    return r;
+}
+
+/* ---------------- rough transmittance (rtrans.h) ---------------- */
+struct RTrans {
+    size_t nEta = 0, nAlpha = 0, nTheta = 0;
+    float etaMin = 0, etaMax = 0, alphaMin = 0, alphaMax = 0;
+    std::vector<float> trans, diff;
+    bool load(const std::string &path) {
+        std::ifstream f(path, std::ios::binary);
+        if (!f) return false;
+        char hdr[17];
+        f.read(hdr, 17);
+        if (!f || std::memcmp(hdr, "MTS_TRANSMITTANCE", 17) != 0) return false;
+        uint64_t sz[3];
+        f.read((char *) sz, 24);
+        nEta = sz[0]; nAlpha = sz[1]; nTheta = sz[2];
+        float mm[4];
+        f.read((char *) mm, 16);
+        etaMin = mm[0]; etaMax = mm[1]; alphaMin = mm[2]; alphaMax = mm[3];
+        size_t ts = 2 * nEta * nAlpha * nTheta, ds = 2 * nEta * nAlpha;
+        std::vector<float> raw(ts + ds);
+        f.read((char *) raw.data(), (std::streamsize) (raw.size() * 4));
+        if (!f) return false;
+        trans.resize(ts);
+        diff.resize(ds);
+        size_t a = 0, b = 0, p = 0;
+        for (size_t i = 0; i < 2 * nEta; ++i)
+            for (size_t j = 0; j < nAlpha; ++j) {
+                for (size_t k = 0; k < nTheta; ++k) trans[a++] = raw[p++];
+                diff[b++] = raw[p++];
+            }
+        return true;
+    }
+    /* setEta (rtrans.h:292-345): returns the 2-D (alpha x theta) slice and the 1-D diffuse slice */
+    void sliceEta(float eta, std::vector<float> &t2, std::vector<float> &d1) const {
+        const float *tr = trans.data(), *dt = diff.data();
+        if (eta < 1) {
+            tr += nEta * nAlpha * nTheta;
+            dt += nEta * nAlpha;
+            eta = 1.0f / eta;
+        }
+        if (eta < etaMin) eta = etaMin;
+        float we = std::pow((eta - etaMin) / (etaMax - etaMin), (float) 0.25f);
+        t2.assign(nAlpha * nTheta, 0.0f);
+        d1.assign(nAlpha, 0.0f);
+        float dA = 1.0f / (nAlpha - 1), dT = 1.0f / (nTheta - 1);
+        for (size_t i = 0; i < nAlpha; ++i) {
+            for (size_t j = 0; j < nTheta; ++j)
+                t2[i * nTheta + j] = cubic3D(j * dT, i * dA, we, tr, nTheta, nAlpha, nEta);
+            d1[i] = cubic2D(i * dA, we, dt, nAlpha, nEta);
+        }
+    }
+};
+
+/* ---------------- Gauss-Legendre (gausssexylingerie.hpp) ---------------- */
+double legendreP(double x, int n) {
+    if (n == 0) return 1.0;
+    if (n == 1) return x;
+    double P0 = 1.0, P1 = x;
+    for (int i = 2; i <= n; ++i) {
+        double Pi = ((2.0 * i - 1.0) * x * P1 - (i - 1.0) * P0) / i;
+        P0 = P1;
+        P1 = Pi;
+    }
+    return P1;
+}
+double legendreD(double x, int n) { return n / (x * x - 1.0) * (x * legendreP(x, n) - legendreP(x, n - 1)); }
+
+void gaussLegendre(int N, std::vector<float> &pts, std::vector<float> &wts) {
+    pts.resize(N);
+    wts.resize(N);
+    for (int i = 0; i < N; ++i) {
+        int k = i + 1;
+        double x = std::cos(kPi * (4.0 * k - 1.0) / (4.0 * N + 2.0)) *
+                   (1.0 - 1.0 / (8.0 * N * N) + 1.0 / (8.0 * N * N * N));
+        for (int it = 0; it < 100; ++it) {
+            double f = legendreP(x, N);
+            x -= f / legendreD(x, N);
+            if (std::abs(f) < 1e-6) break;
+        }
+        pts[i] = float(x);
+        wts[i] = float(2.0 / ((1.0 - pts[i] * pts[i]) * legendreD(pts[i], N) * legendreD(pts[i], N)));
+    }
+}
+
+/* util.cpp:651-681 via util.h:479 */
+float fresnelExt(float cosThetaI_, float eta) {
+    if (eta == 1) return 0.0f;
+    float scale = (cosThetaI_ > 0) ? 1 / eta : eta, cosThetaTSqr = 1 - (1 - cosThetaI_ * cosThetaI_) * (scale * scale);
+    if (cosThetaTSqr <= 0.0f) return 1.0f;
+    float cI = std::abs(cosThetaI_), cT = std::sqrt(cosThetaTSqr);
+    float Rs = (cI - eta * cT) / (cI + eta * cT), Rp = (eta * cI - cT) / (eta * cI + cT);
+    return 0.5f * (Rs * Rs + Rp * Rp);
+}
+
+float gaussDetector(float beta, float theta) {
+    return std::exp(-theta * theta / (2.0f * beta * beta)) / (std::sqrt(2.0f * kPi) * beta);
+}
+float wrappedGauss(float beta, float phi) {
+    float result = 0.0f, delta, shift = 0.0f;
+    do {
+        delta = gaussDetector(beta, phi + shift) + gaussDetector(beta, phi - shift - 2 * kPi);
+        result += delta;
+        shift += 2 * kPi;
+    } while (delta > 1e-4f);
+    return result;
+}
+float lobePhi(float gammaI, float gammaT, int p) { return 2.0f * p * gammaT - 2.0f * gammaI + p * kPi; }
+
+struct F3 {
+    float x, y, z;
+};
+
+/* InterpolatedDistribution1D ctor (InterpolatedDistribution1D.hpp:36-66) -> cdfs + sums */
+void buildIDist(std::vector<float> w, int size, int nd, std::vector<float> &cdf, std::vector<float> &sums) {
+    cdf.assign((size_t) (size + 1) * nd, 0.0f);
+    sums.assign(nd, 0.0f);
+    for (int d = 0; d < nd; ++d) {
+        float *c = &cdf[(size_t) d * (size + 1)];
+        float *p = &w[(size_t) d * size];
+        c[0] = 0.0f;
+        for (int x = 0; x < size; ++x) c[x + 1] = p[x] + c[x];
+        sums[d] = c[size];
+        if (sums[d] < 1e-4f) {
+            float ratio = 1.0f / size;
+            for (int x = 0; x < size; ++x) {
+                p[x] = ratio;
+                c[x] = x * ratio;
+            }
+        } else {
+            float scale = 1.0f / sums[d];
+            for (int x = 0; x < size; ++x) {
+                p[x] *= scale;
+                c[x] *= scale;
+            }
+        }
+        c[size] = 1.0f;
+    }
+}
+
+} // namespace
+
+bool precomputeMarschner(const SceneDesc &d, const std::string &dataDir, MarschnerHost &out, std::string &err) {
+    const float eta = d.intIOR / d.extIOR;
+    const float betaR = 0.1f, betaTT = betaR * 0.5f, betaTRT = betaR * 2.0f;
+    const F3 sigmaA{0.5f, 0.5f, 0.5f};
+    const int R = HPT_AZ_RES, NP = 140, NG = 2048;
+    std::vector<float> pts, wts;
+    gaussLegendre(NP, pts, wts);
+    std::vector<float> gammaI(NP);
+    for (int i = 0; i < NP; ++i) gammaI[i] = std::asin(pts[i]);
+    std::vector<float> Ds(NG);
+    for (int i = 0; i < NG; ++i) Ds[i] = wrappedGauss(betaR, i / (NG - 1.0f) * 2 * kPi);
+    auto approxD = [&](float phi) {
+        float u = std::abs(phi * (1.0 / (2 * kPi) * (NG - 1)));
+        int x0 = int(u), x1 = x0 + 1;
+        u -= x0;
+        return Ds[x0 % NG] * (1.0f - u) + Ds[x1 % NG] * u;
+    };
+    std::vector<F3> vals[3];
+    for (auto &v : vals) v.resize(R * R);
+    std::vector<float> fres(NP), gammaT(NP);
+    std::vector<F3> absorb(NP);
+    for (int y = 0; y < R; ++y) {
+        float ch = y / (R - 1.0f);
+        float iorPrime = std::sqrt(eta * eta - (1.0f - ch * ch)) / ch;
+        float cosThetaT = std::sqrt(1.0f - (1.0f - ch * ch) * (1.0f / eta) * (1.0f / eta));
+        float rc = 1.0f / cosThetaT;
+        F3 sp{sigmaA.x * rc, sigmaA.y * rc, sigmaA.z * rc};
+        for (int i = 0; i < NP; ++i) {
+            gammaT[i] = std::asin(clampf(pts[i] / iorPrime, -1.0f, 1.0f));
+            fres[i] = fresnelExt(1.0f / eta, ch * std::cos(gammaI[i])); /* swapped arguments, :809 */
+            float c = std::cos(gammaT[i]);
+            absorb[i] = {std::exp(-sp.x * 2.0f * c), std::exp(-sp.y * 2.0f * c), std::exp(-sp.z * 2.0f * c)};
+        }
+        for (int phiI = 0; phiI < R; ++phiI) {
+            float phi = kPi * 2 * phiI / (R - 1.0f);
+            float iR = 0.0f;
+            F3 iTT{0, 0, 0}, iTRT{0, 0, 0};
+            for (int i = 0; i < NP; ++i) {
+                float fR = fres[i];
+                F3 T = absorb[i];
+                float k = (1.0f - fR) * (1.0f - fR);
+                F3 ATT{k * T.x, k * T.y, k * T.z};
+                F3 ATRT{ATT.x * fR * T.x, ATT.y * fR * T.y, ATT.z * fR * T.z};
+                iR += wts[i] * approxD(phi - lobePhi(gammaI[i], gammaT[i], 0)) * fR;
+                float wTT = wts[i] * approxD(phi - lobePhi(gammaI[i], gammaT[i], 1));
+                iTT.x += wTT * ATT.x; iTT.y += wTT * ATT.y; iTT.z += wTT * ATT.z;
+                float wTRT = wts[i] * approxD(phi - lobePhi(gammaI[i], gammaT[i], 2));
+                iTRT.x += wTRT * ATRT.x; iTRT.y += wTRT * ATRT.y; iTRT.z += wTRT * ATRT.z;
+            }
+            float hR = 0.5f * iR;
+            vals[0][phiI + y * R] = {hR, hR, hR};
+            vals[1][phiI + y * R] = {0.5f * iTT.x, 0.5f * iTT.y, 0.5f * iTT.z};
+            vals[2][phiI + y * R] = {0.5f * iTRT.x, 0.5f * iTRT.y, 0.5f * iTRT.z};
+        }
+    }
+    for (int l = 0; l < 3; ++l) {
+        out.table[l].resize(R * R);
+        std::vector<float> w(R * R);
+        for (int i = 0; i < R * R; ++i) {
+            const F3 &v = vals[l][i];
+            out.table[l][i] = {v.x, v.y, v.z, 0.0f};
+            w[i] = std::max(std::max(v.x, v.y), v.z);
+        }
+        /* dilation (marschner_diffuse.cpp:47-59) */
+        for (int y = 0; y < R; ++y) {
+            for (int x = 0; x < R - 1; ++x) w[x + y * R] = std::max(w[x + y * R], w[x + 1 + y * R]);
+            for (int x = R - 1; x > 0; --x) w[x + y * R] = std::max(w[x + y * R], w[x - 1 + y * R]);
+        }
+        for (int x = 0; x < R; ++x) {
+            for (int y = 0; y < R - 1; ++y) w[x + y * R] = std::max(w[x + y * R], w[x + (y + 1) * R]);
+            for (int y = R - 1; y > 0; --y) w[x + y * R] = std::max(w[x + y * R], w[x + (y - 1) * R]);
+        }
+        buildIDist(std::move(w), R, R, out.cdf[l], out.sums[l]);
+    }
+    out.vR = betaR * betaR;
+    out.vTT = betaTT * betaTT;
+    out.vTRT = betaTRT * betaTRT;
+    out.scaleAngleRad = -0.1f;
+    /* configure (:193-247) */
+    float spec[3] = {d.specular[0], d.specular[1], d.specular[2]};
+    float smax = std::max(std::max(spec[0], spec[1]), spec[2]);
+    if (smax > 1.0f) {
+        float s = 0.99f * (1.0f / smax);
+        for (auto &v : spec) v *= s;
+    }
+    float dAvg = d.diffuse[0] * 0.212671f + d.diffuse[1] * 0.715160f + d.diffuse[2] * 0.072169f;
+    float sAvg = spec[0] * 0.212671f + spec[1] * 0.715160f + spec[2] * 0.072169f;
+    out.specularSamplingWeight = sAvg / (dAvg + sAvg);
+    out.invEta2 = 1.0f / (eta * eta);
+    for (int i = 0; i < 3; ++i) out.diffuse[i] = d.diffuse[i];
+    /* rough transmittance slices (rtrans.h) */
+    RTrans rt;
+    std::string path = dataDir + "/microfacet/" + d.distribution + ".dat";
+    if (!rt.load(path)) {
+        err = "cannot load rough transmittance data \"" + path + "\"";
+        return false;
+    }
+    float alpha = std::max(d.alpha, 1e-4f);
+    if (eta < 1) { err = "marschner: eta < 1 is not supported by the transmittance tables"; return false; }
+    if (alpha < rt.alphaMin || alpha > rt.alphaMax) {
+        err = "marschner: alpha outside the precomputed range";
+        return false;
+    }
+    std::vector<float> ext2, extD, int2, intD;
+    rt.sliceEta(eta, ext2, extD);
+    rt.sliceEta(1 / eta, int2, intD);
+    float wa = std::pow((alpha - rt.alphaMin) / (rt.alphaMax - rt.alphaMin), (float) 0.25f);
+    out.trans.resize(rt.nTheta);
+    float dT = 1.0f / (rt.nTheta - 1);
+    for (size_t i = 0; i < rt.nTheta; ++i) out.trans[i] = cubic2D(i * dT, wa, ext2.data(), rt.nTheta, rt.nAlpha);
+    float internalDiffuse = cubic1D(wa, intD.data(), rt.nAlpha, 0.0f, 1.0f);
+    internalDiffuse = std::min(1.0f, std::max(0.0f, internalDiffuse));
+    out.fdr = 1 - internalDiffuse;
+    return true;
+}
+
+void configureKajiyaKay(const SceneDesc &d, HptKajiyaKay &out) {
+    float kd[3] = {d.diffuse[0], d.diffuse[1], d.diffuse[2]};
+    float ks[3] = {d.specular[0], d.specular[1], d.specular[2]};
+    float mx = std::max(std::max(ks[0] + kd[0], ks[1] + kd[1]), ks[2] + kd[2]);
+    if (mx > 1.0f) {
+        float s = 0.99f * (1.0f / mx);
+        for (int i = 0; i < 3; ++i) { ks[i] *= s; kd[i] *= s; }
+    }
+    float dAvg = kd[0] * 0.212671f + kd[1] * 0.715160f + kd[2] * 0.072169f;
+    float sAvg = ks[0] * 0.212671f + ks[1] * 0.715160f + ks[2] * 0.072169f;
+    for (int i = 0; i < 3; ++i) { out.kd[i] = kd[i]; out.ks[i] = ks[i]; }
+    out.exponent = d.exponent;
+    out.specularSamplingWeight = sAvg / (dAvg + sAvg);
+}
+
+/* ---------------- IEEE half ---------------- */
+uint16_t floatToHalf(float f) {
+    uint32_t x;
+    std::memcpy(&x, &f, 4);
+    uint32_t sign = (x >> 16) & 0x8000u, ax = x & 0x7fffffffu;
+    if (ax >= 0x7f800000u) return (uint16_t) (sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0u));
+    if (ax >= 0x477ff000u) return (uint16_t) (sign | 0x7c00u);
+    if (ax < 0x38800000u) {
+        if (ax < 0x33000000u) return (uint16_t) sign;
+        uint32_t m = (ax & 0x007fffffu) | 0x00800000u;
+        int shift = 126 - (int) (ax >> 23);
+        uint32_t hm = m >> shift, rem = m & ((1u << shift) - 1u), half = 1u << (shift - 1);
+        if (rem > half || (rem == half && (hm & 1u))) hm++;
+        return (uint16_t) (sign | hm);
+    }
+    uint32_t h = (((ax >> 23) - 112u) << 10) | ((ax >> 13) & 0x3ffu), rem = ax & 0x1fffu;
+    if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+    return (uint16_t) (sign | h);
+}
+
+float halfToFloat(uint16_t h) {
+    uint32_t sign = (uint32_t) (h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu, x;
+    if (e == 0) {
+        if (m == 0) x = sign;
+        else {
+            int ee = -1;
+            do { ee++; m <<= 1; } while (!(m & 0x400u));
+            x = sign | ((uint32_t) (112 - ee) << 23) | ((m & 0x3ffu) << 13);
+        }
+    } else if (e == 31) {
+        x = sign | 0x7f800000u | (m << 13);
+    } else {
+        x = sign | ((e + 112u) << 23) | (m << 13);
+    }
+    float f;
+    std::memcpy(&f, &x, 4);
+    return f;
+}
+
+/* ---------------- environment map (envmap.cpp:244-314) ---------------- */
+void buildEnvMap(EnvHost &env) {
+    const int w = env.w, h = env.h;
+    env.texel.resize((size_t) w * h);
+    for (size_t i = 0; i < (size_t) w * h; ++i) {
+        float c[3];
+        for (int k = 0; k < 3; ++k) c[k] = halfToFloat(floatToHalf(std::max(env.rgb[3 * i + k], 0.0f)));
+        env.texel[i] = {c[0], c[1], c[2], 0.0f};
+    }
+    env.cdfCols.assign((size_t) (w + 1) * h, 0.0f);
+    env.cdfRows.assign(h + 1, 0.0f);
+    env.rowWeights.assign(h, 0.0f);
+    size_t colPos = 0, rowPos = 0;
+    float rowSum = 0.0f;
+    env.cdfRows[rowPos++] = 0;
+    for (int y = 0; y < h; ++y) {
+        float colSum = 0;
+        env.cdfCols[colPos++] = 0;
+        for (int x = 0; x < w; ++x) {
+            const HptF4 &t = env.texel[(size_t) y * w + x];
+            colSum += t.x * 0.212671f + t.y * 0.715160f + t.z * 0.072169f;
+            env.cdfCols[colPos++] = (float) colSum;
+        }
+        float norm = 1.0f / (float) colSum;
+        for (int x = 1; x < w; ++x) env.cdfCols[colPos - x - 1] *= norm;
+        env.cdfCols[colPos - 1] = 1.0f;
+        float weight = std::sin((y + 0.5f) * kPi / h);
+        env.rowWeights[y] = weight;
+        rowSum += colSum * weight;
+        env.cdfRows[rowPos++] = (float) rowSum;
+    }
+    float norm = 1.0f / (float) rowSum;
+    for (int y = 1; y < h; ++y) env.cdfRows[rowPos - y - 1] *= norm;
+    env.cdfRows[rowPos - 1] = 1.0f;
+    if (rowSum == 0) throw std::runtime_error("The environment map is completely black -- this is not allowed.");
+    if (!std::isfinite(rowSum))
+        throw std::runtime_error("The environment map contains an invalid floating point value (nan/inf)");
+    env.normalization = 1.0f / (rowSum * (2 * kPi / w) * (kPi / h));
+    env.pixelSizeX = 2 * kPi / w;
+    env.pixelSizeY = kPi / h;
+}
+
+/*
+ * Stand-in for the sunsky emitter (round 1): the reference rasterises a
+ * Hosek-Wilkie sky plus a QMC-splatted sun disk into a resolution x
+ * resolution/2 lat-long bitmap (sunsky.cpp:100-240) and hands it to envmap.
+ * Until that rasteriser is restated we rasterise a
+ * smooth analytic sky + sun disk with the same bitmap geometry, sun
+ * direction, sun disk radius (SUN_APP_RADIUS * sunRadiusScale) and scales.
+ * The bitmap is an input: the oracle and the device consume identical bits.
+ */
+void rasterizeSunSkyStandIn(const SceneDesc &d, EnvHost &env) {
+    const int W = d.skyResolution, H = d.skyResolution / 2;
+    env.w = W;
+    env.h = H;
+    env.rgb.assign((size_t) W * H * 3, 0.0f);
+    double sx = d.sunDirection[0], sy = d.sunDirection[1], sz = d.sunDirection[2];
+    double sl = std::sqrt(sx * sx + sy * sy + sz * sz);
+    sx /= sl; sy /= sl; sz /= sl;
+    const double sunAppRadius = 0.5358 * M_PI / 180.0; /* sunmodel.h SUN_APP_RADIUS (degrees) */
+    double cosSun = std::cos(0.5 * sunAppRadius * d.sunRadiusScale);
+    double sunElev = std::asin(std::max(-1.0, std::min(1.0, sy)));
+    /* sun colour warms towards the horizon; magnitude ~ sunScale */
+    double sunR = 1.0, sunG = 0.85 + 0.1 * std::sin(sunElev), sunB = 0.65 + 0.25 * std::sin(sunElev);
+    for (int y = 0; y < H; ++y) {
+        double theta = (y + 0.5) * M_PI / H;
+        for (int x = 0; x < W; ++x) {
+            double phi = (x + 0.5) * 2 * M_PI / W;
+            /* envmap lat-long convention (envmap.cpp:589-597): d = (sin phi sin th, cos th, -cos phi sin th) */
+            double dx = std::sin(phi) * std::sin(theta), dy = std::cos(theta), dz = -std::cos(phi) * std::sin(theta);
+            float *px = &env.rgb[3 * ((size_t) y * W + x)];
+            if (dy <= 0) continue; /* black below the horizon (sky.cpp:416-421) */
+            double mu = dx * sx + dy * sy + dz * sz;
+            double gamma = std::acos(std::max(-1.0, std::min(1.0, mu)));
+            double zen = 1.0 - dy;
+            double glow = std::exp(-gamma * 2.5);
+            double base = 0.08 + 0.10 * zen * zen;
+            px[0] = (float) (d.skyScale * (base * 0.45 + 0.25 * glow) * 0.2);
+            px[1] = (float) (d.skyScale * (base * 0.65 + 0.22 * glow) * 0.2);
+            px[2] = (float) (d.skyScale * (base * 1.00 + 0.18 * glow) * 0.2);
+            if (mu >= cosSun) {
+                double s = d.sunScale * 3.0;
+                px[0] += (float) (s * sunR);
+                px[1] += (float) (s * sunG);
+                px[2] += (float) (s * sunB);
+            }
+        }
+    }
+    env.scale = 1.0f;
+    std::memcpy(env.toWorld, d.emitterToWorld, sizeof(env.toWorld));
+}
+
+bool loadEnvFile(const std::string &path, EnvHost &env, std::string &err) {
+    std::ifstream f(path, std::ios::binary);
+    if (!f) { err = "cannot open environment map \"" + path + "\""; return false; }
+    std::string line;
+    std::getline(f, line);
+    if (line == "PF") { /* portable float map */
+        int w, h;
+        float scale;
+        f >> w >> h >> scale;
+        f.get();
+        std::vector<float> data((size_t) w * h * 3);
+        f.read((char *) data.data(), (std::streamsize) (data.size() * 4));
+        env.w = w;
+        env.h = h;
+        env.rgb.resize(data.size());
+        for (int y = 0; y < h; ++y) /* PFM rows are bottom-to-top */
+            std::memcpy(&env.rgb[(size_t) y * w * 3], &data[(size_t) (h - 1 - y) * w * 3], (size_t) w * 3 * 4);
+        return true;
+    }
+    if (line.rfind("#?", 0) == 0) { /* Radiance RGBE */
+        while (std::getline(f, line) && !line.empty()) {}
+        std::getline(f, line);
+        int w = 0, h = 0;
+        char a[3], b[3];
+        if (std::sscanf(line.c_str(), "%2s %d %2s %d", a, &h, b, &w) != 4) { err = "bad RGBE header"; return false; }
+        std::vector<unsigned char> scan((size_t) w * 4);
+        env.w = w;
+        env.h = h;
+        env.rgb.assign((size_t) w * h * 3, 0.0f);
+        for (int y = 0; y < h; ++y) {
+            int c0 = f.get(), c1 = f.get(), c2 = f.get(), c3 = f.get();
+            if (c0 == 2 && c1 == 2 && ((c2 << 8) | c3) == w) { /* new RLE */
+                for (int ch = 0; ch < 4; ++ch) {
+                    int x = 0;
+                    while (x < w) {
+                        int cnt = f.get();
+                        if (cnt > 128) {
+                            cnt -= 128;
+                            int v = f.get();
+                            for (int k = 0; k < cnt && x < w; ++k) scan[(size_t) (x++) * 4 + ch] = (unsigned char) v;
+                        } else {
+                            for (int k = 0; k < cnt && x < w; ++k) scan[(size_t) (x++) * 4 + ch] = (unsigned char) f.get();
+                        }
+                    }
+                }
+            } else {
+                scan[0] = (unsigned char) c0; scan[1] = (unsigned char) c1;
+                scan[2] = (unsigned char) c2; scan[3] = (unsigned char) c3;
+                f.read((char *) scan.data() + 4, (std::streamsize) ((size_t) w * 4 - 4));
+            }
+            for (int x = 0; x < w; ++x) {
+                unsigned char *p = &scan[(size_t) x * 4];
+                float s = p[3] ? std::ldexp(1.0f, p[3] - 136) : 0.0f;
+                float *o = &env.rgb[3 * ((size_t) y * w + x)];
+                o[0] = p[0] * s;
+                o[1] = p[1] * s;
+                o[2] = p[2] * s;
+            }
+        }
+        return true;
+    }
+    err = "unsupported environment map format (need .pfm or Radiance .hdr): " + path;
+    return false;
+}
+
+/* ---------------- camera (perspective.cpp:125-165) ---------------- */
+void setupCamera(const SceneDesc &d, HptCamera &cam) {
+    float aspect = (float) d.width / (float) d.height;
+    float fovX = d.fov;
+    /* sensor.cpp:245-251 fovAxis handling */
+    std::string axis = d.fovAxis;
+    if (axis == "smaller") axis = aspect > 1 ? "y" : "x";
+    else if (axis == "larger") axis = aspect > 1 ? "x" : "y";
+    if (axis == "y") fovX = (float) (2.0 * std::atan(std::tan(d.fov * M_PI / 360.0) * aspect) * 180.0 / M_PI);
+    float cot = 1.0f / std::tan((fovX / 2.0f) * (kPi / 180.0f));
+    float recip = 1.0f / (d.farClip - d.nearClip);
+    float a = d.farClip * recip, b = -d.nearClip * d.farClip * recip;
+    double Pi[16] = {1.0 / cot, 0, 0, 0, 0, 1.0 / cot, 0, 0, 0, 0, 0, 1, 0, 0, 1.0 / b, -(double) a / b};
+    double A[16] = {-2, 0, 0, 1, 0, -2.0 / aspect, 0, 1.0 / aspect, 0, 0, 1, 0, 0, 0, 0, 1};
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) {
+            double acc = 0;
+            for (int k = 0; k < 4; ++k) acc += Pi[r * 4 + k] * A[k * 4 + c];
+            cam.s2c[r * 4 + c] = (float) acc;
+        }
+    std::memcpy(cam.toWorld, d.toWorld, sizeof(cam.toWorld));
+    cam.invResX = 1.0f / (float) d.width;
+    cam.invResY = 1.0f / (float) d.height;
+    cam.nearClip = d.nearClip;
+    cam.farClip = d.farClip;
+    cam.width = d.width;
+    cam.height = d.height;
+    uint32_t r = (uint32_t) std::max(d.width, d.height);
+    r--; r |= r >> 1; r |= r >> 2; r |= r >> 4; r |= r >> 8; r |= r >> 16; r++;
+    cam.resolution = (float) r;
+    uint32_t lg = 0;
+    while ((r >> lg) != 0) lg++;
+    cam.logRes = lg - 1;
+}
+
+void setupTent(float *lut, float &scale) {
+    const int R = HPT_FILTER_RES;
+    const float radius = 1.0f;
+    float sum = 0.0f;
+    for (int i = 0; i < R; ++i) {
+        float x = (radius * i) / R;
+        float v = std::max(0.0f, 1.0f - std::abs(x / radius));
+        lut[i] = v;
+        sum += v;
+    }
+    lut[R] = 0.0f;
+    scale = R / radius;
+    sum *= 2 * radius / R;
+    float norm = 1.0f / sum;
+    for (int i = 0; i < R; ++i) lut[i] *= norm;
+}
+
+/* ---------------- image output ---------------- */
+bool writePFM(const std::string &path, const float *rgb, int w, int h) {
+    std::ofstream f(path, std::ios::binary);
+    if (!f) return false;
+    f << "PF\n" << w << " " << h << "\n-1.0\n";
+    for (int y = h - 1; y >= 0; --y) f.write((const char *) &rgb[(size_t) y * w * 3], (std::streamsize) ((size_t) w * 12));
+    return (bool) f;
+}
+
+namespace {
+uint32_t crc32(const unsigned char *p, size_t n, uint32_t c = 0xffffffffu) {
+    static uint32_t table[256];
+    static bool init = false;
+    if (!init) {
+        for (uint32_t i = 0; i < 256; ++i) {
+            uint32_t v = i;
+            for (int k = 0; k < 8; ++k) v = (v & 1) ? 0xedb88320u ^ (v >> 1) : v >> 1;
+            table[i] = v;
+        }
+        init = true;
+    }
+    for (size_t i = 0; i < n; ++i) c = table[(c ^ p[i]) & 0xff] ^ (c >> 8);
+    return c;
+}
+void be32(std::vector<unsigned char> &v, uint32_t x) {
+    v.push_back((unsigned char) (x >> 24)); v.push_back((unsigned char) (x >> 16));
+    v.push_back((unsigned char) (x >> 8)); v.push_back((unsigned char) x);
+}
+void chunk(std::ofstream &f, const char *type, const std::vector<unsigned char> &data) {
+    std::vector<unsigned char> buf;
+    be32(buf, (uint32_t) data.size());
+    std::vector<unsigned char> td(type, type + 4);
+    td.insert(td.end(), data.begin(), data.end());
+    buf.insert(buf.end(), td.begin(), td.end());
+    be32(buf, crc32(td.data(), td.size()) ^ 0xffffffffu);
+    f.write((const char *) buf.data(), (std::streamsize) buf.size());
+}
+} // namespace
+
+/* ldrfilm.cpp:300-330 develop: gamma (sRGB curve when gamma == -1), 8-bit, stored-deflate PNG */
+bool writePNG8(const std::string &path, const float *rgb, int w, int h, float gamma) {
+    std::ofstream f(path, std::ios::binary);
+    if (!f) return false;
+    const unsigned char sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+    f.write((const char *) sig, 8);
+    std::vector<unsigned char> ihdr;
+    be32(ihdr, (uint32_t) w);
+    be32(ihdr, (uint32_t) h);
+    ihdr.insert(ihdr.end(), {8, 2, 0, 0, 0});
+    chunk(f, "IHDR", ihdr);
+    std::vector<unsigned char> raw;
+    raw.reserve((size_t) h * (1 + 3 * (size_t) w));
+    for (int y = 0; y < h; ++y) {
+        raw.push_back(0);
+        for (int x = 0; x < 3 * w; ++x) {
+            float v = std::max(0.0f, rgb[(size_t) y * w * 3 + x]);
+            if (gamma == -1.0f)
+                v = v <= 0.0031308f ? 12.92f * v : 1.055f * std::pow(v, 1.0f / 2.4f) - 0.055f;
+            else
+                v = std::pow(v, 1.0f / gamma);
+            raw.push_back((unsigned char) std::min(255, (int) (v * 255.0f + 0.5f)));
+        }
+    }
+    std::vector<unsigned char> z = {0x78, 0x01};
+    size_t pos = 0;
+    uint32_t a = 1, b = 0;
+    for (unsigned char c : raw) { a = (a + c) % 65521; b = (b + a) % 65521; }
+    while (pos < raw.size() || pos == 0) {
+        size_t n = std::min((size_t) 65535, raw.size() - pos);
+        bool last = pos + n >= raw.size();
+        z.push_back(last ? 1 : 0);
+        z.push_back((unsigned char) (n & 0xff)); z.push_back((unsigned char) (n >> 8));
+        z.push_back((unsigned char) (~n & 0xff)); z.push_back((unsigned char) ((~n >> 8) & 0xff));
+        z.insert(z.end(), raw.begin() + pos, raw.begin() + pos + n);
+        pos += n;
+        if (last) break;
+    }
+    be32(z, (b << 16) | a);
+    chunk(f, "IDAT", z);
+    chunk(f, "IEND", {});
+    return (bool) f;
+}
+
+} // namespace hpt

@@ -1,0 +1,873 @@
+/*
+ * hpt_capi.cpp -- the C ABI (include/hairpt.h) and the wavefront driver.
+ *
+ * The driver replaces SamplingIntegrator::render / BlockedRenderProcess
+ * (src/librender/integrator.cpp:95-188, renderproc.cpp:26-145): instead of
+ * one CPU worker per 32x32 block it runs every sample of every owned block
+ * as one lane of a wave of paths resident in HBM, bouncing the whole wave
+ * through k_shade -> k_trace -> k_post until its queue drains, then gathers
+ * the wave into the film.  Waves are sized to HBM (hundreds of bytes per
+ * path), so a 512x512x256 frame is a single wave on MI355X.
+ */
+#include <dlfcn.h>
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/hairpt.h"
+#include "host/host_scene.h"
+#include "hpt_device.h"
+#include "kernels/hpt_kernels.h"
+
+using namespace hpt;
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+struct hpt_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::string dataDir;
+    SceneDesc desc;
+    bool haveCamera = false, haveHair = false, haveBSDF = false, haveEnv = false, prepared = false;
+    bool hairFromFile = false;
+    std::string hairPath;
+    float hairRadius = 0.025f, hairAngle = 1.0f;
+    float hairToWorld[16];
+    bool hairHasToWorld = false;
+    HairData hair;
+    KDTreeHost tree;
+    MarschnerHost mar;
+    HptKajiyaKay kk;
+    EnvHost env;
+    bool envFromSunsky = false;
+    std::vector<uint32_t> sobol32;
+    std::vector<uint64_t> vdc, vdcInv;
+    HptScene sc;
+    std::vector<DevBuf> sceneBufs;
+    /* wave buffers */
+    uint64_t capacity = 0;
+    std::vector<DevBuf> waveBufs;
+    HptPaths P;
+    uint32_t *qTrace = nullptr, *qShadow = nullptr, *qShadeA = nullptr, *qShadeB = nullptr;
+    uint32_t *counters = nullptr;
+    uint64_t *dstats = nullptr;
+    hpt_stats stats;
+    std::vector<hipEvent_t> evPool;
+};
+
+namespace {
+
+int setErr(hpt_context *c, int code, const std::string &m) {
+    if (c) c->err = m;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                                   \
+    do {                                                                                                    \
+        hipError_t _e = (expr);                                                                             \
+        if (_e != hipSuccess)                                                                               \
+            return setErr(ctx, HPT_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));            \
+    } while (0)
+
+std::string defaultDataDir() {
+    Dl_info info;
+    if (dladdr((void *) &defaultDataDir, &info) && info.dli_fname) {
+        std::string p = info.dli_fname;
+        size_t s = p.find_last_of('/');
+        std::string dir = s == std::string::npos ? "." : p.substr(0, s);
+        return dir + "/../data";
+    }
+    return "data";
+}
+
+template <typename T> bool readFile(const std::string &path, std::vector<T> &out) {
+    std::ifstream f(path, std::ios::binary | std::ios::ate);
+    if (!f) return false;
+    size_t n = (size_t) f.tellg();
+    f.seekg(0);
+    out.resize(n / sizeof(T));
+    f.read((char *) out.data(), (std::streamsize) (out.size() * sizeof(T)));
+    return (bool) f;
+}
+
+int upload(hpt_context *c, const void *src, size_t bytes, const void **dst) {
+    if (c->device == HPT_HOST_ONLY) { /* keep host pointers: nothing leaves the host */
+        *dst = src;
+        return HPT_OK;
+    }
+    DevBuf b;
+    b.bytes = std::max<size_t>(bytes, 16);
+    HIPCHK(c, hipMalloc(&b.p, b.bytes));
+    if (bytes) HIPCHK(c, hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+    c->sceneBufs.push_back(b);
+    *dst = b.p;
+    return HPT_OK;
+}
+
+void freeBufs(std::vector<DevBuf> &v) {
+    for (auto &b : v)
+        if (b.p) (void) hipFree(b.p);
+    v.clear();
+}
+
+int ensureWave(hpt_context *c, uint64_t n) {
+    if (n <= c->capacity) return HPT_OK;
+    freeBufs(c->waveBufs);
+    c->capacity = 0;
+    auto alloc = [&](size_t bytes, void **p) -> int {
+        DevBuf b;
+        b.bytes = bytes;
+        HIPCHK(c, hipMalloc(&b.p, bytes));
+        c->waveBufs.push_back(b);
+        *p = b.p;
+        return HPT_OK;
+    };
+    int r = 0;
+    r |= alloc(n * 16, (void **) &c->P.ro);
+    r |= alloc(n * 16, (void **) &c->P.rd);
+    r |= alloc(n * 8, (void **) &c->P.pos);
+    r |= alloc(n * 8, (void **) &c->P.sobol);
+    r |= alloc(n * 4, (void **) &c->P.state);
+    r |= alloc(n * 16, (void **) &c->P.thr);
+    r |= alloc(n * 16, (void **) &c->P.li);
+    r |= alloc(n * 16, (void **) &c->P.hit);
+    r |= alloc(n * 16, (void **) &c->P.hitp);
+    r |= alloc(n * 16, (void **) &c->P.bw);
+    r |= alloc(n * 16, (void **) &c->P.sdir);
+    r |= alloc(n * 16, (void **) &c->P.scontrib);
+    r |= alloc(n * 4, (void **) &c->qTrace);
+    r |= alloc(n * 4, (void **) &c->qShadow);
+    r |= alloc(n * 4, (void **) &c->qShadeA);
+    r |= alloc(n * 4, (void **) &c->qShadeB);
+    r |= alloc(HPT_Q_COUNT * 4, (void **) &c->counters);
+    r |= alloc(8 * 8, (void **) &c->dstats);
+    if (r) return HPT_EDEVICE;
+    c->capacity = n;
+    return HPT_OK;
+}
+
+hipEvent_t takeEvent(hpt_context *c, size_t &used) {
+    if (used >= c->evPool.size()) {
+        hipEvent_t e;
+        (void) hipEventCreate(&e);
+        c->evPool.push_back(e);
+    }
+    return c->evPool[used++];
+}
+
+} // namespace
+
+extern "C" {
+
+int hpt_context_create(int device, hpt_context **out) {
+    if (!out) return HPT_EINVAL;
+    *out = nullptr;
+    if (device == HPT_HOST_ONLY) {
+        /* host-only context: parses, loads, builds and exports the scene
+           (kd-tree, tables) for inspection; every render / batch call fails */
+        hpt_context *c = new hpt_context();
+        c->device = HPT_HOST_ONLY;
+        c->dataDir = defaultDataDir();
+        std::memset(&c->sc, 0, sizeof(c->sc));
+        std::memset(&c->stats, 0, sizeof(c->stats));
+        for (int i = 0; i < 16; ++i) c->hairToWorld[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+        *out = c;
+        return HPT_OK;
+    }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return HPT_EDEVICE;
+    if (device < 0 || device >= n) return HPT_EINVAL;
+    if (hipSetDevice(device) != hipSuccess) return HPT_EDEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return HPT_EDEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return HPT_EDEVICE;
+    hpt_context *c = new hpt_context();
+    c->device = device;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return HPT_EDEVICE;
+    }
+    c->dataDir = defaultDataDir();
+    std::memset(&c->sc, 0, sizeof(c->sc));
+    std::memset(&c->stats, 0, sizeof(c->stats));
+    for (int i = 0; i < 16; ++i) c->hairToWorld[i] = (i % 5 == 0) ? 1.0f : 0.0f;
+    *out = c;
+    return HPT_OK;
+}
+
+void hpt_context_destroy(hpt_context *c) {
+    if (!c) return;
+    if (c->device == HPT_HOST_ONLY) {
+        delete c;
+        return;
+    }
+    (void) hipSetDevice(c->device);
+    (void) hipStreamSynchronize(c->stream);
+    freeBufs(c->sceneBufs);
+    freeBufs(c->waveBufs);
+    for (auto e : c->evPool) (void) hipEventDestroy(e);
+    (void) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char *hpt_last_error(const hpt_context *c) { return c ? c->err.c_str() : "null context"; }
+
+int hpt_set_data_dir(hpt_context *c, const char *dir) {
+    if (!c || !dir) return HPT_EINVAL;
+    c->dataDir = dir;
+    return HPT_OK;
+}
+
+int hpt_load_scene_xml(hpt_context *c, const char *path, int n_defines, const char *const *keys,
+                       const char *const *values) {
+    if (!c || !path) return HPT_EINVAL;
+    std::map<std::string, std::string> defs;
+    for (int i = 0; i < n_defines; ++i) defs[keys[i]] = values[i];
+    try {
+        c->desc = parseSceneXML(path, defs);
+    } catch (const std::exception &e) {
+        return setErr(c, HPT_EIO, e.what());
+    }
+    const SceneDesc &d = c->desc;
+    c->haveCamera = true;
+    c->hairFromFile = true;
+    c->hairPath = d.hairFile;
+    c->hairRadius = d.radius;
+    c->hairAngle = d.angleThreshold;
+    c->hairHasToWorld = d.hairHasToWorld;
+    std::memcpy(c->hairToWorld, d.hairToWorld, sizeof(c->hairToWorld));
+    c->haveHair = true;
+    c->haveBSDF = true;
+    c->haveEnv = true;
+    c->envFromSunsky = d.emitter == "sunsky";
+    if (d.emitter == "envmap") {
+        std::string err;
+        c->env = EnvHost();
+        if (!loadEnvFile(d.envFile, c->env, err)) return setErr(c, HPT_EIO, err);
+        c->env.scale = d.envScale;
+        std::memcpy(c->env.toWorld, d.emitterToWorld, sizeof(c->env.toWorld));
+    }
+    c->prepared = false;
+    return HPT_OK;
+}
+
+int hpt_set_camera(hpt_context *c, const float to_world[16], float fov_x_deg, int width, int height,
+                   float near_clip, float far_clip) {
+    if (!c || !to_world || width <= 0 || height <= 0 || !(near_clip > 0) || !(near_clip < far_clip))
+        return setErr(c, HPT_EINVAL, "invalid camera parameters");
+    std::memcpy(c->desc.toWorld, to_world, sizeof(c->desc.toWorld));
+    c->desc.fov = fov_x_deg;
+    c->desc.fovAxis = "x";
+    c->desc.width = width;
+    c->desc.height = height;
+    c->desc.nearClip = near_clip;
+    c->desc.farClip = far_clip;
+    c->haveCamera = true;
+    c->prepared = false;
+    return HPT_OK;
+}
+
+int hpt_set_sampler(hpt_context *c, int spp) {
+    if (!c || spp <= 0) return setErr(c, HPT_EINVAL, "sampleCount must be positive");
+    c->desc.spp = spp;
+    return HPT_OK;
+}
+
+int hpt_set_integrator(hpt_context *c, int max_depth, int rr_depth, int strict_normals, int hide_emitters) {
+    if (!c) return HPT_EINVAL;
+    if (max_depth > 250) return setErr(c, HPT_EINVAL, "maxDepth > 250 exceeds the Sobol dimension table");
+    c->desc.maxDepth = max_depth;
+    c->desc.rrDepth = rr_depth;
+    c->desc.strictNormals = strict_normals != 0;
+    c->desc.hideEmitters = hide_emitters != 0;
+    c->prepared = false;
+    return HPT_OK;
+}
+
+int hpt_set_hair_file(hpt_context *c, const char *path, float radius, float angle, const float *to_world) {
+    if (!c || !path) return HPT_EINVAL;
+    c->hairFromFile = true;
+    c->hairPath = path;
+    c->hairRadius = radius;
+    c->hairAngle = angle;
+    c->hairHasToWorld = to_world != nullptr;
+    if (to_world) std::memcpy(c->hairToWorld, to_world, sizeof(c->hairToWorld));
+    c->haveHair = true;
+    c->prepared = false;
+    return HPT_OK;
+}
+
+int hpt_set_hair_vertices(hpt_context *c, const float *xyz, const uint8_t *starts, uint64_t n, float radius) {
+    if (!c || (!xyz && n)) return HPT_EINVAL;
+    c->hairFromFile = false;
+    c->hair = HairData();
+    c->hair.xyz.assign(xyz, xyz + 3 * n);
+    c->hair.starts.assign(starts, starts + n);
+    c->hair.starts.push_back(1);
+    if (n) c->hair.starts[0] = 1;
+    c->hair.radius = radius;
+    c->haveHair = true;
+    c->prepared = false;
+    return HPT_OK;
+}
+
+int hpt_set_bsdf_marschner(hpt_context *c, float int_ior, float ext_ior, int distribution, float alpha,
+                           const float diffuse[3], const float specular[3]) {
+    if (!c || distribution < 0 || distribution > 2 || !diffuse) return setErr(c, HPT_EINVAL, "bad marschner params");
+    static const char *names[3] = {"beckmann", "ggx", "phong"};
+    c->desc.bsdf = "marschner";
+    c->desc.intIOR = int_ior;
+    c->desc.extIOR = ext_ior;
+    c->desc.distribution = names[distribution];
+    c->desc.alpha = alpha;
+    for (int i = 0; i < 3; ++i) {
+        c->desc.diffuse[i] = diffuse[i];
+        c->desc.specular[i] = specular ? specular[i] : 0.5f;
+    }
+    c->haveBSDF = true;
+    c->prepared = false;
+    return HPT_OK;
+}
+
+int hpt_set_bsdf_kajiyakay(hpt_context *c, const float kd[3], const float ks[3], float exponent) {
+    if (!c || !kd) return HPT_EINVAL;
+    c->desc.bsdf = "kajiyakay";
+    for (int i = 0; i < 3; ++i) {
+        c->desc.diffuse[i] = kd[i];
+        c->desc.specular[i] = ks ? ks[i] : 0.2f;
+    }
+    c->desc.exponent = exponent;
+    c->haveBSDF = true;
+    c->prepared = false;
+    return HPT_OK;
+}
+
+int hpt_set_envmap_rgb(hpt_context *c, const float *rgb, int w, int h, float scale, const float *to_world) {
+    if (!c || !rgb || w <= 0 || h <= 0) return setErr(c, HPT_EINVAL, "bad envmap");
+    c->env = EnvHost();
+    c->env.w = w;
+    c->env.h = h;
+    c->env.rgb.assign(rgb, rgb + (size_t) w * h * 3);
+    c->env.scale = scale;
+    if (to_world) std::memcpy(c->env.toWorld, to_world, sizeof(c->env.toWorld));
+    c->desc.emitter = "envmap";
+    c->envFromSunsky = false;
+    c->haveEnv = true;
+    c->prepared = false;
+    return HPT_OK;
+}
+
+int hpt_set_sunsky(hpt_context *c, const float sun_direction[3], float turbidity, float sky_scale, float sun_scale,
+                   float sun_radius_scale, int resolution) {
+    if (!c || !sun_direction || resolution < 4) return HPT_EINVAL;
+    c->desc.emitter = "sunsky";
+    for (int i = 0; i < 3; ++i) c->desc.sunDirection[i] = sun_direction[i];
+    c->desc.turbidity = turbidity;
+    c->desc.skyScale = sky_scale;
+    c->desc.sunScale = sun_scale;
+    c->desc.sunRadiusScale = sun_radius_scale;
+    c->desc.skyResolution = resolution;
+    c->envFromSunsky = true;
+    c->haveEnv = true;
+    c->prepared = false;
+    return HPT_OK;
+}
+
+int hpt_prepare(hpt_context *c) {
+    if (!c) return HPT_EINVAL;
+    if (!c->haveCamera || !c->haveHair || !c->haveBSDF || !c->haveEnv)
+        return setErr(c, HPT_ESTATE, "scene incomplete: need camera, hair, bsdf and emitter");
+    const bool hostOnly = c->device == HPT_HOST_ONLY;
+    if (!hostOnly) {
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        freeBufs(c->sceneBufs);
+    }
+    const SceneDesc &d = c->desc;
+    try {
+        /* Sobol tables (data/sobol, extracted from src/samplers/sobolseq.cpp) */
+        if (c->sobol32.empty()) {
+            std::string dir = c->dataDir + "/sobol/";
+            if (!readFile(dir + "matrices32.u32", c->sobol32) || c->sobol32.size() != HPT_SOBOL_DIMS * HPT_SOBOL_BITS ||
+                !readFile(dir + "vdc.u64", c->vdc) || !readFile(dir + "vdc_inv.u64", c->vdcInv))
+                return setErr(c, HPT_EIO, "cannot read Sobol tables from " + dir);
+        }
+        if (c->hairFromFile)
+            c->hair = loadHair(c->hairPath, c->hairRadius, c->hairAngle, 0.0f, c->hairHasToWorld ? c->hairToWorld : nullptr);
+        KDBuildParams kp;
+        c->tree = buildHairKDTree(c->hair, kp);
+        if (d.bsdf == "marschner") {
+            std::string err;
+            if (!precomputeMarschner(d, c->dataDir, c->mar, err)) return setErr(c, HPT_EIO, err);
+        } else if (d.bsdf == "kajiyakay") {
+            configureKajiyaKay(d, c->kk);
+        } else {
+            return setErr(c, HPT_EINVAL, "unsupported bsdf " + d.bsdf);
+        }
+        if (c->envFromSunsky) rasterizeSunSkyStandIn(d, c->env);
+        buildEnvMap(c->env);
+    } catch (const std::exception &e) {
+        return setErr(c, HPT_EIO, e.what());
+    }
+    HptScene &sc = c->sc;
+    std::memset(&sc, 0, sizeof(sc));
+    setupCamera(d, sc.cam);
+    int r = 0;
+    r |= upload(c, c->tree.nodes.data(), c->tree.nodes.size() * sizeof(HptNode), (const void **) &sc.nodes);
+    r |= upload(c, c->tree.prims.data(), c->tree.prims.size() * 4, (const void **) &sc.prims);
+    r |= upload(c, c->tree.segs.data(), c->tree.segs.size() * sizeof(HptSegment), (const void **) &sc.segs);
+    for (int i = 0; i < 3; ++i) {
+        sc.aabbMin[i] = c->tree.aabbMin[i];
+        sc.aabbMax[i] = c->tree.aabbMax[i];
+    }
+    sc.radius = c->hair.radius;
+    sc.bsdfKind = d.bsdf == "marschner" ? 0 : 1;
+    if (sc.bsdfKind == 0) {
+        for (int l = 0; l < 3; ++l) {
+            r |= upload(c, c->mar.table[l].data(), c->mar.table[l].size() * 16, (const void **) &sc.mar.table[l]);
+            r |= upload(c, c->mar.cdf[l].data(), c->mar.cdf[l].size() * 4, (const void **) &sc.mar.cdf[l]);
+            r |= upload(c, c->mar.sums[l].data(), c->mar.sums[l].size() * 4, (const void **) &sc.mar.sums[l]);
+        }
+        r |= upload(c, c->mar.trans.data(), c->mar.trans.size() * 4, (const void **) &sc.mar.trans);
+        sc.mar.transSize = (int) c->mar.trans.size();
+        sc.mar.fdr = c->mar.fdr;
+        sc.mar.invEta2 = c->mar.invEta2;
+        sc.mar.specularSamplingWeight = c->mar.specularSamplingWeight;
+        sc.mar.vR = c->mar.vR;
+        sc.mar.vTT = c->mar.vTT;
+        sc.mar.vTRT = c->mar.vTRT;
+        sc.mar.scaleAngleRad = c->mar.scaleAngleRad;
+        for (int i = 0; i < 3; ++i) sc.mar.diffuse[i] = c->mar.diffuse[i];
+    } else {
+        sc.kk = c->kk;
+    }
+    /* environment (envmap.cpp) + scene bounding sphere (scene.cpp:386-412, envmap.cpp:336-347) */
+    HptEnvMap &E = sc.env;
+    r |= upload(c, c->env.texel.data(), c->env.texel.size() * 16, (const void **) &E.texel);
+    r |= upload(c, c->env.cdfRows.data(), c->env.cdfRows.size() * 4, (const void **) &E.cdfRows);
+    r |= upload(c, c->env.cdfCols.data(), c->env.cdfCols.size() * 4, (const void **) &E.cdfCols);
+    r |= upload(c, c->env.rowWeights.data(), c->env.rowWeights.size() * 4, (const void **) &E.rowWeights);
+    E.w = c->env.w;
+    E.h = c->env.h;
+    E.normalization = c->env.normalization;
+    E.scale = c->env.scale;
+    E.pixelSizeX = c->env.pixelSizeX;
+    E.pixelSizeY = c->env.pixelSizeY;
+    E.identity = 1;
+    for (int i = 0; i < 16; ++i) E.identity &= c->env.toWorld[i] == ((i % 5 == 0) ? 1.0f : 0.0f);
+    if (!E.identity) {
+        double m[9], inv[9];
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                E.m[i * 3 + j] = c->env.toWorld[i * 4 + j];
+                m[i * 3 + j] = c->env.toWorld[i * 4 + j];
+            }
+        double det = m[0] * (m[4] * m[8] - m[5] * m[7]) - m[1] * (m[3] * m[8] - m[5] * m[6]) +
+                     m[2] * (m[3] * m[7] - m[4] * m[6]);
+        inv[0] = (m[4] * m[8] - m[5] * m[7]) / det;
+        inv[1] = (m[2] * m[7] - m[1] * m[8]) / det;
+        inv[2] = (m[1] * m[5] - m[2] * m[4]) / det;
+        inv[3] = (m[5] * m[6] - m[3] * m[8]) / det;
+        inv[4] = (m[0] * m[8] - m[2] * m[6]) / det;
+        inv[5] = (m[2] * m[3] - m[0] * m[5]) / det;
+        inv[6] = (m[3] * m[7] - m[4] * m[6]) / det;
+        inv[7] = (m[1] * m[6] - m[0] * m[7]) / det;
+        inv[8] = (m[0] * m[4] - m[1] * m[3]) / det;
+        for (int i = 0; i < 9; ++i) E.minv[i] = (float) inv[i];
+    }
+    {
+        float mn[3], mx[3];
+        for (int i = 0; i < 3; ++i) {
+            mn[i] = sc.aabbMin[i];
+            mx[i] = sc.aabbMax[i];
+        }
+        float cam[3] = {d.toWorld[3], d.toWorld[7], d.toWorld[11]};
+        for (int i = 0; i < 3; ++i) {
+            mn[i] = std::min(mn[i], cam[i]);
+            mx[i] = std::max(mx[i], cam[i]);
+        }
+        float ctr[3], dd[3];
+        for (int i = 0; i < 3; ++i) {
+            ctr[i] = (mx[i] + mn[i]) * 0.5f;
+            dd[i] = ctr[i] - mx[i];
+        }
+        float radius = std::sqrt(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]);
+        for (int i = 0; i < 3; ++i) E.bsCenter[i] = ctr[i];
+        E.bsRadius = std::max(1e-4f, radius * 1.5f);
+    }
+    r |= upload(c, c->sobol32.data(), c->sobol32.size() * 4, (const void **) &sc.sobol);
+    r |= upload(c, c->vdc.data(), c->vdc.size() * 8, (const void **) &sc.vdc);
+    r |= upload(c, c->vdcInv.data(), c->vdcInv.size() * 8, (const void **) &sc.vdcInv);
+    if (r) return HPT_EDEVICE;
+    setupTent(sc.tent, sc.tentScale);
+    sc.maxDepth = d.maxDepth;
+    sc.rrDepth = d.rrDepth;
+    sc.strictNormals = d.strictNormals ? 1 : 0;
+    sc.hideEmitters = d.hideEmitters ? 1 : 0;
+    /* Sobol dimensions consumed: 2 + 5 per bounce (sobol.cpp:225-228 errors past 1024) */
+    if (d.maxDepth > 250)
+        return setErr(c, HPT_EINVAL, "maxDepth > 250 is not supported (8-bit depth field)");
+    if (sc.cam.logRes > (uint32_t) c->vdc.size() / HPT_SOBOL_BITS)
+        return setErr(c, HPT_EINVAL, "image resolution exceeds the Sobol look-up tables");
+    c->prepared = true;
+    return HPT_OK;
+}
+
+int hpt_get_scene_info(hpt_context *c, hpt_scene_info *o) {
+    if (!c || !o) return HPT_EINVAL;
+    std::memset(o, 0, sizeof(*o));
+    const SceneDesc &d = c->desc;
+    o->width = d.width;
+    o->height = d.height;
+    o->spp = d.spp;
+    o->max_depth = d.maxDepth;
+    o->rr_depth = d.rrDepth;
+    o->strict_normals = d.strictNormals;
+    o->hide_emitters = d.hideEmitters;
+    o->bsdf = d.bsdf == "marschner" ? 0 : 1;
+    o->vertices = c->hair.vertexCount();
+    o->segments = c->tree.segs.size();
+    o->kd_nodes = c->tree.nodes.size();
+    o->kd_indices = c->tree.prims.size();
+    o->kd_depth = c->tree.maxDepthUsed;
+    o->kd_build_seconds = c->tree.buildSeconds;
+    for (int i = 0; i < 3; ++i) {
+        o->aabb_min[i] = c->tree.aabbMin[i];
+        o->aabb_max[i] = c->tree.aabbMax[i];
+        o->bsphere_center[i] = c->sc.env.bsCenter[i];
+    }
+    o->bsphere_radius = c->sc.env.bsRadius;
+    return HPT_OK;
+}
+
+static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFilm) {
+    if (c->device == HPT_HOST_ONLY) return setErr(c, HPT_EDEVICE, "host-only context cannot render");
+    if (!c->prepared) return setErr(c, HPT_ESTATE, "hpt_prepare() must succeed before rendering");
+    auto t0 = std::chrono::steady_clock::now();
+    const HptScene &sc = c->sc;
+    const int W = sc.cam.width, H = sc.cam.height;
+    const int nbx = (W + HPT_BLOCK - 1) / HPT_BLOCK, nby = (H + HPT_BLOCK - 1) / HPT_BLOCK;
+    const int nShards = std::max(1, prm->n_shards), shard = prm->shard;
+    if (shard < 0 || shard >= nShards) return setErr(c, HPT_EINVAL, "bad shard");
+    const int nBlocks = nbx * nby;
+    const int localBlocks = nBlocks > shard ? (nBlocks - shard + nShards - 1) / nShards : 0;
+    const uint64_t slots = (uint64_t) localBlocks * 1024u;
+    const int sppBegin = prm->spp_begin, sppEnd = prm->spp_end;
+    if (sppEnd < sppBegin || sppBegin < 0) return setErr(c, HPT_EINVAL, "bad spp range");
+    std::memset(&c->stats, 0, sizeof(c->stats));
+    if (slots == 0 || sppEnd == sppBegin) return HPT_OK;
+    uint64_t maxWave = prm->max_wave_paths ? prm->max_wave_paths : (uint64_t) 1 << 26;
+    uint32_t nSpp = (uint32_t) std::max<uint64_t>(1, std::min<uint64_t>(sppEnd - sppBegin, maxWave / slots));
+    const uint64_t waveCap = slots * nSpp;
+    if (waveCap > 0xffffffffull) return setErr(c, HPT_EINVAL, "wave too large");
+    int r = ensureWave(c, waveCap);
+    if (r) return r;
+    hipStream_t s = c->stream;
+    const bool st = prm->collect_stats != 0;
+    if (st) HIPCHK(c, hipMemsetAsync(c->dstats, 0, 64, s));
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> evTrace, evOther[6];
+    size_t evUsed = 0;
+    auto timed = [&](int cls, auto fn) -> hipError_t {
+        if (!st) return fn();
+        hipEvent_t a = takeEvent(c, evUsed), b = takeEvent(c, evUsed);
+        (void) hipEventRecord(a, s);
+        hipError_t e = fn();
+        (void) hipEventRecord(b, s);
+        if (cls < 0) evTrace.push_back({a, b});
+        else evOther[cls].push_back({a, b});
+        return e;
+    };
+    uint32_t *hostCnt = nullptr;
+    HIPCHK(c, hipHostMalloc((void **) &hostCnt, HPT_Q_COUNT * 4, hipHostMallocDefault));
+    uint64_t bounces = 0;
+    int maxB = 0;
+    hipError_t e = hipSuccess;
+    for (int j0 = sppBegin; j0 < sppEnd && e == hipSuccess; j0 += (int) nSpp) {
+        HptWave w;
+        w.sppBegin = (uint32_t) j0;
+        w.nSpp = (uint32_t) std::min<int>((int) nSpp, sppEnd - j0);
+        w.nPaths = (uint32_t) (slots * w.nSpp);
+        w.width = W;
+        w.height = H;
+        w.nbx = nbx;
+        w.shard = shard;
+        w.nShards = nShards;
+        c->stats.waves++;
+        HIPCHK(c, hipMemsetAsync(c->counters, 0, HPT_Q_COUNT * 4, s));
+        e = timed(0, [&] { return hpt_launch_camera(sc, w, c->P, c->qTrace, c->counters, s); });
+        if (e) break;
+        e = timed(-1, [&] {
+            return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, c->counters, st ? (uint32_t *) c->dstats : nullptr,
+                                    w.nPaths, s);
+        });
+        if (e) break;
+        e = timed(1, [&] { return hpt_launch_primary(sc, c->P, c->qTrace, c->qShadeA, c->counters, w.nPaths, s); });
+        if (e) break;
+        e = hpt_launch_rotate(c->counters, s);
+        uint32_t *shadeIn = c->qShadeA, *shadeOut = c->qShadeB;
+        int bounce = 0;
+        while (e == hipSuccess) {
+            e = hipMemcpyAsync(hostCnt, c->counters, HPT_Q_COUNT * 4, hipMemcpyDeviceToHost, s);
+            if (e) break;
+            e = hipStreamSynchronize(s);
+            if (e) break;
+            const uint32_t n = hostCnt[HPT_Q_SHADE_IN];
+            if (n == 0) break;
+            bounces += n;
+            ++bounce;
+            e = timed(2, [&] { return hpt_launch_shade(sc, c->P, shadeIn, c->qTrace, c->qShadow, c->counters, n, s); });
+            if (e) break;
+            e = timed(-1, [&] {
+                return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, c->counters,
+                                        st ? (uint32_t *) c->dstats : nullptr, 2ull * n, s);
+            });
+            if (e) break;
+            e = timed(3, [&] { return hpt_launch_post(sc, c->P, c->qTrace, shadeOut, c->counters, n, s); });
+            if (e) break;
+            e = hpt_launch_rotate(c->counters, s);
+            std::swap(shadeIn, shadeOut);
+        }
+        maxB = std::max(maxB, bounce);
+        if (e) break;
+        if (hostCnt[HPT_Q_ERROR]) {
+            (void) hipStreamSynchronize(s);
+            (void) hipHostFree(hostCnt);
+            return setErr(c, HPT_EINVAL, "Lookup dimension exceeds the direction number table size! You may have "
+                                         "to reduce the 'maxDepth' parameter of your integrator.");
+        }
+        e = timed(4, [&] { return hpt_launch_gather(sc, w, c->P, dFilm, s); });
+        c->stats.paths += w.nPaths;
+    }
+    hipError_t e2 = hipStreamSynchronize(s);
+    (void) hipHostFree(hostCnt);
+    if (e != hipSuccess || e2 != hipSuccess)
+        return setErr(c, HPT_EDEVICE, std::string("render failed: ") + hipGetErrorString(e ? e : e2));
+    auto sumEv = [](std::vector<std::pair<hipEvent_t, hipEvent_t>> &v) {
+        double tot = 0;
+        for (auto &p : v) {
+            float ms = 0;
+            (void) hipEventElapsedTime(&ms, p.first, p.second);
+            tot += ms;
+        }
+        return tot;
+    };
+    if (st) {
+        c->stats.ms_trace = sumEv(evTrace);
+        c->stats.trace_launches = evTrace.size();
+        c->stats.ms_camera = sumEv(evOther[0]);
+        c->stats.ms_primary = sumEv(evOther[1]);
+        c->stats.ms_shade = sumEv(evOther[2]);
+        c->stats.ms_post = sumEv(evOther[3]);
+        c->stats.ms_gather = sumEv(evOther[4]);
+        uint64_t hs[8];
+        HIPCHK(c, hipMemcpy(hs, c->dstats, 64, hipMemcpyDeviceToHost));
+        c->stats.nodes = hs[0];
+        c->stats.prims = hs[1];
+        c->stats.closest_rays = hs[2];
+        c->stats.shadow_rays = hs[3];
+        c->stats.shadow_unoccluded = hs[4];
+    }
+    c->stats.bounces = bounces;
+    c->stats.max_bounces = maxB;
+    c->stats.ms_total = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return HPT_OK;
+}
+
+int hpt_render_device(hpt_context *c, const hpt_render_params *prm, void *dfilm) {
+    if (!c || !prm || !dfilm) return HPT_EINVAL;
+    if (c->device == HPT_HOST_ONLY) return setErr(c, HPT_EDEVICE, "host-only context cannot render");
+    HIPCHK(c, hipSetDevice(c->device));
+    return renderImpl(c, prm, (float4 *) dfilm);
+}
+
+int hpt_render(hpt_context *c, const hpt_render_params *prm, float *film) {
+    if (!c || !prm || !film) return HPT_EINVAL;
+    if (c->device == HPT_HOST_ONLY) return setErr(c, HPT_EDEVICE, "host-only context cannot render");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t n = (size_t) c->desc.width * c->desc.height;
+    float4 *d = nullptr;
+    HIPCHK(c, hipMalloc(&d, n * 16));
+    hipError_t e = hipMemcpy(d, film, n * 16, hipMemcpyHostToDevice);
+    int r = e == hipSuccess ? renderImpl(c, prm, d) : HPT_EDEVICE;
+    if (r == HPT_OK) e = hipMemcpy(film, d, n * 16, hipMemcpyDeviceToHost);
+    (void) hipFree(d);
+    if (r) return r;
+    if (e != hipSuccess) return setErr(c, HPT_EDEVICE, hipGetErrorString(e));
+    return HPT_OK;
+}
+
+int hpt_get_stats(hpt_context *c, hpt_stats *o) {
+    if (!c || !o) return HPT_EINVAL;
+    *o = c->stats;
+    return HPT_OK;
+}
+
+int64_t hpt_get_hair(hpt_context *c, float *xyz, uint8_t *starts) {
+    if (!c) return HPT_EINVAL;
+    int64_t n = (int64_t) c->hair.vertexCount();
+    if (xyz) std::memcpy(xyz, c->hair.xyz.data(), (size_t) n * 12);
+    if (starts) std::memcpy(starts, c->hair.starts.data(), c->hair.starts.size());
+    return n;
+}
+
+int hpt_get_kdtree(hpt_context *c, uint32_t *nodes, int64_t *n_nodes, uint32_t *indices, int64_t *n_indices,
+                   float aabb[6]) {
+    if (!c || !n_nodes || !n_indices) return HPT_EINVAL;
+    *n_nodes = (int64_t) c->tree.nodes.size();
+    *n_indices = (int64_t) c->tree.prims.size();
+    if (nodes) std::memcpy(nodes, c->tree.nodes.data(), c->tree.nodes.size() * 8);
+    if (indices)
+        for (size_t i = 0; i < c->tree.prims.size(); ++i) indices[i] = c->tree.segFirstVertex[c->tree.prims[i]];
+    if (aabb)
+        for (int i = 0; i < 3; ++i) {
+            aabb[i] = c->tree.aabbMin[i];
+            aabb[3 + i] = c->tree.aabbMax[i];
+        }
+    return HPT_OK;
+}
+
+int hpt_get_envmap(hpt_context *c, float *rgb, int *w, int *h) {
+    if (!c || !w || !h) return HPT_EINVAL;
+    *w = c->env.w;
+    *h = c->env.h;
+    if (rgb) std::memcpy(rgb, c->env.rgb.data(), c->env.rgb.size() * 4);
+    return HPT_OK;
+}
+
+int hpt_get_marschner_tables(hpt_context *c, float *nR, float *nTT, float *nTRT, float *fdr, float *trans,
+                             float *specw) {
+    if (!c || c->sc.bsdfKind != 0 || !c->prepared) return setErr(c, HPT_ESTATE, "no marschner bsdf prepared");
+    float *outs[3] = {nR, nTT, nTRT};
+    for (int l = 0; l < 3; ++l)
+        if (outs[l])
+            for (size_t i = 0; i < c->mar.table[l].size(); ++i) {
+                outs[l][3 * i] = c->mar.table[l][i].x;
+                outs[l][3 * i + 1] = c->mar.table[l][i].y;
+                outs[l][3 * i + 2] = c->mar.table[l][i].z;
+            }
+    if (fdr) *fdr = c->mar.fdr;
+    if (trans) std::memcpy(trans, c->mar.trans.data(), std::min<size_t>(100, c->mar.trans.size()) * 4);
+    if (specw) *specw = c->mar.specularSamplingWeight;
+    return HPT_OK;
+}
+
+/* ---- batch helpers ---- */
+} /* extern "C" */
+namespace {
+struct Scratch {
+    std::vector<void *> ptrs;
+    ~Scratch() {
+        for (void *p : ptrs) (void) hipFree(p);
+    }
+    template <typename T> T *in(const T *src, size_t n) {
+        void *p = nullptr;
+        if (hipMalloc(&p, std::max<size_t>(n * sizeof(T), 16)) != hipSuccess) return nullptr;
+        ptrs.push_back(p);
+        if (src && n) (void) hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice);
+        return (T *) p;
+    }
+};
+template <typename T> void fetch(T *dst, const T *src, size_t n) {
+    if (dst) (void) hipMemcpy(dst, src, n * sizeof(T), hipMemcpyDeviceToHost);
+}
+} // namespace
+extern "C" {
+
+int hpt_sobol_batch(hpt_context *c, int m, int n, const uint32_t *frame, const uint32_t *px, const uint32_t *py,
+                    const uint32_t *dim, uint64_t *oi, float *ov) {
+    if (!c || !c->prepared) return setErr(c, HPT_ESTATE, "prepare first");
+    if (c->device == HPT_HOST_ONLY) return setErr(c, HPT_EDEVICE, "host-only context has no device");
+    HIPCHK(c, hipSetDevice(c->device));
+    Scratch S;
+    const uint32_t *df = S.in(frame, n), *dx = S.in(px, n), *dy = S.in(py, n), *dd = S.in(dim, n);
+    uint64_t *di = S.in<uint64_t>(nullptr, n);
+    float *dv = S.in<float>(nullptr, n);
+    HIPCHK(c, hpt_launch_sobol_batch(c->sc, m, n, df, dx, dy, dd, di, dv, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    fetch(oi, di, n);
+    fetch(ov, dv, n);
+    return HPT_OK;
+}
+
+int hpt_trace_batch(hpt_context *c, int n, const float *o, const float *d, const float *mint, const float *maxt,
+                    int shadow, float *ot, int32_t *oiv, float *op, uint8_t *oh) {
+    if (!c || !c->prepared) return setErr(c, HPT_ESTATE, "prepare first");
+    if (c->device == HPT_HOST_ONLY) return setErr(c, HPT_EDEVICE, "host-only context has no device");
+    HIPCHK(c, hipSetDevice(c->device));
+    Scratch S;
+    const float *a = S.in(o, 3 * (size_t) n), *b = S.in(d, 3 * (size_t) n), *mi = S.in(mint, n), *ma = S.in(maxt, n);
+    float *dt = S.in<float>(nullptr, n), *dp = S.in<float>(nullptr, 3 * (size_t) n);
+    int32_t *ds = S.in<int32_t>(nullptr, n);
+    uint8_t *dh = S.in<uint8_t>(nullptr, n);
+    HIPCHK(c, hpt_launch_trace_batch(c->sc, n, a, b, mi, ma, shadow, dt, ds, dp, dh, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (shadow) {
+        fetch(oh, dh, n);
+    } else {
+        fetch(ot, dt, n);
+        fetch(op, dp, 3 * (size_t) n);
+        std::vector<int32_t> seg(n);
+        fetch(seg.data(), ds, n);
+        if (oiv)
+            for (int i = 0; i < n; ++i) oiv[i] = seg[i] < 0 ? -1 : (int32_t) c->tree.segFirstVertex[seg[i]];
+    }
+    return HPT_OK;
+}
+
+int hpt_bsdf_batch(hpt_context *c, int n, const float *wi, const float *wo, const float *u, float *oe, float *op,
+                   float *owo, float *ow, float *osp, uint32_t *ot) {
+    if (!c || !c->prepared) return setErr(c, HPT_ESTATE, "prepare first");
+    if (c->device == HPT_HOST_ONLY) return setErr(c, HPT_EDEVICE, "host-only context has no device");
+    HIPCHK(c, hipSetDevice(c->device));
+    Scratch S;
+    const float *a = S.in(wi, 3 * (size_t) n), *b = S.in(wo, 3 * (size_t) n), *uu = S.in(u, 2 * (size_t) n);
+    float *de = S.in<float>(nullptr, 3 * (size_t) n), *dp = S.in<float>(nullptr, n);
+    float *dwo = S.in<float>(nullptr, 3 * (size_t) n), *dw = S.in<float>(nullptr, 3 * (size_t) n);
+    float *dsp = S.in<float>(nullptr, n);
+    uint32_t *dt = S.in<uint32_t>(nullptr, n);
+    HIPCHK(c, hpt_launch_bsdf_batch(c->sc, n, a, b, uu, de, dp, dwo, dw, dsp, dt, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    fetch(oe, de, 3 * (size_t) n);
+    fetch(op, dp, n);
+    fetch(owo, dwo, 3 * (size_t) n);
+    fetch(ow, dw, 3 * (size_t) n);
+    fetch(osp, dsp, n);
+    fetch(ot, dt, n);
+    return HPT_OK;
+}
+
+int hpt_env_batch(hpt_context *c, int n, const float *refp, const float *u, const float *dq, float *od, float *ov,
+                  float *op, float *odist, float *oe, float *oep) {
+    if (!c || !c->prepared) return setErr(c, HPT_ESTATE, "prepare first");
+    if (c->device == HPT_HOST_ONLY) return setErr(c, HPT_EDEVICE, "host-only context has no device");
+    HIPCHK(c, hipSetDevice(c->device));
+    Scratch S;
+    const float *a = S.in(refp, 3 * (size_t) n), *uu = S.in(u, 2 * (size_t) n), *q = S.in(dq, 3 * (size_t) n);
+    float *dd = S.in<float>(nullptr, 3 * (size_t) n), *dv = S.in<float>(nullptr, 3 * (size_t) n);
+    float *dp = S.in<float>(nullptr, n), *ddist = S.in<float>(nullptr, n), *de = S.in<float>(nullptr, 3 * (size_t) n);
+    float *dep = S.in<float>(nullptr, n);
+    HIPCHK(c, hpt_launch_env_batch(c->sc, n, a, uu, q, dd, dv, dp, ddist, de, dep, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    fetch(od, dd, 3 * (size_t) n);
+    fetch(ov, dv, 3 * (size_t) n);
+    fetch(op, dp, n);
+    fetch(odist, ddist, n);
+    fetch(oe, de, 3 * (size_t) n);
+    fetch(oep, dep, n);
+    return HPT_OK;
+}
+
+} /* extern "C" */

@@ -1,0 +1,107 @@
+/*
+ * hpt_device.h -- data layout shared by the host builder and the gfx950
+ * kernels of the wavefront hair path tracer.
+ *
+ * Everything here is POD.  The host fills these structures once per scene
+ * (hpt_prepare) and uploads them to HBM; kernels receive the scene by value.
+ */
+#ifndef HPT_DEVICE_H
+#define HPT_DEVICE_H
+#include <stdint.h>
+
+/* 16-byte vector used for coalesced dwordx4 traffic (host-compatible POD) */
+struct __attribute__((aligned(16))) HptF4 {
+    float x, y, z, w;
+};
+
+#define HPT_AZ_RES 64          /* marschner_diffuse.cpp:66 AzimuthalResolution */
+#define HPT_SOBOL_DIMS 1024    /* sobolseq.h:33 */
+#define HPT_SOBOL_BITS 52      /* sobolseq.h:34 */
+#define HPT_BLOCK 32           /* mitsuba.cpp:144 block size */
+#define HPT_FILTER_RES 31      /* rfilter.h:28 MTS_FILTER_RESOLUTION */
+
+/* BSDF type flags (render/bsdf.h:224-285) */
+#define HPT_ENULL 0x00001u
+#define HPT_EDIFFUSE_REFLECTION 0x00002u
+#define HPT_EGLOSSY_REFLECTION 0x00008u
+#define HPT_EDELTA_REFLECTION 0x00020u
+#define HPT_EDELTA (0x00001u | 0x00020u | 0x00040u)
+
+/* One hair segment, everything the fp64 cylinder/miter test needs
+ * (hair.cpp:485-548) precomputed on the host in double exactly as the
+ * reference computes it per test: v1, axis = normalize(v2 - v1), miter
+ * normals n1/n2 (hair.cpp:578-596), v2.  128 bytes = one cache line. */
+struct HptSegment {
+    double v1[3];
+    double axis[3];
+    double n1[3];
+    double n2[3];
+    double v2[3];
+    uint32_t iv;   /* first vertex index (reference prim id, for parity) */
+    uint32_t pad;
+};
+
+/* kd-tree node, 8 bytes (gkdtree.h:452-583 layout with absolute child index):
+ *   inner: w0 = (left << 2) | axis, w1 = float bits of split; right = left + 1
+ *   leaf : w0 = 0x80000000 | primStart, w1 = primEnd (indices into prim list) */
+struct HptNode {
+    uint32_t w0, w1;
+};
+
+struct HptCamera {
+    float s2c[16];      /* sampleToCamera, row-major (perspective.cpp:155) */
+    float toWorld[16];  /* camera-to-world, row-major */
+    float invResX, invResY, nearClip, farClip;
+    float resolution;   /* Sobol pixel resolution (sobol.cpp:147-158) */
+    int width, height;
+    uint32_t logRes;
+};
+
+struct HptMarschner {
+    const HptF4 *table[3];     /* R, TT, TRT: 64x64 RGB(+pad), index x + y*64 */
+    const float *cdf[3];        /* InterpolatedDistribution1D cdfs: 64 dists x 65 */
+    const float *sums[3];       /* 64 */
+    const float *trans;         /* external rough transmittance 1D slice */
+    int transSize;
+    float fdr, invEta2, specularSamplingWeight;
+    float vR, vTT, vTRT, scaleAngleRad;
+    float diffuse[3];
+};
+
+struct HptKajiyaKay {
+    float kd[3], ks[3];
+    float exponent, specularSamplingWeight;
+};
+
+struct HptEnvMap {
+    const HptF4 *texel;        /* w*h, half-rounded RGB stored as float */
+    const float *cdfRows;       /* h+1 */
+    const float *cdfCols;       /* h*(w+1) */
+    const float *rowWeights;    /* h */
+    int w, h;
+    float normalization, scale, pixelSizeX, pixelSizeY;
+    float bsCenter[3], bsRadius;
+    int identity;
+    float m[9], minv[9];
+};
+
+struct HptScene {
+    HptCamera cam;
+    const HptNode *nodes;
+    const uint32_t *prims;      /* leaf primitive list -> segment index */
+    const HptSegment *segs;
+    float aabbMin[3], aabbMax[3];
+    float radius;
+    int bsdfKind;               /* 0 = marschner, 1 = kajiyakay */
+    HptMarschner mar;
+    HptKajiyaKay kk;
+    HptEnvMap env;
+    const uint32_t *sobol;      /* 1024 x 52 */
+    const uint64_t *vdc;        /* rows x 52 */
+    const uint64_t *vdcInv;     /* rows x 52 */
+    float tent[HPT_FILTER_RES + 1];
+    float tentScale;
+    int maxDepth, rrDepth, strictNormals, hideEmitters;
+};
+
+#endif

@@ -1,0 +1,68 @@
+/*
+ * hpt_kernels.h -- launch-side view of the wavefront kernels (hpt_render.hip).
+ */
+#ifndef HPT_KERNELS_H
+#define HPT_KERNELS_H
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../hpt_device.h"
+
+/* queue counter slots */
+#define HPT_Q_TRACE 0
+#define HPT_Q_SHADOW 1
+#define HPT_Q_SHADE_IN 2
+#define HPT_Q_SHADE_OUT 3
+#define HPT_Q_ERROR 4     /* set when a path runs out of Sobol dimensions */
+#define HPT_Q_COUNT 8
+
+/* One wave of paths: every pixel of this shard's 32x32 blocks x samples
+   [sppBegin, sppBegin + nSpp).  Path id = slot * nSpp + (j - sppBegin),
+   slot = (localBlock << 10) | (y%32 << 5) | (x%32). */
+struct HptWave {
+    uint32_t nPaths;
+    uint32_t sppBegin, nSpp;
+    int width, height, nbx;
+    int shard, nShards;
+};
+
+/* path state, structure of arrays in HBM (16-byte rows where possible) */
+struct HptPaths {
+    float4 *ro;        /* ray origin xyz, mint                       */
+    float4 *rd;        /* ray direction xyz, maxt                    */
+    float2 *pos;       /* film sample position (pixels)              */
+    uint64_t *sobol;   /* Sobol index of the sample (look_up)        */
+    uint32_t *state;   /* dim[0:16) | depth[16:24) | sampledType[24:32) */
+    float4 *thr;       /* throughput rgb                             */
+    float4 *li;        /* accumulated radiance rgb                   */
+    float4 *hit;       /* segment id (int bits), t                   */
+    float4 *hitp;      /* hit point xyz (fp64 -> fp32, hair.cpp:526) */
+    float4 *bw;        /* bsdf weight rgb, bsdf pdf                  */
+    float4 *sdir;      /* shadow ray direction xyz, maxt             */
+    float4 *scontrib;  /* NEE contribution rgb (added if unoccluded) */
+};
+
+
+/* launch wrappers (hpt_render.hip) */
+hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPaths &P, uint32_t *traceQ,
+                             uint32_t *counters, hipStream_t s);
+hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
+                            const uint32_t *counters, uint32_t *stats, uint64_t maxItems, hipStream_t s);
+hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
+                              uint32_t *counters, uint64_t maxItems, hipStream_t s);
+hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *traceQ,
+                            uint32_t *shadowQ, uint32_t *counters, uint64_t maxItems, hipStream_t s);
+hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
+                           uint32_t *counters, uint64_t maxItems, hipStream_t s);
+hipError_t hpt_launch_rotate(uint32_t *counters, hipStream_t s);
+hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *film, hipStream_t s);
+hipError_t hpt_launch_sobol_batch(const HptScene &sc, int m, int n, const uint32_t *frame, const uint32_t *px,
+                                  const uint32_t *py, const uint32_t *dim, uint64_t *oi, float *ov, hipStream_t s);
+hipError_t hpt_launch_trace_batch(const HptScene &sc, int n, const float *o, const float *d, const float *mint,
+                                  const float *maxt, int shadow, float *ot, int32_t *os, float *op, uint8_t *oh,
+                                  hipStream_t s);
+hipError_t hpt_launch_bsdf_batch(const HptScene &sc, int n, const float *wi, const float *wo, const float *u,
+                                 float *oe, float *op, float *owo, float *ow, float *osp, uint32_t *ot, hipStream_t s);
+hipError_t hpt_launch_env_batch(const HptScene &sc, int n, const float *refp, const float *u, const float *dq,
+                                float *od, float *ov, float *op, float *odist, float *oe, float *oep, hipStream_t s);
+#endif

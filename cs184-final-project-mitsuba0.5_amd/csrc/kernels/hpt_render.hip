@@ -1,0 +1,1149 @@
+/*
+ * hpt_render.hip -- gfx950 wavefront kernels for the reference's `path`
+ * integrator over the `hair` shape with the `marschner` / `kajiyakay` BSDFs.
+ *
+ * MIPathTracer::Li (src/integrators/path/path.cpp:119-294) is split at its
+ * two ray casts.  One path = one lane; paths live in SoA slots in HBM and
+ * are driven by index queues:
+ *
+ *   k_camera      sampler->generate + camera ray (integrator.cpp:165-178)
+ *   k_trace       closest-hit rays (continuation) and any-hit shadow rays in
+ *                 one launch; kd-tree traversal with an LDS stack and the
+ *                 fp64 cylinder/miter test (hair.cpp:485-548)
+ *   k_primary     primary misses -> environment (path.cpp:136-143)
+ *   k_shade       its -> strictNormals, NEE sample + BSDF eval (:170-199),
+ *                 BSDF sample (:206-221); emits one shadow ray + one
+ *                 continuation ray per path
+ *   k_post        env hit + MIS (:236-264), throughput, Russian roulette
+ *                 (:270-286); survivors re-enter the shade queue
+ *   k_gather      deterministic tent-filter gather of all samples into an
+ *                 RGBW film (imageblock.h:124-204)
+ *
+ * Queues are compacted with a wave64 ballot + one atomic per wave.  A
+ * path's arithmetic never depends on its queue position, so results are
+ * independent of compaction order.
+ */
+#include <hip/hip_runtime.h>
+
+#include "../hpt_device.h"
+#include "hpt_kernels.h"
+#include "hpt_math.h"
+
+using namespace hk;
+
+namespace {
+
+/* ------------------------------------------------------------------ */
+/* Sobol sampler: sobolseq.h:43-58 (sampleSingle), :99-131 (look_up),   */
+/* sobol.cpp:204-250 (setSampleIndex / next1D / next2D)                 */
+/* ------------------------------------------------------------------ */
+HD float sobolSample(const HptScene &sc, uint64_t index, uint32_t dim) {
+    uint32_t result = 0;
+    const uint32_t *m = sc.sobol + dim * HPT_SOBOL_BITS;
+    uint32_t lo = (uint32_t) index, hi = (uint32_t) (index >> 32);
+    for (int i = 0; lo; lo >>= 1, ++i)
+        if (lo & 1u) result ^= m[i];
+    for (int i = 32; hi; hi >>= 1, ++i)
+        if (hi & 1u) result ^= m[i];
+    return fminr((float) result * (1.0f / 4294967296.0f), kOneMinusEps);
+}
+
+HD uint64_t sobolLookUp(const HptScene &sc, uint32_t m, uint32_t frame, uint32_t px, uint32_t py) {
+    uint64_t index = (uint64_t) frame << (m << 1);
+    uint64_t delta = 0;
+    const uint64_t *vdc = sc.vdc + (m - 1) * HPT_SOBOL_BITS;
+    const uint64_t *inv = sc.vdcInv + (m - 1) * HPT_SOBOL_BITS;
+    for (uint32_t c = 0; frame; frame >>= 1, ++c)
+        if (frame & 1u) delta ^= vdc[c];
+    uint64_t b = (((uint64_t) px << m) | py) ^ delta;
+    for (uint32_t c = 0; b; b >>= 1, ++c)
+        if (b & 1u) index ^= inv[c];
+    return index;
+}
+
+/* ------------------------------------------------------------------ */
+/* Camera (perspective.cpp:271-298)                                     */
+/* ------------------------------------------------------------------ */
+HD V3 xformPoint(const float *M, V3 p) {
+    float x = M[0] * p.x + M[1] * p.y + M[2] * p.z + M[3];
+    float y = M[4] * p.x + M[5] * p.y + M[6] * p.z + M[7];
+    float z = M[8] * p.x + M[9] * p.y + M[10] * p.z + M[11];
+    float w = M[12] * p.x + M[13] * p.y + M[14] * p.z + M[15];
+    if (w == 1.0f) return v3(x, y, z);
+    return divs(v3(x, y, z), w);
+}
+HD V3 xformVector(const float *M, V3 v) {
+    return v3(M[0] * v.x + M[1] * v.y + M[2] * v.z, M[4] * v.x + M[5] * v.y + M[6] * v.z,
+              M[8] * v.x + M[9] * v.y + M[10] * v.z);
+}
+
+/* ------------------------------------------------------------------ */
+/* Ray / AABB (aabb.h:308-338)                                          */
+/* ------------------------------------------------------------------ */
+HD bool aabbIntersect(const HptScene &sc, V3 o, V3 d, V3 rcp, float &nearT, float &farT) {
+    nearT = -finf();
+    farT = finf();
+    for (int i = 0; i < 3; ++i) {
+        float origin = o[i], mn = sc.aabbMin[i], mx = sc.aabbMax[i];
+        if (d[i] == 0) {
+            if (origin < mn || origin > mx) return false;
+        } else {
+            float t1 = (mn - origin) * rcp[i], t2 = (mx - origin) * rcp[i];
+            if (t1 > t2) {
+                float t = t1;
+                t1 = t2;
+                t2 = t;
+            }
+            nearT = fmaxr(t1, nearT);
+            farT = fminr(t2, farT);
+            if (!(nearT <= farT)) return false;
+        }
+    }
+    return true;
+}
+
+/* ------------------------------------------------------------------ */
+/* Hair segment test: HairKDTree::intersect (hair.cpp:485-548) in fp64  */
+/* ------------------------------------------------------------------ */
+HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, const D3 &rayO, const D3 &rayD,
+                     double r2, float mint, float maxt, float &t, D3 &p) {
+    const double *rec = reinterpret_cast<const double *>(segs + s);
+    D3 v1 = d3(rec[0], rec[1], rec[2]);
+    D3 axis = d3(rec[3], rec[4], rec[5]);
+    D3 relOrigin = rayO - v1;
+    D3 projOrigin = relOrigin - axis * dot(axis, relOrigin);
+    D3 projDirection = rayD - axis * dot(axis, rayD);
+    const double A = dot(projDirection, projDirection);
+    const double B = 2 * dot(projOrigin, projDirection);
+    const double C = dot(projOrigin, projOrigin) - r2;
+    double nearT, farT;
+    if (!solveQuadraticDouble(A, B, C, nearT, farT)) return false;
+    if (!(nearT <= (double) maxt && farT >= (double) mint)) return false;
+    D3 pointNear = rayO + rayD * nearT;
+    D3 pointFar = rayO + rayD * farT;
+    D3 n1 = d3(rec[6], rec[7], rec[8]);
+    D3 n2 = d3(rec[9], rec[10], rec[11]);
+    D3 v2 = d3(rec[12], rec[13], rec[14]);
+    if (dot(pointNear - v1, n1) >= 0 && dot(pointNear - v2, n2) <= 0 && nearT >= (double) mint) {
+        p = pointNear;
+        t = (float) nearT;
+    } else if (dot(pointFar - v1, n1) >= 0 && dot(pointFar - v2, n2) <= 0) {
+        if (farT > (double) maxt) return false;
+        p = pointFar;
+        t = (float) farT;
+    } else {
+        return false;
+    }
+    return true;
+}
+
+/* ------------------------------------------------------------------ */
+/* kd-tree traversal (front-to-back, LDS ring stack with kd-restart).   */
+/* Primitive tests use the ray's [mint, best t] interval exactly like   */
+/* rayIntersectHavran (sahkdtree3.h:275-297), so the closest hit does    */
+/* not depend on the tree or on the traversal order.                     */
+/* ------------------------------------------------------------------ */
+template <int STACK, bool SHADOW>
+HD bool traverse(const HptScene &sc, V3 o, V3 d, V3 rcp, float mint, float maxt, uint2 *stk, int stride,
+                 float &tHit, uint32_t &segHit, D3 &pHit, uint32_t &nNodes, uint32_t &nPrims) {
+    const HptNode *__restrict__ nodes = sc.nodes;
+    const uint32_t *__restrict__ prims = sc.prims;
+    const D3 rayO = d3(o.x, o.y, o.z), rayD = d3(d.x, d.y, d.z);
+    const double r2 = (double) (sc.radius * sc.radius); /* Float product (hair.cpp:500) */
+    float tmin = mint, tmax = maxt;
+    tHit = maxt;
+    bool found = false;
+    uint32_t node = 0;
+    int sp = 0, top = 0; /* ring buffer: entries [top-sp, top) modulo STACK */
+    bool lost = false;
+    while (true) {
+        HptNode nd = nodes[node];
+        while (!(nd.w0 & 0x80000000u)) {
+            ++nNodes;
+            const int axis = (int) (nd.w0 & 3u);
+            const uint32_t left = nd.w0 >> 2;
+            const float split = __uint_as_float(nd.w1);
+            const float oa = o[axis], da = d[axis];
+            const float tsplit = (split - oa) * rcp[axis];
+            const bool belowFirst = (oa < split) || (oa == split && da <= 0.0f);
+            const uint32_t first = belowFirst ? left : left + 1, second = belowFirst ? left + 1 : left;
+            if (!(tsplit <= tmax) || tsplit <= 0.0f) {
+                node = first;
+            } else if (tsplit < tmin) {
+                node = second;
+            } else {
+                stk[(top % STACK) * stride] = make_uint2(second, __float_as_uint(tmax));
+                top++;
+                if (sp < STACK) sp++;
+                else lost = true;
+                node = first;
+                tmax = tsplit;
+            }
+            nd = nodes[node];
+        }
+        ++nNodes;
+        for (uint32_t e = nd.w0 & 0x7fffffffu, last = nd.w1; e < last; ++e) {
+            const uint32_t s = prims[e];
+            ++nPrims;
+            float t;
+            D3 p;
+            if (segIntersect(sc.segs, s, rayO, rayD, r2, mint, tHit, t, p)) {
+                if (SHADOW) return true;
+                tHit = t;
+                segHit = s;
+                pHit = p;
+                found = true;
+            }
+        }
+        if (found && tHit <= tmax) break;
+        if (sp == 0) {
+            if (!lost || tmax >= maxt) break;
+            /* kd-restart from the root for the remaining interval */
+            lost = false;
+            node = 0;
+            tmin = tmax;
+            tmax = maxt;
+            continue;
+        }
+        top--;
+        sp--;
+        uint2 e = stk[(top % STACK) * stride];
+        node = e.x;
+        tmin = tmax;
+        tmax = __uint_as_float(e.y);
+        if (tmin > tHit) break;
+    }
+    return found;
+}
+
+/* ------------------------------------------------------------------ */
+/* Marschner (marschner_diffuse.cpp)                                    */
+/* ------------------------------------------------------------------ */
+HD float trigInverse(float x) { return fminr(sqrtf(fmaxr(1.0f - x * x, 0.0f)), 1.0f); }
+
+HD float I0(float x) { /* :279-290 */
+    float result = 1.0f, xSq = x * x, xi = xSq, denom = 4.0f;
+#pragma unroll
+    for (int i = 1; i <= 10; ++i) {
+        result += xi / denom;
+        xi *= xSq;
+        denom *= 4.0f * float((i + 1) * (i + 1));
+    }
+    return result;
+}
+HD float logI0(float x) { /* :292-299 */
+    if (x > 12.0f) return x + 0.5f * (logf(1.0f / (kPi * 2.0f * x)) + 1.0f / (8.0f * x));
+    return logf(I0(x));
+}
+HD float longitudinalM(float v, float sinThetaI, float sinThetaO, float cosThetaI, float cosThetaO) { /* :364-374 */
+    float a = cosThetaI * cosThetaO / v;
+    float b = sinThetaI * sinThetaO / v;
+    if (v < 0.1f) return expf(-b + logI0(a) - 1.0f / v + 0.6931f + logf(1.0f / (2.0f * v)));
+    return expf(-b) * I0(a) / (2.0f * v * sinhf(1.0f / v));
+}
+
+/* Azimuthal::eval (:80-94) */
+HD V3 azEval(const HptF4 *__restrict__ tab, float phi, float cosThetaD) {
+    float u = (HPT_AZ_RES - 1) * phi * (1.0f / (2.0f * kPi));
+    float v = (HPT_AZ_RES - 1) * cosThetaD;
+    int x0 = clampi(int(u), 0, HPT_AZ_RES - 2), y0 = clampi(int(v), 0, HPT_AZ_RES - 2);
+    int x1 = x0 + 1, y1 = y0 + 1;
+    u = clampf(u - x0, 0.0f, 1.0f);
+    v = clampf(v - y0, 0.0f, 1.0f);
+    HptF4 a = tab[x0 + y0 * HPT_AZ_RES], b = tab[x1 + y0 * HPT_AZ_RES];
+    HptF4 c = tab[x0 + y1 * HPT_AZ_RES], e = tab[x1 + y1 * HPT_AZ_RES];
+    V3 r0 = v3(a.x, a.y, a.z) * (1.0f - u) + v3(b.x, b.y, b.z) * u;
+    V3 r1 = v3(c.x, c.y, c.z) * (1.0f - u) + v3(e.x, e.y, e.z) * u;
+    return r0 * (1.0f - v) + r1 * v;
+}
+/* InterpolatedDistribution1D::sum via Azimuthal::weight (:102-106) */
+HD float azWeight(const float *__restrict__ sums, float cosThetaD) {
+    float dist = (HPT_AZ_RES - 1) * cosThetaD;
+    int d0 = clampi(int(dist), 0, HPT_AZ_RES - 1), d1 = imin(d0 + 1, HPT_AZ_RES - 1);
+    float v = clampf(dist - d0, 0.0f, 1.0f);
+    return (sums[d0] * (1.0f - v) + sums[d1] * v) * (2.0f * kPi / HPT_AZ_RES);
+}
+/* Azimuthal::sample (:68-77) -> InterpolatedDistribution1D::warp (:69-92) */
+HD float azSample(const float *__restrict__ cdfs, float cosThetaD, float xi) {
+    float dist = (HPT_AZ_RES - 1) * cosThetaD;
+    int d0 = clampi(int(dist), 0, HPT_AZ_RES - 1), d1 = imin(d0 + 1, HPT_AZ_RES - 1);
+    float v = clampf(dist - d0, 0.0f, 1.0f);
+    const float *c0 = cdfs + d0 * (HPT_AZ_RES + 1), *c1 = cdfs + d1 * (HPT_AZ_RES + 1);
+    int lower = 0, upper = HPT_AZ_RES;
+    float lowerU = 0.0f, upperU = 1.0f;
+    while (upper - lower != 1) {
+        int mid = (upper + lower) / 2;
+        float mu = c0[mid] * (1.0f - v) + c1[mid] * v;
+        if (mu < xi) {
+            lower = mid;
+            lowerU = mu;
+        } else {
+            upper = mid;
+            upperU = mu;
+        }
+    }
+    float u = clampf((xi - lowerU) / (upperU - lowerU), 0.0f, 1.0f);
+    return 2.0f * kPi * (lower + u) * (1.0f / HPT_AZ_RES);
+}
+
+/* rtrans.h:183-199 (eta and alpha fixed) + spline.cpp:23-61 */
+HD float roughTrans(const HptMarschner &m, float cosTheta) {
+    float w = powf(fabsf(cosTheta), 0.25f);
+    if (!(cosTheta >= 0)) return 0.f;
+    float result;
+    if (!(w >= 0.0f && w <= 1.0f)) {
+        result = 0.0f;
+    } else {
+        const size_t size = (size_t) m.transSize;
+        float t = ((w - 0.0f) * (size - 1)) / (1.0f - 0.0f);
+        size_t k = (size_t) t < size - 2 ? (size_t) t : size - 2;
+        const float *val = m.trans;
+        float f0 = val[k], f1 = val[k + 1], d0, d1;
+        d0 = (k > 0) ? 0.5f * (val[k + 1] - val[k - 1]) : val[k + 1] - val[k];
+        d1 = (k + 2 < size) ? 0.5f * (val[k + 2] - val[k]) : val[k + 1] - val[k];
+        t = t - (float) k;
+        float t2 = t * t, t3 = t2 * t;
+        result = (2 * t3 - 3 * t2 + 1) * f0 + (-2 * t3 + 3 * t2) * f1 + (t3 - 2 * t2 + t) * d0 + (t3 - t2) * d1;
+    }
+    return fminr(1.0f, fmaxr(0.0f, result));
+}
+
+/* MarschnerDiffuse::eval (:377-482), hasDiffuse = true */
+HD V3 marschnerEval(const HptMarschner &m, V3 wi, V3 wo) {
+    float sinThetaI = wi.y, sinThetaO = wo.y;
+    float cosThetaO = trigInverse(sinThetaO);
+    float thetaI = asinf(clampf(sinThetaI, -1.0f, 1.0f));
+    float thetaO = asinf(clampf(sinThetaO, -1.0f, 1.0f));
+    float thetaD = (thetaO - thetaI) * 0.5f;
+    float cosThetaD = cosf(thetaD);
+    float phi = atan2f(wo.x, wo.z);
+    if (phi < 0.0f) phi += kPi * 2.0f;
+    float thetaIR = thetaI - 2.0f * m.scaleAngleRad;
+    float thetaITT = thetaI + m.scaleAngleRad;
+    float thetaITRT = thetaI + 4.0f * m.scaleAngleRad;
+    float MR = longitudinalM(m.vR, sinf(thetaIR), sinThetaO, cosf(thetaIR), cosThetaO);
+    float MTT = longitudinalM(m.vTT, sinf(thetaITT), sinThetaO, cosf(thetaITT), cosThetaO);
+    float MTRT = longitudinalM(m.vTRT, sinf(thetaITRT), sinThetaO, cosf(thetaITRT), cosThetaO);
+    V3 result = (0.15f * MR) * azEval(m.table[0], phi, cosThetaD) + MTT * azEval(m.table[1], phi, cosThetaD) +
+                MTRT * azEval(m.table[2], phi, cosThetaD);
+    V3 diff = v3(m.diffuse[0], m.diffuse[1], m.diffuse[2]);
+    float T12 = roughTrans(m, wi.z);
+    float T21 = roughTrans(m, wo.z);
+    diff = divs(diff, 1 - m.fdr);
+    result = result + diff * (kInvPi * wo.z * T12 * T21 * m.invEta2);
+    return result;
+}
+
+/* sampleM (:582-592) */
+HD float sampleM(float v, float sinThetaI, float cosThetaI, float xi1, float xi2) {
+    float cosTheta = 1.0f + v * logf(xi1 + (1.0f - xi1) * expf(-2.0f / v));
+    float sinTheta = trigInverse(cosTheta);
+    float cosPhi = cosf(2 * kPi * xi2);
+    return -cosTheta * sinThetaI + sinTheta * cosPhi * cosThetaI;
+}
+
+/* MarschnerDiffuse::sample (:594-744); pdf() == 1 (:517-520) */
+HD V3 marschnerSample(const HptMarschner &m, V3 wi, float sx, float sy, V3 &wo, uint32_t &type) {
+    float sinThetaI = wi.y;
+    float cosThetaI = trigInverse(sinThetaI);
+    float thetaI = asinf(clampf(sinThetaI, -1.0f, 1.0f));
+    float thetaIR = thetaI - 2.0f * m.scaleAngleRad;
+    float thetaITT = thetaI + m.scaleAngleRad;
+    float thetaITRT = thetaI + 4.0f * m.scaleAngleRad;
+    float weightR = azWeight(m.sums[0], cosThetaI);
+    float weightTT = azWeight(m.sums[1], cosThetaI);
+    float weightTRT = azWeight(m.sums[2], cosThetaI);
+    int lobe;
+    float v, theta;
+    float target = sx * (weightR + weightTT + weightTRT);
+    if (target < weightR) {
+        lobe = 0; v = m.vR; theta = thetaIR;
+    } else if (target < weightR + weightTT) {
+        lobe = 1; v = m.vTT; theta = thetaITT;
+    } else {
+        lobe = 2; v = m.vTRT; theta = thetaITRT;
+    }
+    float sinThetaO = sampleM(v, sinf(theta), cosf(theta), sx, sy);
+    float cosThetaO = trigInverse(sinThetaO);
+    float thetaO = asinf(clampf(sinThetaO, -1.0f, 1.0f));
+    float thetaD = (thetaO - thetaI) * 0.5f;
+    float cosThetaD = cosf(thetaD);
+    float phi = azSample(m.cdf[lobe], cosThetaD, sy);
+    float sinPhi = sinf(phi), cosPhi = cosf(phi);
+    float probSpecular = 1 - roughTrans(m, wi.z);
+    float w = m.specularSamplingWeight;
+    probSpecular = (probSpecular * w) / (probSpecular * w + (1 - probSpecular) * (1 - w));
+    if (sy < probSpecular) {
+        wo = v3(sinPhi * cosThetaO, sinThetaO, cosPhi * cosThetaO);
+        type = HPT_EDELTA_REFLECTION;
+    } else {
+        type = HPT_EDIFFUSE_REFLECTION;
+        wo = squareToCosineHemisphere(sx, sy);
+    }
+    V3 e = marschnerEval(m, wi, wo);
+    return divs(e, 1.0f);
+}
+
+/* ------------------------------------------------------------------ */
+/* Kajiya-Kay (kajiyakay.cpp:122-265)                                   */
+/* ------------------------------------------------------------------ */
+HD V3 kkEval(const HptKajiyaKay &k, V3 wi, V3 wo) {
+    if (wi.z <= 0 || wo.z <= 0) return v3(0, 0, 0);
+    V3 result = v3(0, 0, 0);
+    float tl = fabsf(wi.x), te = fabsf(wo.x);
+    float sin_tl = sqrtf(1 - tl * tl), sin_te = sqrtf(1 - te * te);
+    float a = tl * te + sin_tl * sin_te;
+    if (a > 0.0f && wi.x * wo.x < 0) {
+        V3 ks = v3(k.ks[0], k.ks[1], k.ks[2]);
+        V3 res = (ks * 0.15f) * ((k.exponent + 2) * kInvFourPi * powf(a, k.exponent));
+        result = result + res;
+    }
+    result = result + v3(k.kd[0], k.kd[1], k.kd[2]) * kInvPi;
+    return result * wo.z;
+}
+HD float kkPdf(const HptKajiyaKay &k, V3 wi, V3 wo) {
+    if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+    float diffuseProb = kInvPi * wo.z, specProb = 0.0f;
+    float a = dot(wo, v3(-wi.x, -wi.y, wi.z));
+    if (a > 0) specProb = powf(a, k.exponent) * (k.exponent + 1.0f) / (2.0f * kPi);
+    return k.specularSamplingWeight * specProb + (1 - k.specularSamplingWeight) * diffuseProb;
+}
+HD V3 kkSample(const HptKajiyaKay &k, V3 wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
+    bool choseSpecular = true;
+    if (sx <= k.specularSamplingWeight) {
+        sx /= k.specularSamplingWeight;
+    } else {
+        sx = (sx - k.specularSamplingWeight) / (1 - k.specularSamplingWeight);
+        choseSpecular = false;
+    }
+    if (choseSpecular) {
+        V3 R = v3(-wi.x, -wi.y, wi.z);
+        float sinAlpha = sqrtf(1 - powf(sy, 2 / (k.exponent + 1)));
+        float cosAlpha = powf(sy, 1 / (k.exponent + 1));
+        float phi = (2.0f * kPi) * sx;
+        V3 local = v3(sinAlpha * cosf(phi), sinAlpha * sinf(phi), cosAlpha);
+        Frame f;
+        f.n = R;
+        coordinateSystem(R, f.s, f.t);
+        wo = f.toWorld(local);
+        type = HPT_EGLOSSY_REFLECTION;
+        if (wo.z <= 0) {
+            pdf = 0.0f;
+            return v3(0, 0, 0);
+        }
+    } else {
+        wo = squareToCosineHemisphere(sx, sy);
+        type = HPT_EDIFFUSE_REFLECTION;
+    }
+    pdf = kkPdf(k, wi, wo);
+    if (pdf == 0) return v3(0, 0, 0);
+    return divs(kkEval(k, wi, wo), pdf);
+}
+
+HD V3 bsdfEval(const HptScene &sc, V3 wi, V3 wo) {
+    return sc.bsdfKind == 0 ? marschnerEval(sc.mar, wi, wo) : kkEval(sc.kk, wi, wo);
+}
+HD float bsdfPdf(const HptScene &sc, V3 wi, V3 wo) { return sc.bsdfKind == 0 ? 1.0f : kkPdf(sc.kk, wi, wo); }
+HD V3 bsdfSample(const HptScene &sc, V3 wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
+    if (sc.bsdfKind == 0) {
+        pdf = 1.0f;
+        return marschnerSample(sc.mar, wi, sx, sy, wo, type);
+    }
+    return kkSample(sc.kk, wi, sx, sy, wo, pdf, type);
+}
+
+/* ------------------------------------------------------------------ */
+/* Environment map (envmap.cpp)                                         */
+/* ------------------------------------------------------------------ */
+HD V3 texel(const HptEnvMap &e, int x, int y) { /* mipmap.h:503-563: u repeat, v clamp */
+    if (x < 0 || x >= e.w) {
+        int r = x % e.w;
+        x = (r < 0) ? r + e.w : r;
+    }
+    if (y < 0 || y >= e.h) y = clampi(y, 0, e.h - 1);
+    HptF4 t = e.texel[y * e.w + x];
+    return v3(t.x, t.y, t.z);
+}
+HD V3 envToLocal(const HptEnvMap &e, V3 v) {
+    if (e.identity) return v;
+    return v3(e.minv[0] * v.x + e.minv[1] * v.y + e.minv[2] * v.z, e.minv[3] * v.x + e.minv[4] * v.y + e.minv[5] * v.z,
+              e.minv[6] * v.x + e.minv[7] * v.y + e.minv[8] * v.z);
+}
+HD V3 envToWorld(const HptEnvMap &e, V3 v) {
+    if (e.identity) return v;
+    return v3(e.m[0] * v.x + e.m[1] * v.y + e.m[2] * v.z, e.m[3] * v.x + e.m[4] * v.y + e.m[5] * v.z,
+              e.m[6] * v.x + e.m[7] * v.y + e.m[8] * v.z);
+}
+/* evalEnvironment (:380-410) with the level-0 bilinear lookup (mipmap.h:575-596) */
+HD V3 envEval(const HptEnvMap &e, V3 dir) {
+    V3 v = envToLocal(e, dir);
+    float uvx = atan2f(v.x, -v.z) * kInvTwoPi, uvy = acosf(fminr(1.0f, fmaxr(-1.0f, v.y))) * kInvPi;
+    V3 value;
+    if (!isfinite(uvx) || !isfinite(uvy)) {
+        value = v3(0, 0, 0);
+    } else {
+        float u = uvx * e.w - 0.5f, vv = uvy * e.h - 0.5f;
+        int xPos = (int) floorf(u), yPos = (int) floorf(vv);
+        float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = vv - yPos, dy2 = 1.0f - dy1;
+        value = texel(e, xPos, yPos) * dx2 * dy2 + texel(e, xPos, yPos + 1) * dx2 * dy1 +
+                texel(e, xPos + 1, yPos) * dx1 * dy2 + texel(e, xPos + 1, yPos + 1) * dx1 * dy1;
+    }
+    return value * e.scale;
+}
+/* internalPdfDirection (:603-633) */
+HD float envPdf(const HptEnvMap &e, V3 d) {
+    float uvx = atan2f(d.x, -d.z) * kInvTwoPi, uvy = acosf(fminr(1.0f, fmaxr(-1.0f, d.y))) * kInvPi;
+    if (!isfinite(uvx) || !isfinite(uvy)) return 0.0f;
+    float u = uvx * e.w - 0.5f, v = uvy * e.h - 0.5f;
+    int xPos = (int) floorf(u), yPos = (int) floorf(v);
+    float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = v - yPos, dy2 = 1.0f - dy1;
+    V3 value1 = texel(e, xPos, yPos) * dx2 * dy2 + texel(e, xPos + 1, yPos) * dx1 * dy2;
+    V3 value2 = texel(e, xPos, yPos + 1) * dx2 * dy1 + texel(e, xPos + 1, yPos + 1) * dx1 * dy1;
+    float sinTheta = sqrtf(fmaxr(0.0f, 1 - d.y * d.y));
+    return (lum(value1) * e.rowWeights[clampi(yPos, 0, e.h - 1)] +
+            lum(value2) * e.rowWeights[clampi(yPos + 1, 0, e.h - 1)]) *
+           e.normalization / fmaxr(fabsf(sinTheta), kEpsilon);
+}
+/* sampleReuse (:657-662): std::lower_bound + rescale */
+HD uint32_t sampleReuse(const float *cdf, uint32_t size, float &sample) {
+    uint32_t lo = 0, n = size + 1;
+    while (n > 0) { /* first entry >= sample */
+        uint32_t half = n >> 1;
+        if (cdf[lo + half] < sample) {
+            lo += half + 1;
+            n -= half + 1;
+        } else {
+            n = half;
+        }
+    }
+    int idx = (int) lo - 1;
+    uint32_t index = (uint32_t) imax(0, idx);
+    if (index > size - 1) index = size - 1;
+    sample = (sample - cdf[index]) / (cdf[index + 1] - cdf[index]);
+    return index;
+}
+/* internalSampleDirection (:567-600) */
+HD void envSampleDir(const HptEnvMap &e, float sx, float sy, V3 &d, V3 &value, float &pdf) {
+    uint32_t row = sampleReuse(e.cdfRows, (uint32_t) e.h, sy);
+    uint32_t col = sampleReuse(e.cdfCols + row * (e.w + 1), (uint32_t) e.w, sx);
+    float posx = (float) col + intervalToTent(sx), posy = (float) row + intervalToTent(sy);
+    int xPos = (int) floorf(posx), yPos = (int) floorf(posy);
+    float dx1 = posx - xPos, dx2 = 1.0f - dx1, dy1 = posy - yPos, dy2 = 1.0f - dy1;
+    V3 value1 = texel(e, xPos, yPos) * dx2 * dy2 + texel(e, xPos + 1, yPos) * dx1 * dy2;
+    V3 value2 = texel(e, xPos, yPos + 1) * dx2 * dy1 + texel(e, xPos + 1, yPos + 1) * dx1 * dy1;
+    value = (value1 + value2) * e.scale;
+    pdf = (lum(value1) * e.rowWeights[clampi(yPos, 0, e.h - 1)] +
+           lum(value2) * e.rowWeights[clampi(yPos + 1, 0, e.h - 1)]) *
+          e.normalization;
+    float sinPhi = sinf(e.pixelSizeX * (posx + 0.5f)), cosPhi = cosf(e.pixelSizeX * (posx + 0.5f));
+    float sinTheta = sinf(e.pixelSizeY * (posy + 0.5f)), cosTheta = cosf(e.pixelSizeY * (posy + 0.5f));
+    d = v3(sinPhi * sinTheta, cosTheta, -cosPhi * sinTheta);
+    pdf /= fmaxr(fabsf(sinTheta), kEpsilon);
+}
+HD bool bsphereIntersect(const HptEnvMap &e, V3 o, V3 d, float &nearT, float &farT) { /* bsphere.h:88-95 */
+    V3 oo = o - v3(e.bsCenter[0], e.bsCenter[1], e.bsCenter[2]);
+    float A = dot(d, d);
+    float B = 2 * dot(oo, d);
+    float C = dot(oo, oo) - e.bsRadius * e.bsRadius;
+    return solveQuadratic(A, B, C, nearT, farT);
+}
+
+HD float miWeight(float pdfA, float pdfB) { /* path.cpp:296-300 */
+    pdfA *= pdfA;
+    pdfB *= pdfB;
+    return pdfA / (pdfA + pdfB);
+}
+
+/* adaptive ray epsilon: skdtree.cpp:126-129 (closest) / :213-216 (shadow) */
+HD float adaptiveMint(V3 o, float mint, bool shadow) {
+    if (mint != kEpsilon) return mint;
+    float m = fmaxr(fmaxr(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    if (!shadow) m = fmaxr(m, kEpsilon);
+    return mint * m;
+}
+
+/* append to a queue: one atomic per wave (wave64 ballot + mbcnt) */
+HD void qpush(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
+    uint64_t mask = __ballot(pred);
+    if (mask == 0) return;
+    uint32_t lane = __lane_id();
+    uint32_t leader = __ffsll((unsigned long long) mask) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(counter, (uint32_t) __popcll(mask));
+    base = __shfl(base, leader);
+    if (pred) {
+        uint64_t below = mask & ((1ull << lane) - 1ull);
+        queue[base + __popcll(below)] = value;
+    }
+}
+
+} // namespace
+
+/* ================================================================== */
+/* Kernels                                                             */
+/* ================================================================== */
+
+/* Decode a path id of the current wave: id = slot * nSpp + (j - sppBegin),
+   slot enumerates the 32x32 blocks owned by this shard in block order. */
+HD bool decodePath(const HptWave &w, uint32_t id, int &px, int &py, uint32_t &j) {
+    uint32_t slot = id / w.nSpp;
+    j = w.sppBegin + (id - slot * w.nSpp);
+    uint32_t lb = slot >> 10, inner = slot & 1023u;
+    uint32_t b = lb * w.nShards + w.shard;
+    px = (int) ((b % w.nbx) * HPT_BLOCK + (inner & 31u));
+    py = (int) ((b / w.nbx) * HPT_BLOCK + (inner >> 5));
+    return px < w.width && py < w.height;
+}
+
+extern "C" __global__ __launch_bounds__(256) void k_camera(HptScene sc, HptWave w, HptPaths P,
+                                                            uint32_t *__restrict__ traceQ,
+                                                            uint32_t *__restrict__ counters) {
+    uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
+    bool valid = id < w.nPaths;
+    int px = 0, py = 0;
+    uint32_t j = 0;
+    if (valid) valid = decodePath(w, id, px, py, j);
+    if (valid) {
+        const HptCamera &c = sc.cam;
+        uint64_t sidx = (c.logRes > 1) ? sobolLookUp(sc, c.logRes, j, (uint32_t) px, (uint32_t) py) : (uint64_t) j;
+        float ox, oy;
+        if (sidx != (uint64_t) j) {
+            ox = sobolSample(sc, sidx, 0) * c.resolution - px;
+            oy = sobolSample(sc, sidx, 1) * c.resolution - py;
+        } else {
+            ox = sobolSample(sc, sidx, 0);
+            oy = sobolSample(sc, sidx, 1);
+        }
+        float posx = px + ox, posy = py + oy;
+        V3 nearP = xformPoint(c.s2c, v3(posx * c.invResX, posy * c.invResY, 0.0f));
+        V3 d = normalize(nearP);
+        float invZ = 1.0f / d.z;
+        const float *T = c.toWorld;
+        V3 o = v3(T[0] * 0.0f + T[1] * 0.0f + T[2] * 0.0f + T[3], T[4] * 0.0f + T[5] * 0.0f + T[6] * 0.0f + T[7],
+                  T[8] * 0.0f + T[9] * 0.0f + T[10] * 0.0f + T[11]);
+        V3 dw = xformVector(T, d);
+        P.ro[id] = make_float4(o.x, o.y, o.z, c.nearClip * invZ);
+        P.rd[id] = make_float4(dw.x, dw.y, dw.z, c.farClip * invZ);
+        P.pos[id] = make_float2(posx, posy);
+        P.sobol[id] = sidx;
+        P.state[id] = 2u | (1u << 16); /* dim = 2, depth = 1 */
+        P.thr[id] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+        P.li[id] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    } else if (id < w.nPaths) {
+        P.state[id] = 0xffffffffu; /* outside the image */
+        P.li[id] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    }
+    qpush(valid, id, traceQ, &counters[HPT_Q_TRACE]);
+}
+
+/* closest-hit for traceQ[0, nTrace) and any-hit shadow rays for shadowQ */
+template <int STACK>
+__device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ,
+                                          const uint32_t *shadowQ, const uint32_t *counters, uint2 *stk,
+                                          int stride, uint32_t *stats) {
+    const uint32_t nTrace = counters[HPT_Q_TRACE], nShadow = counters[HPT_Q_SHADOW];
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t nNodes = 0, nPrims = 0, nU = 0;
+    if (tid < nTrace) {
+        const uint32_t id = traceQ[tid];
+        float4 ro = P.ro[id], rd = P.rd[id];
+        V3 o = v3(ro.x, ro.y, ro.z), d = v3(rd.x, rd.y, rd.z);
+        V3 rcp = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        float mint, maxt;
+        float rmint = ro.w, rmaxt = rd.w;
+        int32_t seg = -1;
+        float thit = finf();
+        D3 p = d3(0, 0, 0);
+        if (aabbIntersect(sc, o, d, rcp, mint, maxt)) {
+            float rayMinT = adaptiveMint(o, rmint, false);
+            if (rayMinT > mint) mint = rayMinT;
+            if (rmaxt < maxt) maxt = rmaxt;
+            if (maxt > mint) {
+                float t;
+                uint32_t s = 0;
+                if (traverse<STACK, false>(sc, o, d, rcp, mint, maxt, stk, stride, t, s, p, nNodes, nPrims)) {
+                    seg = (int32_t) s;
+                    thit = t;
+                }
+            }
+        }
+        P.hit[id] = make_float4(__int_as_float(seg), thit, 0.0f, 0.0f);
+        P.hitp[id] = make_float4((float) p.x, (float) p.y, (float) p.z, 0.0f);
+    } else if (tid < nTrace + nShadow) {
+        const uint32_t id = shadowQ[tid - nTrace];
+        float4 ro = P.ro[id], sd = P.sdir[id];
+        V3 o = v3(ro.x, ro.y, ro.z), d = v3(sd.x, sd.y, sd.z);
+        V3 rcp = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+        float mint, maxt;
+        bool occluded = false;
+        if (aabbIntersect(sc, o, d, rcp, mint, maxt)) {
+            float rayMinT = adaptiveMint(o, kEpsilon, true);
+            if (rayMinT > mint) mint = rayMinT;
+            if (sd.w < maxt) maxt = sd.w;
+            if (maxt > mint) {
+                float t;
+                uint32_t s;
+                D3 p;
+                occluded = traverse<STACK, true>(sc, o, d, rcp, mint, maxt, stk, stride, t, s, p, nNodes, nPrims);
+            }
+        }
+        if (!occluded) {
+            nU = 1;
+            float4 c = P.scontrib[id], l = P.li[id];
+            P.li[id] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
+        }
+    }
+    if (stats) {
+        /* traversal counters for the algorithmic byte model:
+           [0] node visits [1] primitive tests [2] closest rays [3] shadow rays
+           [4] unoccluded shadow rays; per-wave reduction, one atomic each */
+        uint32_t nC = tid < nTrace ? 1u : 0u, nS = (tid >= nTrace && tid < nTrace + nShadow) ? 1u : 0u;
+        for (int off = 32; off > 0; off >>= 1) {
+            nNodes += __shfl_down(nNodes, off);
+            nPrims += __shfl_down(nPrims, off);
+            nC += __shfl_down(nC, off);
+            nS += __shfl_down(nS, off);
+            nU += __shfl_down(nU, off);
+        }
+        if (__lane_id() == 0 && (nC | nS)) {
+            unsigned long long *st = (unsigned long long *) stats;
+            atomicAdd(&st[0], (unsigned long long) nNodes);
+            atomicAdd(&st[1], (unsigned long long) nPrims);
+            atomicAdd(&st[2], (unsigned long long) nC);
+            atomicAdd(&st[3], (unsigned long long) nS);
+            atomicAdd(&st[4], (unsigned long long) nU);
+        }
+    }
+}
+
+#define HPT_TRACE_BLOCK 128
+#define HPT_STACK 32
+
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace(HptScene sc, HptPaths P,
+                                                                      const uint32_t *__restrict__ traceQ,
+                                                                      const uint32_t *__restrict__ shadowQ,
+                                                                      const uint32_t *__restrict__ counters,
+                                                                      uint32_t *stats) {
+    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    traceBody<HPT_STACK>(sc, P, traceQ, shadowQ, counters, stk + threadIdx.x, HPT_TRACE_BLOCK, stats);
+}
+
+/* fill the intersection record: hair.cpp:825-862 + skdtree.h:422-427 */
+HD void fillIts(const HptScene &sc, uint32_t seg, V3 hp, V3 rayD, V3 &p, Frame &geo, Frame &sh, V3 &wi) {
+    const double *rec = reinterpret_cast<const double *>(sc.segs + seg);
+    V3 v1 = v3((float) rec[0], (float) rec[1], (float) rec[2]);
+    V3 v2 = v3((float) rec[12], (float) rec[13], (float) rec[14]);
+    V3 axis = normalize(v2 - v1);
+    geo.s = axis;
+    V3 rel = hp - v1;
+    geo.n = normalize(rel - axis * dot(axis, rel));
+    geo.t = cross(geo.n, geo.s);
+    V3 local = geo.toLocal(rel);
+    p = hp + geo.n * (sc.radius - sqrtf(local.y * local.y + local.z * local.z));
+    sh.n = geo.n;
+    sh.s = normalize(geo.s - sh.n * dot(sh.n, geo.s));
+    sh.t = cross(sh.n, sh.s);
+    wi = sh.toLocal(-rayD);
+}
+
+/* primary hits / misses (path.cpp:128-143) */
+extern "C" __global__ __launch_bounds__(256) void k_primary(HptScene sc, HptPaths P,
+                                                             const uint32_t *__restrict__ traceQ,
+                                                             uint32_t *__restrict__ shadeQ,
+                                                             uint32_t *__restrict__ counters) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = counters[HPT_Q_TRACE];
+    bool alive = false;
+    uint32_t id = 0;
+    if (tid < n) {
+        id = traceQ[tid];
+        float4 h = P.hit[id];
+        if (__float_as_int(h.x) >= 0) {
+            alive = true;
+        } else if (!sc.hideEmitters) {
+            float4 rd = P.rd[id];
+            V3 L = envEval(sc.env, v3(rd.x, rd.y, rd.z)); /* throughput == 1 */
+            V3 T = v3(1.0f, 1.0f, 1.0f);
+            V3 c = mul(T, L);
+            P.li[id] = make_float4(0.0f + c.x, 0.0f + c.y, 0.0f + c.z, 0.0f);
+        }
+    }
+    qpush(alive, id, shadeQ, &counters[HPT_Q_SHADE_OUT]);
+}
+
+/* one bounce of shading: path.cpp:145-232 up to the continuation ray cast */
+extern "C" __global__ __launch_bounds__(256) void k_shade(HptScene sc, HptPaths P,
+                                                           const uint32_t *__restrict__ shadeQ,
+                                                           uint32_t *__restrict__ traceQ,
+                                                           uint32_t *__restrict__ shadowQ,
+                                                           uint32_t *__restrict__ counters) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = counters[HPT_Q_SHADE_IN];
+    bool cont = false, shadow = false;
+    uint32_t id = 0;
+    if (tid < n) {
+        id = shadeQ[tid];
+        uint32_t st = P.state[id];
+        uint32_t dim = st & 0xffffu, depth = (st >> 16) & 0xffu;
+        float4 h = P.hit[id], hp = P.hitp[id], rd = P.rd[id];
+        V3 rayD = v3(rd.x, rd.y, rd.z);
+        V3 p, wi;
+        Frame geo, sh;
+        fillIts(sc, (uint32_t) __float_as_int(h.x), v3(hp.x, hp.y, hp.z), rayD, p, geo, sh, wi);
+        bool stop = ((int) depth >= sc.maxDepth && sc.maxDepth > 0) ||
+                    (sc.strictNormals && dot(rayD, geo.n) * wi.z >= 0);
+        if (!stop && dim + 3 >= HPT_SOBOL_DIMS) {
+            /* sobol.cpp:236-238 raises "Lookup dimension exceeds the direction number table size" */
+            atomicOr(&counters[HPT_Q_ERROR], 1u);
+            stop = true;
+        }
+        if (!stop) {
+            const uint64_t sidx = P.sobol[id];
+            float4 thr = P.thr[id];
+            V3 T = v3(thr.x, thr.y, thr.z);
+            /* ---- direct illumination (scene.cpp:828-852, envmap.cpp:516-543) ---- */
+            float nx = sobolSample(sc, sidx, dim), ny = sobolSample(sc, sidx, dim + 1);
+            dim += 2;
+            {
+                V3 dl, value;
+                float pdf;
+                envSampleDir(sc.env, nx, ny, dl, value, pdf);
+                V3 dW = envToWorld(sc.env, dl);
+                float nearT, farT;
+                if (!(isZero(value) || pdf == 0 || !bsphereIntersect(sc.env, p, dW, nearT, farT) || nearT >= 0 ||
+                      farT <= 0)) {
+                    V3 val = divs(value, pdf);
+                    V3 wo = sh.toLocal(dW);
+                    V3 bsdfVal = bsdfEval(sc, wi, wo);
+                    if (!isZero(bsdfVal) && (!sc.strictNormals || dot(geo.n, dW) * wo.z > 0)) {
+                        float bp = bsdfPdf(sc, wi, wo);
+                        float weight = miWeight(pdf, bp);
+                        V3 c = mul(mul(T, val), bsdfVal) * weight;
+                        P.sdir[id] = make_float4(dW.x, dW.y, dW.z, farT * (1 - kShadowEpsilon));
+                        P.scontrib[id] = make_float4(c.x, c.y, c.z, 0.0f);
+                        shadow = true;
+                    }
+                }
+            }
+            /* ---- BSDF sampling ---- */
+            float bx = sobolSample(sc, sidx, dim), by = sobolSample(sc, sidx, dim + 1);
+            dim += 2;
+            V3 woL;
+            float bpdf = 0.0f;
+            uint32_t type = 0;
+            V3 w = bsdfSample(sc, wi, bx, by, woL, bpdf, type);
+            if (!isZero(w)) {
+                V3 wo = sh.toWorld(woL);
+                float woDotGeoN = dot(geo.n, wo);
+                if (!(sc.strictNormals && woDotGeoN * woL.z <= 0)) {
+                    P.ro[id] = make_float4(p.x, p.y, p.z, kEpsilon);
+                    P.rd[id] = make_float4(wo.x, wo.y, wo.z, finf());
+                    P.bw[id] = make_float4(w.x, w.y, w.z, bpdf);
+                    cont = true;
+                    st = (st & 0x00ffffffu) | (type << 24);
+                }
+            }
+            if (shadow && !cont) P.ro[id] = make_float4(p.x, p.y, p.z, kEpsilon);
+        }
+        P.state[id] = (st & 0xffff0000u) | dim;
+    }
+    qpush(cont, id, traceQ, &counters[HPT_Q_TRACE]);
+    qpush(shadow, id, shadowQ, &counters[HPT_Q_SHADOW]);
+}
+
+/* continuation result: path.cpp:225-286 */
+extern "C" __global__ __launch_bounds__(256) void k_post(HptScene sc, HptPaths P,
+                                                          const uint32_t *__restrict__ traceQ,
+                                                          uint32_t *__restrict__ shadeQ,
+                                                          uint32_t *__restrict__ counters) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = counters[HPT_Q_TRACE];
+    bool alive = false;
+    uint32_t id = 0;
+    if (tid < n) {
+        id = traceQ[tid];
+        uint32_t st = P.state[id];
+        uint32_t dim = st & 0xffffu, depth = (st >> 16) & 0xffu, type = st >> 24;
+        float4 h = P.hit[id], bw = P.bw[id], thr = P.thr[id], rd = P.rd[id];
+        bool hit = __float_as_int(h.x) >= 0;
+        V3 T = v3(thr.x, thr.y, thr.z);
+        bool done = false, hitEmitter = false;
+        V3 value = v3(0, 0, 0);
+        V3 d = v3(rd.x, rd.y, rd.z);
+        if (!hit) {
+            /* path.cpp:239: 'hideEmitters && !scattered' never holds here -- every
+               sampled type of marschner / kajiyakay differs from ENull */
+            value = envEval(sc.env, d);
+            float4 ro = P.ro[id];
+            float nearT, farT;
+            if (!bsphereIntersect(sc.env, v3(ro.x, ro.y, ro.z), d, nearT, farT) || nearT > 0 || farT < 0) {
+                done = true;
+                hitEmitter = false;
+            } else {
+                hitEmitter = true;
+            }
+        }
+        if (!(done && !hitEmitter)) {
+            T = mul(T, v3(bw.x, bw.y, bw.z));
+            if (hitEmitter) {
+                float lumPdf = (!(type & HPT_EDELTA)) ? envPdf(sc.env, envToLocal(sc.env, d)) : 0.0f;
+                V3 c = mul(T, value) * miWeight(bw.w, lumPdf);
+                float4 l = P.li[id];
+                P.li[id] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
+            }
+            if (hit) {
+                alive = true;
+                if ((int) depth >= sc.rrDepth && dim >= HPT_SOBOL_DIMS) {
+                    atomicOr(&counters[HPT_Q_ERROR], 1u);
+                    alive = false;
+                } else if ((int) depth >= sc.rrDepth) {
+                    float q = fminr(maxc(T) * 1.0f * 1.0f, 0.95f);
+                    float u = sobolSample(sc, P.sobol[id], dim);
+                    dim += 1;
+                    if (u >= q) alive = false;
+                    else T = divs(T, q);
+                }
+                depth += 1;
+                P.thr[id] = make_float4(T.x, T.y, T.z, 0.0f);
+                P.state[id] = (st & 0xff000000u) | (depth << 16) | dim;
+            }
+        }
+    }
+    qpush(alive, id, shadeQ, &counters[HPT_Q_SHADE_OUT]);
+}
+
+/* Deterministic film gather (imageblock.h:124-204 + renderproc.cpp:142-145):
+   every pixel sums, in a fixed order, the tent-weighted samples of its 3x3
+   neighbour pixels that belong to this shard and this wave.  Weights use
+   the sample's block-relative coordinates exactly like ImageBlock::put. */
+extern "C" __global__ __launch_bounds__(256) void k_gather(HptScene sc, HptWave w, HptPaths P, float4 *film) {
+    const uint32_t pix = blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= (uint32_t) (w.width * w.height)) return;
+    const int x = (int) (pix % (uint32_t) w.width), y = (int) (pix / (uint32_t) w.width);
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    bool any = false;
+    for (int qy = y - 1; qy <= y + 1; ++qy) {
+        if (qy < 0 || qy >= w.height) continue;
+        for (int qx = x - 1; qx <= x + 1; ++qx) {
+            if (qx < 0 || qx >= w.width) continue;
+            const int bx = qx / HPT_BLOCK, by = qy / HPT_BLOCK;
+            const uint32_t b = (uint32_t) (by * w.nbx + bx);
+            if ((int) (b % w.nShards) != w.shard) continue;
+            const uint32_t slot = ((b / w.nShards) << 10) | ((uint32_t) (qy & 31) << 5) | (uint32_t) (qx & 31);
+            const float ox = (float) (bx * HPT_BLOCK - 1), oy = (float) (by * HPT_BLOCK - 1);
+            const float xr = (float) (x - (bx * HPT_BLOCK - 1)), yr = (float) (y - (by * HPT_BLOCK - 1));
+            for (uint32_t jj = 0; jj < w.nSpp; ++jj) {
+                const uint32_t id = slot * w.nSpp + jj;
+                float4 l = P.li[id];
+                if (!(isfinite(l.x) && isfinite(l.y) && isfinite(l.z)) || l.x < 0 || l.y < 0 || l.z < 0) continue;
+                float2 ps = P.pos[id];
+                const float rx = ps.x - 0.5f - ox, ry = ps.y - 0.5f - oy;
+                /* inside [ceil(r-1), floor(r+1)] <=> |xr - r| <= 1 up to the LUT's zero tail */
+                const float dx = xr - rx, dy = yr - ry;
+                if (xr < ceilf(rx - 1.0f) || xr > floorf(rx + 1.0f) || yr < ceilf(ry - 1.0f) || yr > floorf(ry + 1.0f))
+                    continue;
+                const float wx = sc.tent[imin((int) fabsf(dx * sc.tentScale), HPT_FILTER_RES)];
+                const float wy = sc.tent[imin((int) fabsf(dy * sc.tentScale), HPT_FILTER_RES)];
+                const float wgt = wx * wy;
+                acc[0] += wgt * l.x;
+                acc[1] += wgt * l.y;
+                acc[2] += wgt * l.z;
+                acc[3] += wgt * 1.0f;
+                any = true;
+            }
+        }
+    }
+    if (any) {
+        float4 f = film[pix];
+        film[pix] = make_float4(f.x + acc[0], f.y + acc[1], f.z + acc[2], f.w + acc[3]);
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* Batch entry points for unit parity tests                             */
+/* ------------------------------------------------------------------ */
+extern "C" __global__ void k_sobol_batch(HptScene sc, int m, int n, const uint32_t *frame, const uint32_t *px,
+                                         const uint32_t *py, const uint32_t *dim, uint64_t *outIdx, float *outVal) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t idx = (m > 1) ? sobolLookUp(sc, (uint32_t) m, frame[i], px[i], py[i]) : (uint64_t) frame[i];
+    outIdx[i] = idx;
+    outVal[i] = sobolSample(sc, idx, dim[i]);
+}
+
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptScene sc, int n, const float *o,
+                                                                            const float *d, const float *mint,
+                                                                            const float *maxt, int shadow,
+                                                                            float *outT, int32_t *outSeg,
+                                                                            float *outP, uint8_t *outHit) {
+    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    V3 oo = v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), dd = v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
+    V3 rcp = v3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
+    float mn, mx;
+    uint32_t nn = 0, np = 0;
+    bool ok = false;
+    float t = finf();
+    uint32_t s = 0;
+    D3 p = d3(0, 0, 0);
+    if (aabbIntersect(sc, oo, dd, rcp, mn, mx)) {
+        float rayMinT = adaptiveMint(oo, mint[i], shadow != 0);
+        if (rayMinT > mn) mn = rayMinT;
+        if (maxt[i] < mx) mx = maxt[i];
+        if (mx > mn) {
+            if (shadow)
+                ok = traverse<HPT_STACK, true>(sc, oo, dd, rcp, mn, mx, stk + threadIdx.x, HPT_TRACE_BLOCK, t, s, p, nn, np);
+            else
+                ok = traverse<HPT_STACK, false>(sc, oo, dd, rcp, mn, mx, stk + threadIdx.x, HPT_TRACE_BLOCK, t, s, p, nn, np);
+        }
+    }
+    if (shadow) {
+        outHit[i] = ok ? 1 : 0;
+    } else {
+        outT[i] = ok ? t : finf();
+        outSeg[i] = ok ? (int32_t) s : -1;
+        outP[3 * i] = ok ? (float) p.x : 0.0f;
+        outP[3 * i + 1] = ok ? (float) p.y : 0.0f;
+        outP[3 * i + 2] = ok ? (float) p.z : 0.0f;
+    }
+}
+
+extern "C" __global__ void k_bsdf_batch(HptScene sc, int n, const float *wi, const float *wo, const float *u,
+                                        float *outEval, float *outPdf, float *outWo, float *outW, float *outSPdf,
+                                        uint32_t *outType) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    V3 a = v3(wi[3 * i], wi[3 * i + 1], wi[3 * i + 2]), b = v3(wo[3 * i], wo[3 * i + 1], wo[3 * i + 2]);
+    V3 e = bsdfEval(sc, a, b);
+    outEval[3 * i] = e.x;
+    outEval[3 * i + 1] = e.y;
+    outEval[3 * i + 2] = e.z;
+    outPdf[i] = bsdfPdf(sc, a, b);
+    V3 so;
+    float pdf = 0;
+    uint32_t type = 0;
+    V3 w = bsdfSample(sc, a, u[2 * i], u[2 * i + 1], so, pdf, type);
+    outWo[3 * i] = so.x;
+    outWo[3 * i + 1] = so.y;
+    outWo[3 * i + 2] = so.z;
+    outW[3 * i] = w.x;
+    outW[3 * i + 1] = w.y;
+    outW[3 * i + 2] = w.z;
+    outSPdf[i] = pdf;
+    outType[i] = type;
+}
+
+extern "C" __global__ void k_env_batch(HptScene sc, int n, const float *refp, const float *u, const float *dq,
+                                       float *outD, float *outV, float *outPdf, float *outDist, float *outEval,
+                                       float *outEvalPdf) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    V3 dl, value;
+    float pdf;
+    envSampleDir(sc.env, u[2 * i], u[2 * i + 1], dl, value, pdf);
+    V3 dW = envToWorld(sc.env, dl);
+    V3 ref = v3(refp[3 * i], refp[3 * i + 1], refp[3 * i + 2]);
+    float nearT, farT;
+    bool ok = !(isZero(value) || pdf == 0 || !bsphereIntersect(sc.env, ref, dW, nearT, farT) || nearT >= 0 || farT <= 0);
+    V3 v = ok ? divs(value, pdf) : v3(0, 0, 0);
+    outD[3 * i] = dW.x;
+    outD[3 * i + 1] = dW.y;
+    outD[3 * i + 2] = dW.z;
+    outV[3 * i] = v.x;
+    outV[3 * i + 1] = v.y;
+    outV[3 * i + 2] = v.z;
+    outPdf[i] = ok ? pdf : 0.0f;
+    outDist[i] = ok ? farT : 0.0f;
+    V3 q = v3(dq[3 * i], dq[3 * i + 1], dq[3 * i + 2]);
+    V3 e = envEval(sc.env, q);
+    outEval[3 * i] = e.x;
+    outEval[3 * i + 1] = e.y;
+    outEval[3 * i + 2] = e.z;
+    outEvalPdf[i] = envPdf(sc.env, envToLocal(sc.env, q));
+}
+
+/* tiny queue-rotation kernel: shade_in <- shade_out, reset the rest */
+extern "C" __global__ void k_rotate(uint32_t *counters) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        counters[HPT_Q_SHADE_IN] = counters[HPT_Q_SHADE_OUT];
+        counters[HPT_Q_SHADE_OUT] = 0;
+        counters[HPT_Q_TRACE] = 0;
+        counters[HPT_Q_SHADOW] = 0;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* host-side launch wrappers (declared in hpt_kernels.h)               */
+/* ------------------------------------------------------------------ */
+static inline unsigned blocksFor(uint64_t n, unsigned bs) { return (unsigned) ((n + bs - 1) / bs); }
+
+hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPaths &P, uint32_t *traceQ,
+                             uint32_t *counters, hipStream_t s) {
+    if (w.nPaths == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_camera, dim3(blocksFor(w.nPaths, 256)), dim3(256), 0, s, sc, w, P, traceQ, counters);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
+                            const uint32_t *counters, uint32_t *stats, uint64_t maxItems, hipStream_t s) {
+    if (maxItems == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_trace, dim3(blocksFor(maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ,
+                       shadowQ, counters, stats);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
+                              uint32_t *counters, uint64_t maxItems, hipStream_t s) {
+    if (maxItems == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_primary, dim3(blocksFor(maxItems, 256)), dim3(256), 0, s, sc, P, traceQ, shadeQ, counters);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *traceQ,
+                            uint32_t *shadowQ, uint32_t *counters, uint64_t maxItems, hipStream_t s) {
+    if (maxItems == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_shade, dim3(blocksFor(maxItems, 256)), dim3(256), 0, s, sc, P, shadeQ, traceQ, shadowQ,
+                       counters);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
+                           uint32_t *counters, uint64_t maxItems, hipStream_t s) {
+    if (maxItems == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_post, dim3(blocksFor(maxItems, 256)), dim3(256), 0, s, sc, P, traceQ, shadeQ, counters);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_rotate(uint32_t *counters, hipStream_t s) {
+    hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, s, counters);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *film, hipStream_t s) {
+    uint64_t n = (uint64_t) w.width * (uint64_t) w.height;
+    hipLaunchKernelGGL(k_gather, dim3(blocksFor(n, 256)), dim3(256), 0, s, sc, w, P, film);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_sobol_batch(const HptScene &sc, int m, int n, const uint32_t *frame, const uint32_t *px,
+                                  const uint32_t *py, const uint32_t *dim, uint64_t *oi, float *ov, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sobol_batch, dim3(blocksFor(n, 256)), dim3(256), 0, s, sc, m, n, frame, px, py, dim, oi, ov);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_trace_batch(const HptScene &sc, int n, const float *o, const float *d, const float *mint,
+                                  const float *maxt, int shadow, float *ot, int32_t *os, float *op, uint8_t *oh,
+                                  hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_trace_batch, dim3(blocksFor(n, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc, n, o, d,
+                       mint, maxt, shadow, ot, os, op, oh);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_bsdf_batch(const HptScene &sc, int n, const float *wi, const float *wo, const float *u,
+                                 float *oe, float *op, float *owo, float *ow, float *osp, uint32_t *ot, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_bsdf_batch, dim3(blocksFor(n, 256)), dim3(256), 0, s, sc, n, wi, wo, u, oe, op, owo, ow, osp,
+                       ot);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_env_batch(const HptScene &sc, int n, const float *refp, const float *u, const float *dq,
+                                float *od, float *ov, float *op, float *odist, float *oe, float *oep, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_env_batch, dim3(blocksFor(n, 256)), dim3(256), 0, s, sc, n, refp, u, dq, od, ov, op, odist,
+                       oe, oep);
+    return hipGetLastError();
+}

@@ -1,0 +1,317 @@
+"""ctypes binding of libhairpt.so (include/hairpt.h).
+
+This is the Python mirror of the reference's render entry points
+(SamplingIntegrator::render -> MIPathTracer::Li, src/librender/integrator.cpp
+:95-188, src/integrators/path/path.cpp:119-294).  There is no CPU fallback:
+if the HIP library is missing or no gfx950 device is present, every call
+raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG, "lib", "libhairpt.so")
+DATA_DIR = os.path.join(PKG, "data")
+HOST_ONLY = -1  # include/hairpt.h HPT_HOST_ONLY: build/export the scene without a device
+
+_f = C.POINTER(C.c_float)
+_u8 = C.POINTER(C.c_uint8)
+_u32 = C.POINTER(C.c_uint32)
+_i32 = C.POINTER(C.c_int32)
+_u64 = C.POINTER(C.c_uint64)
+_i64 = C.POINTER(C.c_int64)
+
+
+class SceneInfo(C.Structure):
+    _fields_ = [("width", C.c_int), ("height", C.c_int), ("spp", C.c_int), ("max_depth", C.c_int),
+                ("rr_depth", C.c_int), ("strict_normals", C.c_int), ("hide_emitters", C.c_int), ("bsdf", C.c_int),
+                ("vertices", C.c_uint64), ("segments", C.c_uint64), ("kd_nodes", C.c_uint64),
+                ("kd_indices", C.c_uint64), ("kd_depth", C.c_int), ("kd_build_seconds", C.c_double),
+                ("aabb_min", C.c_float * 3), ("aabb_max", C.c_float * 3), ("bsphere_center", C.c_float * 3),
+                ("bsphere_radius", C.c_float)]
+
+
+class RenderParams(C.Structure):
+    _fields_ = [("spp_begin", C.c_int), ("spp_end", C.c_int), ("shard", C.c_int), ("n_shards", C.c_int),
+                ("max_wave_paths", C.c_uint64), ("collect_stats", C.c_int)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("ms_total", C.c_double), ("ms_camera", C.c_double), ("ms_trace", C.c_double),
+                ("ms_primary", C.c_double), ("ms_shade", C.c_double), ("ms_post", C.c_double),
+                ("ms_gather", C.c_double), ("trace_launches", C.c_uint64), ("paths", C.c_uint64),
+                ("closest_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("nodes", C.c_uint64),
+                ("prims", C.c_uint64), ("bounces", C.c_uint64), ("shadow_unoccluded", C.c_uint64),
+                ("waves", C.c_uint64), ("max_bounces", C.c_int)]
+
+
+# every symbol declared in include/hairpt.h: (restype, argtypes)
+SIGNATURES = {
+    "hpt_context_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "hpt_context_destroy": (None, [C.c_void_p]),
+    "hpt_last_error": (C.c_char_p, [C.c_void_p]),
+    "hpt_set_data_dir": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "hpt_load_scene_xml": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]),
+    "hpt_set_camera": (C.c_int, [C.c_void_p, _f, C.c_float, C.c_int, C.c_int, C.c_float, C.c_float]),
+    "hpt_set_sampler": (C.c_int, [C.c_void_p, C.c_int]),
+    "hpt_set_integrator": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "hpt_set_hair_file": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_float, _f]),
+    "hpt_set_hair_vertices": (C.c_int, [C.c_void_p, _f, _u8, C.c_uint64, C.c_float]),
+    "hpt_set_bsdf_marschner": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_int, C.c_float, _f, _f]),
+    "hpt_set_bsdf_kajiyakay": (C.c_int, [C.c_void_p, _f, _f, C.c_float]),
+    "hpt_set_envmap_rgb": (C.c_int, [C.c_void_p, _f, C.c_int, C.c_int, C.c_float, _f]),
+    "hpt_set_sunsky": (C.c_int, [C.c_void_p, _f, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int]),
+    "hpt_prepare": (C.c_int, [C.c_void_p]),
+    "hpt_get_scene_info": (C.c_int, [C.c_void_p, C.POINTER(SceneInfo)]),
+    "hpt_render": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), _f]),
+    "hpt_render_device": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]),
+    "hpt_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+    "hpt_get_hair": (C.c_int64, [C.c_void_p, _f, _u8]),
+    "hpt_get_kdtree": (C.c_int, [C.c_void_p, _u32, _i64, _u32, _i64, _f]),
+    "hpt_get_envmap": (C.c_int, [C.c_void_p, _f, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "hpt_get_marschner_tables": (C.c_int, [C.c_void_p, _f, _f, _f, _f, _f, _f]),
+    "hpt_sobol_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u32, _u32, _u32, _u32, _u64, _f]),
+    "hpt_trace_batch": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f, C.c_int, _f, _i32, _f, _u8]),
+    "hpt_bsdf_batch": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f, _f, _f, _f, _u32]),
+    "hpt_env_batch": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f, _f, _f, _f, _f]),
+}
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libhairpt.so (raises OSError if it was not built -- no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(path):
+            raise OSError("libhairpt.so not built at %s (run __graft_entry__.build())" % path)
+        lib = C.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t) if a is not None else None
+
+
+def _f32(a, n=None):
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    return a
+
+
+class HairPTError(RuntimeError):
+    pass
+
+
+class Renderer:
+    """One HIP context on one MI355X (the drop-in for a Mitsuba render job)."""
+
+    def __init__(self, device: int = 0, data_dir: str = DATA_DIR):
+        self.lib = load_library()
+        h = C.c_void_p()
+        rc = self.lib.hpt_context_create(device, C.byref(h))
+        if rc != 0:
+            raise HairPTError("hpt_context_create(%d) failed (%d): no gfx950 device?" % (device, rc))
+        self.h = h
+        self._check(self.lib.hpt_set_data_dir(self.h, data_dir.encode()))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.hpt_context_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise HairPTError("hairpt error %d: %s" % (rc, self.lib.hpt_last_error(self.h).decode()))
+        return rc
+
+    # ---- scene ----
+    def load_scene_xml(self, path: str, defines: dict | None = None):
+        defines = defines or {}
+        keys = (C.c_char_p * max(1, len(defines)))(*[k.encode() for k in defines])
+        vals = (C.c_char_p * max(1, len(defines)))(*[str(v).encode() for v in defines.values()])
+        self._check(self.lib.hpt_load_scene_xml(self.h, path.encode(), len(defines), keys, vals))
+
+    def set_camera(self, to_world, fov_x, width, height, near=1e-2, far=1e4):
+        m = _f32(to_world).reshape(16)
+        self._check(self.lib.hpt_set_camera(self.h, _p(m, _f), fov_x, width, height, near, far))
+
+    def set_sampler(self, spp):
+        self._check(self.lib.hpt_set_sampler(self.h, spp))
+
+    def set_integrator(self, max_depth, rr_depth=5, strict_normals=True, hide_emitters=False):
+        self._check(self.lib.hpt_set_integrator(self.h, max_depth, rr_depth, int(strict_normals), int(hide_emitters)))
+
+    def set_hair_file(self, path, radius, angle_threshold=1.0):
+        self._check(self.lib.hpt_set_hair_file(self.h, path.encode(), radius, angle_threshold, None))
+
+    def set_hair_vertices(self, xyz, starts, radius):
+        xyz = _f32(xyz).reshape(-1, 3)
+        st = np.ascontiguousarray(starts, dtype=np.uint8)
+        self._check(self.lib.hpt_set_hair_vertices(self.h, _p(xyz, _f), _p(st, _u8), xyz.shape[0], radius))
+
+    def set_marschner(self, int_ior=1.55, ext_ior=1.0, distribution=1, alpha=0.2, diffuse=(0.5, 0.5, 0.5),
+                      specular=(0.5, 0.5, 0.5)):
+        d = _f32(diffuse)
+        s = _f32(specular)
+        self._check(self.lib.hpt_set_bsdf_marschner(self.h, int_ior, ext_ior, distribution, alpha, _p(d, _f), _p(s, _f)))
+
+    def set_kajiyakay(self, kd, ks=(0.2, 0.2, 0.2), exponent=30.0):
+        a = _f32(kd)
+        b = _f32(ks)
+        self._check(self.lib.hpt_set_bsdf_kajiyakay(self.h, _p(a, _f), _p(b, _f), exponent))
+
+    def set_envmap(self, rgb, scale=1.0):
+        rgb = _f32(rgb)
+        h, w = rgb.shape[:2]
+        self._check(self.lib.hpt_set_envmap_rgb(self.h, _p(rgb, _f), w, h, scale, None))
+
+    def set_sunsky(self, sun_dir, turbidity=3.0, sky_scale=1.0, sun_scale=1.0, sun_radius_scale=1.0, resolution=512):
+        d = _f32(sun_dir)
+        self._check(self.lib.hpt_set_sunsky(self.h, _p(d, _f), turbidity, sky_scale, sun_scale, sun_radius_scale,
+                                            resolution))
+
+    def prepare(self):
+        self._check(self.lib.hpt_prepare(self.h))
+
+    def info(self) -> SceneInfo:
+        si = SceneInfo()
+        self._check(self.lib.hpt_get_scene_info(self.h, C.byref(si)))
+        return si
+
+    # ---- render ----
+    def render(self, spp_begin=0, spp_end=None, shard=0, n_shards=1, max_wave_paths=0, collect_stats=False,
+               film=None) -> np.ndarray:
+        si = self.info()
+        if spp_end is None:
+            spp_end = si.spp
+        if film is None:
+            film = np.zeros((si.height, si.width, 4), dtype=np.float32)
+        p = RenderParams(spp_begin, spp_end, shard, n_shards, max_wave_paths, int(collect_stats))
+        self._check(self.lib.hpt_render(self.h, C.byref(p), _p(film, _f)))
+        return film
+
+    def render_device(self, device_ptr: int, spp_begin=0, spp_end=None, shard=0, n_shards=1, max_wave_paths=0,
+                      collect_stats=False):
+        si = self.info()
+        if spp_end is None:
+            spp_end = si.spp
+        p = RenderParams(spp_begin, spp_end, shard, n_shards, max_wave_paths, int(collect_stats))
+        self._check(self.lib.hpt_render_device(self.h, C.byref(p), C.c_void_p(device_ptr)))
+
+    def stats(self) -> Stats:
+        s = Stats()
+        self._check(self.lib.hpt_get_stats(self.h, C.byref(s)))
+        return s
+
+    # ---- exports ----
+    def hair(self):
+        n = self.lib.hpt_get_hair(self.h, None, None)
+        xyz = np.zeros((n, 3), np.float32)
+        st = np.zeros(n + 1, np.uint8)
+        self.lib.hpt_get_hair(self.h, _p(xyz, _f), _p(st, _u8))
+        return xyz, st
+
+    def kdtree(self):
+        nn = C.c_int64()
+        ni = C.c_int64()
+        self._check(self.lib.hpt_get_kdtree(self.h, None, C.byref(nn), None, C.byref(ni), None))
+        nodes = np.zeros((nn.value, 2), np.uint32)
+        idx = np.zeros(ni.value, np.uint32)
+        aabb = np.zeros(6, np.float32)
+        self._check(self.lib.hpt_get_kdtree(self.h, _p(nodes, _u32), C.byref(nn), _p(idx, _u32), C.byref(ni),
+                                            _p(aabb, _f)))
+        return nodes, idx, aabb
+
+    def envmap(self):
+        w = C.c_int()
+        h = C.c_int()
+        self._check(self.lib.hpt_get_envmap(self.h, None, C.byref(w), C.byref(h)))
+        rgb = np.zeros((h.value, w.value, 3), np.float32)
+        self._check(self.lib.hpt_get_envmap(self.h, _p(rgb, _f), C.byref(w), C.byref(h)))
+        return rgb
+
+    def marschner_tables(self):
+        t = [np.zeros((64 * 64, 3), np.float32) for _ in range(3)]
+        fdr = np.zeros(1, np.float32)
+        tr = np.zeros(100, np.float32)
+        sw = np.zeros(1, np.float32)
+        self._check(self.lib.hpt_get_marschner_tables(self.h, _p(t[0], _f), _p(t[1], _f), _p(t[2], _f), _p(fdr, _f),
+                                                      _p(tr, _f), _p(sw, _f)))
+        return t, float(fdr[0]), tr, float(sw[0])
+
+    # ---- batch kernels ----
+    def sobol(self, m, frame, px, py, dim):
+        frame, px, py, dim = [np.ascontiguousarray(a, np.uint32) for a in (frame, px, py, dim)]
+        n = frame.size
+        oi = np.zeros(n, np.uint64)
+        ov = np.zeros(n, np.float32)
+        self._check(self.lib.hpt_sobol_batch(self.h, m, n, _p(frame, _u32), _p(px, _u32), _p(py, _u32), _p(dim, _u32),
+                                             _p(oi, _u64), _p(ov, _f)))
+        return oi, ov
+
+    def trace(self, o, d, mint, maxt, shadow=False):
+        o = _f32(o).reshape(-1, 3)
+        d = _f32(d).reshape(-1, 3)
+        n = o.shape[0]
+        mint = _f32(np.broadcast_to(mint, (n,)))
+        maxt = _f32(np.broadcast_to(maxt, (n,)))
+        ot = np.zeros(n, np.float32)
+        oiv = np.zeros(n, np.int32)
+        op = np.zeros((n, 3), np.float32)
+        oh = np.zeros(n, np.uint8)
+        self._check(self.lib.hpt_trace_batch(self.h, n, _p(o, _f), _p(d, _f), _p(mint, _f), _p(maxt, _f), int(shadow),
+                                             _p(ot, _f), _p(oiv, _i32), _p(op, _f), _p(oh, _u8)))
+        return oh.astype(bool) if shadow else (ot, oiv, op)
+
+    def bsdf(self, wi, wo, u):
+        wi = _f32(wi).reshape(-1, 3)
+        wo = _f32(wo).reshape(-1, 3)
+        u = _f32(u).reshape(-1, 2)
+        n = wi.shape[0]
+        oe = np.zeros((n, 3), np.float32)
+        opdf = np.zeros(n, np.float32)
+        owo = np.zeros((n, 3), np.float32)
+        ow = np.zeros((n, 3), np.float32)
+        osp = np.zeros(n, np.float32)
+        ot = np.zeros(n, np.uint32)
+        self._check(self.lib.hpt_bsdf_batch(self.h, n, _p(wi, _f), _p(wo, _f), _p(u, _f), _p(oe, _f), _p(opdf, _f),
+                                            _p(owo, _f), _p(ow, _f), _p(osp, _f), _p(ot, _u32)))
+        return oe, opdf, owo, ow, osp, ot
+
+    def env(self, ref_p, u, dq):
+        ref_p = _f32(ref_p).reshape(-1, 3)
+        u = _f32(u).reshape(-1, 2)
+        dq = _f32(dq).reshape(-1, 3)
+        n = ref_p.shape[0]
+        od = np.zeros((n, 3), np.float32)
+        ov = np.zeros((n, 3), np.float32)
+        op = np.zeros(n, np.float32)
+        odist = np.zeros(n, np.float32)
+        oe = np.zeros((n, 3), np.float32)
+        oep = np.zeros(n, np.float32)
+        self._check(self.lib.hpt_env_batch(self.h, n, _p(ref_p, _f), _p(u, _f), _p(dq, _f), _p(od, _f), _p(ov, _f),
+                                           _p(op, _f), _p(odist, _f), _p(oe, _f), _p(oep, _f)))
+        return od, ov, op, odist, oe, oep
+
+
+def develop(film: np.ndarray) -> np.ndarray:
+    """RGBW film -> linear RGB (ΣwL / Σw), as the film's develop step (ldrfilm.cpp:300-330)."""
+    w = film[..., 3:4]
+    out = np.zeros(film.shape[:-1] + (3,), np.float32)
+    np.divide(film[..., :3], w, out=out, where=w != 0)
+    return out

@@ -1,0 +1,154 @@
+/*
+ * hairpt.h -- C ABI of the MI355X hair path tracer (libhairpt.so).
+ *
+ * This is the drop-in boundary for the reference's hair hot path
+ * (ja5087/cs184-final-project-mitsuba0.5).  The reference exposes the path
+ * as C++ plugins loaded by dlopen (include/mitsuba/core/cobject.h:99-107,
+ * src/libcore/plugin.cpp:71-121) and driven by the `mitsuba` CLI
+ * (src/mitsuba/mitsuba.cpp:52-400).  Mitsuba's C++ plugin ABI (boost-typed
+ * Properties, ref<> counting) cannot be linked here, so the boundary is
+ * re-expressed as plain C entry points: each entry point names the reference
+ * interface it replaces.  Conventions:
+ *   - every function returns 0 on success and a negative HPT_E* code on
+ *     failure; hpt_last_error() holds the message (the reference throws
+ *     std::runtime_error through Log(EError, ...));
+ *   - all buffers are caller-owned; host pointers unless the name says
+ *     "device";
+ *   - a context drives one HIP device; calls on one context are not
+ *     thread-safe (one context per rank / GPU).
+ */
+#ifndef HAIRPT_H
+#define HAIRPT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HPT_OK 0
+#define HPT_EINVAL -1   /* bad argument / missing scene component          */
+#define HPT_EIO -2      /* file could not be read or parsed                */
+#define HPT_EDEVICE -3  /* HIP runtime error or no gfx950 device            */
+#define HPT_ESTATE -4   /* call order violated (e.g. render before prepare) */
+
+typedef struct hpt_context hpt_context;
+
+/* pass as 'device' to create a host-only context: it parses, loads, builds
+   and exports the scene (kd-tree, tables) but cannot render */
+#define HPT_HOST_ONLY -1
+
+/* Context lifetime.  Replaces the Scheduler/LocalWorker setup of
+   src/mitsuba/mitsuba.cpp:281-329 for one device. */
+int hpt_context_create(int device, hpt_context **out);
+void hpt_context_destroy(hpt_context *ctx);
+const char *hpt_last_error(const hpt_context *ctx);
+/* Directory holding sobol/ and microfacet/ data (default: <lib>/../data). */
+int hpt_set_data_dir(hpt_context *ctx, const char *dir);
+
+/* Parse a Mitsuba scene XML (src/librender/scenehandler.cpp) with -D style
+   defines: integrator "path", sensor "perspective" + sampler "sobol" + film,
+   shape "hair", bsdf "marschner"/"kajiyakay", emitter "sunsky"/"envmap". */
+int hpt_load_scene_xml(hpt_context *ctx, const char *path, int n_defines, const char *const *keys,
+                       const char *const *values);
+
+/* ---- low-level scene setters (what a Mitsuba plugin shim would call) ---- */
+/* PerspectiveCameraImpl (src/sensors/perspective.cpp:108-165); row-major 4x4 */
+int hpt_set_camera(hpt_context *ctx, const float to_world[16], float fov_x_deg, int width, int height,
+                   float near_clip, float far_clip);
+/* SobolSampler sampleCount (src/samplers/sobol.cpp:80-106) */
+int hpt_set_sampler(hpt_context *ctx, int sample_count);
+/* MonteCarloIntegrator params (src/librender/integrator.cpp:190-203) */
+int hpt_set_integrator(hpt_context *ctx, int max_depth, int rr_depth, int strict_normals, int hide_emitters);
+/* HairShape(Properties) (src/shapes/hair.cpp:609-785); to_world may be NULL */
+int hpt_set_hair_file(hpt_context *ctx, const char *path, float radius, float angle_threshold_deg,
+                      const float *to_world);
+/* HairShape(Stream) equivalent (hair.cpp:787-801): vertices already merged;
+   starts_fiber has n_vertices entries (a trailing terminator is implied). */
+int hpt_set_hair_vertices(hpt_context *ctx, const float *xyz, const uint8_t *starts_fiber, uint64_t n_vertices,
+                          float radius);
+/* MarschnerDiffuse(Properties) (src/bsdfs/marschner_diffuse.cpp:113-160, plugin
+   "marschner"); distribution 0 = beckmann, 1 = ggx, 2 = phong */
+int hpt_set_bsdf_marschner(hpt_context *ctx, float int_ior, float ext_ior, int distribution, float alpha,
+                           const float diffuse[3], const float specular[3]);
+/* KajiyaKay(Properties) (src/bsdfs/kajiyakay.cpp:60-69) */
+int hpt_set_bsdf_kajiyakay(hpt_context *ctx, const float kd[3], const float ks[3], float exponent);
+/* EnvironmentMap from a bitmap (src/emitters/envmap.cpp:105-189); rgb is w*h*3
+   linear floats, to_world may be NULL */
+int hpt_set_envmap_rgb(hpt_context *ctx, const float *rgb, int w, int h, float scale, const float *to_world);
+/* SunSkyEmitter (src/emitters/sunsky.cpp:100-240) -- round-1 stand-in sky
+   rasteriser with the same bitmap geometry */
+int hpt_set_sunsky(hpt_context *ctx, const float sun_direction[3], float turbidity, float sky_scale,
+                   float sun_scale, float sun_radius_scale, int resolution);
+
+/* Build the hair kd-tree (HairKDTree ctor, hair.cpp:108-159), precompute the
+   BSDF / envmap tables and upload the scene to HBM (Scene::preprocess). */
+int hpt_prepare(hpt_context *ctx);
+
+typedef struct hpt_scene_info {
+    int width, height, spp, max_depth, rr_depth, strict_normals, hide_emitters;
+    int bsdf;                      /* 0 marschner, 1 kajiyakay */
+    uint64_t vertices, segments, kd_nodes, kd_indices;
+    int kd_depth;
+    double kd_build_seconds;
+    float aabb_min[3], aabb_max[3];
+    float bsphere_center[3], bsphere_radius;
+} hpt_scene_info;
+int hpt_get_scene_info(hpt_context *ctx, hpt_scene_info *out);
+
+typedef struct hpt_render_params {
+    int spp_begin, spp_end;        /* render samples [spp_begin, spp_end) of every pixel */
+    int shard, n_shards;           /* 32x32 blocks b with b % n_shards == shard (multi-GPU) */
+    uint64_t max_wave_paths;       /* 0 = automatic (HBM-sized waves) */
+    int collect_stats;             /* traversal counters + per-kernel HIP event timing */
+} hpt_render_params;
+
+/* SamplingIntegrator::render/renderBlock + MIPathTracer::Li + ImageBlock::put
+   (src/librender/integrator.cpp:95-188, src/integrators/path/path.cpp:119-294,
+   include/mitsuba/render/imageblock.h:124-204).  film_rgbw is W*H*4 floats
+   (sum of w*L per channel, sum of w) and is ACCUMULATED into. */
+int hpt_render(hpt_context *ctx, const hpt_render_params *params, float *film_rgbw);
+/* Same, accumulating into a device buffer of W*H float4 on this context's device. */
+int hpt_render_device(hpt_context *ctx, const hpt_render_params *params, void *device_film_rgbw);
+
+typedef struct hpt_stats {
+    double ms_total;               /* host wall time of the render call */
+    double ms_camera, ms_trace, ms_primary, ms_shade, ms_post, ms_gather; /* HIP event sums */
+    uint64_t trace_launches;
+    uint64_t paths, closest_rays, shadow_rays, nodes, prims, bounces;
+    uint64_t shadow_unoccluded;    /* shadow rays that reached the emitter */
+    uint64_t waves;
+    int max_bounces;
+} hpt_stats;
+int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
+
+/* ---- exports used by the parity tests ---- */
+/* vertex count is returned; pass NULL buffers to query the size */
+int64_t hpt_get_hair(hpt_context *ctx, float *xyz, uint8_t *starts_fiber /* n+1 */);
+/* nodes: 2 u32 per node; indices: first-vertex index of each leaf entry */
+int hpt_get_kdtree(hpt_context *ctx, uint32_t *nodes, int64_t *n_nodes, uint32_t *indices, int64_t *n_indices,
+                   float aabb[6]);
+int hpt_get_envmap(hpt_context *ctx, float *rgb, int *w, int *h);
+int hpt_get_marschner_tables(hpt_context *ctx, float *n_r, float *n_tt, float *n_trt, float *fdr, float *trans100,
+                             float *spec_weight);
+
+/* ---- per-function batch kernels (host arrays in/out, run on the device) ---- */
+/* sobol::look_up + sobol::sampleSingle (src/samplers/sobolseq.h:43-131) */
+int hpt_sobol_batch(hpt_context *ctx, int m, int n, const uint32_t *frame, const uint32_t *px, const uint32_t *py,
+                    const uint32_t *dim, uint64_t *out_index, float *out_value);
+/* ShapeKDTree::rayIntersect closest (skdtree.cpp:112-141) or shadow (:207-226);
+   out_iv is the reference's primitive id (first vertex index of the segment) */
+int hpt_trace_batch(hpt_context *ctx, int n, const float *o, const float *d, const float *mint, const float *maxt,
+                    int shadow, float *out_t, int32_t *out_iv, float *out_p, uint8_t *out_hit);
+/* BSDF::eval / pdf / sample for the scene's hair BSDF (local frame) */
+int hpt_bsdf_batch(hpt_context *ctx, int n, const float *wi, const float *wo, const float *u, float *out_eval,
+                   float *out_pdf, float *out_wo, float *out_weight, float *out_sample_pdf, uint32_t *out_type);
+/* EnvironmentMap::sampleDirect (envmap.cpp:516-543) for points ref_p and
+   evalEnvironment / pdfDirect (:380-410, :545-556) for directions dq */
+int hpt_env_batch(hpt_context *ctx, int n, const float *ref_p, const float *u, const float *dq, float *out_d,
+                  float *out_value, float *out_pdf, float *out_dist, float *out_eval, float *out_eval_pdf);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

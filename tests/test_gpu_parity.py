@@ -1,0 +1,155 @@
+"""GPU parity: HIP kernels (through the C ABI) vs the oracle on identical inputs.
+
+Tolerances:
+  - Sobol index/values, kd-tree hits (segment id, t, hit point): bit-exact.
+  - BSDF / envmap values: float32 transcendental functions differ between
+    ROCm's ocml and glibc by <= ~2 ulp, so values are compared with
+    rtol 2e-5 and discrete outcomes (sampled lobe/type) must agree for
+    > 99.9 % of samples.
+  - Rendered film: per-pixel L2 on linear HDR RGB, RMSE < 1e-3 relative to
+    mean luminance (north_star "per-pixel L2 error < 1e-3").
+"""
+import numpy as np
+import pytest
+
+import oracle_lib
+import scene_util
+from mitsuba_amd import native
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def furball():
+    xml, r, o = scene_util.make("furball_marschner", 3000, 48, 40, 8, device=0)
+    return xml, r, o
+
+
+@pytest.fixture(scope="module")
+def straight():
+    xml, r, o = scene_util.make("straight_kk", 1500, 48, 40, 8, device=0)
+    return xml, r, o
+
+
+def test_sobol_bit_exact(furball):
+    _, r, o = furball
+    rng = np.random.default_rng(1)
+    n = 20000
+    m = 6
+    frame = rng.integers(0, 1000, n).astype(np.uint32)
+    px = rng.integers(0, 64, n).astype(np.uint32)
+    py = rng.integers(0, 64, n).astype(np.uint32)
+    dim = rng.integers(0, 400, n).astype(np.uint32)
+    gi, gv = r.sobol(m, frame, px, py, dim)
+    oi = o.sobol_lookup(m, frame, px, py)
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_array_equal(gv, o.sobol_sample(oi, dim))
+
+
+def _rays(o, n, seed, width=48, height=40):
+    rng = np.random.default_rng(seed)
+    pos = np.stack([rng.uniform(0, width, n // 2), rng.uniform(0, height, n // 2)], 1)
+    co, cd, cmin, cmax = o.camera_rays(pos)
+    centre = np.array([0.0, 12.3, 0.0])
+    a = centre + rng.normal(0, 2.0, (n // 2, 3))
+    b = centre + rng.normal(0, 2.0, (n // 2, 3))
+    d = (b - a) / np.linalg.norm(b - a, axis=1, keepdims=True)
+    orig = np.concatenate([co, a]).astype(np.float32)
+    dirs = np.concatenate([cd, d]).astype(np.float32)
+    mint = np.concatenate([cmin, np.full(n // 2, 1e-4, np.float32)])
+    maxt = np.concatenate([cmax, np.full(n // 2, np.inf, np.float32)])
+    return orig, dirs, mint, maxt
+
+
+@pytest.mark.parametrize("fixture", ["furball", "straight"])
+def test_trace_bit_exact(fixture, request):
+    _, r, o = request.getfixturevalue(fixture)
+    orig, dirs, mint, maxt = _rays(o, 40000, 3)
+    gt, giv, gp = r.trace(orig, dirs, mint, maxt)
+    ot, oiv, op = o.trace(orig, dirs, mint, maxt)
+    assert (oiv >= 0).sum() > 1000
+    np.testing.assert_array_equal(giv, oiv)
+    np.testing.assert_array_equal(gt, ot)
+    np.testing.assert_array_equal(gp, op)
+    sm = np.minimum(maxt, 3.0).astype(np.float32)
+    np.testing.assert_array_equal(r.trace(orig, dirs, mint, sm, shadow=True), o.trace(orig, dirs, mint, sm, shadow=True))
+
+
+def _dirs(rng, n):
+    v = rng.normal(size=(n, 3))
+    return (v / np.linalg.norm(v, axis=1, keepdims=True)).astype(np.float32)
+
+
+@pytest.mark.parametrize("fixture", ["furball", "straight"])
+def test_bsdf_matches_oracle(fixture, request):
+    _, r, o = request.getfixturevalue(fixture)
+    rng = np.random.default_rng(7)
+    n = 50000
+    wi = _dirs(rng, n)
+    wo = _dirs(rng, n)
+    u = rng.random((n, 2)).astype(np.float32)
+    ge, gpdf, gwo, gw, gsp, gt = r.bsdf(wi, wo, u)
+    oe, opdf = o.bsdf_eval(wi, wo)
+    np.testing.assert_allclose(ge, oe, rtol=2e-5, atol=1e-7)
+    np.testing.assert_allclose(gpdf, opdf, rtol=2e-5, atol=1e-7)
+    owo, ow, osp, ot = o.bsdf_sample(wi, u)
+    agree = gt == ot
+    assert agree.mean() > 0.999
+    np.testing.assert_allclose(gwo[agree], owo[agree], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(gw[agree], ow[agree], rtol=1e-3, atol=1e-6)
+
+
+def test_envmap_matches_oracle(furball):
+    _, r, o = furball
+    rng = np.random.default_rng(9)
+    n = 30000
+    ref = (np.array([0.0, 12.3, 0.0]) + rng.normal(0, 1.0, (n, 3))).astype(np.float32)
+    u = rng.random((n, 2)).astype(np.float32)
+    dq = _dirs(rng, n)
+    gd, gv, gp, gdist, ge, gep = r.env(ref, u, dq)
+    od, ov, op, odist = o.env_sample(ref, u)
+    np.testing.assert_allclose(gd, od, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(gv, ov, rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(gp, op, rtol=1e-4, atol=1e-7)
+    np.testing.assert_allclose(gdist, odist, rtol=1e-5)
+    oe, oep = o.env_eval(dq)
+    np.testing.assert_allclose(ge, oe, rtol=2e-5, atol=1e-7)
+    np.testing.assert_allclose(gep, oep, rtol=2e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("fixture", ["furball", "straight"])
+def test_render_matches_oracle(fixture, request):
+    """Full wavefront render vs the oracle's MIPathTracer::Li restatement."""
+    _, r, o = request.getfixturevalue(fixture)
+    si = r.info()
+    film = r.render(0, si.spp, collect_stats=True)
+    ofilm, ostats = o.render(0, si.spp, width=si.width, height=si.height)
+    assert int(ostats[5]) == 0, "EWA lookups that do not reduce to bilinear"
+    # the sample weights are identical bit for bit up to summation order
+    np.testing.assert_allclose(film[..., 3], ofilm[..., 3], rtol=1e-5)
+    a = native.develop(film)
+    b = native.develop(ofilm)
+    m = scene_util.l2_metrics(b, a)
+    assert m["rel_rmse"] < 1e-3, m
+    s = r.stats()
+    assert s.paths == si.width * si.height * si.spp or s.paths >= si.width * si.height * si.spp
+    assert s.nodes > 0 and s.prims > 0 and s.trace_launches > 1
+
+
+def test_render_deterministic_and_sharded(furball):
+    _, r, o = furball
+    si = r.info()
+    a = r.render(0, si.spp)
+    b = r.render(0, si.spp)
+    np.testing.assert_array_equal(a, b)
+    # two shards of 32x32 blocks summed == the full frame (up to summation order)
+    s = r.render(0, si.spp, shard=0, n_shards=2)
+    s = r.render(0, si.spp, shard=1, n_shards=2, film=s)
+    np.testing.assert_allclose(s, a, rtol=1e-5, atol=1e-6)
+    # spp ranges accumulate: [0, 3) + [3, spp) == [0, spp)
+    c = r.render(0, 3)
+    c = r.render(3, si.spp, film=c)
+    np.testing.assert_allclose(c, a, rtol=1e-5, atol=1e-6)
+    # small waves give the same result as one wave
+    d = r.render(0, si.spp, max_wave_paths=4096)
+    np.testing.assert_allclose(d, a, rtol=1e-5, atol=1e-6)
