@@ -156,7 +156,10 @@ HD bool traverse(const HptScene &sc, V3 o, V3 d, V3 rcp, float mint, float maxt,
     uint32_t node = 0;
     int sp = 0, top = 0; /* ring buffer: entries [top-sp, top) modulo STACK */
     bool lost = false;
+    int restarts = 0, leaves = 0;
     while (true) {
+        /* hard bounds so every wave drains even on a malformed tree */
+        if (++leaves > (1 << 18)) break;
         HptNode nd = nodes[node];
         while (!(nd.w0 & 0x80000000u)) {
             ++nNodes;
@@ -197,7 +200,7 @@ HD bool traverse(const HptScene &sc, V3 o, V3 d, V3 rcp, float mint, float maxt,
         }
         if (found && tHit <= tmax) break;
         if (sp == 0) {
-            if (!lost || tmax >= maxt) break;
+            if (!lost || tmax >= maxt || ++restarts > 64) break;
             /* kd-restart from the root for the remaining interval */
             lost = false;
             node = 0;

@@ -1138,6 +1138,7 @@ struct orc_scene {
     EnvMap env;
     bool hasEnv = false;
     int maxDepth = -1, rrDepth = 5;
+    int sampleCount = 1; /* sampler->getSampleCount() for the ray-differential scale */
     bool strictNormals = false, hideEmitters = false;
     bool prepared = false;
 };
@@ -1257,6 +1258,10 @@ CamRay cameraRay(const orc_scene *s, float sx, float sy) {
     cr.ray = Ray(o, xformVector(T, d), mint, maxt);
     cr.rxDir = xformVector(T, normalize(nearP + V3(s->dx[0], s->dx[1], s->dx[2])));
     cr.ryDir = xformVector(T, normalize(nearP + V3(s->dy[0], s->dy[1], s->dy[2])));
+    /* integrator.cpp:143-144,178: sensorRay.scaleDifferential(1/sqrt(sampleCount)) (ray.h:163-168) */
+    const float amount = 1.0f / std::sqrt((float) s->sampleCount);
+    cr.rxDir = cr.ray.d + (cr.rxDir - cr.ray.d) * amount;
+    cr.ryDir = cr.ray.d + (cr.ryDir - cr.ray.d) * amount;
     return cr;
 }
 
@@ -1898,6 +1903,11 @@ int orc_set_envmap(orc_scene *s, const float *rgb, int w, int h, float scale, co
     }
     s->env.build(rgb);
     s->hasEnv = true;
+    return 0;
+}
+
+int orc_set_sample_count(orc_scene *s, int spp) {
+    s->sampleCount = spp > 0 ? spp : 1;
     return 0;
 }
 

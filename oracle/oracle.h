@@ -62,6 +62,8 @@ int orc_set_envmap(orc_scene *s, const float *rgb, int w, int h, float scale,
                    const float *to_world);
 int orc_set_integrator(orc_scene *s, int max_depth, int rr_depth, int strict_normals,
                        int hide_emitters);
+/* SobolSampler sampleCount: scales the primary ray differentials (integrator.cpp:143) */
+int orc_set_sample_count(orc_scene *s, int spp);
 int orc_prepare(orc_scene *s);
 
 /* Render samples [spp_begin, spp_end) of every pixel; film_rgbw = W*H*4 floats

@@ -41,6 +41,7 @@ _SIG = {
     "orc_set_envmap": (C.c_int, [C.c_void_p, _f, C.c_int, C.c_int, C.c_float, _f]),
     "orc_set_integrator": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
     "orc_prepare": (C.c_int, [C.c_void_p]),
+    "orc_set_sample_count": (C.c_int, [C.c_void_p, C.c_int]),
     "orc_render": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, _f, _u64]),
     "orc_render_shard": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _f, _u64]),
     "orc_sobol_lookup": (None, [C.c_void_p, C.c_int, C.c_int, _u32, _u32, _u32, _u64]),
@@ -118,8 +119,9 @@ class Oracle:
 
     # ---- scene from a parsed config ----
     def setup(self, cam, fov, width, height, hair_file, radius, bsdf, env_rgb, max_depth, rr_depth=5,
-              strict=True, hide=False, near=1e-2, far=1e4):
+              strict=True, hide=False, near=1e-2, far=1e4, spp=1):
         cam = f32(cam).reshape(16)
+        self.check(self.lib.orc_set_sample_count(self.s, spp))
         self.check(self.lib.orc_set_camera(self.s, p(cam, _f), fov, width, height, near, far))
         self.check(self.lib.orc_load_hair(self.s, hair_file.encode(), radius, 1.0, None))
         kind = bsdf["type"]

@@ -43,10 +43,30 @@ def make(name, n_strands, width, height, spp, max_depth=None, device=native.HOST
     nodes, idx, _ = r.kdtree()
     o = oracle_lib.Oracle()
     hair_file = os.path.join(WORK, "%s_%d.mitshair" % (cfg["geom"], n_strands))
-    o.setup(cam, 35.0, width, height, hair_file, float(cfg["radius"]), bsdf, env, max_depth)
+    o.setup(cam, 35.0, width, height, hair_file, float(cfg["radius"]), bsdf, env, max_depth, spp=spp)
     o.set_kdtree(nodes, idx)
     o.prepare()
     return xml, r, o
+
+
+def reference_flags_floor(name, n_strands, r, width, height, spp):
+    """L2 between the strict oracle and the oracle built with the reference's
+    own compiler flags (liboracle_ref.so): the float-nondeterminism floor that
+    any re-implementation of the path inherits (SURVEY.md 7 'Hard parts' i)."""
+    cfg, cam, bsdf = config_params(name)
+    hair_file = os.path.join(WORK, "%s_%d.mitshair" % (cfg["geom"], n_strands))
+    films = []
+    nodes, idx, _ = r.kdtree()
+    for variant in ("parity", "ref"):
+        o = oracle_lib.Oracle(variant=variant)
+        o.setup(cam, 35.0, width, height, hair_file, float(cfg["radius"]), bsdf, r.envmap(), cfg["max_depth"],
+                spp=spp)
+        o.set_kdtree(nodes, idx)
+        o.prepare()
+        films.append(native.develop(o.render(0, spp, width=width, height=height)[0]))
+    a, b = films
+    same = np.all(np.abs(a - b) <= 1e-5 * np.abs(a) + 1e-7, axis=-1)
+    return l2_metrics(a, b), float(same.mean())
 
 
 def l2_metrics(a, b):

@@ -175,3 +175,15 @@ def test_kdtree_structure():
     xyz, st = r.hair()
     seg_first = np.nonzero(st[1:-0 or None][: xyz.shape[0] - 1] == 0)[0]
     assert set(np.unique(idx).tolist()) == set(seg_first.tolist())
+
+
+@pytest.mark.parametrize("name,n", [("furball_marschner", 3000), ("straight_kk", 1500)])
+def test_reference_flags_noise_floor(name, n):
+    """The oracle built with the reference's own flags (-funsafe-math-optimizations)
+    differs from the strict build only through rare discrete-event flips: this
+    floor bounds what any faithful re-implementation can reach (see
+    test_gpu_parity.test_render_matches_oracle)."""
+    _, r, o = scene_util.make(name, n, 48, 40, 8)
+    floor, same = scene_util.reference_flags_floor(name, n, r, 48, 40, 8)
+    assert floor["rmse"] < 1e-3, floor
+    assert same > 0.7
