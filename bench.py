@@ -37,8 +37,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 #   closest ray: queue id 4 + ray 32 + hit record 32 = 68 B
 #   shadow ray:  queue id 4 + origin 16 + direction/maxt 16 = 36 B, +48 B (contribution + radiance RMW)
 #                when unoccluded
-#   node visit 8 B, primitive test 4 B leaf index + 128 B segment record
-BYTES_CLOSEST, BYTES_SHADOW, BYTES_UNOCC, BYTES_NODE, BYTES_PRIM = 68, 36, 48, 8, 132
+#   node visit 8 B; primitive test 4 B leaf index + 32 B fp32 pre-test record;
+#   exact fp64 test (pre-test survivors) + 128 B segment record
+BYTES_CLOSEST, BYTES_SHADOW, BYTES_UNOCC, BYTES_NODE, BYTES_PRIM, BYTES_EXACT = 68, 36, 48, 8, 36, 128
 
 
 def parse():
@@ -53,7 +54,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--max-depth", type=int, default=None)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    ap.add_argument("--cpu-spp", type=int, default=2, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-spp", type=int, default=96, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--workdir", default=os.path.join(tempfile.gettempdir(), "hpt_bench"))
     return ap.parse_args()
@@ -123,7 +124,7 @@ def main():
     t0 = time.perf_counter()
     ms_trace = 0.0
     launches = 0
-    tot = dict(nodes=0, prims=0, closest=0, shadow=0, unocc=0, bounces=0)
+    tot = dict(nodes=0, prims=0, exact=0, closest=0, shadow=0, unocc=0, bounces=0)
     for _ in range(args.steps):
         step()
         s = r.stats()
@@ -131,6 +132,7 @@ def main():
         launches += s.trace_launches
         tot["nodes"] += s.nodes
         tot["prims"] += s.prims
+        tot["exact"] += s.prim_exact
         tot["closest"] += s.closest_rays
         tot["shadow"] += s.shadow_rays
         tot["unocc"] += s.shadow_unoccluded
@@ -147,7 +149,7 @@ def main():
     paths_total = W * H * spp * args.steps
     value = paths_total / dt / 1e6
     bytes_alg = (BYTES_CLOSEST * tot["closest"] + BYTES_SHADOW * tot["shadow"] + BYTES_UNOCC * tot["unocc"]
-                 + BYTES_NODE * tot["nodes"] + BYTES_PRIM * tot["prims"])
+                 + BYTES_NODE * tot["nodes"] + BYTES_PRIM * tot["prims"] + BYTES_EXACT * tot["exact"])
     achieved = bytes_alg / (ms_trace * 1e-3) / 1e9 if ms_trace > 0 else 0.0
     out = None
     if rank == 0:
@@ -183,6 +185,7 @@ def main():
             "stats": {"bounces_per_path": round(tot["bounces"] / max(1, paths_total / world), 4),
                       "nodes_per_ray": round(tot["nodes"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "prims_per_ray": round(tot["prims"] / max(1, tot["closest"] + tot["shadow"]), 2),
+                      "exact_tests_per_ray": round(tot["exact"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "image_mean": float(img.mean())},
         }
         print(json.dumps(out), flush=True)

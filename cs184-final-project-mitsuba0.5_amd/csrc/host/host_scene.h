@@ -93,6 +93,7 @@ struct KDTreeHost {
     std::vector<HptNode> nodes;
     std::vector<uint32_t> prims;          /* segment index per leaf entry */
     std::vector<HptSegment> segs;         /* per segment (index = segment id) */
+    std::vector<HptSegF> segsF;           /* fp32 pre-test records, same indexing */
     std::vector<uint32_t> segFirstVertex; /* segment id -> first vertex index */
     float aabbMin[3], aabbMax[3];
     int maxDepthUsed = 0;

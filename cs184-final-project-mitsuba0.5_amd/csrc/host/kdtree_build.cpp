@@ -423,6 +423,7 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
 
     /* double-precision per-segment records (hair.cpp:551-596) */
     t.segs.resize(S);
+    t.segsF.resize(S);
     for (size_t s = 0; s < S; ++s) {
         uint32_t iv = segIv[s];
         auto vd = [&](uint32_t i) {
@@ -455,6 +456,12 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
         }
         r.iv = iv;
         r.pad = 0;
+        HptSegF &f = t.segsF[s];
+        for (int k = 0; k < 3; ++k) {
+            f.v1[k] = hair.xyz[3 * iv + k];
+            f.axis[k] = (float) axis[k];
+        }
+        f.pad[0] = f.pad[1] = 0.0f;
     }
 
     /* primitive bounds + tree AABB (gkdtree.h:990-994) */

@@ -429,6 +429,7 @@ int hpt_prepare(hpt_context *c) {
     r |= upload(c, c->tree.nodes.data(), c->tree.nodes.size() * sizeof(HptNode), (const void **) &sc.nodes);
     r |= upload(c, c->tree.prims.data(), c->tree.prims.size() * 4, (const void **) &sc.prims);
     r |= upload(c, c->tree.segs.data(), c->tree.segs.size() * sizeof(HptSegment), (const void **) &sc.segs);
+    r |= upload(c, c->tree.segsF.data(), c->tree.segsF.size() * sizeof(HptSegF), (const void **) &sc.segsF);
     for (int i = 0; i < 3; ++i) {
         sc.aabbMin[i] = c->tree.aabbMin[i];
         sc.aabbMax[i] = c->tree.aabbMax[i];
@@ -679,6 +680,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         c->stats.closest_rays = hs[2];
         c->stats.shadow_rays = hs[3];
         c->stats.shadow_unoccluded = hs[4];
+        c->stats.prim_exact = hs[5];
     }
     c->stats.bounces = bounces;
     c->stats.max_bounces = maxB;
@@ -803,7 +805,8 @@ int hpt_sobol_batch(hpt_context *c, int m, int n, const uint32_t *frame, const u
 }
 
 int hpt_trace_batch(hpt_context *c, int n, const float *o, const float *d, const float *mint, const float *maxt,
-                    int shadow, float *ot, int32_t *oiv, float *op, uint8_t *oh) {
+                    int flags, float *ot, int32_t *oiv, float *op, uint8_t *oh) {
+    const int shadow = flags & HPT_TRACE_SHADOW;
     if (!c || !c->prepared) return setErr(c, HPT_ESTATE, "prepare first");
     if (c->device == HPT_HOST_ONLY) return setErr(c, HPT_EDEVICE, "host-only context has no device");
     HIPCHK(c, hipSetDevice(c->device));
@@ -812,7 +815,7 @@ int hpt_trace_batch(hpt_context *c, int n, const float *o, const float *d, const
     float *dt = S.in<float>(nullptr, n), *dp = S.in<float>(nullptr, 3 * (size_t) n);
     int32_t *ds = S.in<int32_t>(nullptr, n);
     uint8_t *dh = S.in<uint8_t>(nullptr, n);
-    HIPCHK(c, hpt_launch_trace_batch(c->sc, n, a, b, mi, ma, shadow, dt, ds, dp, dh, c->stream));
+    HIPCHK(c, hpt_launch_trace_batch(c->sc, n, a, b, mi, ma, flags, dt, ds, dp, dh, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (shadow) {
         fetch(oh, dh, n);

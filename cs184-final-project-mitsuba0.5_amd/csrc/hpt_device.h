@@ -41,6 +41,17 @@ struct HptSegment {
     uint32_t pad;
 };
 
+/* fp32 shadow of a segment for the conservative pre-test (32 bytes): the
+ * ray line must pass within radius of the axis line for the fp64 quadratic
+ * to have real roots; the pre-test rejects only when fp32 says the distance
+ * exceeds radius by far more than its rounding error, so the set of segments
+ * reaching the exact fp64 test is a superset of those that can hit. */
+struct HptSegF {
+    float v1[3];
+    float axis[3];
+    float pad[2];
+};
+
 /* kd-tree node, 8 bytes (gkdtree.h:452-583 layout with absolute child index):
  *   inner: w0 = (left << 2) | axis, w1 = float bits of split; right = left + 1
  *   leaf : w0 = 0x80000000 | primStart, w1 = primEnd (indices into prim list) */
@@ -90,6 +101,7 @@ struct HptScene {
     const HptNode *nodes;
     const uint32_t *prims;      /* leaf primitive list -> segment index */
     const HptSegment *segs;
+    const HptSegF *segsF;
     float aabbMin[3], aabbMax[3];
     float radius;
     int bsdfKind;               /* 0 = marschner, 1 = kajiyakay */

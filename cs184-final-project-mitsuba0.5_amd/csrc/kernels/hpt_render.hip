@@ -106,7 +106,7 @@ HD bool aabbIntersect(const HptScene &sc, V3 o, V3 d, V3 rcp, float &nearT, floa
 /* Hair segment test: HairKDTree::intersect (hair.cpp:485-548) in fp64  */
 /* ------------------------------------------------------------------ */
 HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, const D3 &rayO, const D3 &rayD,
-                     double r2, float mint, float maxt, float &t, D3 &p) {
+                     double r2, float mint, float maxt, float &t, V3 &p) {
     const double *rec = reinterpret_cast<const double *>(segs + s);
     D3 v1 = d3(rec[0], rec[1], rec[2]);
     D3 axis = d3(rec[3], rec[4], rec[5]);
@@ -125,16 +125,35 @@ HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, const D3 &
     D3 n2 = d3(rec[9], rec[10], rec[11]);
     D3 v2 = d3(rec[12], rec[13], rec[14]);
     if (dot(pointNear - v1, n1) >= 0 && dot(pointNear - v2, n2) <= 0 && nearT >= (double) mint) {
-        p = pointNear;
+        p = v3((float) pointNear.x, (float) pointNear.y, (float) pointNear.z);
         t = (float) nearT;
     } else if (dot(pointFar - v1, n1) >= 0 && dot(pointFar - v2, n2) <= 0) {
         if (farT > (double) maxt) return false;
-        p = pointFar;
+        p = v3((float) pointFar.x, (float) pointFar.y, (float) pointFar.z);
         t = (float) farT;
     } else {
         return false;
     }
     return true;
+}
+
+/* Conservative fp32 pre-test (see HptSegF): false only when the ray line
+   provably passes farther than radius from the segment's axis line, i.e.
+   when the fp64 quadratic of segIntersect has no real root.  Error budget:
+   |computed - exact| of w.n is below 4e-7 (|w| + r) + 2e-7 |w| |n| for
+   |n| >= 0.01 (fp32 cross/dot rounding and the fp32-rounded axis), which the
+   1e-4 (r + |w|_1) slack covers with two orders of magnitude to spare. */
+HD bool segMayHit(const HptSegF *__restrict__ segsF, uint32_t s, V3 o, V3 d, float r) {
+    const float4 *f = reinterpret_cast<const float4 *>(segsF + s);
+    const float4 a = f[0], b = f[1];
+    const float wx = o.x - a.x, wy = o.y - a.y, wz = o.z - a.z;
+    const float ax = a.w, ay = b.x, az = b.y; /* axis */
+    const float nx = d.y * az - d.z * ay, ny = d.z * ax - d.x * az, nz = d.x * ay - d.y * ax;
+    const float nn = nx * nx + ny * ny + nz * nz;
+    if (nn < 1e-4f) return true; /* near-parallel: leave it to the exact test */
+    const float wn = fabsf(wx * nx + wy * ny + wz * nz);
+    const float slack = r + 1e-4f * (r + fabsf(wx) + fabsf(wy) + fabsf(wz));
+    return wn * wn <= slack * slack * nn;
 }
 
 /* ------------------------------------------------------------------ */
@@ -145,8 +164,9 @@ HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, const D3 &
 /* ------------------------------------------------------------------ */
 template <int STACK, bool SHADOW>
 HD bool traverse(const HptScene &sc, V3 o, V3 d, V3 rcp, float mint, float maxt, uint2 *stk, int stride,
-                 float &tHit, uint32_t &segHit, D3 &pHit, uint32_t &nNodes, uint32_t &nPrims) {
+                 float &tHit, uint32_t &segHit, V3 &pHit, uint32_t &nNodes, uint32_t &nPrims, uint32_t &nExact) {
     const HptNode *__restrict__ nodes = sc.nodes;
+    const float radius = sc.radius;
     const uint32_t *__restrict__ prims = sc.prims;
     const D3 rayO = d3(o.x, o.y, o.z), rayD = d3(d.x, d.y, d.z);
     const double r2 = (double) (sc.radius * sc.radius); /* Float product (hair.cpp:500) */
@@ -188,8 +208,10 @@ HD bool traverse(const HptScene &sc, V3 o, V3 d, V3 rcp, float mint, float maxt,
         for (uint32_t e = nd.w0 & 0x7fffffffu, last = nd.w1; e < last; ++e) {
             const uint32_t s = prims[e];
             ++nPrims;
+            if (!segMayHit(sc.segsF, s, o, d, radius)) continue;
+            ++nExact;
             float t;
-            D3 p;
+            V3 p;
             if (segIntersect(sc.segs, s, rayO, rayD, r2, mint, tHit, t, p)) {
                 if (SHADOW) return true;
                 tHit = t;
@@ -646,7 +668,7 @@ __device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P,
                                           int stride, uint32_t *stats) {
     const uint32_t nTrace = counters[HPT_Q_TRACE], nShadow = counters[HPT_Q_SHADOW];
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t nNodes = 0, nPrims = 0, nU = 0;
+    uint32_t nNodes = 0, nPrims = 0, nExact = 0, nU = 0;
     if (tid < nTrace) {
         const uint32_t id = traceQ[tid];
         float4 ro = P.ro[id], rd = P.rd[id];
@@ -656,7 +678,7 @@ __device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P,
         float rmint = ro.w, rmaxt = rd.w;
         int32_t seg = -1;
         float thit = finf();
-        D3 p = d3(0, 0, 0);
+        V3 p = v3(0.0f, 0.0f, 0.0f);
         if (aabbIntersect(sc, o, d, rcp, mint, maxt)) {
             float rayMinT = adaptiveMint(o, rmint, false);
             if (rayMinT > mint) mint = rayMinT;
@@ -664,14 +686,14 @@ __device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P,
             if (maxt > mint) {
                 float t;
                 uint32_t s = 0;
-                if (traverse<STACK, false>(sc, o, d, rcp, mint, maxt, stk, stride, t, s, p, nNodes, nPrims)) {
+                if (traverse<STACK, false>(sc, o, d, rcp, mint, maxt, stk, stride, t, s, p, nNodes, nPrims, nExact)) {
                     seg = (int32_t) s;
                     thit = t;
                 }
             }
         }
         P.hit[id] = make_float4(__int_as_float(seg), thit, 0.0f, 0.0f);
-        P.hitp[id] = make_float4((float) p.x, (float) p.y, (float) p.z, 0.0f);
+        P.hitp[id] = make_float4(p.x, p.y, p.z, 0.0f);
     } else if (tid < nTrace + nShadow) {
         const uint32_t id = shadowQ[tid - nTrace];
         float4 ro = P.ro[id], sd = P.sdir[id];
@@ -686,8 +708,8 @@ __device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P,
             if (maxt > mint) {
                 float t;
                 uint32_t s;
-                D3 p;
-                occluded = traverse<STACK, true>(sc, o, d, rcp, mint, maxt, stk, stride, t, s, p, nNodes, nPrims);
+                V3 p;
+                occluded = traverse<STACK, true>(sc, o, d, rcp, mint, maxt, stk, stride, t, s, p, nNodes, nPrims, nExact);
             }
         }
         if (!occluded) {
@@ -699,7 +721,8 @@ __device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P,
     if (stats) {
         /* traversal counters for the algorithmic byte model:
            [0] node visits [1] primitive tests [2] closest rays [3] shadow rays
-           [4] unoccluded shadow rays; per-wave reduction, one atomic each */
+           [4] unoccluded shadow rays [5] exact fp64 segment tests (pre-test
+           survivors); per-wave reduction, one atomic each */
         uint32_t nC = tid < nTrace ? 1u : 0u, nS = (tid >= nTrace && tid < nTrace + nShadow) ? 1u : 0u;
         for (int off = 32; off > 0; off >>= 1) {
             nNodes += __shfl_down(nNodes, off);
@@ -707,6 +730,7 @@ __device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P,
             nC += __shfl_down(nC, off);
             nS += __shfl_down(nS, off);
             nU += __shfl_down(nU, off);
+            nExact += __shfl_down(nExact, off);
         }
         if (__lane_id() == 0 && (nC | nS)) {
             unsigned long long *st = (unsigned long long *) stats;
@@ -715,12 +739,13 @@ __device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P,
             atomicAdd(&st[2], (unsigned long long) nC);
             atomicAdd(&st[3], (unsigned long long) nS);
             atomicAdd(&st[4], (unsigned long long) nU);
+            atomicAdd(&st[5], (unsigned long long) nExact);
         }
     }
 }
 
 #define HPT_TRACE_BLOCK 128
-#define HPT_STACK 32
+#define HPT_STACK 16
 
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace(HptScene sc, HptPaths P,
                                                                       const uint32_t *__restrict__ traceQ,
@@ -974,31 +999,32 @@ extern "C" __global__ void k_sobol_batch(HptScene sc, int m, int n, const uint32
     outVal[i] = sobolSample(sc, idx, dim[i]);
 }
 
-extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptScene sc, int n, const float *o,
-                                                                            const float *d, const float *mint,
-                                                                            const float *maxt, int shadow,
-                                                                            float *outT, int32_t *outSeg,
-                                                                            float *outP, uint8_t *outHit) {
-    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+/* flags: bit 0 = any-hit shadow query, bit 1 = 2-entry stack (exercises the
+   kd-restart path of traverse for the parity tests) */
+template <int STACK>
+__device__ __forceinline__ void traceBatchBody(const HptScene &sc, int n, const float *o, const float *d,
+                                               const float *mint, const float *maxt, int flags, float *outT,
+                                               int32_t *outSeg, float *outP, uint8_t *outHit, uint2 *stk) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    const bool shadow = (flags & 1) != 0;
     V3 oo = v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), dd = v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
     V3 rcp = v3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
     float mn, mx;
-    uint32_t nn = 0, np = 0;
+    uint32_t nn = 0, np = 0, ne = 0;
     bool ok = false;
     float t = finf();
     uint32_t s = 0;
-    D3 p = d3(0, 0, 0);
+    V3 p = v3(0.0f, 0.0f, 0.0f);
     if (aabbIntersect(sc, oo, dd, rcp, mn, mx)) {
-        float rayMinT = adaptiveMint(oo, mint[i], shadow != 0);
+        float rayMinT = adaptiveMint(oo, mint[i], shadow);
         if (rayMinT > mn) mn = rayMinT;
         if (maxt[i] < mx) mx = maxt[i];
         if (mx > mn) {
             if (shadow)
-                ok = traverse<HPT_STACK, true>(sc, oo, dd, rcp, mn, mx, stk + threadIdx.x, HPT_TRACE_BLOCK, t, s, p, nn, np);
+                ok = traverse<STACK, true>(sc, oo, dd, rcp, mn, mx, stk, HPT_TRACE_BLOCK, t, s, p, nn, np, ne);
             else
-                ok = traverse<HPT_STACK, false>(sc, oo, dd, rcp, mn, mx, stk + threadIdx.x, HPT_TRACE_BLOCK, t, s, p, nn, np);
+                ok = traverse<STACK, false>(sc, oo, dd, rcp, mn, mx, stk, HPT_TRACE_BLOCK, t, s, p, nn, np, ne);
         }
     }
     if (shadow) {
@@ -1006,10 +1032,22 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptS
     } else {
         outT[i] = ok ? t : finf();
         outSeg[i] = ok ? (int32_t) s : -1;
-        outP[3 * i] = ok ? (float) p.x : 0.0f;
-        outP[3 * i + 1] = ok ? (float) p.y : 0.0f;
-        outP[3 * i + 2] = ok ? (float) p.z : 0.0f;
+        outP[3 * i] = ok ? p.x : 0.0f;
+        outP[3 * i + 1] = ok ? p.y : 0.0f;
+        outP[3 * i + 2] = ok ? p.z : 0.0f;
     }
+}
+
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptScene sc, int n, const float *o,
+                                                                            const float *d, const float *mint,
+                                                                            const float *maxt, int flags,
+                                                                            float *outT, int32_t *outSeg,
+                                                                            float *outP, uint8_t *outHit) {
+    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    if (flags & 2)
+        traceBatchBody<2>(sc, n, o, d, mint, maxt, flags, outT, outSeg, outP, outHit, stk + threadIdx.x);
+    else
+        traceBatchBody<HPT_STACK>(sc, n, o, d, mint, maxt, flags, outT, outSeg, outP, outHit, stk + threadIdx.x);
 }
 
 extern "C" __global__ void k_bsdf_batch(HptScene sc, int n, const float *wi, const float *wo, const float *u,

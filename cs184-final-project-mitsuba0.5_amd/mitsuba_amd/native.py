@@ -46,7 +46,7 @@ class Stats(C.Structure):
                 ("ms_gather", C.c_double), ("trace_launches", C.c_uint64), ("paths", C.c_uint64),
                 ("closest_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("nodes", C.c_uint64),
                 ("prims", C.c_uint64), ("bounces", C.c_uint64), ("shadow_unoccluded", C.c_uint64),
-                ("waves", C.c_uint64), ("max_bounces", C.c_int)]
+                ("waves", C.c_uint64), ("max_bounces", C.c_int), ("prim_exact", C.c_uint64)]
 
 
 # every symbol declared in include/hairpt.h: (restype, argtypes)
@@ -264,7 +264,7 @@ class Renderer:
                                              _p(oi, _u64), _p(ov, _f)))
         return oi, ov
 
-    def trace(self, o, d, mint, maxt, shadow=False):
+    def trace(self, o, d, mint, maxt, shadow=False, tiny_stack=False):
         o = _f32(o).reshape(-1, 3)
         d = _f32(d).reshape(-1, 3)
         n = o.shape[0]
@@ -274,7 +274,8 @@ class Renderer:
         oiv = np.zeros(n, np.int32)
         op = np.zeros((n, 3), np.float32)
         oh = np.zeros(n, np.uint8)
-        self._check(self.lib.hpt_trace_batch(self.h, n, _p(o, _f), _p(d, _f), _p(mint, _f), _p(maxt, _f), int(shadow),
+        self._check(self.lib.hpt_trace_batch(self.h, n, _p(o, _f), _p(d, _f), _p(mint, _f), _p(maxt, _f),
+                                             (1 if shadow else 0) | (2 if tiny_stack else 0),
                                              _p(ot, _f), _p(oiv, _i32), _p(op, _f), _p(oh, _u8)))
         return oh.astype(bool) if shadow else (ot, oiv, op)
 

@@ -119,6 +119,7 @@ typedef struct hpt_stats {
     uint64_t shadow_unoccluded;    /* shadow rays that reached the emitter */
     uint64_t waves;
     int max_bounces;
+    uint64_t prim_exact;           /* segments that passed the fp32 pre-test (fp64 tests run) */
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 
@@ -138,8 +139,10 @@ int hpt_sobol_batch(hpt_context *ctx, int m, int n, const uint32_t *frame, const
                     const uint32_t *dim, uint64_t *out_index, float *out_value);
 /* ShapeKDTree::rayIntersect closest (skdtree.cpp:112-141) or shadow (:207-226);
    out_iv is the reference's primitive id (first vertex index of the segment) */
+#define HPT_TRACE_SHADOW 1      /* any-hit query (out_hit) instead of closest hit */
+#define HPT_TRACE_TINY_STACK 2  /* test hook: 2-entry traversal stack, forces kd-restarts */
 int hpt_trace_batch(hpt_context *ctx, int n, const float *o, const float *d, const float *mint, const float *maxt,
-                    int shadow, float *out_t, int32_t *out_iv, float *out_p, uint8_t *out_hit);
+                    int flags, float *out_t, int32_t *out_iv, float *out_p, uint8_t *out_hit);
 /* BSDF::eval / pdf / sample for the scene's hair BSDF (local frame) */
 int hpt_bsdf_batch(hpt_context *ctx, int n, const float *wi, const float *wo, const float *u, float *out_eval,
                    float *out_pdf, float *out_wo, float *out_weight, float *out_sample_pdf, uint32_t *out_type);

@@ -61,10 +61,41 @@ def _rays(o, n, seed, width=48, height=40):
     return orig, dirs, mint, maxt
 
 
+def _grazing_rays(r, n, seed, radius):
+    """Rays whose line passes the axis of a random segment at radius * (1 +- 1e-4),
+    from origins 0.05..40 units away: the worst case for the fp32 pre-test
+    (HptSegF in hpt_device.h), which must never reject a segment the exact
+    fp64 test accepts."""
+    rng = np.random.default_rng(seed)
+    xyz, st = r.hair()
+    segs = np.nonzero(st[1:len(xyz)] == 0)[0]
+    s = rng.choice(segs, n)
+    v1, v2 = xyz[s].astype(np.float64), xyz[s + 1].astype(np.float64)
+    axis = (v2 - v1) / np.linalg.norm(v2 - v1, axis=1, keepdims=True)
+    q = rng.normal(size=(n, 3))
+    u = q - axis * np.sum(q * axis, 1, keepdims=True)
+    u /= np.linalg.norm(u, axis=1, keepdims=True)
+    w = np.cross(axis, u)
+    # direction perpendicular to u: mixes the axis and the third frame vector
+    ang = rng.uniform(0.05, np.pi - 0.05, n)[:, None]
+    d = np.cos(ang) * axis + np.sin(ang) * w
+    f = rng.uniform(0, 1, n)[:, None]
+    dist = radius * (1 + rng.uniform(-1e-4, 1e-4, n))[:, None]
+    pt = v1 + f * (v2 - v1) + u * dist
+    L = np.exp(rng.uniform(np.log(0.05), np.log(40.0), n))[:, None]
+    orig = (pt - d * L).astype(np.float32)
+    return orig, d.astype(np.float32), np.full(n, 1e-4, np.float32), np.full(n, np.inf, np.float32)
+
+
 @pytest.mark.parametrize("fixture", ["furball", "straight"])
-def test_trace_bit_exact(fixture, request):
+@pytest.mark.parametrize("kind", ["mixed", "grazing"])
+def test_trace_bit_exact(fixture, kind, request):
     _, r, o = request.getfixturevalue(fixture)
-    orig, dirs, mint, maxt = _rays(o, 40000, 3)
+    if kind == "mixed":
+        orig, dirs, mint, maxt = _rays(o, 40000, 3)
+    else:
+        name = {"furball": "furball_marschner", "straight": "straight_kk"}[fixture]
+        orig, dirs, mint, maxt = _grazing_rays(r, 40000, 5, float(scene_util.scenes.CONFIGS[name]["radius"]))
     gt, giv, gp = r.trace(orig, dirs, mint, maxt)
     ot, oiv, op = o.trace(orig, dirs, mint, maxt)
     assert (oiv >= 0).sum() > 1000
@@ -72,7 +103,13 @@ def test_trace_bit_exact(fixture, request):
     np.testing.assert_array_equal(gt, ot)
     np.testing.assert_array_equal(gp, op)
     sm = np.minimum(maxt, 3.0).astype(np.float32)
-    np.testing.assert_array_equal(r.trace(orig, dirs, mint, sm, shadow=True), o.trace(orig, dirs, mint, sm, shadow=True))
+    osh = o.trace(orig, dirs, mint, sm, shadow=True)
+    np.testing.assert_array_equal(r.trace(orig, dirs, mint, sm, shadow=True), osh)
+    # kd-restart path: a 2-entry stack overflows constantly and must give the same answers
+    tt, tiv, tp = r.trace(orig, dirs, mint, maxt, tiny_stack=True)
+    np.testing.assert_array_equal(tiv, oiv)
+    np.testing.assert_array_equal(tt, ot)
+    np.testing.assert_array_equal(r.trace(orig, dirs, mint, sm, shadow=True, tiny_stack=True), osh)
 
 
 def _dirs(rng, n):
