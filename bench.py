@@ -37,9 +37,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 #   closest ray: queue id 4 + ray 32 + hit record 32 = 68 B
 #   shadow ray:  queue id 4 + origin 16 + direction/maxt 16 = 36 B, +48 B (contribution + radiance RMW)
 #                when unoccluded
-#   node visit 8 B; primitive test 4 B leaf index + 32 B fp32 pre-test record;
+#   node visit 8 B; primitive test 32 B leaf-ordered fp32 pre-test record;
 #   exact fp64 test (pre-test survivors) + 128 B segment record
-BYTES_CLOSEST, BYTES_SHADOW, BYTES_UNOCC, BYTES_NODE, BYTES_PRIM, BYTES_EXACT = 68, 36, 48, 8, 36, 128
+BYTES_CLOSEST, BYTES_SHADOW, BYTES_UNOCC, BYTES_NODE, BYTES_PRIM, BYTES_EXACT = 68, 36, 48, 8, 32, 128
 
 
 def parse():
@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--max-depth", type=int, default=None)
+    ap.add_argument("--kd", default="", help="kd-tree build overrides k=v,... (hair shape kd* properties)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-spp", type=int, default=96, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -99,6 +100,8 @@ def main():
     defines = {"width": W, "height": H, "spp": spp, "maxDepth": max_depth}
     workdir = os.path.join(args.workdir, "r%d" % rank)
     xml = scenes.make_scene(args.config, workdir, n_strands=n)
+    if args.kd:
+        xml = scenes.with_kd_params(xml, dict(kv.split("=") for kv in args.kd.split(",") if kv))
     hair_file = os.path.join(workdir, "%s_%d.mitshair" % (cfg["geom"], n))
 
     r = native.Renderer(device=local)
@@ -109,34 +112,32 @@ def main():
     info = r.info()
     film = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:%d" % local)
 
-    def step():
+    def step(level):
         film.zero_()
         torch.cuda.synchronize()
-        r.render_device(film.data_ptr(), 0, spp, shard=rank, n_shards=world, collect_stats=True)
+        r.render_device(film.data_ptr(), 0, spp, shard=rank, n_shards=world, collect_stats=level)
         if world > 1:
             dist.reduce(film, 0)
 
     for _ in range(args.warmup):
-        step()
+        step(1)
+    # one untimed counted frame: traversal counters for the byte model (the
+    # render is deterministic, so every frame has exactly these counts)
+    step(2)
+    c = r.stats()
+    frame = dict(nodes=c.nodes, prims=c.prims, exact=c.prim_exact, closest=c.closest_rays, shadow=c.shadow_rays,
+                 unocc=c.shadow_unoccluded, bounces=c.bounces, launches=c.trace_launches)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ms_trace = 0.0
     launches = 0
-    tot = dict(nodes=0, prims=0, exact=0, closest=0, shadow=0, unocc=0, bounces=0)
     for _ in range(args.steps):
-        step()
+        step(1)  # HIP events around every kernel (on the library's stream), no counters
         s = r.stats()
         ms_trace += s.ms_trace
         launches += s.trace_launches
-        tot["nodes"] += s.nodes
-        tot["prims"] += s.prims
-        tot["exact"] += s.prim_exact
-        tot["closest"] += s.closest_rays
-        tot["shadow"] += s.shadow_rays
-        tot["unocc"] += s.shadow_unoccluded
-        tot["bounces"] += s.bounces
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -145,6 +146,7 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
+    tot = {k: v * args.steps for k, v in frame.items()}
 
     paths_total = W * H * spp * args.steps
     value = paths_total / dt / 1e6

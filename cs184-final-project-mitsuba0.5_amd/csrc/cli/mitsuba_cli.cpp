@@ -160,7 +160,7 @@ int main(int argc, char **argv) {
                 p.spp_end = spp;
                 p.shard = g;
                 p.n_shards = G;
-                p.collect_stats = o.stats ? 1 : 0;
+                p.collect_stats = o.stats ? 2 : 0;
                 rcs[g] = hpt_render(ctx[g], &p, films[g].data());
             });
         for (auto &t : th) t.join();

@@ -23,6 +23,26 @@ struct Vec3f {
     float x = 0, y = 0, z = 0;
 };
 
+/* SAH kd-tree build parameters.  Defaults are HairKDTree's (hair.cpp:130-136,
+ * gkdtree.h:731-746) except stopPrims: the reference splits down to single
+ * segments; on gfx950 a leaf of up to 4 segments is cheaper to test (fp32
+ * pre-test over contiguous records) than the extra dependent node fetches
+ * (measured: +19% Mpaths/s on the furball).  The scene-level names of scene.cpp:44-78 (kdIntersectionCost,
+ * kdTraversalCost, kdEmptySpaceBonus, kdStopPrims, kdMaxDepth, kdClip,
+ * kdMaxBadRefines) may be set on the hair shape.  The tree never changes a
+ * result (traversal finds the exact closest hit), only the speed. */
+struct KDBuildParams {
+    float traversalCost = 10.0f;
+    float queryCost = 15.0f;
+    float emptySpaceBonus = 0.9f;
+    int stopPrims = 4;             /* reference HairKDTree: 1 */
+    int maxBadRefines = 3;
+    int maxDepth = 0;              /* 0 = automatic: min(8 + 1.3 log2 N, 48) */
+    int bins = 128;                /* min-max bins */
+    bool clip = true;              /* perfect splits via getClippedAABB */
+    int threads = 0;               /* 0 = hardware concurrency */
+};
+
 /* ---- parsed scene description (subset of the Mitsuba 0.5 scene schema) ---- */
 struct SceneDesc {
     /* integrator (integrator.cpp:190-203, path.cpp) */
@@ -47,6 +67,7 @@ struct SceneDesc {
     float radius = 0.025f, angleThreshold = 1.0f, reduction = 0.0f;
     float hairToWorld[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     bool hairHasToWorld = false;
+    KDBuildParams kd;
     /* bsdf */
     std::string bsdf = "";
     float intIOR = 1.5046f, extIOR = 1.000277f;   /* ior.h: bk7 / air defaults */
@@ -93,23 +114,12 @@ struct KDTreeHost {
     std::vector<HptNode> nodes;
     std::vector<uint32_t> prims;          /* segment index per leaf entry */
     std::vector<HptSegment> segs;         /* per segment (index = segment id) */
-    std::vector<HptSegF> segsF;           /* fp32 pre-test records, same indexing */
+    std::vector<HptSegF> leafF;           /* fp32 pre-test records in leaf (prims) order */
     std::vector<uint32_t> segFirstVertex; /* segment id -> first vertex index */
     float aabbMin[3], aabbMax[3];
     int maxDepthUsed = 0;
     size_t leaves = 0, emptyLeaves = 0;
     double buildSeconds = 0;
-};
-
-struct KDBuildParams {
-    float traversalCost = 10.0f;   /* hair.cpp:130-136 */
-    float queryCost = 15.0f;
-    float emptySpaceBonus = 0.9f;
-    int stopPrims = 1;
-    int maxBadRefines = 3;         /* gkdtree.h:731-746 */
-    int bins = 128;                /* min-max bins */
-    bool clip = true;              /* perfect splits via getClippedAABB */
-    int threads = 0;               /* 0 = hardware concurrency */
 };
 
 KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params);

@@ -423,7 +423,6 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
 
     /* double-precision per-segment records (hair.cpp:551-596) */
     t.segs.resize(S);
-    t.segsF.resize(S);
     for (size_t s = 0; s < S; ++s) {
         uint32_t iv = segIv[s];
         auto vd = [&](uint32_t i) {
@@ -456,12 +455,6 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
         }
         r.iv = iv;
         r.pad = 0;
-        HptSegF &f = t.segsF[s];
-        for (int k = 0; k < 3; ++k) {
-            f.v1[k] = hair.xyz[3 * iv + k];
-            f.axis[k] = (float) axis[k];
-        }
-        f.pad[0] = f.pad[1] = 0.0f;
     }
 
     /* primitive bounds + tree AABB (gkdtree.h:990-994) */
@@ -483,11 +476,24 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
     }
     int lg = 0;
     while ((S >> (lg + 1)) != 0) lg++;
-    Builder b{g, segIv, params, std::min((int) (8 + 1.3f * lg), 48)};
+    const int autoDepth = std::min((int) (8 + 1.3f * lg), 48);
+    Builder b{g, segIv, params, params.maxDepth > 0 ? std::min(params.maxDepth, 64) : autoDepth};
     std::unique_ptr<BNode> tree = b.build(std::move(refs), root, 0, 0);
     t.nodes.reserve(2 * S);
     t.nodes.push_back({0, 0});
     flatten(tree.get(), 0, 0, t);
+    /* leaf-ordered fp32 pre-test records */
+    t.leafF.resize(t.prims.size());
+    for (size_t e = 0; e < t.prims.size(); ++e) {
+        const uint32_t s = t.prims[e];
+        HptSegF &f = t.leafF[e];
+        for (int k = 0; k < 3; ++k) {
+            f.v1[k] = hair.xyz[3 * segIv[s] + k];
+            f.axis[k] = (float) t.segs[s].axis[k];
+        }
+        f.seg = s;
+        f.pad = 0;
+    }
     t.buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return t;
 }

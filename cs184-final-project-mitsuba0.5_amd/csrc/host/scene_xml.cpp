@@ -436,6 +436,13 @@ void parseObject(Ctx &c, const XNode &nd, SceneDesc &d) {
         d.radius = num1(p, "radius", 0.025f);
         d.angleThreshold = num1(p, "angleThreshold", 1.0f);
         d.reduction = num1(p, "reduction", 0.0f);
+        d.kd.queryCost = num1(p, "kdIntersectionCost", d.kd.queryCost);
+        d.kd.traversalCost = num1(p, "kdTraversalCost", d.kd.traversalCost);
+        d.kd.emptySpaceBonus = num1(p, "kdEmptySpaceBonus", d.kd.emptySpaceBonus);
+        d.kd.stopPrims = (int) num1(p, "kdStopPrims", (float) d.kd.stopPrims);
+        d.kd.maxDepth = (int) num1(p, "kdMaxDepth", (float) d.kd.maxDepth);
+        d.kd.maxBadRefines = (int) num1(p, "kdMaxBadRefines", (float) d.kd.maxBadRefines);
+        d.kd.clip = num1(p, "kdClip", d.kd.clip ? 1.0f : 0.0f) != 0.0f;
         if (p.xform.count("toWorld")) {
             parseTransform(c, *p.xform["toWorld"], d.hairToWorld);
             d.hairHasToWorld = true;

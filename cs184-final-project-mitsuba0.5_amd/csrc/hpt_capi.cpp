@@ -407,8 +407,7 @@ int hpt_prepare(hpt_context *c) {
         }
         if (c->hairFromFile)
             c->hair = loadHair(c->hairPath, c->hairRadius, c->hairAngle, 0.0f, c->hairHasToWorld ? c->hairToWorld : nullptr);
-        KDBuildParams kp;
-        c->tree = buildHairKDTree(c->hair, kp);
+        c->tree = buildHairKDTree(c->hair, d.kd);
         if (d.bsdf == "marschner") {
             std::string err;
             if (!precomputeMarschner(d, c->dataDir, c->mar, err)) return setErr(c, HPT_EIO, err);
@@ -427,9 +426,8 @@ int hpt_prepare(hpt_context *c) {
     setupCamera(d, sc.cam);
     int r = 0;
     r |= upload(c, c->tree.nodes.data(), c->tree.nodes.size() * sizeof(HptNode), (const void **) &sc.nodes);
-    r |= upload(c, c->tree.prims.data(), c->tree.prims.size() * 4, (const void **) &sc.prims);
+    r |= upload(c, c->tree.leafF.data(), c->tree.leafF.size() * sizeof(HptSegF), (const void **) &sc.leafF);
     r |= upload(c, c->tree.segs.data(), c->tree.segs.size() * sizeof(HptSegment), (const void **) &sc.segs);
-    r |= upload(c, c->tree.segsF.data(), c->tree.segsF.size() * sizeof(HptSegF), (const void **) &sc.segsF);
     for (int i = 0; i < 3; ++i) {
         sc.aabbMin[i] = c->tree.aabbMin[i];
         sc.aabbMax[i] = c->tree.aabbMax[i];
@@ -577,8 +575,9 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     int r = ensureWave(c, waveCap);
     if (r) return r;
     hipStream_t s = c->stream;
-    const bool st = prm->collect_stats != 0;
-    if (st) HIPCHK(c, hipMemsetAsync(c->dstats, 0, 64, s));
+    const bool st = prm->collect_stats != 0;      /* HIP event timing per kernel class */
+    const bool counted = prm->collect_stats >= 2; /* + traversal counters (k_trace_counted) */
+    if (counted) HIPCHK(c, hipMemsetAsync(c->dstats, 0, 64, s));
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evTrace, evOther[6];
     size_t evUsed = 0;
     auto timed = [&](int cls, auto fn) -> hipError_t {
@@ -611,8 +610,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         e = timed(0, [&] { return hpt_launch_camera(sc, w, c->P, c->qTrace, c->counters, s); });
         if (e) break;
         e = timed(-1, [&] {
-            return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, c->counters, st ? (uint32_t *) c->dstats : nullptr,
-                                    w.nPaths, s);
+            return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, c->counters,
+                                    counted ? (uint32_t *) c->dstats : nullptr, w.nPaths, s);
         });
         if (e) break;
         e = timed(1, [&] { return hpt_launch_primary(sc, c->P, c->qTrace, c->qShadeA, c->counters, w.nPaths, s); });
@@ -633,7 +632,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             if (e) break;
             e = timed(-1, [&] {
                 return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, c->counters,
-                                        st ? (uint32_t *) c->dstats : nullptr, 2ull * n, s);
+                                        counted ? (uint32_t *) c->dstats : nullptr, 2ull * n, s);
             });
             if (e) break;
             e = timed(3, [&] { return hpt_launch_post(sc, c->P, c->qTrace, shadeOut, c->counters, n, s); });
@@ -673,6 +672,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         c->stats.ms_shade = sumEv(evOther[2]);
         c->stats.ms_post = sumEv(evOther[3]);
         c->stats.ms_gather = sumEv(evOther[4]);
+    }
+    if (counted) {
         uint64_t hs[8];
         HIPCHK(c, hipMemcpy(hs, c->dstats, 64, hipMemcpyDeviceToHost));
         c->stats.nodes = hs[0];

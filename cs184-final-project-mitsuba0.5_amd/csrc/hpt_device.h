@@ -41,15 +41,18 @@ struct HptSegment {
     uint32_t pad;
 };
 
-/* fp32 shadow of a segment for the conservative pre-test (32 bytes): the
- * ray line must pass within radius of the axis line for the fp64 quadratic
- * to have real roots; the pre-test rejects only when fp32 says the distance
- * exceeds radius by far more than its rounding error, so the set of segments
- * reaching the exact fp64 test is a superset of those that can hit. */
+/* fp32 shadow of a segment for the conservative pre-test (32 bytes), stored
+ * in leaf order (one record per leaf reference, so a leaf's candidates are
+ * contiguous and need no index indirection).  The ray line must pass within
+ * radius of the axis line for the fp64 quadratic to have real roots; the
+ * pre-test rejects only when fp32 says the distance exceeds the radius by far
+ * more than its rounding error, so the set of segments reaching the exact
+ * fp64 test is a superset of those that can hit. */
 struct HptSegF {
     float v1[3];
     float axis[3];
-    float pad[2];
+    uint32_t seg;  /* segment index (into HptScene::segs) */
+    uint32_t pad;
 };
 
 /* kd-tree node, 8 bytes (gkdtree.h:452-583 layout with absolute child index):
@@ -99,9 +102,8 @@ struct HptEnvMap {
 struct HptScene {
     HptCamera cam;
     const HptNode *nodes;
-    const uint32_t *prims;      /* leaf primitive list -> segment index */
+    const HptSegF *leafF;       /* leaf primitive list (fp32 pre-test records) */
     const HptSegment *segs;
-    const HptSegF *segsF;
     float aabbMin[3], aabbMax[3];
     float radius;
     int bsdfKind;               /* 0 = marschner, 1 = kajiyakay */

@@ -105,36 +105,55 @@ HD bool aabbIntersect(const HptScene &sc, V3 o, V3 d, V3 rcp, float &nearT, floa
 /* ------------------------------------------------------------------ */
 /* Hair segment test: HairKDTree::intersect (hair.cpp:485-548) in fp64  */
 /* ------------------------------------------------------------------ */
-HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, const D3 &rayO, const D3 &rayD,
-                     double r2, float mint, float maxt, float &t, V3 &p) {
+/* Register-lean staging: the quadratic needs only v1/axis, the miter tests
+   load n1/v1 and n2/v2 when they are reached, and the memory clobbers keep
+   the scheduler from hoisting those loads (which would keep ~30 extra VGPRs
+   live across the traversal loop).  The arithmetic is operation for
+   operation the reference's (dot = x*x' + y*y' + z*z', no contraction). */
+HD bool insideMiters(const double *__restrict__ rec, D3 q) {
+    asm volatile("" ::: "memory");
+    const D3 v1 = d3(rec[0], rec[1], rec[2]), n1 = d3(rec[6], rec[7], rec[8]);
+    if (!(dot(q - v1, n1) >= 0)) return false;
+    asm volatile("" ::: "memory");
+    const D3 v2 = d3(rec[12], rec[13], rec[14]), n2 = d3(rec[9], rec[10], rec[11]);
+    return dot(q - v2, n2) <= 0;
+}
+
+HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, V3 of, V3 df, double r2, float mint,
+                     float maxt, float &t, V3 &p) {
+    /* keep the fp64 ray out of the traversal loop's live registers: the
+       conversions are re-done per exact test (rare: the fp32 pre-test passes
+       ~2 segments per ray), which the opaque moves below enforce */
+    float ox = of.x, oy = of.y, oz = of.z, dx = df.x, dy = df.y, dz = df.z;
+    asm volatile("" : "+v"(ox), "+v"(oy), "+v"(oz), "+v"(dx), "+v"(dy), "+v"(dz));
+    const D3 rayO = d3(ox, oy, oz), rayD = d3(dx, dy, dz);
     const double *rec = reinterpret_cast<const double *>(segs + s);
-    D3 v1 = d3(rec[0], rec[1], rec[2]);
-    D3 axis = d3(rec[3], rec[4], rec[5]);
-    D3 relOrigin = rayO - v1;
-    D3 projOrigin = relOrigin - axis * dot(axis, relOrigin);
-    D3 projDirection = rayD - axis * dot(axis, rayD);
-    const double A = dot(projDirection, projDirection);
-    const double B = 2 * dot(projOrigin, projDirection);
-    const double C = dot(projOrigin, projOrigin) - r2;
     double nearT, farT;
-    if (!solveQuadraticDouble(A, B, C, nearT, farT)) return false;
+    {
+        const D3 axis = d3(rec[3], rec[4], rec[5]);
+        const D3 relOrigin = rayO - d3(rec[0], rec[1], rec[2]);
+        const D3 projOrigin = relOrigin - axis * dot(axis, relOrigin);
+        const D3 projDirection = rayD - axis * dot(axis, rayD);
+        const double A = dot(projDirection, projDirection);
+        const double B = 2 * dot(projOrigin, projDirection);
+        const double C = dot(projOrigin, projOrigin) - r2;
+        if (!solveQuadraticDouble(A, B, C, nearT, farT)) return false;
+    }
     if (!(nearT <= (double) maxt && farT >= (double) mint)) return false;
-    D3 pointNear = rayO + rayD * nearT;
-    D3 pointFar = rayO + rayD * farT;
-    D3 n1 = d3(rec[6], rec[7], rec[8]);
-    D3 n2 = d3(rec[9], rec[10], rec[11]);
-    D3 v2 = d3(rec[12], rec[13], rec[14]);
-    if (dot(pointNear - v1, n1) >= 0 && dot(pointNear - v2, n2) <= 0 && nearT >= (double) mint) {
+    const D3 pointNear = rayO + rayD * nearT;
+    if (insideMiters(rec, pointNear) && nearT >= (double) mint) {
         p = v3((float) pointNear.x, (float) pointNear.y, (float) pointNear.z);
         t = (float) nearT;
-    } else if (dot(pointFar - v1, n1) >= 0 && dot(pointFar - v2, n2) <= 0) {
+        return true;
+    }
+    const D3 pointFar = rayO + rayD * farT;
+    if (insideMiters(rec, pointFar)) {
         if (farT > (double) maxt) return false;
         p = v3((float) pointFar.x, (float) pointFar.y, (float) pointFar.z);
         t = (float) farT;
-    } else {
-        return false;
+        return true;
     }
-    return true;
+    return false;
 }
 
 /* Conservative fp32 pre-test (see HptSegF): false only when the ray line
@@ -143,9 +162,7 @@ HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, const D3 &
    |computed - exact| of w.n is below 4e-7 (|w| + r) + 2e-7 |w| |n| for
    |n| >= 0.01 (fp32 cross/dot rounding and the fp32-rounded axis), which the
    1e-4 (r + |w|_1) slack covers with two orders of magnitude to spare. */
-HD bool segMayHit(const HptSegF *__restrict__ segsF, uint32_t s, V3 o, V3 d, float r) {
-    const float4 *f = reinterpret_cast<const float4 *>(segsF + s);
-    const float4 a = f[0], b = f[1];
+HD bool segMayHit(const float4 a, const float4 b, V3 o, V3 d, float r) {
     const float wx = o.x - a.x, wy = o.y - a.y, wz = o.z - a.z;
     const float ax = a.w, ay = b.x, az = b.y; /* axis */
     const float nx = d.y * az - d.z * ay, ny = d.z * ax - d.x * az, nz = d.x * ay - d.y * ax;
@@ -155,6 +172,33 @@ HD bool segMayHit(const HptSegF *__restrict__ segsF, uint32_t s, V3 o, V3 d, flo
     const float slack = r + 1e-4f * (r + fabsf(wx) + fabsf(wy) + fabsf(wz));
     return wn * wn <= slack * slack * nn;
 }
+
+#ifdef HPT_EXPERIMENT_FP32
+/* timing experiment only (never the product): the cylinder test in fp32 */
+HD bool segIntersectF32(const HptSegment *__restrict__ segs, uint32_t s, V3 o, V3 d, float r, float mint,
+                        float maxt, float &t, V3 &p) {
+    const float4 *rec = reinterpret_cast<const float4 *>(segs + s);
+    const double *rd = reinterpret_cast<const double *>(segs + s);
+    V3 v1 = v3((float) rd[0], (float) rd[1], (float) rd[2]), axis = v3((float) rd[3], (float) rd[4], (float) rd[5]);
+    V3 rel = o - v1;
+    V3 po = rel - axis * dot(axis, rel), pd = d - axis * dot(axis, d);
+    float A = dot(pd, pd), B = 2 * dot(po, pd), C = dot(po, po) - r * r;
+    float nearT, farT;
+    if (!solveQuadratic(A, B, C, nearT, farT)) return false;
+    if (!(nearT <= maxt && farT >= mint)) return false;
+    V3 n1 = v3((float) rd[6], (float) rd[7], (float) rd[8]), n2 = v3((float) rd[9], (float) rd[10], (float) rd[11]);
+    V3 v2 = v3((float) rd[12], (float) rd[13], (float) rd[14]);
+    V3 pn = o + d * nearT;
+    if (dot(pn - v1, n1) >= 0 && dot(pn - v2, n2) <= 0 && nearT >= mint) { p = pn; t = nearT; return true; }
+    V3 pf = o + d * farT;
+    if (dot(pf - v1, n1) >= 0 && dot(pf - v2, n2) <= 0 && farT <= maxt) { p = pf; t = farT; return true; }
+    (void) rec;
+    return false;
+}
+#define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, p) segIntersectF32(segs, s, o, d, radius, mint, maxt, t, p)
+#else
+#define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, p) segIntersect(segs, s, o, d, r2, mint, maxt, t, p)
+#endif
 
 /* ------------------------------------------------------------------ */
 /* kd-tree traversal (front-to-back, LDS ring stack with kd-restart).   */
@@ -167,8 +211,7 @@ HD bool traverse(const HptScene &sc, V3 o, V3 d, V3 rcp, float mint, float maxt,
                  float &tHit, uint32_t &segHit, V3 &pHit, uint32_t &nNodes, uint32_t &nPrims, uint32_t &nExact) {
     const HptNode *__restrict__ nodes = sc.nodes;
     const float radius = sc.radius;
-    const uint32_t *__restrict__ prims = sc.prims;
-    const D3 rayO = d3(o.x, o.y, o.z), rayD = d3(d.x, d.y, d.z);
+    const float4 *__restrict__ leafF = reinterpret_cast<const float4 *>(sc.leafF);
     const double r2 = (double) (sc.radius * sc.radius); /* Float product (hair.cpp:500) */
     float tmin = mint, tmax = maxt;
     tHit = maxt;
@@ -206,13 +249,14 @@ HD bool traverse(const HptScene &sc, V3 o, V3 d, V3 rcp, float mint, float maxt,
         }
         ++nNodes;
         for (uint32_t e = nd.w0 & 0x7fffffffu, last = nd.w1; e < last; ++e) {
-            const uint32_t s = prims[e];
+            const float4 fa = leafF[2 * e], fb = leafF[2 * e + 1];
             ++nPrims;
-            if (!segMayHit(sc.segsF, s, o, d, radius)) continue;
+            if (!segMayHit(fa, fb, o, d, radius)) continue;
+            const uint32_t s = __float_as_uint(fb.z);
             ++nExact;
             float t;
             V3 p;
-            if (segIntersect(sc.segs, s, rayO, rayD, r2, mint, tHit, t, p)) {
+            if (HPT_SEG_TEST(sc.segs, s, o, d, r2, mint, tHit, t, p)) {
                 if (SHADOW) return true;
                 tHit = t;
                 segHit = s;
@@ -662,7 +706,7 @@ extern "C" __global__ __launch_bounds__(256) void k_camera(HptScene sc, HptWave 
 }
 
 /* closest-hit for traceQ[0, nTrace) and any-hit shadow rays for shadowQ */
-template <int STACK>
+template <int STACK, bool STATS>
 __device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ,
                                           const uint32_t *shadowQ, const uint32_t *counters, uint2 *stk,
                                           int stride, uint32_t *stats) {
@@ -718,7 +762,7 @@ __device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P,
             P.li[id] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
         }
     }
-    if (stats) {
+    if (STATS) {
         /* traversal counters for the algorithmic byte model:
            [0] node visits [1] primitive tests [2] closest rays [3] shadow rays
            [4] unoccluded shadow rays [5] exact fp64 segment tests (pre-test
@@ -744,16 +788,42 @@ __device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P,
     }
 }
 
-#define HPT_TRACE_BLOCK 128
-#define HPT_STACK 16
+/* k_trace launch shape (measured on MI355X, furball 512^2 @ 256 spp):
+   one-wave blocks release their LDS stack as soon as their own rays finish
+   (+10% over 128-thread blocks); a 12-entry ring stack (96 B/lane) lets LDS
+   hold more blocks than the 16-entry one; and a 5-waves/SIMD register target
+   (96 VGPRs, 2 spilled to scratch outside the node loop) beats the natural 98-VGPR
+   allocation at 4 waves/SIMD.  Overridable for experiments (make variant). */
+#ifndef HPT_TRACE_BLOCK
+#define HPT_TRACE_BLOCK 64
+#endif
+#ifndef HPT_STACK
+#define HPT_STACK 12
+#endif
+#ifndef HPT_TRACE_WAVES
+#define HPT_TRACE_WAVES 5
+#endif
+#if HPT_TRACE_WAVES > 0 /* occupancy target (waves per SIMD) for k_trace's register allocation */
+#define HPT_TRACE_OCCUPANCY __attribute__((amdgpu_waves_per_eu(HPT_TRACE_WAVES)))
+#else
+#define HPT_TRACE_OCCUPANCY
+#endif
 
-extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace(HptScene sc, HptPaths P,
-                                                                      const uint32_t *__restrict__ traceQ,
-                                                                      const uint32_t *__restrict__ shadowQ,
-                                                                      const uint32_t *__restrict__ counters,
-                                                                      uint32_t *stats) {
+/* k_trace: production traversal; k_trace_counted: the same plus the
+   traversal counters of the byte model (one counted frame per bench run) */
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
+    HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
+    const uint32_t *__restrict__ counters) {
     __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
-    traceBody<HPT_STACK>(sc, P, traceQ, shadowQ, counters, stk + threadIdx.x, HPT_TRACE_BLOCK, stats);
+    traceBody<HPT_STACK, false>(sc, P, traceQ, shadowQ, counters, stk + threadIdx.x, HPT_TRACE_BLOCK, nullptr);
+}
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(HptScene sc, HptPaths P,
+                                                                              const uint32_t *__restrict__ traceQ,
+                                                                              const uint32_t *__restrict__ shadowQ,
+                                                                              const uint32_t *__restrict__ counters,
+                                                                              uint32_t *stats) {
+    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    traceBody<HPT_STACK, true>(sc, P, traceQ, shadowQ, counters, stk + threadIdx.x, HPT_TRACE_BLOCK, stats);
 }
 
 /* fill the intersection record: hair.cpp:825-862 + skdtree.h:422-427 */
@@ -1128,8 +1198,12 @@ hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPath
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *counters, uint32_t *stats, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_trace, dim3(blocksFor(maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ,
-                       shadowQ, counters, stats);
+    if (stats)
+        hipLaunchKernelGGL(k_trace_counted, dim3(blocksFor(maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc,
+                           P, traceQ, shadowQ, counters, stats);
+    else
+        hipLaunchKernelGGL(k_trace, dim3(blocksFor(maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc, P,
+                           traceQ, shadowQ, counters);
     return hipGetLastError();
 }
 hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,

@@ -83,9 +83,12 @@ SIGNATURES = {
 _lib = None
 
 
-def load_library(path: str = LIB_PATH):
-    """Load libhairpt.so (raises OSError if it was not built -- no fallback)."""
+def load_library(path: str = None):
+    """Load libhairpt.so (raises OSError if it was not built -- no fallback).
+    HAIRPT_LIB selects another build of the same library (kernel experiments)."""
     global _lib
+    if path is None:
+        path = os.environ.get("HAIRPT_LIB") or LIB_PATH
     if _lib is None:
         if not os.path.exists(path):
             raise OSError("libhairpt.so not built at %s (run __graft_entry__.build())" % path)

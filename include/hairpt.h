@@ -100,7 +100,8 @@ typedef struct hpt_render_params {
     int spp_begin, spp_end;        /* render samples [spp_begin, spp_end) of every pixel */
     int shard, n_shards;           /* 32x32 blocks b with b % n_shards == shard (multi-GPU) */
     uint64_t max_wave_paths;       /* 0 = automatic (HBM-sized waves) */
-    int collect_stats;             /* traversal counters + per-kernel HIP event timing */
+    int collect_stats;             /* 0 none, 1 per-kernel HIP event timing,
+                                      2 timing + traversal counters (slower k_trace variant) */
 } hpt_render_params;
 
 /* SamplingIntegrator::render/renderBlock + MIPathTracer::Li + ImageBlock::put

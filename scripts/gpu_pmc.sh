@@ -1,0 +1,17 @@
+#!/bin/bash
+# Occupancy / stall / cache counters of the bench kernels (one rocprofv3 --pmc pass per group).
+# Usage: scripts/gpu_pmc.sh <tag> [bench args...]
+set -eo pipefail
+TAG=${1:-pmc}; shift || true
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/pmc_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+i=0
+for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU" \
+           "TCC_HIT_sum TCC_MISS_sum" ; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/g$i" -o pmc -- \
+      python3 "$ROOT/bench.py" --cpu-baseline off "$@" > "$OUT/g$i.log" 2>&1
+done
+echo "pmc $TAG done"

@@ -173,7 +173,7 @@ def test_render_matches_oracle(fixture, request):
     """Full wavefront render vs the oracle's MIPathTracer::Li restatement."""
     _, r, o = request.getfixturevalue(fixture)
     si = r.info()
-    film = r.render(0, si.spp, collect_stats=True)
+    film = r.render(0, si.spp, collect_stats=2)
     ofilm, ostats = o.render(0, si.spp, width=si.width, height=si.height)
     assert int(ostats[5]) == 0, "EWA lookups that do not reduce to bilinear"
     # the sample weights are identical bit for bit up to summation order
