@@ -158,19 +158,21 @@ HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, V3 of, V3 
 
 /* Conservative fp32 pre-test (see HptSegF): false only when the ray line
    provably passes farther than radius from the segment's axis line, i.e.
-   when the fp64 quadratic of segIntersect has no real root.  Error budget:
-   |computed - exact| of w.n is below 4e-7 (|w| + r) + 2e-7 |w| |n| for
-   |n| >= 0.01 (fp32 cross/dot rounding and the fp32-rounded axis), which the
-   1e-4 (r + |w|_1) slack covers with two orders of magnitude to spare. */
+   when the fp64 quadratic of segIntersect has no real root.  With
+   n = d x axis, the exact condition is |w.n| <= r |n| (w = o - v1).  Error
+   budget (u = 2^-24, |d| = |axis| = 1): rounding of w, of the cross product
+   and of the fp32 axis against the fp64 one moves the computed |w.n| by at
+   most 11u |w|_1 and r|n| by at most 12u r; the test keeps a 4x margin on
+   both (3e-6 (r + |w|_1)) and never divides by |n|, so it holds for rays
+   of any direction, near-parallel ones included. */
 HD bool segMayHit(const float4 a, const float4 b, V3 o, V3 d, float r) {
     const float wx = o.x - a.x, wy = o.y - a.y, wz = o.z - a.z;
     const float ax = a.w, ay = b.x, az = b.y; /* axis */
     const float nx = d.y * az - d.z * ay, ny = d.z * ax - d.x * az, nz = d.x * ay - d.y * ax;
     const float nn = nx * nx + ny * ny + nz * nz;
-    if (nn < 1e-4f) return true; /* near-parallel: leave it to the exact test */
     const float wn = fabsf(wx * nx + wy * ny + wz * nz);
-    const float slack = r + 1e-4f * (r + fabsf(wx) + fabsf(wy) + fabsf(wz));
-    return wn * wn <= slack * slack * nn;
+    /* v_sqrt_f32 (<= 1 ulp) is covered by the 1e-6 relative margin */
+    return wn <= r * __builtin_amdgcn_sqrtf(nn) * 1.000001f + 3e-6f * (r + fabsf(wx) + fabsf(wy) + fabsf(wz));
 }
 
 #ifdef HPT_EXPERIMENT_FP32
@@ -216,8 +218,10 @@ HD bool traverse(const HptScene &sc, V3 o, V3 d, V3 rcp, float mint, float maxt,
     float tmin = mint, tmax = maxt;
     tHit = maxt;
     bool found = false;
+    static_assert((STACK & (STACK - 1)) == 0, "the ring stack index is masked");
     uint32_t node = 0;
-    int sp = 0, top = 0; /* ring buffer: entries [top-sp, top) modulo STACK */
+    uint32_t top = 0; /* ring buffer: entries [top-sp, top) modulo STACK */
+    int sp = 0;
     bool lost = false;
     int restarts = 0, leaves = 0;
     while (true) {
@@ -226,30 +230,43 @@ HD bool traverse(const HptScene &sc, V3 o, V3 d, V3 rcp, float mint, float maxt,
         HptNode nd = nodes[node];
         while (!(nd.w0 & 0x80000000u)) {
             ++nNodes;
-            const int axis = (int) (nd.w0 & 3u);
+            const uint32_t axis = nd.w0 & 3u;
             const uint32_t left = nd.w0 >> 2;
             const float split = __uint_as_float(nd.w1);
-            const float oa = o[axis], da = d[axis];
-            const float tsplit = (split - oa) * rcp[axis];
-            const bool belowFirst = (oa < split) || (oa == split && da <= 0.0f);
-            const uint32_t first = belowFirst ? left : left + 1, second = belowFirst ? left + 1 : left;
-            if (!(tsplit <= tmax) || tsplit <= 0.0f) {
-                node = first;
-            } else if (tsplit < tmin) {
-                node = second;
-            } else {
-                stk[(top % STACK) * stride] = make_uint2(second, __float_as_uint(tmax));
-                top++;
-                if (sp < STACK) sp++;
-                else lost = true;
-                node = first;
-                tmax = tsplit;
-            }
+            /* per-axis selects (v_cndmask), not a dynamically indexed vector */
+            const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+            const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+            const float ra = axis == 0 ? rcp.x : (axis == 1 ? rcp.y : rcp.z);
+            const float tsplit = (split - oa) * ra;
+            /* branch-free front-to-back order (bitwise, so the wave keeps one path) */
+            const bool belowFirst = (oa < split) | ((oa == split) & (da <= 0.0f));
+            const uint32_t first = left + (belowFirst ? 0u : 1u), second = left + (belowFirst ? 1u : 0u);
+            const bool nearOnly = !(tsplit <= tmax) | (tsplit <= 0.0f);
+            const bool farOnly = !nearOnly & (tsplit < tmin);
+            const bool both = !(nearOnly | farOnly);
+            if (both) stk[(top & (STACK - 1)) * stride] = make_uint2(second, __float_as_uint(tmax));
+            lost = lost | (both & (sp == STACK));
+            top += both ? 1u : 0u;
+            sp += (both & (sp < STACK)) ? 1 : 0;
+            node = farOnly ? second : first;
+            tmax = both ? tsplit : tmax;
             nd = nodes[node];
         }
         ++nNodes;
-        for (uint32_t e = nd.w0 & 0x7fffffffu, last = nd.w1; e < last; ++e) {
-            const float4 fa = leafF[2 * e], fb = leafF[2 * e + 1];
+        /* leaf: records are contiguous; the next one is fetched before the
+           current one is tested, so the loads of a leaf overlap */
+        const uint32_t first = nd.w0 & 0x7fffffffu, last = nd.w1;
+        float4 na = make_float4(0, 0, 0, 0), nb = na;
+        if (first < last) {
+            na = leafF[2 * first];
+            nb = leafF[2 * first + 1];
+        }
+        for (uint32_t e = first; e < last; ++e) {
+            const float4 fa = na, fb = nb;
+            if (e + 1 < last) {
+                na = leafF[2 * e + 2];
+                nb = leafF[2 * e + 3];
+            }
             ++nPrims;
             if (!segMayHit(fa, fb, o, d, radius)) continue;
             const uint32_t s = __float_as_uint(fb.z);
@@ -276,7 +293,7 @@ HD bool traverse(const HptScene &sc, V3 o, V3 d, V3 rcp, float mint, float maxt,
         }
         top--;
         sp--;
-        uint2 e = stk[(top % STACK) * stride];
+        uint2 e = stk[(top & (STACK - 1)) * stride];
         node = e.x;
         tmin = tmax;
         tmax = __uint_as_float(e.y);
@@ -790,15 +807,15 @@ __device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P,
 
 /* k_trace launch shape (measured on MI355X, furball 512^2 @ 256 spp):
    one-wave blocks release their LDS stack as soon as their own rays finish
-   (+10% over 128-thread blocks); a 12-entry ring stack (96 B/lane) lets LDS
-   hold more blocks than the 16-entry one; and a 5-waves/SIMD register target
-   (96 VGPRs, 2 spilled to scratch outside the node loop) beats the natural 98-VGPR
-   allocation at 4 waves/SIMD.  Overridable for experiments (make variant). */
+   (+10% over 128-thread blocks); an 8-entry ring stack (64 B/lane, kd-restart
+   on overflow) beats 16 (-5%) and 4 (-11%, +12% node visits) entries; and a
+   5-waves/SIMD register target (96 VGPRs, 2 spilled) beats the natural
+   allocation at 4 waves/SIMD (+12%).  Overridable for experiments (make variant). */
 #ifndef HPT_TRACE_BLOCK
 #define HPT_TRACE_BLOCK 64
 #endif
 #ifndef HPT_STACK
-#define HPT_STACK 12
+#define HPT_STACK 8
 #endif
 #ifndef HPT_TRACE_WAVES
 #define HPT_TRACE_WAVES 5
