@@ -126,7 +126,8 @@ def main():
     step(2)
     c = r.stats()
     frame = dict(nodes=c.nodes, prims=c.prims, exact=c.prim_exact, closest=c.closest_rays, shadow=c.shadow_rays,
-                 unocc=c.shadow_unoccluded, bounces=c.bounces, launches=c.trace_launches)
+                 unocc=c.shadow_unoccluded, bounces=c.bounces, launches=c.trace_launches,
+                 node_slots=c.node_slots, prim_slots=c.prim_slots)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -188,6 +189,8 @@ def main():
                       "nodes_per_ray": round(tot["nodes"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "prims_per_ray": round(tot["prims"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "exact_tests_per_ray": round(tot["exact"] / max(1, tot["closest"] + tot["shadow"]), 2),
+                      "simd_util_nodes": round(tot["nodes"] / max(1, tot["node_slots"]), 3),
+                      "simd_util_prims": round(tot["prims"] / max(1, tot["prim_slots"]), 3),
                       "image_mean": float(img.mean())},
         }
         print(json.dumps(out), flush=True)

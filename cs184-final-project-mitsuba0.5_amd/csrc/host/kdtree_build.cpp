@@ -18,8 +18,9 @@
  * getAABB over all segments, which the traversal uses for its entry clip
  * (hair.cpp:200-217, skdtree.cpp:124).
  *
- * Output layout (hpt_device.h HptNode): depth-first with sibling pairs, so
- * an inner node's children are nodes[left] and nodes[left+1].
+ * Output layout (hpt_device.h HptNode): sibling pairs, so an inner node's
+ * children are nodes[left] and nodes[left+1], packed breadth-first into
+ * 128-byte treelet blocks (layoutTreelets).
  */
 #include <algorithm>
 #include <array>
@@ -383,27 +384,67 @@ struct Builder {
     }
 };
 
-void flatten(const BNode *n, uint32_t idx, int depth, KDTreeHost &t) {
-    t.maxDepthUsed = std::max(t.maxDepthUsed, depth);
-    if (n->axis < 0) {
-        uint32_t start = (uint32_t) t.prims.size();
-        for (uint32_t p : n->prims) t.prims.push_back(p);
-        t.nodes[idx].w0 = 0x80000000u | start;
-        t.nodes[idx].w1 = (uint32_t) t.prims.size();
-        t.leaves++;
-        if (n->prims.empty()) t.emptyLeaves++;
-        return;
+/* Node layout: sibling pairs (16 B) packed into 128-byte blocks (one L2
+ * line) treelet by treelet.  A block is filled breadth-first from a pair, so
+ * a ray descending through the top three levels below it touches one line;
+ * when a treelet ends before its block is full, the next pending treelet
+ * continues in the same block (no padding).  Node 0 is the root, node 1 an
+ * unused slot that keeps every pair 16-byte aligned. */
+void layoutTreelets(const BNode *root, KDTreeHost &t) {
+    const uint32_t kPairsPerBlock = 8;
+    t.nodes.assign(2, HptNode{0x80000000u, 0u});
+    struct Item {
+        const BNode *n;
+        uint32_t idx;
+        int depth;
+    };
+    auto emit = [&](const Item &it) {
+        t.maxDepthUsed = std::max(t.maxDepthUsed, it.depth);
+        if (it.n->axis < 0) {
+            uint32_t start = (uint32_t) t.prims.size();
+            for (uint32_t p : it.n->prims) t.prims.push_back(p);
+            t.nodes[it.idx].w0 = 0x80000000u | start;
+            t.nodes[it.idx].w1 = (uint32_t) t.prims.size();
+            t.leaves++;
+            if (it.n->prims.empty()) t.emptyLeaves++;
+            return false;
+        }
+        return true;
+    };
+    std::vector<Item> pending; /* inner nodes whose child pair is not placed yet (FIFO) */
+    size_t head = 0;
+    if (emit({root, 0, 0})) pending.push_back({root, 0, 0});
+    uint32_t used = 1; /* pairs used in the current block (slot 0 = root + pad) */
+    while (head < pending.size()) {
+        /* one treelet: breadth-first from pending[head] while the block has room */
+        std::vector<Item> local{pending[head++]};
+        size_t lh = 0;
+        while (lh < local.size()) {
+            if (used == kPairsPerBlock) {
+                used = 0; /* block full: the rest of this treelet starts later blocks */
+                for (size_t i = lh; i < local.size(); ++i) pending.push_back(local[i]);
+                break;
+            }
+            const Item it = local[lh++];
+            const uint32_t left = (uint32_t) t.nodes.size();
+            if (left >= (1u << 29)) throw std::runtime_error("kd-tree too large");
+            t.nodes.push_back({0, 0});
+            t.nodes.push_back({0, 0});
+            ++used;
+            uint32_t sb;
+            std::memcpy(&sb, &it.n->split, 4);
+            t.nodes[it.idx].w0 = (left << 2) | (uint32_t) it.n->axis;
+            t.nodes[it.idx].w1 = sb;
+            for (int k = 0; k < 2; ++k) {
+                Item c{it.n->kid[k].get(), left + (uint32_t) k, it.depth + 1};
+                if (emit(c)) local.push_back(c);
+            }
+        }
+        if (head > (1u << 20) && head * 2 > pending.size()) { /* compact the FIFO */
+            pending.erase(pending.begin(), pending.begin() + (std::ptrdiff_t) head);
+            head = 0;
+        }
     }
-    uint32_t left = (uint32_t) t.nodes.size();
-    if (left >= (1u << 29)) throw std::runtime_error("kd-tree too large");
-    t.nodes.push_back({0, 0});
-    t.nodes.push_back({0, 0});
-    uint32_t sb;
-    std::memcpy(&sb, &n->split, 4);
-    t.nodes[idx].w0 = (left << 2) | (uint32_t) n->axis;
-    t.nodes[idx].w1 = sb;
-    flatten(n->kid[0].get(), left, depth + 1, t);
-    flatten(n->kid[1].get(), left + 1, depth + 1, t);
 }
 
 } // namespace
@@ -480,8 +521,7 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
     Builder b{g, segIv, params, params.maxDepth > 0 ? std::min(params.maxDepth, 64) : autoDepth};
     std::unique_ptr<BNode> tree = b.build(std::move(refs), root, 0, 0);
     t.nodes.reserve(2 * S);
-    t.nodes.push_back({0, 0});
-    flatten(tree.get(), 0, 0, t);
+    layoutTreelets(tree.get(), t);
     /* leaf-ordered fp32 pre-test records */
     t.leafF.resize(t.prims.size());
     for (size_t e = 0; e < t.prims.size(); ++e) {

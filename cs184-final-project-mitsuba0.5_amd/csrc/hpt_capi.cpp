@@ -682,6 +682,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         c->stats.shadow_rays = hs[3];
         c->stats.shadow_unoccluded = hs[4];
         c->stats.prim_exact = hs[5];
+        c->stats.node_slots = hs[6];
+        c->stats.prim_slots = hs[7];
     }
     c->stats.bounces = bounces;
     c->stats.max_bounces = maxB;
@@ -816,7 +818,8 @@ int hpt_trace_batch(hpt_context *c, int n, const float *o, const float *d, const
     float *dt = S.in<float>(nullptr, n), *dp = S.in<float>(nullptr, 3 * (size_t) n);
     int32_t *ds = S.in<int32_t>(nullptr, n);
     uint8_t *dh = S.in<uint8_t>(nullptr, n);
-    HIPCHK(c, hpt_launch_trace_batch(c->sc, n, a, b, mi, ma, flags, dt, ds, dp, dh, c->stream));
+    uint32_t *cur = S.in<uint32_t>(nullptr, 1);
+    HIPCHK(c, hpt_launch_trace_batch(c->sc, n, a, b, mi, ma, flags, dt, ds, dp, dh, cur, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (shadow) {
         fetch(oh, dh, n);

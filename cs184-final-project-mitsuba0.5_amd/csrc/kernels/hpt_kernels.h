@@ -14,6 +14,7 @@
 #define HPT_Q_SHADE_IN 2
 #define HPT_Q_SHADE_OUT 3
 #define HPT_Q_ERROR 4     /* set when a path runs out of Sobol dimensions */
+#define HPT_Q_CURSOR 5    /* k_trace work cursor (persistent waves claim rays from it) */
 #define HPT_Q_COUNT 8
 
 /* One wave of paths: every pixel of this shard's 32x32 blocks x samples
@@ -47,7 +48,7 @@ struct HptPaths {
 hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPaths &P, uint32_t *traceQ,
                              uint32_t *counters, hipStream_t s);
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
-                            const uint32_t *counters, uint32_t *stats, uint64_t maxItems, hipStream_t s);
+                            uint32_t *counters, uint32_t *stats, uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
                               uint32_t *counters, uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *traceQ,
@@ -59,8 +60,8 @@ hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPath
 hipError_t hpt_launch_sobol_batch(const HptScene &sc, int m, int n, const uint32_t *frame, const uint32_t *px,
                                   const uint32_t *py, const uint32_t *dim, uint64_t *oi, float *ov, hipStream_t s);
 hipError_t hpt_launch_trace_batch(const HptScene &sc, int n, const float *o, const float *d, const float *mint,
-                                  const float *maxt, int shadow, float *ot, int32_t *os, float *op, uint8_t *oh,
-                                  hipStream_t s);
+                                  const float *maxt, int flags, float *ot, int32_t *os, float *op, uint8_t *oh,
+                                  uint32_t *cursor, hipStream_t s);
 hipError_t hpt_launch_bsdf_batch(const HptScene &sc, int n, const float *wi, const float *wo, const float *u,
                                  float *oe, float *op, float *owo, float *ow, float *osp, uint32_t *ot, hipStream_t s);
 hipError_t hpt_launch_env_batch(const HptScene &sc, int n, const float *refp, const float *u, const float *dq,

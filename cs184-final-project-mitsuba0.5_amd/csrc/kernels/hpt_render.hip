@@ -25,6 +25,8 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "../hpt_device.h"
 #include "hpt_kernels.h"
 #include "hpt_math.h"
@@ -202,104 +204,238 @@ HD bool segIntersectF32(const HptSegment *__restrict__ segs, uint32_t s, V3 o, V
 #define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, p) segIntersect(segs, s, o, d, r2, mint, maxt, t, p)
 #endif
 
+/* adaptive ray epsilon: skdtree.cpp:126-129 (closest) / :213-216 (shadow) */
+HD float adaptiveMint(V3 o, float mint, bool shadow) {
+    if (mint != kEpsilon) return mint;
+    float m = fmaxr(fmaxr(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
+    if (!shadow) m = fmaxr(m, kEpsilon);
+    return mint * m;
+}
+
 /* ------------------------------------------------------------------ */
-/* kd-tree traversal (front-to-back, LDS ring stack with kd-restart).   */
-/* Primitive tests use the ray's [mint, best t] interval exactly like   */
-/* rayIntersectHavran (sahkdtree3.h:275-297), so the closest hit does    */
-/* not depend on the tree or on the traversal order.                     */
+/* kd-tree traversal (front-to-back, LDS ring stack with kd-restart),   */
+/* as a resumable per-lane state machine so persistent waves can refill */
+/* finished lanes with new rays.  Primitive tests use the ray's [mint,  */
+/* best t] interval exactly like rayIntersectHavran (sahkdtree3.h:      */
+/* 275-297), so the closest hit does not depend on the tree or on the   */
+/* traversal order.                                                      */
 /* ------------------------------------------------------------------ */
-template <int STACK, bool SHADOW>
-HD bool traverse(const HptScene &sc, V3 o, V3 d, V3 rcp, float mint, float maxt, uint2 *stk, int stride,
-                 float &tHit, uint32_t &segHit, V3 &pHit, uint32_t &nNodes, uint32_t &nPrims, uint32_t &nExact) {
-    const HptNode *__restrict__ nodes = sc.nodes;
-    const float radius = sc.radius;
-    const float4 *__restrict__ leafF = reinterpret_cast<const float4 *>(sc.leafF);
-    const double r2 = (double) (sc.radius * sc.radius); /* Float product (hair.cpp:500) */
-    float tmin = mint, tmax = maxt;
-    tHit = maxt;
-    bool found = false;
+struct TraceRay {
+    V3 o, d, rcp;
+    float mint, maxt;   /* ray interval after the scene-AABB clip and adaptive epsilon */
+    float tmin, tmax;   /* interval of the current subtree */
+    float tHit;
+    V3 pHit;
+    uint32_t node, top, segHit;
+    int sp, restarts, leaves;
+    bool lost, found, shadow;
+};
+
+/* ShapeKDTree::rayIntersect / rayIntersect(shadow) prologue: scene AABB
+   clip + adaptive ray epsilon (skdtree.cpp:112-141, :207-226).  False when
+   there is nothing to traverse (the ray misses). */
+HD bool beginRay(const HptScene &sc, TraceRay &r, V3 o, V3 d, float rmint, float rmaxt, bool shadow) {
+    r.o = o;
+    r.d = d;
+    r.rcp = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    r.shadow = shadow;
+    r.found = false;
+    r.tHit = finf();
+    r.segHit = 0;
+    r.pHit = v3(0.0f, 0.0f, 0.0f);
+    float mint, maxt;
+    if (!aabbIntersect(sc, o, d, r.rcp, mint, maxt)) return false;
+    const float rayMinT = adaptiveMint(o, rmint, shadow);
+    if (rayMinT > mint) mint = rayMinT;
+    if (rmaxt < maxt) maxt = rmaxt;
+    if (!(maxt > mint)) return false;
+    r.mint = r.tmin = mint;
+    r.maxt = r.tmax = r.tHit = maxt;
+    r.node = 0;
+    r.top = 0;
+    r.sp = 0;
+    r.restarts = 0;
+    r.leaves = 0;
+    r.lost = false;
+    return true;
+}
+
+struct TraceCounters {
+    uint32_t nodes = 0, prims = 0, exact = 0, nodeSlots = 0, primSlots = 0;
+};
+
+HD bool waveLeader() { return __lane_id() == (uint32_t) (__ffsll((unsigned long long) __ballot(1)) - 1); }
+
+/* One round: descend to the next leaf, test its segments, pop.  Returns
+   true when the ray is finished (r.found / r.tHit / r.segHit / r.pHit hold
+   the answer). */
+template <int STACK, bool STATS>
+HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, TraceCounters &tc) {
     static_assert((STACK & (STACK - 1)) == 0, "the ring stack index is masked");
-    uint32_t node = 0;
-    uint32_t top = 0; /* ring buffer: entries [top-sp, top) modulo STACK */
-    int sp = 0;
-    bool lost = false;
-    int restarts = 0, leaves = 0;
+    const HptNode *__restrict__ nodes = sc.nodes;
+    const float4 *__restrict__ leafF = reinterpret_cast<const float4 *>(sc.leafF);
+    /* hard bound so every wave drains even on a malformed tree */
+    if (++r.leaves > (1 << 18)) return true;
+    HptNode nd = nodes[r.node];
+    while (!(nd.w0 & 0x80000000u)) {
+        if (STATS) {
+            ++tc.nodes;
+            if (waveLeader()) tc.nodeSlots += 64;
+        }
+        const uint32_t axis = nd.w0 & 3u;
+        const uint32_t left = nd.w0 >> 2;
+        const float split = __uint_as_float(nd.w1);
+        /* per-axis selects (v_cndmask), not a dynamically indexed vector */
+        const float oa = axis == 0 ? r.o.x : (axis == 1 ? r.o.y : r.o.z);
+        const float da = axis == 0 ? r.d.x : (axis == 1 ? r.d.y : r.d.z);
+        const float ra = axis == 0 ? r.rcp.x : (axis == 1 ? r.rcp.y : r.rcp.z);
+        const float tsplit = (split - oa) * ra;
+        /* branch-free front-to-back order (bitwise, so the wave keeps one path) */
+        const bool belowFirst = (oa < split) | ((oa == split) & (da <= 0.0f));
+        const uint32_t first = left + (belowFirst ? 0u : 1u), second = left + (belowFirst ? 1u : 0u);
+        const bool nearOnly = !(tsplit <= r.tmax) | (tsplit <= 0.0f);
+        const bool farOnly = !nearOnly & (tsplit < r.tmin);
+        const bool both = !(nearOnly | farOnly);
+        if (both) stk[(r.top & (STACK - 1)) * stride] = make_uint2(second, __float_as_uint(r.tmax));
+        r.lost = r.lost | (both & (r.sp == STACK));
+        r.top += both ? 1u : 0u;
+        r.sp += (both & (r.sp < STACK)) ? 1 : 0;
+        r.node = farOnly ? second : first;
+        r.tmax = both ? tsplit : r.tmax;
+        nd = nodes[r.node];
+    }
+    if (STATS) {
+        ++tc.nodes;
+        if (waveLeader()) tc.nodeSlots += 64;
+    }
+    /* leaf: records are contiguous; the next one is fetched before the
+       current one is tested, so the loads of a leaf overlap */
+    const uint32_t first = nd.w0 & 0x7fffffffu, last = nd.w1;
+    float4 na = make_float4(0, 0, 0, 0), nb = na;
+    if (first < last) {
+        na = leafF[2 * first];
+        nb = leafF[2 * first + 1];
+    }
+    const double r2 = (double) (sc.radius * sc.radius); /* Float product (hair.cpp:500) */
+    for (uint32_t e = first; e < last; ++e) {
+        const float4 fa = na, fb = nb;
+        if (e + 1 < last) {
+            na = leafF[2 * e + 2];
+            nb = leafF[2 * e + 3];
+        }
+        if (STATS) {
+            ++tc.prims;
+            if (waveLeader()) tc.primSlots += 64;
+        }
+        if (!segMayHit(fa, fb, r.o, r.d, sc.radius)) continue;
+        const uint32_t s = __float_as_uint(fb.z);
+        if (STATS) ++tc.exact;
+        float t;
+        V3 p;
+        if (HPT_SEG_TEST(sc.segs, s, r.o, r.d, r2, r.mint, r.tHit, t, p)) {
+            r.found = true;
+            if (r.shadow) return true;
+            r.tHit = t;
+            r.segHit = s;
+            r.pHit = p;
+        }
+    }
+    if (r.found && r.tHit <= r.tmax) return true;
+    if (r.sp == 0) {
+        if (!r.lost || r.tmax >= r.maxt || ++r.restarts > 64) return true;
+        /* kd-restart from the root for the remaining interval */
+        r.lost = false;
+        r.node = 0;
+        r.tmin = r.tmax;
+        r.tmax = r.maxt;
+        return false;
+    }
+    r.top--;
+    r.sp--;
+    const uint2 e = stk[(r.top & (STACK - 1)) * stride];
+    r.node = e.x;
+    r.tmin = r.tmax;
+    r.tmax = __uint_as_float(e.y);
+    return r.tmin > r.tHit;
+}
+
+#ifndef HPT_REFILL
+#define HPT_REFILL 16 /* idle lanes that trigger a refill of the wave */
+#endif
+
+/* Persistent traversal: each wave keeps its 64 lanes busy by claiming new
+   rays (one atomic per refill) whenever HPT_REFILL lanes have finished.
+   IO supplies count(), begin(k, r) (load ray k; false = nothing to trace)
+   and finish(k, r).  Every wave exits once the cursor passes the total and
+   its lanes have drained, so the grid always completes. */
+template <int STACK, bool STATS, class IO>
+__device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint32_t *cursor, uint2 *stk,
+                                                uint32_t *stats) {
+    const uint32_t total = io.count();
+    const uint32_t lane = __lane_id();
+    TraceRay r;
+    TraceCounters tc;
+    uint32_t item = 0, nC = 0, nS = 0, nU = 0;
+    bool active = false, exhausted = false;
     while (true) {
-        /* hard bounds so every wave drains even on a malformed tree */
-        if (++leaves > (1 << 18)) break;
-        HptNode nd = nodes[node];
-        while (!(nd.w0 & 0x80000000u)) {
-            ++nNodes;
-            const uint32_t axis = nd.w0 & 3u;
-            const uint32_t left = nd.w0 >> 2;
-            const float split = __uint_as_float(nd.w1);
-            /* per-axis selects (v_cndmask), not a dynamically indexed vector */
-            const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
-            const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
-            const float ra = axis == 0 ? rcp.x : (axis == 1 ? rcp.y : rcp.z);
-            const float tsplit = (split - oa) * ra;
-            /* branch-free front-to-back order (bitwise, so the wave keeps one path) */
-            const bool belowFirst = (oa < split) | ((oa == split) & (da <= 0.0f));
-            const uint32_t first = left + (belowFirst ? 0u : 1u), second = left + (belowFirst ? 1u : 0u);
-            const bool nearOnly = !(tsplit <= tmax) | (tsplit <= 0.0f);
-            const bool farOnly = !nearOnly & (tsplit < tmin);
-            const bool both = !(nearOnly | farOnly);
-            if (both) stk[(top & (STACK - 1)) * stride] = make_uint2(second, __float_as_uint(tmax));
-            lost = lost | (both & (sp == STACK));
-            top += both ? 1u : 0u;
-            sp += (both & (sp < STACK)) ? 1 : 0;
-            node = farOnly ? second : first;
-            tmax = both ? tsplit : tmax;
-            nd = nodes[node];
-        }
-        ++nNodes;
-        /* leaf: records are contiguous; the next one is fetched before the
-           current one is tested, so the loads of a leaf overlap */
-        const uint32_t first = nd.w0 & 0x7fffffffu, last = nd.w1;
-        float4 na = make_float4(0, 0, 0, 0), nb = na;
-        if (first < last) {
-            na = leafF[2 * first];
-            nb = leafF[2 * first + 1];
-        }
-        for (uint32_t e = first; e < last; ++e) {
-            const float4 fa = na, fb = nb;
-            if (e + 1 < last) {
-                na = leafF[2 * e + 2];
-                nb = leafF[2 * e + 3];
-            }
-            ++nPrims;
-            if (!segMayHit(fa, fb, o, d, radius)) continue;
-            const uint32_t s = __float_as_uint(fb.z);
-            ++nExact;
-            float t;
-            V3 p;
-            if (HPT_SEG_TEST(sc.segs, s, o, d, r2, mint, tHit, t, p)) {
-                if (SHADOW) return true;
-                tHit = t;
-                segHit = s;
-                pHit = p;
-                found = true;
+        const uint64_t idle = __ballot(!active);
+        if (!exhausted && __popcll(idle) >= HPT_REFILL) {
+            const uint32_t n = (uint32_t) __popcll(idle);
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(cursor, n);
+            base = __shfl(base, 0);
+            exhausted = base + n >= total;
+            if (!active) {
+                const uint32_t k = base + (uint32_t) __popcll(idle & ((1ull << lane) - 1ull));
+                if (k < total) {
+                    item = k;
+                    active = io.begin(sc, k, r);
+                    if (STATS) {
+                        nC += r.shadow ? 0u : 1u;
+                        nS += r.shadow ? 1u : 0u;
+                    }
+                    if (!active) nU += io.finish(k, r);
+                }
             }
         }
-        if (found && tHit <= tmax) break;
-        if (sp == 0) {
-            if (!lost || tmax >= maxt || ++restarts > 64) break;
-            /* kd-restart from the root for the remaining interval */
-            lost = false;
-            node = 0;
-            tmin = tmax;
-            tmax = maxt;
+        if (__ballot(active) == 0) {
+            if (exhausted) break;
             continue;
         }
-        top--;
-        sp--;
-        uint2 e = stk[(top & (STACK - 1)) * stride];
-        node = e.x;
-        tmin = tmax;
-        tmax = __uint_as_float(e.y);
-        if (tmin > tHit) break;
+        if (active && traceRound<STACK, STATS>(sc, r, stk, 64, tc)) {
+            nU += io.finish(item, r);
+            active = false;
+        }
     }
-    return found;
+    if (STATS) {
+        /* traversal counters for the algorithmic byte model (DESIGN.md):
+           [0] node visits [1] primitive tests [2] closest rays [3] shadow rays
+           [4] unoccluded shadow rays [5] exact fp64 segment tests (pre-test
+           survivors) [6]/[7] SIMD slots of the node / primitive loops (64
+           per wave iteration: [0]/[6] is the lane utilisation); per-wave
+           reduction, one atomic each */
+        for (int off = 32; off > 0; off >>= 1) {
+            tc.nodes += __shfl_down(tc.nodes, off);
+            tc.prims += __shfl_down(tc.prims, off);
+            tc.exact += __shfl_down(tc.exact, off);
+            tc.nodeSlots += __shfl_down(tc.nodeSlots, off);
+            tc.primSlots += __shfl_down(tc.primSlots, off);
+            nC += __shfl_down(nC, off);
+            nS += __shfl_down(nS, off);
+            nU += __shfl_down(nU, off);
+        }
+        if (lane == 0) {
+            unsigned long long *st = (unsigned long long *) stats;
+            atomicAdd(&st[0], (unsigned long long) tc.nodes);
+            atomicAdd(&st[1], (unsigned long long) tc.prims);
+            atomicAdd(&st[2], (unsigned long long) nC);
+            atomicAdd(&st[3], (unsigned long long) nS);
+            atomicAdd(&st[4], (unsigned long long) nU);
+            atomicAdd(&st[5], (unsigned long long) tc.exact);
+            atomicAdd(&st[6], (unsigned long long) tc.nodeSlots);
+            atomicAdd(&st[7], (unsigned long long) tc.primSlots);
+        }
+    }
 }
 
 /* ------------------------------------------------------------------ */
@@ -640,13 +776,6 @@ HD float miWeight(float pdfA, float pdfB) { /* path.cpp:296-300 */
     return pdfA / (pdfA + pdfB);
 }
 
-/* adaptive ray epsilon: skdtree.cpp:126-129 (closest) / :213-216 (shadow) */
-HD float adaptiveMint(V3 o, float mint, bool shadow) {
-    if (mint != kEpsilon) return mint;
-    float m = fmaxr(fmaxr(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
-    if (!shadow) m = fmaxr(m, kEpsilon);
-    return mint * m;
-}
 
 /* append to a queue: one atomic per wave (wave64 ballot + mbcnt) */
 HD void qpush(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
@@ -722,88 +851,38 @@ extern "C" __global__ __launch_bounds__(256) void k_camera(HptScene sc, HptWave 
     qpush(valid, id, traceQ, &counters[HPT_Q_TRACE]);
 }
 
-/* closest-hit for traceQ[0, nTrace) and any-hit shadow rays for shadowQ */
-template <int STACK, bool STATS>
-__device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ,
-                                          const uint32_t *shadowQ, const uint32_t *counters, uint2 *stk,
-                                          int stride, uint32_t *stats) {
-    const uint32_t nTrace = counters[HPT_Q_TRACE], nShadow = counters[HPT_Q_SHADOW];
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t nNodes = 0, nPrims = 0, nExact = 0, nU = 0;
-    if (tid < nTrace) {
-        const uint32_t id = traceQ[tid];
-        float4 ro = P.ro[id], rd = P.rd[id];
-        V3 o = v3(ro.x, ro.y, ro.z), d = v3(rd.x, rd.y, rd.z);
-        V3 rcp = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-        float mint, maxt;
-        float rmint = ro.w, rmaxt = rd.w;
-        int32_t seg = -1;
-        float thit = finf();
-        V3 p = v3(0.0f, 0.0f, 0.0f);
-        if (aabbIntersect(sc, o, d, rcp, mint, maxt)) {
-            float rayMinT = adaptiveMint(o, rmint, false);
-            if (rayMinT > mint) mint = rayMinT;
-            if (rmaxt < maxt) maxt = rmaxt;
-            if (maxt > mint) {
-                float t;
-                uint32_t s = 0;
-                if (traverse<STACK, false>(sc, o, d, rcp, mint, maxt, stk, stride, t, s, p, nNodes, nPrims, nExact)) {
-                    seg = (int32_t) s;
-                    thit = t;
-                }
-            }
+/* k_trace: the wave's closest-hit rays (traceQ[0, nTrace)) then its any-hit
+   shadow rays (shadowQ) as one persistent grid; k_trace_counted adds the
+   traversal counters of the byte model (one counted frame per bench run) */
+struct PathIO {
+    HptPaths P;
+    const uint32_t *traceQ, *shadowQ;
+    uint32_t nTrace, nShadow, id;
+    HD uint32_t count() const { return nTrace + nShadow; }
+    HD bool begin(const HptScene &sc, uint32_t k, TraceRay &r) {
+        if (k < nTrace) {
+            id = traceQ[k];
+            const float4 ro = P.ro[id], rd = P.rd[id];
+            return beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(rd.x, rd.y, rd.z), ro.w, rd.w, false);
         }
-        P.hit[id] = make_float4(__int_as_float(seg), thit, 0.0f, 0.0f);
-        P.hitp[id] = make_float4(p.x, p.y, p.z, 0.0f);
-    } else if (tid < nTrace + nShadow) {
-        const uint32_t id = shadowQ[tid - nTrace];
-        float4 ro = P.ro[id], sd = P.sdir[id];
-        V3 o = v3(ro.x, ro.y, ro.z), d = v3(sd.x, sd.y, sd.z);
-        V3 rcp = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-        float mint, maxt;
-        bool occluded = false;
-        if (aabbIntersect(sc, o, d, rcp, mint, maxt)) {
-            float rayMinT = adaptiveMint(o, kEpsilon, true);
-            if (rayMinT > mint) mint = rayMinT;
-            if (sd.w < maxt) maxt = sd.w;
-            if (maxt > mint) {
-                float t;
-                uint32_t s;
-                V3 p;
-                occluded = traverse<STACK, true>(sc, o, d, rcp, mint, maxt, stk, stride, t, s, p, nNodes, nPrims, nExact);
-            }
-        }
-        if (!occluded) {
-            nU = 1;
-            float4 c = P.scontrib[id], l = P.li[id];
-            P.li[id] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
-        }
+        id = shadowQ[k - nTrace];
+        const float4 ro = P.ro[id], sd = P.sdir[id];
+        return beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(sd.x, sd.y, sd.z), kEpsilon, sd.w, true);
     }
-    if (STATS) {
-        /* traversal counters for the algorithmic byte model (DESIGN.md):
-           [0] node visits [1] primitive tests [2] closest rays [3] shadow rays
-           [4] unoccluded shadow rays [5] exact fp64 segment tests (pre-test
-           survivors); per-wave reduction, one atomic each */
-        uint32_t nC = tid < nTrace ? 1u : 0u, nS = (tid >= nTrace && tid < nTrace + nShadow) ? 1u : 0u;
-        for (int off = 32; off > 0; off >>= 1) {
-            nNodes += __shfl_down(nNodes, off);
-            nPrims += __shfl_down(nPrims, off);
-            nC += __shfl_down(nC, off);
-            nS += __shfl_down(nS, off);
-            nU += __shfl_down(nU, off);
-            nExact += __shfl_down(nExact, off);
+    /* returns 1 for an unoccluded shadow ray */
+    HD uint32_t finish(uint32_t k, const TraceRay &r) {
+        if (!r.shadow) {
+            P.hit[id] = make_float4(__int_as_float(r.found ? (int32_t) r.segHit : -1), r.found ? r.tHit : finf(),
+                                    0.0f, 0.0f);
+            P.hitp[id] = r.found ? make_float4(r.pHit.x, r.pHit.y, r.pHit.z, 0.0f) : make_float4(0, 0, 0, 0);
+            return 0;
         }
-        if (__lane_id() == 0 && (nC | nS)) {
-            unsigned long long *st = (unsigned long long *) stats;
-            atomicAdd(&st[0], (unsigned long long) nNodes);
-            atomicAdd(&st[1], (unsigned long long) nPrims);
-            atomicAdd(&st[2], (unsigned long long) nC);
-            atomicAdd(&st[3], (unsigned long long) nS);
-            atomicAdd(&st[4], (unsigned long long) nU);
-            atomicAdd(&st[5], (unsigned long long) nExact);
-        }
+        if (r.found) return 0;
+        const float4 c = P.scontrib[id], l = P.li[id];
+        P.li[id] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
+        return 1;
     }
-}
+};
 
 /* k_trace launch shape (measured on MI355X, furball 512^2 @ 256 spp):
    one-wave blocks release their LDS stack as soon as their own rays finish
@@ -826,21 +905,21 @@ __device__ __forceinline__ void traceBody(const HptScene &sc, const HptPaths &P,
 #define HPT_TRACE_OCCUPANCY
 #endif
 
-/* k_trace: production traversal; k_trace_counted: the same plus the
-   traversal counters of the byte model (one counted frame per bench run) */
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
-    const uint32_t *__restrict__ counters) {
+    uint32_t *__restrict__ counters) {
     __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
-    traceBody<HPT_STACK, false>(sc, P, traceQ, shadowQ, counters, stk + threadIdx.x, HPT_TRACE_BLOCK, nullptr);
+    PathIO io{P, traceQ, shadowQ, counters[HPT_Q_TRACE], counters[HPT_Q_SHADOW], 0};
+    tracePersistent<HPT_STACK, false>(sc, io, &counters[HPT_Q_CURSOR], stk + threadIdx.x, nullptr);
 }
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(HptScene sc, HptPaths P,
                                                                               const uint32_t *__restrict__ traceQ,
                                                                               const uint32_t *__restrict__ shadowQ,
-                                                                              const uint32_t *__restrict__ counters,
+                                                                              uint32_t *__restrict__ counters,
                                                                               uint32_t *stats) {
     __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
-    traceBody<HPT_STACK, true>(sc, P, traceQ, shadowQ, counters, stk + threadIdx.x, HPT_TRACE_BLOCK, stats);
+    PathIO io{P, traceQ, shadowQ, counters[HPT_Q_TRACE], counters[HPT_Q_SHADOW], 0};
+    tracePersistent<HPT_STACK, true>(sc, io, &counters[HPT_Q_CURSOR], stk + threadIdx.x, stats);
 }
 
 /* fill the intersection record: hair.cpp:825-862 + skdtree.h:422-427 */
@@ -1086,55 +1165,47 @@ extern "C" __global__ void k_sobol_batch(HptScene sc, int m, int n, const uint32
     outVal[i] = sobolSample(sc, idx, dim[i]);
 }
 
-/* flags: bit 0 = any-hit shadow query, bit 1 = 2-entry stack (exercises the
-   kd-restart path of traverse for the parity tests) */
-template <int STACK>
-__device__ __forceinline__ void traceBatchBody(const HptScene &sc, int n, const float *o, const float *d,
-                                               const float *mint, const float *maxt, int flags, float *outT,
-                                               int32_t *outSeg, float *outP, uint8_t *outHit, uint2 *stk) {
-    int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const bool shadow = (flags & 1) != 0;
-    V3 oo = v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), dd = v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]);
-    V3 rcp = v3(1.0f / dd.x, 1.0f / dd.y, 1.0f / dd.z);
-    float mn, mx;
-    uint32_t nn = 0, np = 0, ne = 0;
-    bool ok = false;
-    float t = finf();
-    uint32_t s = 0;
-    V3 p = v3(0.0f, 0.0f, 0.0f);
-    if (aabbIntersect(sc, oo, dd, rcp, mn, mx)) {
-        float rayMinT = adaptiveMint(oo, mint[i], shadow);
-        if (rayMinT > mn) mn = rayMinT;
-        if (maxt[i] < mx) mx = maxt[i];
-        if (mx > mn) {
-            if (shadow)
-                ok = traverse<STACK, true>(sc, oo, dd, rcp, mn, mx, stk, HPT_TRACE_BLOCK, t, s, p, nn, np, ne);
-            else
-                ok = traverse<STACK, false>(sc, oo, dd, rcp, mn, mx, stk, HPT_TRACE_BLOCK, t, s, p, nn, np, ne);
+/* Batch trace through the production traversal (tracePersistent).  flags:
+   bit 0 = any-hit shadow query, bit 1 = 2-entry stack (exercises the
+   kd-restart path for the parity tests) */
+struct BatchIO {
+    const float *o, *d, *mint, *maxt;
+    float *outT, *outP;
+    int32_t *outSeg;
+    uint8_t *outHit;
+    uint32_t n;
+    bool shadow;
+    HD uint32_t count() const { return n; }
+    HD bool begin(const HptScene &sc, uint32_t i, TraceRay &r) {
+        return beginRay(sc, r, v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
+                        mint[i], maxt[i], shadow);
+    }
+    HD uint32_t finish(uint32_t i, const TraceRay &r) {
+        if (shadow) {
+            outHit[i] = r.found ? 1 : 0;
+            return 0;
         }
+        outT[i] = r.found ? r.tHit : finf();
+        outSeg[i] = r.found ? (int32_t) r.segHit : -1;
+        outP[3 * i] = r.found ? r.pHit.x : 0.0f;
+        outP[3 * i + 1] = r.found ? r.pHit.y : 0.0f;
+        outP[3 * i + 2] = r.found ? r.pHit.z : 0.0f;
+        return 0;
     }
-    if (shadow) {
-        outHit[i] = ok ? 1 : 0;
-    } else {
-        outT[i] = ok ? t : finf();
-        outSeg[i] = ok ? (int32_t) s : -1;
-        outP[3 * i] = ok ? p.x : 0.0f;
-        outP[3 * i + 1] = ok ? p.y : 0.0f;
-        outP[3 * i + 2] = ok ? p.z : 0.0f;
-    }
-}
+};
 
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptScene sc, int n, const float *o,
                                                                             const float *d, const float *mint,
                                                                             const float *maxt, int flags,
                                                                             float *outT, int32_t *outSeg,
-                                                                            float *outP, uint8_t *outHit) {
+                                                                            float *outP, uint8_t *outHit,
+                                                                            uint32_t *cursor) {
     __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    BatchIO io{o, d, mint, maxt, outT, outP, outSeg, outHit, (uint32_t) n, (flags & 1) != 0};
     if (flags & 2)
-        traceBatchBody<2>(sc, n, o, d, mint, maxt, flags, outT, outSeg, outP, outHit, stk + threadIdx.x);
+        tracePersistent<2, false>(sc, io, cursor, stk + threadIdx.x, nullptr);
     else
-        traceBatchBody<HPT_STACK>(sc, n, o, d, mint, maxt, flags, outT, outSeg, outP, outHit, stk + threadIdx.x);
+        tracePersistent<HPT_STACK, false>(sc, io, cursor, stk + threadIdx.x, nullptr);
 }
 
 extern "C" __global__ void k_bsdf_batch(HptScene sc, int n, const float *wi, const float *wo, const float *u,
@@ -1198,6 +1269,7 @@ extern "C" __global__ void k_rotate(uint32_t *counters) {
         counters[HPT_Q_SHADE_OUT] = 0;
         counters[HPT_Q_TRACE] = 0;
         counters[HPT_Q_SHADOW] = 0;
+        counters[HPT_Q_CURSOR] = 0;
     }
 }
 
@@ -1212,15 +1284,33 @@ hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPath
     hipLaunchKernelGGL(k_camera, dim3(blocksFor(w.nPaths, 256)), dim3(256), 0, s, sc, w, P, traceQ, counters);
     return hipGetLastError();
 }
+/* persistent grid: as many one-wave blocks as can be resident at once
+   (occupancy API x CUs), capped by the work */
+static unsigned persistentBlocks(const void *kernel, uint64_t items) {
+    static int cached[2] = {0, 0};
+    const int slot = kernel == (const void *) k_trace ? 0 : 1;
+    if (cached[slot] == 0) {
+        int dev = 0, perCU = 0;
+        hipDeviceProp_t prop;
+        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, HPT_TRACE_BLOCK, 0) != hipSuccess ||
+            perCU <= 0)
+            perCU = 8, prop.multiProcessorCount = 256;
+        cached[slot] = perCU * prop.multiProcessorCount;
+    }
+    const uint64_t need = (items + HPT_TRACE_BLOCK - 1) / HPT_TRACE_BLOCK;
+    return (unsigned) std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t) cached[slot]));
+}
+
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
-                            const uint32_t *counters, uint32_t *stats, uint64_t maxItems, hipStream_t s) {
+                            uint32_t *counters, uint32_t *stats, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
     if (stats)
-        hipLaunchKernelGGL(k_trace_counted, dim3(blocksFor(maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc,
-                           P, traceQ, shadowQ, counters, stats);
+        hipLaunchKernelGGL(k_trace_counted, dim3(persistentBlocks((const void *) k_trace_counted, maxItems)),
+                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, counters, stats);
     else
-        hipLaunchKernelGGL(k_trace, dim3(blocksFor(maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc, P,
-                           traceQ, shadowQ, counters);
+        hipLaunchKernelGGL(k_trace, dim3(persistentBlocks((const void *) k_trace, maxItems)), dim3(HPT_TRACE_BLOCK),
+                           0, s, sc, P, traceQ, shadowQ, counters);
     return hipGetLastError();
 }
 hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
@@ -1258,11 +1348,13 @@ hipError_t hpt_launch_sobol_batch(const HptScene &sc, int m, int n, const uint32
     return hipGetLastError();
 }
 hipError_t hpt_launch_trace_batch(const HptScene &sc, int n, const float *o, const float *d, const float *mint,
-                                  const float *maxt, int shadow, float *ot, int32_t *os, float *op, uint8_t *oh,
-                                  hipStream_t s) {
+                                  const float *maxt, int flags, float *ot, int32_t *os, float *op, uint8_t *oh,
+                                  uint32_t *cursor, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_trace_batch, dim3(blocksFor(n, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc, n, o, d,
-                       mint, maxt, shadow, ot, os, op, oh);
+    hipError_t e = hipMemsetAsync(cursor, 0, 4, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_trace_batch, dim3(persistentBlocks((const void *) k_trace_batch, (uint64_t) n)),
+                       dim3(HPT_TRACE_BLOCK), 0, s, sc, n, o, d, mint, maxt, flags, ot, os, op, oh, cursor);
     return hipGetLastError();
 }
 hipError_t hpt_launch_bsdf_batch(const HptScene &sc, int n, const float *wi, const float *wo, const float *u,
