@@ -274,6 +274,9 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     static_assert((STACK & (STACK - 1)) == 0, "the ring stack index is masked");
     const HptNode *__restrict__ nodes = sc.nodes;
     const float4 *__restrict__ leafF = reinterpret_cast<const float4 *>(sc.leafF);
+    /* the ray as plain values: selecting among struct members by axis would be
+       folded into a dynamically addressed load and push the state to scratch */
+    const V3 o = r.o, d = r.d, rcp = r.rcp;
     /* hard bound so every wave drains even on a malformed tree */
     if (++r.leaves > (1 << 18)) return true;
     HptNode nd = nodes[r.node];
@@ -286,9 +289,9 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
         const uint32_t left = nd.w0 >> 2;
         const float split = __uint_as_float(nd.w1);
         /* per-axis selects (v_cndmask), not a dynamically indexed vector */
-        const float oa = axis == 0 ? r.o.x : (axis == 1 ? r.o.y : r.o.z);
-        const float da = axis == 0 ? r.d.x : (axis == 1 ? r.d.y : r.d.z);
-        const float ra = axis == 0 ? r.rcp.x : (axis == 1 ? r.rcp.y : r.rcp.z);
+        const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+        const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+        const float ra = axis == 0 ? rcp.x : (axis == 1 ? rcp.y : rcp.z);
         const float tsplit = (split - oa) * ra;
         /* branch-free front-to-back order (bitwise, so the wave keeps one path) */
         const bool belowFirst = (oa < split) | ((oa == split) & (da <= 0.0f));
@@ -327,12 +330,12 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
             ++tc.prims;
             if (waveLeader()) tc.primSlots += 64;
         }
-        if (!segMayHit(fa, fb, r.o, r.d, sc.radius)) continue;
+        if (!segMayHit(fa, fb, o, d, sc.radius)) continue;
         const uint32_t s = __float_as_uint(fb.z);
         if (STATS) ++tc.exact;
         float t;
         V3 p;
-        if (HPT_SEG_TEST(sc.segs, s, r.o, r.d, r2, r.mint, r.tHit, t, p)) {
+        if (HPT_SEG_TEST(sc.segs, s, o, d, r2, r.mint, r.tHit, t, p)) {
             r.found = true;
             if (r.shadow) return true;
             r.tHit = t;
