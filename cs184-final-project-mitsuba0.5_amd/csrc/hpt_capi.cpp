@@ -64,6 +64,8 @@ struct hpt_context {
     uint32_t *qTrace = nullptr, *qShadow = nullptr, *qShadeA = nullptr, *qShadeB = nullptr;
     uint32_t *counters = nullptr;
     uint64_t *dstats = nullptr;
+    float4 *partial = nullptr;     /* film splat partials: slots x 9 (k_splat -> k_gather) */
+    uint64_t partialSlots = 0;
     hpt_stats stats;
     std::vector<hipEvent_t> evPool;
 };
@@ -218,6 +220,7 @@ void hpt_context_destroy(hpt_context *c) {
     (void) hipStreamSynchronize(c->stream);
     freeBufs(c->sceneBufs);
     freeBufs(c->waveBufs);
+    if (c->partial) (void) hipFree(c->partial);
     for (auto e : c->evPool) (void) hipEventDestroy(e);
     (void) hipStreamDestroy(c->stream);
     delete c;
@@ -574,6 +577,13 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     if (waveCap > 0xffffffffull) return setErr(c, HPT_EINVAL, "wave too large");
     int r = ensureWave(c, waveCap);
     if (r) return r;
+    if (slots > c->partialSlots) {
+        if (c->partial) (void) hipFree(c->partial);
+        c->partial = nullptr;
+        c->partialSlots = 0;
+        HIPCHK(c, hipMalloc((void **) &c->partial, slots * 9 * sizeof(float4)));
+        c->partialSlots = slots;
+    }
     hipStream_t s = c->stream;
     const bool st = prm->collect_stats != 0;      /* HIP event timing per kernel class */
     const bool counted = prm->collect_stats >= 2; /* + traversal counters (k_trace_counted) */
@@ -648,7 +658,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             return setErr(c, HPT_EINVAL, "Lookup dimension exceeds the direction number table size! You may have "
                                          "to reduce the 'maxDepth' parameter of your integrator.");
         }
-        e = timed(4, [&] { return hpt_launch_gather(sc, w, c->P, dFilm, s); });
+        e = timed(4, [&] { return hpt_launch_gather(sc, w, c->P, c->partial, dFilm, s); });
         c->stats.paths += w.nPaths;
     }
     hipError_t e2 = hipStreamSynchronize(s);

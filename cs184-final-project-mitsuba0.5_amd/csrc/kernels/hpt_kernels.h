@@ -56,7 +56,9 @@ hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_
 hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
                            uint32_t *counters, uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_rotate(uint32_t *counters, hipStream_t s);
-hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *film, hipStream_t s);
+/* k_splat + k_gather; partial = (nPaths / nSpp) * 9 float4 of scratch */
+hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *partial, float4 *film,
+                             hipStream_t s);
 hipError_t hpt_launch_sobol_batch(const HptScene &sc, int m, int n, const uint32_t *frame, const uint32_t *px,
                                   const uint32_t *py, const uint32_t *dim, uint64_t *oi, float *ov, hipStream_t s);
 hipError_t hpt_launch_trace_batch(const HptScene &sc, int n, const float *o, const float *d, const float *mint,

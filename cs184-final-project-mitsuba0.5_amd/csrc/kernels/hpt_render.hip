@@ -16,8 +16,8 @@
  *                 continuation ray per path
  *   k_post        env hit + MIS (:236-264), throughput, Russian roulette
  *                 (:270-286); survivors re-enter the shade queue
- *   k_gather      deterministic tent-filter gather of all samples into an
- *                 RGBW film (imageblock.h:124-204)
+ *   k_splat/k_gather  deterministic tent-filter accumulation of all samples
+ *                 into an RGBW film (imageblock.h:124-204)
  *
  * Queues are compacted with a wave64 ballot + one atomic per wave.  A
  * path's arithmetic never depends on its queue position, so results are
@@ -1109,15 +1109,76 @@ extern "C" __global__ __launch_bounds__(256) void k_post(HptScene sc, HptPaths P
     qpush(alive, id, shadeQ, &counters[HPT_Q_SHADE_OUT]);
 }
 
-/* Deterministic film gather (imageblock.h:124-204 + renderproc.cpp:142-145):
-   every pixel sums, in a fixed order, the tent-weighted samples of its 3x3
-   neighbour pixels that belong to this shard and this wave.  Weights use
-   the sample's block-relative coordinates exactly like ImageBlock::put. */
-extern "C" __global__ __launch_bounds__(256) void k_gather(HptScene sc, HptWave w, HptPaths P, float4 *film) {
+/* Deterministic film accumulation (imageblock.h:124-204 + renderproc.cpp:
+   142-145) in two passes.  Weights use the sample's block-relative
+   coordinates exactly like ImageBlock::put, and invalid samples (non-finite
+   or negative, imageblock.h:147-151) are skipped.
+
+   k_splat: one wave per owned pixel slot; its lanes read the slot's samples
+   (consecutive path ids: coalesced) and accumulate the tent-weighted
+   contribution to each of the 3x3 neighbour pixels, reduced across the wave
+   with a fixed xor tree -> partial[slot][9] (RGB, weight). */
+extern "C" __global__ __launch_bounds__(256) void k_splat(HptScene sc, HptWave w, HptPaths P,
+                                                           float4 *__restrict__ partial) {
+    const uint32_t slot = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t nSlots = w.nPaths / w.nSpp;
+    if (slot >= nSlots) return; /* wave-uniform */
+    const uint32_t lb = slot >> 10, inner = slot & 1023u;
+    const uint32_t b = lb * w.nShards + w.shard;
+    const int bx = (int) (b % w.nbx), by = (int) (b / w.nbx);
+    const int px = bx * HPT_BLOCK + (int) (inner & 31u), py = by * HPT_BLOCK + (int) (inner >> 5);
+    if (px >= w.width || py >= w.height) return; /* wave-uniform: never read back */
+    const float ox = (float) (bx * HPT_BLOCK - 1), oy = (float) (by * HPT_BLOCK - 1);
+    float acc[9][4];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
+    for (uint32_t jj = lane; jj < w.nSpp; jj += 64) {
+        const uint32_t id = slot * w.nSpp + jj;
+        const float4 l = P.li[id];
+        if (!(isfinite(l.x) && isfinite(l.y) && isfinite(l.z)) || l.x < 0 || l.y < 0 || l.z < 0) continue;
+        const float2 ps = P.pos[id];
+        const float rx = ps.x - 0.5f - ox, ry = ps.y - 0.5f - oy;
+        const float x0 = ceilf(rx - 1.0f), x1 = floorf(rx + 1.0f), y0 = ceilf(ry - 1.0f), y1 = floorf(ry + 1.0f);
+#pragma unroll
+        for (int dy = -1; dy <= 1; ++dy) {
+            const float yr = (float) (py + dy) - oy;
+            if (yr < y0 || yr > y1) continue;
+            const float wy = sc.tent[imin((int) fabsf((yr - ry) * sc.tentScale), HPT_FILTER_RES)];
+#pragma unroll
+            for (int dx = -1; dx <= 1; ++dx) {
+                const float xr = (float) (px + dx) - ox;
+                if (xr < x0 || xr > x1) continue;
+                const float wx = sc.tent[imin((int) fabsf((xr - rx) * sc.tentScale), HPT_FILTER_RES)];
+                const float wgt = wx * wy;
+                float *a = acc[(dy + 1) * 3 + (dx + 1)];
+                a[0] += wgt * l.x;
+                a[1] += wgt * l.y;
+                a[2] += wgt * l.z;
+                a[3] += wgt * 1.0f;
+            }
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) acc[k][c] += __shfl_xor(acc[k][c], off);
+    if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) partial[(size_t) slot * 9 + k] = make_float4(acc[k][0], acc[k][1], acc[k][2], acc[k][3]);
+    }
+}
+
+/* k_gather: every pixel adds, in a fixed neighbour order, the partial sums
+   its 3x3 neighbours (owned by this shard) addressed to it. */
+extern "C" __global__ __launch_bounds__(256) void k_gather(HptScene sc, HptWave w, const float4 *__restrict__ partial,
+                                                            float4 *film) {
     const uint32_t pix = blockIdx.x * blockDim.x + threadIdx.x;
     if (pix >= (uint32_t) (w.width * w.height)) return;
     const int x = (int) (pix % (uint32_t) w.width), y = (int) (pix / (uint32_t) w.width);
-    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     bool any = false;
     for (int qy = y - 1; qy <= y + 1; ++qy) {
         if (qy < 0 || qy >= w.height) continue;
@@ -1127,32 +1188,17 @@ extern "C" __global__ __launch_bounds__(256) void k_gather(HptScene sc, HptWave 
             const uint32_t b = (uint32_t) (by * w.nbx + bx);
             if ((int) (b % w.nShards) != w.shard) continue;
             const uint32_t slot = ((b / w.nShards) << 10) | ((uint32_t) (qy & 31) << 5) | (uint32_t) (qx & 31);
-            const float ox = (float) (bx * HPT_BLOCK - 1), oy = (float) (by * HPT_BLOCK - 1);
-            const float xr = (float) (x - (bx * HPT_BLOCK - 1)), yr = (float) (y - (by * HPT_BLOCK - 1));
-            for (uint32_t jj = 0; jj < w.nSpp; ++jj) {
-                const uint32_t id = slot * w.nSpp + jj;
-                float4 l = P.li[id];
-                if (!(isfinite(l.x) && isfinite(l.y) && isfinite(l.z)) || l.x < 0 || l.y < 0 || l.z < 0) continue;
-                float2 ps = P.pos[id];
-                const float rx = ps.x - 0.5f - ox, ry = ps.y - 0.5f - oy;
-                /* inside [ceil(r-1), floor(r+1)] <=> |xr - r| <= 1 up to the LUT's zero tail */
-                const float dx = xr - rx, dy = yr - ry;
-                if (xr < ceilf(rx - 1.0f) || xr > floorf(rx + 1.0f) || yr < ceilf(ry - 1.0f) || yr > floorf(ry + 1.0f))
-                    continue;
-                const float wx = sc.tent[imin((int) fabsf(dx * sc.tentScale), HPT_FILTER_RES)];
-                const float wy = sc.tent[imin((int) fabsf(dy * sc.tentScale), HPT_FILTER_RES)];
-                const float wgt = wx * wy;
-                acc[0] += wgt * l.x;
-                acc[1] += wgt * l.y;
-                acc[2] += wgt * l.z;
-                acc[3] += wgt * 1.0f;
-                any = true;
-            }
+            const float4 p = partial[(size_t) slot * 9 + (y - qy + 1) * 3 + (x - qx + 1)];
+            acc.x += p.x;
+            acc.y += p.y;
+            acc.z += p.z;
+            acc.w += p.w;
+            any = true;
         }
     }
     if (any) {
         float4 f = film[pix];
-        film[pix] = make_float4(f.x + acc[0], f.y + acc[1], f.z + acc[2], f.w + acc[3]);
+        film[pix] = make_float4(f.x + acc.x, f.y + acc.y, f.z + acc.z, f.w + acc.w);
     }
 }
 
@@ -1339,9 +1385,12 @@ hipError_t hpt_launch_rotate(uint32_t *counters, hipStream_t s) {
     hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, s, counters);
     return hipGetLastError();
 }
-hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *film, hipStream_t s) {
-    uint64_t n = (uint64_t) w.width * (uint64_t) w.height;
-    hipLaunchKernelGGL(k_gather, dim3(blocksFor(n, 256)), dim3(256), 0, s, sc, w, P, film);
+hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *partial, float4 *film,
+                             hipStream_t s) {
+    const uint64_t slots = w.nPaths / w.nSpp;
+    hipLaunchKernelGGL(k_splat, dim3(blocksFor(slots * 64, 256)), dim3(256), 0, s, sc, w, P, partial);
+    const uint64_t n = (uint64_t) w.width * (uint64_t) w.height;
+    hipLaunchKernelGGL(k_gather, dim3(blocksFor(n, 256)), dim3(256), 0, s, sc, w, (const float4 *) partial, film);
     return hipGetLastError();
 }
 hipError_t hpt_launch_sobol_batch(const HptScene &sc, int m, int n, const uint32_t *frame, const uint32_t *px,
