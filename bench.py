@@ -29,7 +29,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402  (import first: one HIP runtime per process)
 import torch.distributed as dist  # noqa: E402
 
-from mitsuba_amd import native, scenes  # noqa: E402
+from mitsuba_amd import distributed, native, scenes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
@@ -115,9 +115,10 @@ def main():
     def step(level):
         film.zero_()
         torch.cuda.synchronize()
-        r.render_device(film.data_ptr(), 0, spp, shard=rank, n_shards=world, collect_stats=level)
-        if world > 1:
-            dist.reduce(film, 0)
+        distributed.render_frame(
+            lambda shard, n_shards, f: r.render_device(f.data_ptr(), 0, spp, shard=shard, n_shards=n_shards,
+                                                        collect_stats=level),
+            film, rank, world, dist)
 
     for _ in range(args.warmup):
         step(1)

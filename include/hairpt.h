@@ -121,8 +121,9 @@ typedef struct hpt_stats {
     uint64_t waves;
     int max_bounces;
     uint64_t prim_exact;           /* segments that passed the fp32 pre-test (fp64 tests run) */
-    uint64_t node_slots, prim_slots; /* 64 x per-wave max of node visits / primitive tests:
-                                        nodes / node_slots is the SIMD lane utilisation */
+    uint64_t node_slots, prim_slots; /* SIMD lanes occupied by the node / primitive loops
+                                        (64 per wave iteration): nodes / node_slots is the
+                                        lane utilisation */
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 
