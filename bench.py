@@ -150,11 +150,22 @@ def main():
     dt = float(t.item())
     tot = {k: v * args.steps for k, v in frame.items()}
 
+    workload = "%s %dx%d @ %d spp, maxDepth %d, %d strands / %d segments" % (
+        args.config, W, H, spp, max_depth, n, info.segments)
     paths_total = W * H * spp * args.steps
     value = paths_total / dt / 1e6
     bytes_alg = (BYTES_CLOSEST * tot["closest"] + BYTES_SHADOW * tot["shadow"] + BYTES_UNOCC * tot["unocc"]
                  + BYTES_NODE * tot["nodes"] + BYTES_PRIM * tot["prims"] + BYTES_EXACT * tot["exact"])
     achieved = bytes_alg / (ms_trace * 1e-3) / 1e9 if ms_trace > 0 else 0.0
+    traffic, traffic_src = None, None
+    tj = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
+    if os.path.exists(tj):
+        # HBM-side bytes per k_trace launch from the committed rocprofv3 PMC passes
+        # (scripts/gpu_profile.sh + tools/rocpd_summary.py) of this same workload
+        t = json.load(open(tj))
+        if t.get("workload") == workload and "k_trace" in t.get("kernels", {}):
+            traffic = round(t["kernels"]["k_trace"]["bytes_per_launch"])
+            traffic_src = "profiles/" + os.path.basename(tj)
     out = None
     if rank == 0:
         cpu = None
@@ -175,13 +186,14 @@ def main():
             "vs_baseline": None,
             "dtype": "f32 (f64 cylinder tests)",
             "data": "synthetic hair (seeded, BINARY_HAIR) + sunsky stand-in envmap; reference blobs absent",
-            "config": {"workload": "%s %dx%d @ %d spp, maxDepth %d, %d strands / %d segments"
-                                   % (args.config, W, H, spp, max_depth, n, info.segments),
+            "config": {"workload": workload,
                        "paths_per_step": W * H * spp, "parallelism": "tiles%d" % world,
                        "kd_nodes": int(info.kd_nodes), "kd_depth": int(info.kd_depth),
                        "prepare_s": round(t_prep, 3)},
             "roofline": {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "algorithmic_bytes_per_launch": int(bytes_alg // max(1, launches)),
                          "avg_launch_ms": round(ms_trace / max(1, launches), 4), "launches": int(launches),
                          "bytes_per_step": int(bytes_alg // args.steps),
                          "rank0_trace_ms_per_step": round(ms_trace / args.steps, 3)},

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("prof_dir", help="gpurun_out/prof_<tag> (trace/, fetch/, write/)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--title", default="")
+    ap.add_argument("--json", default=None, help="also write per-launch traffic as JSON (read by bench.py)")
+    ap.add_argument("--workload", default="", help="workload string the traffic belongs to (bench config)")
     a = ap.parse_args()
     lines = []
     if a.title:
@@ -60,6 +62,19 @@ def main():
             kn = kn if len(kn) < 60 else kn[:57] + "..."
             lines.append("| %s | %d | %.1f | %.1f | %.1f |" % (kn, f[0], fm, wm, fm + wm))
     open(a.out, "w").write("\n".join(lines) + "\n")
+    if a.json:
+        import json
+
+        out = {"workload": a.workload, "source": os.path.basename(a.out),
+               "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and --pmc WRITE_SIZE in separate passes; "
+                         "bytes per launch averaged over all launches of the kernel", "kernels": {}}
+        for kn, v in traffic.items():
+            f = v.get("FETCH_SIZE", (1, 0.0, 0))
+            w = v.get("WRITE_SIZE", (1, 0.0, 0))
+            out["kernels"][kn] = {"launches": f[0], "fetch_bytes": 2.0 * f[1] * 1024 / max(1, f[0]),
+                                  "write_bytes": w[1] * 1024 / max(1, w[0])}
+            out["kernels"][kn]["bytes_per_launch"] = out["kernels"][kn]["fetch_bytes"] + out["kernels"][kn]["write_bytes"]
+        json.dump(out, open(a.json, "w"), indent=1)
     print("\n".join(lines))
 
 
