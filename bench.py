@@ -185,7 +185,7 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32 (f64 cylinder tests)",
-            "data": "synthetic hair (seeded, BINARY_HAIR) + sunsky stand-in envmap; reference blobs absent",
+            "data": "synthetic hair (seeded, BINARY_HAIR; reference hair blobs absent) lit by the scene's sunsky (Hosek-Wilkie sky + Preetham sun rasterised like sunsky.cpp)",
             "config": {"workload": workload,
                        "paths_per_step": W * H * spp, "parallelism": "tiles%d" % world,
                        "kd_nodes": int(info.kd_nodes), "kd_depth": int(info.kd_depth),

@@ -86,6 +86,11 @@ struct SceneDesc {
     float sunDirection[3] = {0, 1, 0};
     bool sunDirectionGiven = false;
     int skyResolution = 512;
+    float skyAlbedo[3] = {0.2f, 0.2f, 0.2f}, skyStretch = 1.0f;   /* sky.cpp:222-228 */
+    /* date / time / location of the sun when no sunDirection is given (sunmodel.h:223-234) */
+    float sunLatitude = 35.6894f, sunLongitude = 139.6917f, sunTimezone = 9.0f;
+    int sunYear = 2010, sunMonth = 7, sunDay = 10;
+    float sunHour = 15.0f, sunMinute = 0.0f, sunSecond = 0.0f;
     float emitterToWorld[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     std::string sceneDir;
 };
@@ -148,7 +153,19 @@ struct EnvHost {
 };
 
 void buildEnvMap(EnvHost &env);                           /* envmap.cpp:244-314 */
-void rasterizeSunSkyStandIn(const SceneDesc &d, EnvHost &env); /* see DESIGN.md */
+
+/* sunsky (sunsky.cpp): tables extracted from the reference (tools/extract_sunsky_tables.py) */
+struct SunSkyTables {
+    std::vector<double> hosek;     /* datasetRGB1..3 (3 x 1080), datasetRGBRad1..3 (3 x 120) */
+    std::vector<float> cie;        /* CIE 1931 wavelengths, x, y, z (4 x 471) */
+    std::vector<float> kOWl, kOAmp, kGWl, kGAmp, kWaWl, kWaAmp, solWl, solAmp;
+};
+bool loadSunSkyTables(const std::string &dataDir, SunSkyTables &t, std::string &err);
+void rasterizeSunSky(const SceneDesc &d, const SunSkyTables &t, EnvHost &env); /* sunsky.cpp:100-225 */
+/* pieces exported for the golden-vector tests */
+void hosekSkyRGB(const SunSkyTables &t, double turbidity, double albedo, double solarElevation, double theta,
+                 double gamma, double out[3]);
+void sunRadianceRGB(const SunSkyTables &t, float theta, float turbidity, float rgb[3]);
 bool loadEnvFile(const std::string &path, EnvHost &env, std::string &err); /* .hdr / .pfm */
 
 void setupCamera(const SceneDesc &d, HptCamera &cam);      /* perspective.cpp:125-165 */

@@ -456,55 +456,6 @@ void buildEnvMap(EnvHost &env) {
     env.pixelSizeY = kPi / h;
 }
 
-/*
- * Stand-in for the sunsky emitter (round 1): the reference rasterises a
- * Hosek-Wilkie sky plus a QMC-splatted sun disk into a resolution x
- * resolution/2 lat-long bitmap (sunsky.cpp:100-240) and hands it to envmap.
- * Until that rasteriser is restated we rasterise a
- * smooth analytic sky + sun disk with the same bitmap geometry, sun
- * direction, sun disk radius (SUN_APP_RADIUS * sunRadiusScale) and scales.
- * The bitmap is an input: the oracle and the device consume identical bits.
- */
-void rasterizeSunSkyStandIn(const SceneDesc &d, EnvHost &env) {
-    const int W = d.skyResolution, H = d.skyResolution / 2;
-    env.w = W;
-    env.h = H;
-    env.rgb.assign((size_t) W * H * 3, 0.0f);
-    double sx = d.sunDirection[0], sy = d.sunDirection[1], sz = d.sunDirection[2];
-    double sl = std::sqrt(sx * sx + sy * sy + sz * sz);
-    sx /= sl; sy /= sl; sz /= sl;
-    const double sunAppRadius = 0.5358 * M_PI / 180.0; /* sunmodel.h SUN_APP_RADIUS (degrees) */
-    double cosSun = std::cos(0.5 * sunAppRadius * d.sunRadiusScale);
-    double sunElev = std::asin(std::max(-1.0, std::min(1.0, sy)));
-    /* sun colour warms towards the horizon; magnitude ~ sunScale */
-    double sunR = 1.0, sunG = 0.85 + 0.1 * std::sin(sunElev), sunB = 0.65 + 0.25 * std::sin(sunElev);
-    for (int y = 0; y < H; ++y) {
-        double theta = (y + 0.5) * M_PI / H;
-        for (int x = 0; x < W; ++x) {
-            double phi = (x + 0.5) * 2 * M_PI / W;
-            /* envmap lat-long convention (envmap.cpp:589-597): d = (sin phi sin th, cos th, -cos phi sin th) */
-            double dx = std::sin(phi) * std::sin(theta), dy = std::cos(theta), dz = -std::cos(phi) * std::sin(theta);
-            float *px = &env.rgb[3 * ((size_t) y * W + x)];
-            if (dy <= 0) continue; /* black below the horizon (sky.cpp:416-421) */
-            double mu = dx * sx + dy * sy + dz * sz;
-            double gamma = std::acos(std::max(-1.0, std::min(1.0, mu)));
-            double zen = 1.0 - dy;
-            double glow = std::exp(-gamma * 2.5);
-            double base = 0.08 + 0.10 * zen * zen;
-            px[0] = (float) (d.skyScale * (base * 0.45 + 0.25 * glow) * 0.2);
-            px[1] = (float) (d.skyScale * (base * 0.65 + 0.22 * glow) * 0.2);
-            px[2] = (float) (d.skyScale * (base * 1.00 + 0.18 * glow) * 0.2);
-            if (mu >= cosSun) {
-                double s = d.sunScale * 3.0;
-                px[0] += (float) (s * sunR);
-                px[1] += (float) (s * sunG);
-                px[2] += (float) (s * sunB);
-            }
-        }
-    }
-    env.scale = 1.0f;
-    std::memcpy(env.toWorld, d.emitterToWorld, sizeof(env.toWorld));
-}
 
 bool loadEnvFile(const std::string &path, EnvHost &env, std::string &err) {
     std::ifstream f(path, std::ios::binary);

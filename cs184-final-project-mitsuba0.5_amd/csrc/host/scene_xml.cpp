@@ -471,11 +471,29 @@ void parseObject(Ctx &c, const XNode &nd, SceneDesc &d) {
             d.sunRadiusScale = num1(p, "sunRadiusScale", 1.0f);
             d.turbidity = num1(p, "turbidity", 3.0f);
             d.skyResolution = (int) num1(p, "resolution", 512);
+            d.skyStretch = num1(p, "stretch", 1.0f);
+            if (p.num.count("albedo")) {
+                auto &v = p.num["albedo"];
+                for (int i = 0; i < 3; ++i) d.skyAlbedo[i] = v[v.size() == 1 ? 0 : i];
+            }
             if (p.num.count("sunDirection")) {
                 auto &v = p.num["sunDirection"];
                 for (int i = 0; i < 3; ++i) d.sunDirection[i] = v[i];
                 d.sunDirectionGiven = true;
+                for (const char *k : {"latitude", "longitude", "timezone", "day", "time"})
+                    if (p.num.count(k))
+                        fail(c.file, nd.line, "Both the 'sunDirection' parameter and time/location information "
+                                              "were provided -- only one of them can be specified at a time!");
             }
+            d.sunLatitude = num1(p, "latitude", d.sunLatitude);
+            d.sunLongitude = num1(p, "longitude", d.sunLongitude);
+            d.sunTimezone = num1(p, "timezone", d.sunTimezone);
+            d.sunYear = (int) num1(p, "year", (float) d.sunYear);
+            d.sunMonth = (int) num1(p, "month", (float) d.sunMonth);
+            d.sunDay = (int) num1(p, "day", (float) d.sunDay);
+            d.sunHour = num1(p, "hour", d.sunHour);
+            d.sunMinute = num1(p, "minute", d.sunMinute);
+            d.sunSecond = num1(p, "second", d.sunSecond);
         } else if (type == "envmap") {
             if (!p.str.count("filename")) fail(c.file, nd.line, "envmap needs a filename");
             d.envFile = p.str["filename"];

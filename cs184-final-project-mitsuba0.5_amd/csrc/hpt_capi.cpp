@@ -53,6 +53,7 @@ struct hpt_context {
     HptKajiyaKay kk;
     EnvHost env;
     bool envFromSunsky = false;
+    SunSkyTables sunsky;
     std::vector<uint32_t> sobol32;
     std::vector<uint64_t> vdc, vdcInv;
     HptScene sc;
@@ -383,6 +384,7 @@ int hpt_set_sunsky(hpt_context *c, const float sun_direction[3], float turbidity
     c->desc.sunScale = sun_scale;
     c->desc.sunRadiusScale = sun_radius_scale;
     c->desc.skyResolution = resolution;
+    c->desc.sunDirectionGiven = true;
     c->envFromSunsky = true;
     c->haveEnv = true;
     c->prepared = false;
@@ -419,7 +421,14 @@ int hpt_prepare(hpt_context *c) {
         } else {
             return setErr(c, HPT_EINVAL, "unsupported bsdf " + d.bsdf);
         }
-        if (c->envFromSunsky) rasterizeSunSkyStandIn(d, c->env);
+        if (c->envFromSunsky) {
+            if (c->sunsky.hosek.empty()) {
+                std::string err;
+                if (!loadSunSkyTables(c->dataDir, c->sunsky, err)) return setErr(c, HPT_EIO, err);
+            }
+            c->env = EnvHost();
+            rasterizeSunSky(d, c->sunsky, c->env);
+        }
         buildEnvMap(c->env);
     } catch (const std::exception &e) {
         return setErr(c, HPT_EIO, e.what());

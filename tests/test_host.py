@@ -187,3 +187,47 @@ def test_reference_flags_noise_floor(name, n):
     floor, same = scene_util.reference_flags_floor(name, n, r, 48, 40, 8)
     assert floor["rmse"] < 1e-3, floor
     assert same > 0.7
+
+
+def test_sunsky_tables_match_extraction_record():
+    """data/sunsky holds exactly what tools/extract_sunsky_tables.py read from the
+    reference (skymodeldata.h RGB datasets, spectrum.cpp CIE 1931, sunmodel.h)."""
+    import hashlib
+    import json
+
+    d = os.path.join(ROOT, "cs184-final-project-mitsuba0.5_amd", "data", "sunsky")
+    meta = json.load(open(os.path.join(d, "meta.json")))
+    for f, h in meta.items():
+        assert hashlib.sha256(open(os.path.join(d, f), "rb").read()).hexdigest() == h, f
+    hosek = np.fromfile(os.path.join(d, "hosek_rgb.f64"), "<f8")
+    cie = np.fromfile(os.path.join(d, "cie1931.f32"), "<f4").reshape(4, 471)
+    assert hosek.size == 3 * 1080 + 3 * 120 and np.all(np.isfinite(hosek))
+    np.testing.assert_array_equal(cie[0], np.arange(360, 831, dtype=np.float32))
+    assert abs(cie[2].max() - 1.0) < 1e-3  # CIE y peaks at 1 (555 nm)
+
+
+def test_sunsky_rasterisation_geometry():
+    """sunsky.cpp:100-225: sky black below the horizon, blue zenith, the sun
+    disk centred on sunDirection with the scaled apparent radius."""
+    _, r, _ = scene_util.make("furball_marschner", 600, 32, 32, 2)
+    env = r.envmap().astype(np.float64)
+    H, W, _ = env.shape
+    assert np.all(env[H // 2 + 1:] == 0)
+    zen = env[0].mean(0)
+    assert zen[2] > zen[1] > zen[0] > 0
+    lum = env @ np.array([0.212671, 0.715160, 0.072169])
+    theta = (np.arange(H) + 0.5) * np.pi / H
+    phi = (np.arange(W) + 0.5) * 2 * np.pi / W
+    dirs = np.stack([np.sin(phi)[None, :] * np.sin(theta)[:, None], np.cos(theta)[:, None] * np.ones((1, W)),
+                     -np.cos(phi)[None, :] * np.sin(theta)[:, None]], -1)
+    sd = np.array([-0.376047, 0.758426, 0.532333])
+    sd /= np.linalg.norm(sd)
+    ang = np.degrees(np.arccos(np.clip(dirs @ sd, -1, 1)))
+    sky_hi = np.percentile(lum[ang > 20], 99.9)
+    sun = lum > 5 * sky_hi
+    radius = 0.5358 * 0.5 * 37.9165  # SUN_APP_RADIUS / 2 * sunRadiusScale (furball scene.xml)
+    assert sun.sum() > 100
+    assert ang[sun].max() < radius + 1.0
+    assert np.all(lum[ang < radius - 1.5] > sky_hi)
+    c = env[sun].mean(0)
+    assert c[0] >= c[1] >= c[2] > 0  # attenuated solar spectrum: warm white
