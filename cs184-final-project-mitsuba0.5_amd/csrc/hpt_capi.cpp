@@ -155,7 +155,7 @@ int ensureWave(hpt_context *c, uint64_t n) {
     r |= alloc(n * 4, (void **) &c->qShadow);
     r |= alloc(n * 4, (void **) &c->qShadeA);
     r |= alloc(n * 4, (void **) &c->qShadeB);
-    r |= alloc(HPT_Q_COUNT * 4, (void **) &c->counters);
+    r |= alloc(HPT_COUNTER_WORDS * 4, (void **) &c->counters);
     r |= alloc(8 * 8, (void **) &c->dstats);
     if (r) return HPT_EDEVICE;
     c->capacity = n;
@@ -625,7 +625,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         w.shard = shard;
         w.nShards = nShards;
         c->stats.waves++;
-        HIPCHK(c, hipMemsetAsync(c->counters, 0, HPT_Q_COUNT * 4, s));
+        HIPCHK(c, hipMemsetAsync(c->counters, 0, HPT_COUNTER_WORDS * 4, s));
         e = timed(0, [&] { return hpt_launch_camera(sc, w, c->P, c->qTrace, c->counters, s); });
         if (e) break;
         e = timed(-1, [&] {
@@ -837,7 +837,7 @@ int hpt_trace_batch(hpt_context *c, int n, const float *o, const float *d, const
     float *dt = S.in<float>(nullptr, n), *dp = S.in<float>(nullptr, 3 * (size_t) n);
     int32_t *ds = S.in<int32_t>(nullptr, n);
     uint8_t *dh = S.in<uint8_t>(nullptr, n);
-    uint32_t *cur = S.in<uint32_t>(nullptr, 1);
+    uint32_t *cur = S.in<uint32_t>(nullptr, HPT_CURSORS * HPT_CURSOR_STRIDE);
     HIPCHK(c, hpt_launch_trace_batch(c->sc, n, a, b, mi, ma, flags, dt, ds, dp, dh, cur, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (shadow) {

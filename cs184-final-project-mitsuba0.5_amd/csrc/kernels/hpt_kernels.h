@@ -14,8 +14,13 @@
 #define HPT_Q_SHADE_IN 2
 #define HPT_Q_SHADE_OUT 3
 #define HPT_Q_ERROR 4     /* set when a path runs out of Sobol dimensions */
-#define HPT_Q_CURSOR 5    /* k_trace work cursor (persistent waves claim rays from it) */
 #define HPT_Q_COUNT 8
+/* k_trace work cursors (persistent waves claim rays from them), one per
+   128-byte line, stored after the queue counters in the same buffer */
+#define HPT_CURSORS 64
+#define HPT_CURSOR_STRIDE 32
+#define HPT_CURSOR_OFFSET 64
+#define HPT_COUNTER_WORDS (HPT_CURSOR_OFFSET + HPT_CURSORS * HPT_CURSOR_STRIDE)
 
 /* One wave of paths: every pixel of this shard's 32x32 blocks x samples
    [sppBegin, sppBegin + nSpp).  Path id = slot * nSpp + (j - sppBegin),

@@ -33,6 +33,11 @@
 
 using namespace hk;
 
+/* block size of the queue-producing kernels (k_camera, k_primary, k_shade, k_post) */
+#ifndef HPT_QBLOCK
+#define HPT_QBLOCK 1024
+#endif
+
 namespace {
 
 /* ------------------------------------------------------------------ */
@@ -367,12 +372,17 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
 #endif
 
 /* Persistent traversal: each wave keeps its 64 lanes busy by claiming new
-   rays (one atomic per refill) whenever HPT_REFILL lanes have finished.
+   rays whenever HPT_REFILL lanes have finished.  The work range is split
+   into HPT_CURSORS contiguous shards, each with its own cursor on its own
+   128-byte line; a wave starts on shard (wave id mod HPT_CURSORS) and moves
+   to the next one when its shard runs dry, so claims spread over 64
+   addresses instead of serialising on one (device-scope atomics to a single
+   word cost ~10 ns each) and neighbouring rays stay together.
    IO supplies count(), begin(k, r) (load ray k; false = nothing to trace)
-   and finish(k, r).  Every wave exits once the cursor passes the total and
-   its lanes have drained, so the grid always completes. */
+   and finish(k, r).  Every wave exits once all shards are exhausted and its
+   lanes have drained, so the grid always completes. */
 template <int STACK, bool STATS, class IO>
-__device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint32_t *cursor, uint2 *stk,
+__device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint32_t *cursors, uint2 *stk,
                                                 uint32_t *stats) {
     const uint32_t total = io.count();
     const uint32_t lane = __lane_id();
@@ -380,17 +390,34 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
     TraceCounters tc;
     uint32_t item = 0, nC = 0, nS = 0, nU = 0;
     bool active = false, exhausted = false;
+    uint32_t shard = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % HPT_CURSORS;
+    int tried = 0;
     while (true) {
         const uint64_t idle = __ballot(!active);
         if (!exhausted && __popcll(idle) >= HPT_REFILL) {
             const uint32_t n = (uint32_t) __popcll(idle);
-            uint32_t base = 0;
-            if (lane == 0) base = atomicAdd(cursor, n);
-            base = __shfl(base, 0);
-            exhausted = base + n >= total;
+            uint32_t start = 0, got = 0;
+            while (true) { /* wave-uniform */
+                const uint32_t lo = (uint32_t) ((uint64_t) total * shard / HPT_CURSORS);
+                const uint32_t size = (uint32_t) ((uint64_t) total * (shard + 1) / HPT_CURSORS) - lo;
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&cursors[shard * HPT_CURSOR_STRIDE], n);
+                base = __shfl(base, 0);
+                if (base < size) {
+                    start = lo + base;
+                    got = min(n, size - base);
+                    break;
+                }
+                if (++tried >= HPT_CURSORS) {
+                    exhausted = true;
+                    break;
+                }
+                shard = (shard + 1) % HPT_CURSORS;
+            }
             if (!active) {
-                const uint32_t k = base + (uint32_t) __popcll(idle & ((1ull << lane) - 1ull));
-                if (k < total) {
+                const uint32_t rank = (uint32_t) __popcll(idle & ((1ull << lane) - 1ull));
+                const uint32_t k = start + rank;
+                if (rank < got) {
                     item = k;
                     active = io.begin(sc, k, r);
                     if (STATS) {
@@ -780,6 +807,34 @@ HD float miWeight(float pdfA, float pdfB) { /* path.cpp:296-300 */
 }
 
 
+/* Append to a queue with one atomic per BLOCK: wave ballots give per-wave
+   counts, the block's waves are laid out in wave order after a single
+   atomicAdd by thread 0.  A million same-address atomics per launch (one per
+   wave) serialised in L2 and dominated k_camera / k_primary; per block they
+   are 16x fewer.  Every thread of the block must call it (no early exits). */
+template <int BLOCK>
+__device__ __forceinline__ void qpushBlock(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
+    constexpr int NW = BLOCK / 64;
+    __shared__ uint32_t waveCount[NW];
+    __shared__ uint32_t blockBase;
+    const uint64_t mask = __ballot(pred);
+    const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+    if (lane == 0) waveCount[wave] = (uint32_t) __popcll(mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t c = waveCount[w];
+            waveCount[w] = tot;
+            tot += c;
+        }
+        blockBase = tot ? atomicAdd(counter, tot) : 0u;
+    }
+    __syncthreads();
+    if (pred) queue[blockBase + waveCount[wave] + (uint32_t) __popcll(mask & ((1ull << lane) - 1ull))] = value;
+    __syncthreads(); /* waveCount / blockBase may be reused by a second push */
+}
+
 /* append to a queue: one atomic per wave (wave64 ballot + mbcnt) */
 HD void qpush(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
     uint64_t mask = __ballot(pred);
@@ -813,7 +868,7 @@ HD bool decodePath(const HptWave &w, uint32_t id, int &px, int &py, uint32_t &j)
     return px < w.width && py < w.height;
 }
 
-extern "C" __global__ __launch_bounds__(256) void k_camera(HptScene sc, HptWave w, HptPaths P,
+extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, HptWave w, HptPaths P,
                                                             uint32_t *__restrict__ traceQ,
                                                             uint32_t *__restrict__ counters) {
     uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
@@ -851,7 +906,7 @@ extern "C" __global__ __launch_bounds__(256) void k_camera(HptScene sc, HptWave 
         P.state[id] = 0xffffffffu; /* outside the image */
         P.li[id] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
-    qpush(valid, id, traceQ, &counters[HPT_Q_TRACE]);
+    qpushBlock<HPT_QBLOCK>(valid, id, traceQ, &counters[HPT_Q_TRACE]);
 }
 
 /* k_trace: the wave's closest-hit rays (traceQ[0, nTrace)) then its any-hit
@@ -910,19 +965,20 @@ struct PathIO {
 
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
-    uint32_t *__restrict__ counters) {
+    uint32_t *__restrict__ counters, uint32_t *__restrict__ cursors) {
     __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
     PathIO io{P, traceQ, shadowQ, counters[HPT_Q_TRACE], counters[HPT_Q_SHADOW], 0};
-    tracePersistent<HPT_STACK, false>(sc, io, &counters[HPT_Q_CURSOR], stk + threadIdx.x, nullptr);
+    tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(HptScene sc, HptPaths P,
                                                                               const uint32_t *__restrict__ traceQ,
                                                                               const uint32_t *__restrict__ shadowQ,
                                                                               uint32_t *__restrict__ counters,
+                                                                              uint32_t *__restrict__ cursors,
                                                                               uint32_t *stats) {
     __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
     PathIO io{P, traceQ, shadowQ, counters[HPT_Q_TRACE], counters[HPT_Q_SHADOW], 0};
-    tracePersistent<HPT_STACK, true>(sc, io, &counters[HPT_Q_CURSOR], stk + threadIdx.x, stats);
+    tracePersistent<HPT_STACK, true>(sc, io, cursors, stk + threadIdx.x, stats);
 }
 
 /* fill the intersection record: hair.cpp:825-862 + skdtree.h:422-427 */
@@ -944,7 +1000,7 @@ HD void fillIts(const HptScene &sc, uint32_t seg, V3 hp, V3 rayD, V3 &p, Frame &
 }
 
 /* primary hits / misses (path.cpp:128-143) */
-extern "C" __global__ __launch_bounds__(256) void k_primary(HptScene sc, HptPaths P,
+extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, HptPaths P,
                                                              const uint32_t *__restrict__ traceQ,
                                                              uint32_t *__restrict__ shadeQ,
                                                              uint32_t *__restrict__ counters) {
@@ -965,11 +1021,11 @@ extern "C" __global__ __launch_bounds__(256) void k_primary(HptScene sc, HptPath
             P.li[id] = make_float4(0.0f + c.x, 0.0f + c.y, 0.0f + c.z, 0.0f);
         }
     }
-    qpush(alive, id, shadeQ, &counters[HPT_Q_SHADE_OUT]);
+    qpushBlock<HPT_QBLOCK>(alive, id, shadeQ, &counters[HPT_Q_SHADE_OUT]);
 }
 
 /* one bounce of shading: path.cpp:145-232 up to the continuation ray cast */
-extern "C" __global__ __launch_bounds__(256) void k_shade(HptScene sc, HptPaths P,
+extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade(HptScene sc, HptPaths P,
                                                            const uint32_t *__restrict__ shadeQ,
                                                            uint32_t *__restrict__ traceQ,
                                                            uint32_t *__restrict__ shadowQ,
@@ -1044,12 +1100,12 @@ extern "C" __global__ __launch_bounds__(256) void k_shade(HptScene sc, HptPaths 
         }
         P.state[id] = (st & 0xffff0000u) | dim;
     }
-    qpush(cont, id, traceQ, &counters[HPT_Q_TRACE]);
-    qpush(shadow, id, shadowQ, &counters[HPT_Q_SHADOW]);
+    qpushBlock<HPT_QBLOCK>(cont, id, traceQ, &counters[HPT_Q_TRACE]);
+    qpushBlock<HPT_QBLOCK>(shadow, id, shadowQ, &counters[HPT_Q_SHADOW]);
 }
 
 /* continuation result: path.cpp:225-286 */
-extern "C" __global__ __launch_bounds__(256) void k_post(HptScene sc, HptPaths P,
+extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_post(HptScene sc, HptPaths P,
                                                           const uint32_t *__restrict__ traceQ,
                                                           uint32_t *__restrict__ shadeQ,
                                                           uint32_t *__restrict__ counters) {
@@ -1106,7 +1162,7 @@ extern "C" __global__ __launch_bounds__(256) void k_post(HptScene sc, HptPaths P
             }
         }
     }
-    qpush(alive, id, shadeQ, &counters[HPT_Q_SHADE_OUT]);
+    qpushBlock<HPT_QBLOCK>(alive, id, shadeQ, &counters[HPT_Q_SHADE_OUT]);
 }
 
 /* Deterministic film accumulation (imageblock.h:124-204 + renderproc.cpp:
@@ -1312,13 +1368,13 @@ extern "C" __global__ void k_env_batch(HptScene sc, int n, const float *refp, co
 }
 
 /* tiny queue-rotation kernel: shade_in <- shade_out, reset the rest */
-extern "C" __global__ void k_rotate(uint32_t *counters) {
+extern "C" __global__ void k_rotate(uint32_t *counters, uint32_t *cursors) {
+    for (uint32_t i = threadIdx.x; i < HPT_CURSORS; i += blockDim.x) cursors[i * HPT_CURSOR_STRIDE] = 0;
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         counters[HPT_Q_SHADE_IN] = counters[HPT_Q_SHADE_OUT];
         counters[HPT_Q_SHADE_OUT] = 0;
         counters[HPT_Q_TRACE] = 0;
         counters[HPT_Q_SHADOW] = 0;
-        counters[HPT_Q_CURSOR] = 0;
     }
 }
 
@@ -1330,7 +1386,7 @@ static inline unsigned blocksFor(uint64_t n, unsigned bs) { return (unsigned) ((
 hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPaths &P, uint32_t *traceQ,
                              uint32_t *counters, hipStream_t s) {
     if (w.nPaths == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_camera, dim3(blocksFor(w.nPaths, 256)), dim3(256), 0, s, sc, w, P, traceQ, counters);
+    hipLaunchKernelGGL(k_camera, dim3(blocksFor(w.nPaths, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, w, P, traceQ, counters);
     return hipGetLastError();
 }
 /* persistent grid: as many one-wave blocks as can be resident at once
@@ -1356,33 +1412,34 @@ hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_
     if (maxItems == 0) return hipSuccess;
     if (stats)
         hipLaunchKernelGGL(k_trace_counted, dim3(persistentBlocks((const void *) k_trace_counted, maxItems)),
-                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, counters, stats);
+                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, counters,
+                           counters + HPT_CURSOR_OFFSET, stats);
     else
         hipLaunchKernelGGL(k_trace, dim3(persistentBlocks((const void *) k_trace, maxItems)), dim3(HPT_TRACE_BLOCK),
-                           0, s, sc, P, traceQ, shadowQ, counters);
+                           0, s, sc, P, traceQ, shadowQ, counters, counters + HPT_CURSOR_OFFSET);
     return hipGetLastError();
 }
 hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
                               uint32_t *counters, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_primary, dim3(blocksFor(maxItems, 256)), dim3(256), 0, s, sc, P, traceQ, shadeQ, counters);
+    hipLaunchKernelGGL(k_primary, dim3(blocksFor(maxItems, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, P, traceQ, shadeQ, counters);
     return hipGetLastError();
 }
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *traceQ,
                             uint32_t *shadowQ, uint32_t *counters, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_shade, dim3(blocksFor(maxItems, 256)), dim3(256), 0, s, sc, P, shadeQ, traceQ, shadowQ,
+    hipLaunchKernelGGL(k_shade, dim3(blocksFor(maxItems, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, P, shadeQ, traceQ, shadowQ,
                        counters);
     return hipGetLastError();
 }
 hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
                            uint32_t *counters, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_post, dim3(blocksFor(maxItems, 256)), dim3(256), 0, s, sc, P, traceQ, shadeQ, counters);
+    hipLaunchKernelGGL(k_post, dim3(blocksFor(maxItems, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, P, traceQ, shadeQ, counters);
     return hipGetLastError();
 }
 hipError_t hpt_launch_rotate(uint32_t *counters, hipStream_t s) {
-    hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, s, counters);
+    hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, s, counters, counters + HPT_CURSOR_OFFSET);
     return hipGetLastError();
 }
 hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *partial, float4 *film,
@@ -1403,7 +1460,7 @@ hipError_t hpt_launch_trace_batch(const HptScene &sc, int n, const float *o, con
                                   const float *maxt, int flags, float *ot, int32_t *os, float *op, uint8_t *oh,
                                   uint32_t *cursor, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(cursor, 0, 4, s);
+    hipError_t e = hipMemsetAsync(cursor, 0, HPT_CURSORS * HPT_CURSOR_STRIDE * 4, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_trace_batch, dim3(persistentBlocks((const void *) k_trace_batch, (uint64_t) n)),
                        dim3(HPT_TRACE_BLOCK), 0, s, sc, n, o, d, mint, maxt, flags, ot, os, op, oh, cursor);
