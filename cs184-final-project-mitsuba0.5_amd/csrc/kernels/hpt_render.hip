@@ -33,6 +33,9 @@
 
 using namespace hk;
 
+#ifndef HPT_LEAF_MODE
+#define HPT_LEAF_MODE 2 /* 0 prefetch next record, 1 no prefetch, 2 mask then exact (fastest) */
+#endif
 /* block size of the queue-producing kernels (k_camera, k_primary, k_shade, k_post) */
 #ifndef HPT_QBLOCK
 #define HPT_QBLOCK 1024
@@ -230,7 +233,6 @@ struct TraceRay {
     float mint, maxt;   /* ray interval after the scene-AABB clip and adaptive epsilon */
     float tmin, tmax;   /* interval of the current subtree */
     float tHit;
-    V3 pHit;
     uint32_t node, top, segHit;
     int sp, restarts, leaves;
     bool lost, found, shadow;
@@ -247,7 +249,6 @@ HD bool beginRay(const HptScene &sc, TraceRay &r, V3 o, V3 d, float rmint, float
     r.found = false;
     r.tHit = finf();
     r.segHit = 0;
-    r.pHit = v3(0.0f, 0.0f, 0.0f);
     float mint, maxt;
     if (!aabbIntersect(sc, o, d, r.rcp, mint, maxt)) return false;
     const float rayMinT = adaptiveMint(o, rmint, shadow);
@@ -272,7 +273,7 @@ struct TraceCounters {
 HD bool waveLeader() { return __lane_id() == (uint32_t) (__ffsll((unsigned long long) __ballot(1)) - 1); }
 
 /* One round: descend to the next leaf, test its segments, pop.  Returns
-   true when the ray is finished (r.found / r.tHit / r.segHit / r.pHit hold
+   true when the ray is finished (r.found / r.tHit / r.segHit hold
    the answer). */
 template <int STACK, bool STATS>
 HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, TraceCounters &tc) {
@@ -316,6 +317,45 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
         ++tc.nodes;
         if (waveLeader()) tc.nodeSlots += 64;
     }
+#if HPT_LEAF_MODE == 2
+    /* leaf, two passes: the fp32 pre-test marks candidates in a bit mask
+       (32 records per chunk), then the exact fp64 test runs on the marked
+       ones -- the prefetched records are dead by then, so the fp64 test's
+       registers do not stack on top of them */
+    const uint32_t first = nd.w0 & 0x7fffffffu, last = nd.w1;
+    const double r2 = (double) (sc.radius * sc.radius); /* Float product (hair.cpp:500) */
+    for (uint32_t c0 = first; c0 < last; c0 += 32) {
+        const uint32_t c1 = min(last, c0 + 32);
+        uint32_t mask = 0;
+        float4 na = leafF[2 * c0], nb = leafF[2 * c0 + 1];
+        for (uint32_t e = c0; e < c1; ++e) {
+            const float4 fa = na, fb = nb;
+            if (e + 1 < c1) {
+                na = leafF[2 * e + 2];
+                nb = leafF[2 * e + 3];
+            }
+            if (STATS) {
+                ++tc.prims;
+                if (waveLeader()) tc.primSlots += 64;
+            }
+            if (segMayHit(fa, fb, o, d, sc.radius)) mask |= 1u << (e - c0);
+        }
+        while (mask) {
+            const uint32_t e = c0 + (uint32_t) (__ffs(mask) - 1);
+            mask &= mask - 1;
+            const uint32_t s = __float_as_uint(leafF[2 * e + 1].z);
+            if (STATS) ++tc.exact;
+            float t;
+            V3 p;
+            if (HPT_SEG_TEST(sc.segs, s, o, d, r2, r.mint, r.tHit, t, p)) {
+                r.found = true;
+                if (r.shadow) return true;
+                r.tHit = t;
+                r.segHit = s;
+            }
+        }
+    }
+#else
     /* leaf: records are contiguous; the next one is fetched before the
        current one is tested, so the loads of a leaf overlap */
     const uint32_t first = nd.w0 & 0x7fffffffu, last = nd.w1;
@@ -326,11 +366,15 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     }
     const double r2 = (double) (sc.radius * sc.radius); /* Float product (hair.cpp:500) */
     for (uint32_t e = first; e < last; ++e) {
+#if HPT_LEAF_MODE == 1
+        const float4 fa = leafF[2 * e], fb = leafF[2 * e + 1];
+#else
         const float4 fa = na, fb = nb;
         if (e + 1 < last) {
             na = leafF[2 * e + 2];
             nb = leafF[2 * e + 3];
         }
+#endif
         if (STATS) {
             ++tc.prims;
             if (waveLeader()) tc.primSlots += 64;
@@ -345,9 +389,9 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
             if (r.shadow) return true;
             r.tHit = t;
             r.segHit = s;
-            r.pHit = p;
         }
     }
+#endif
     if (r.found && r.tHit <= r.tmax) return true;
     if (r.sp == 0) {
         if (!r.lost || r.tmax >= r.maxt || ++r.restarts > 64) return true;
@@ -365,6 +409,20 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     r.tmin = r.tmax;
     r.tmax = __uint_as_float(e.y);
     return r.tmin > r.tHit;
+}
+
+/* The hit point of a finished closest-hit ray: the exact test of the
+   winning segment re-run with an open far end takes the same branch (near /
+   far root, hair.cpp:519-541) as when it was accepted, so p is the value the
+   traversal saw -- recomputing it here keeps three registers out of the
+   traversal loop. */
+HD V3 hitPoint(const HptScene &sc, const TraceRay &r) {
+    if (!r.found) return v3(0.0f, 0.0f, 0.0f);
+    float t;
+    V3 p = v3(0.0f, 0.0f, 0.0f);
+    const double r2 = (double) (sc.radius * sc.radius);
+    segIntersect(sc.segs, r.segHit, r.o, r.d, r2, r.mint, finf(), t, p);
+    return p;
 }
 
 #ifndef HPT_REFILL
@@ -424,7 +482,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
                         nC += r.shadow ? 0u : 1u;
                         nS += r.shadow ? 1u : 0u;
                     }
-                    if (!active) nU += io.finish(k, r);
+                    if (!active) nU += io.finish(sc, k, r);
                 }
             }
         }
@@ -433,7 +491,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             continue;
         }
         if (active && traceRound<STACK, STATS>(sc, r, stk, 64, tc)) {
-            nU += io.finish(item, r);
+            nU += io.finish(sc, item, r);
             active = false;
         }
     }
@@ -928,11 +986,12 @@ struct PathIO {
         return beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(sd.x, sd.y, sd.z), kEpsilon, sd.w, true);
     }
     /* returns 1 for an unoccluded shadow ray */
-    HD uint32_t finish(uint32_t k, const TraceRay &r) {
+    HD uint32_t finish(const HptScene &sc, uint32_t k, const TraceRay &r) {
         if (!r.shadow) {
             P.hit[id] = make_float4(__int_as_float(r.found ? (int32_t) r.segHit : -1), r.found ? r.tHit : finf(),
                                     0.0f, 0.0f);
-            P.hitp[id] = r.found ? make_float4(r.pHit.x, r.pHit.y, r.pHit.z, 0.0f) : make_float4(0, 0, 0, 0);
+            const V3 p = hitPoint(sc, r);
+            P.hitp[id] = make_float4(p.x, p.y, p.z, 0.0f);
             return 0;
         }
         if (r.found) return 0;
@@ -1285,16 +1344,17 @@ struct BatchIO {
         return beginRay(sc, r, v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
                         mint[i], maxt[i], shadow);
     }
-    HD uint32_t finish(uint32_t i, const TraceRay &r) {
+    HD uint32_t finish(const HptScene &sc, uint32_t i, const TraceRay &r) {
         if (shadow) {
             outHit[i] = r.found ? 1 : 0;
             return 0;
         }
         outT[i] = r.found ? r.tHit : finf();
         outSeg[i] = r.found ? (int32_t) r.segHit : -1;
-        outP[3 * i] = r.found ? r.pHit.x : 0.0f;
-        outP[3 * i + 1] = r.found ? r.pHit.y : 0.0f;
-        outP[3 * i + 2] = r.found ? r.pHit.z : 0.0f;
+        const V3 p = hitPoint(sc, r);
+        outP[3 * i] = p.x;
+        outP[3 * i + 1] = p.y;
+        outP[3 * i + 2] = p.z;
         return 0;
     }
 };
