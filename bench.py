@@ -204,7 +204,10 @@ def main():
                       "exact_tests_per_ray": round(tot["exact"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "simd_util_nodes": round(tot["nodes"] / max(1, tot["node_slots"]), 3),
                       "simd_util_prims": round(tot["prims"] / max(1, tot["prim_slots"]), 3),
-                      "image_mean": float(img.mean())},
+                      "image_mean": float(img.mean()),
+                      # exact-arithmetic fingerprint of the frame (sum of the RGBW film in fp64):
+                      # identical for every traversal variant, since hits are bit-exact
+                      "film_fingerprint": float(film.double().sum().item())},
         }
         print(json.dumps(out), flush=True)
     r.close()

@@ -490,7 +490,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             if (exhausted) break;
             continue;
         }
-        if (active && traceRound<STACK, STATS>(sc, r, stk, 64, tc)) {
+        if (active && traceRound<STACK, STATS>(sc, r, stk, (int) blockDim.x, tc)) {
             nU += io.finish(sc, item, r);
             active = false;
         }
@@ -1002,13 +1002,12 @@ struct PathIO {
 };
 
 /* k_trace launch shape (measured on MI355X, furball 512^2 @ 256 spp):
-   one-wave blocks release their LDS stack as soon as their own rays finish
-   (+10% over 128-thread blocks); an 8-entry ring stack (64 B/lane, kd-restart
-   on overflow) beats 16 (-5%) and 4 (-11%, +12% node visits) entries; and a
-   5-waves/SIMD register target (96 VGPRs, 2 spilled) beats the natural
-   allocation at 4 waves/SIMD (+12%).  Overridable for experiments (make variant). */
+   persistent 256-thread blocks (64 and 128 are within 1.5%); an 8-entry ring
+   stack (64 B/lane, kd-restart on overflow) beats 16 (-5%) and 4 (-11%, +12%
+   node visits) entries; a 5-waves/SIMD register target beats the natural
+   allocation at 4 waves/SIMD.  Overridable for experiments (make variant). */
 #ifndef HPT_TRACE_BLOCK
-#define HPT_TRACE_BLOCK 64
+#define HPT_TRACE_BLOCK 256
 #endif
 #ifndef HPT_STACK
 #define HPT_STACK 8

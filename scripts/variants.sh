@@ -8,5 +8,5 @@ for v in lib "$@"; do
   python -c "
 import json
 d=json.loads(open('gpurun_out/var.log').read().strip().splitlines()[-1])
-print('%-10s %8.2f Mpaths/s trace %7.1f ms/step %.1f GB/s nodes/ray %.1f prims/ray %.1f' % ('$v', d['value'], d['roofline']['rank0_trace_ms_per_step'], d['roofline']['achieved'], d['stats']['nodes_per_ray'], d['stats']['prims_per_ray']))"
+print('%-10s %8.2f Mpaths/s trace %7.1f ms/step %.1f GB/s nodes/ray %.1f prims/ray %.1f film %.9e' % ('$v', d['value'], d['roofline']['rank0_trace_ms_per_step'], d['roofline']['achieved'], d['stats']['nodes_per_ray'], d['stats']['prims_per_ray'], d['stats'].get('film_fingerprint', 0)))"
 done
