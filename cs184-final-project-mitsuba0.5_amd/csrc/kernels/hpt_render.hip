@@ -425,6 +425,9 @@ HD V3 hitPoint(const HptScene &sc, const TraceRay &r) {
     return p;
 }
 
+#ifndef HPT_XCD_SHARDS
+#define HPT_XCD_SHARDS 0 /* 1: waves claim their own XCD's shards first */
+#endif
 #ifndef HPT_REFILL
 #define HPT_REFILL 16 /* idle lanes that trigger a refill of the wave */
 #endif
@@ -448,8 +451,22 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
     TraceCounters tc;
     uint32_t item = 0, nC = 0, nS = 0, nU = 0;
     bool active = false, exhausted = false;
+#if HPT_XCD_SHARDS
+    /* XCD-aware claiming: the 64 shards are 8 groups of 8 contiguous
+       shards; a wave walks its own XCD's group first (HW_REG_XCC_ID,
+       placement used for L2 affinity only), then the other groups, so each
+       XCD's L2 mostly sees the tree region of one eighth of the queue
+       (queue order follows the image's block order) */
+    uint32_t xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    xcc &= 7u;
+    const uint32_t sub = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) / 8u;
+    int tried = 0;
+    uint32_t shard = xcc * 8u + sub % 8u;
+#else
     uint32_t shard = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % HPT_CURSORS;
     int tried = 0;
+#endif
     while (true) {
         const uint64_t idle = __ballot(!active);
         if (!exhausted && __popcll(idle) >= HPT_REFILL) {
@@ -470,7 +487,11 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
                     exhausted = true;
                     break;
                 }
+#if HPT_XCD_SHARDS
+                shard = ((xcc + (uint32_t) tried / 8u) % 8u) * 8u + (sub + (uint32_t) tried) % 8u;
+#else
                 shard = (shard + 1) % HPT_CURSORS;
+#endif
             }
             if (!active) {
                 const uint32_t rank = (uint32_t) __popcll(idle & ((1ull << lane) - 1ull));

@@ -9,9 +9,10 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 i=0
 for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU" \
-           "TCC_HIT_sum TCC_MISS_sum" ; do
+           "SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC" \
+           "TCC_HIT_sum TCC_MISS_sum" "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $grp -d "$OUT/g$i" -o pmc -- \
-      python3 "$ROOT/bench.py" --cpu-baseline off "$@" > "$OUT/g$i.log" 2>&1
+      python3 "$ROOT/bench.py" --cpu-baseline off "$@" > "$OUT/g$i.log" 2>&1 || echo "group $i failed: $grp"
 done
 echo "pmc $TAG done"
