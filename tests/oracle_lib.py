@@ -162,7 +162,7 @@ class Oracle:
         return mn, mx
 
     def render(self, spp_begin, spp_end, threads=None, shard=0, n_shards=1, width=None, height=None):
-        threads = threads or os.cpu_count()
+        threads = threads or min(16, os.cpu_count() or 1)  # the GPU box's CPU share is 16
         film = np.zeros((height, width, 4), np.float32)
         stats = np.zeros(8, np.uint64)
         self.check(self.lib.orc_render_shard(self.s, spp_begin, spp_end, threads, shard, n_shards, p(film, _f),

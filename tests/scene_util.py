@@ -63,7 +63,7 @@ def reference_flags_floor(name, n_strands, r, width, height, spp):
                 spp=spp)
         o.set_kdtree(nodes, idx)
         o.prepare()
-        films.append(native.develop(o.render(0, spp, width=width, height=height)[0]))
+        films.append(native.develop(o.render(0, spp, threads=16, width=width, height=height)[0]))
     a, b = films
     same = np.all(np.abs(a - b) <= 1e-5 * np.abs(a) + 1e-7, axis=-1)
     return l2_metrics(a, b), float(same.mean())
