@@ -37,9 +37,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 #   closest ray: queue id 4 + ray 32 + hit record 32 = 68 B
 #   shadow ray:  queue id 4 + origin 16 + direction/maxt 16 = 36 B, +48 B (contribution + radiance RMW)
 #                when unoccluded
-#   node visit 8 B; primitive test 32 B leaf-ordered fp32 pre-test record;
+#   node visit 32 B (two-level HptNode4); primitive test 32 B leaf-ordered fp32 pre-test record;
 #   exact fp64 test (pre-test survivors) + 128 B segment record
-BYTES_CLOSEST, BYTES_SHADOW, BYTES_UNOCC, BYTES_NODE, BYTES_PRIM, BYTES_EXACT = 68, 36, 48, 8, 32, 128
+BYTES_CLOSEST, BYTES_SHADOW, BYTES_UNOCC, BYTES_NODE, BYTES_PRIM, BYTES_EXACT = 68, 36, 48, 32, 32, 128
 
 
 def parse():

@@ -245,6 +245,7 @@ struct BNode {
     float split = 0;
     std::unique_ptr<BNode> kid[2];
     std::vector<uint32_t> prims;
+    uint32_t pStart = 0, pEnd = 0; /* range in KDTreeHost::prims once laid out */
 };
 
 struct Builder {
@@ -403,6 +404,9 @@ void layoutTreelets(const BNode *root, KDTreeHost &t) {
         if (it.n->axis < 0) {
             uint32_t start = (uint32_t) t.prims.size();
             for (uint32_t p : it.n->prims) t.prims.push_back(p);
+            BNode *ln = const_cast<BNode *>(it.n);
+            ln->pStart = start;
+            ln->pEnd = (uint32_t) t.prims.size();
             t.nodes[it.idx].w0 = 0x80000000u | start;
             t.nodes[it.idx].w1 = (uint32_t) t.prims.size();
             t.leaves++;
@@ -445,6 +449,64 @@ void layoutTreelets(const BNode *root, KDTreeHost &t) {
             head = 0;
         }
     }
+}
+
+/* Two-level node layout for the device traversal (HptNode4, hpt_device.h):
+ * every node fuses a binary node with its two children, so one 32-byte fetch
+ * advances the descent by two levels.  Built breadth-first from the binary
+ * tree after layoutTreelets has assigned the leaves' primitive ranges. */
+uint32_t leafRef(const BNode *n, KDTreeHost &t) {
+    const uint32_t count = n->pEnd - n->pStart;
+    if (count < HPT_LEAF_INLINE_MAX && n->pStart < (1u << 24)) return 0x80000000u | (count << 24) | n->pStart;
+    const uint32_t idx = (uint32_t) t.leafTable.size() / 2;
+    t.leafTable.push_back(n->pStart);
+    t.leafTable.push_back(n->pEnd);
+    return 0x80000000u | (HPT_LEAF_INLINE_MAX << 24) | idx;
+}
+
+void buildNode4(const BNode *root, KDTreeHost &t) {
+    t.nodes4.clear();
+    t.leafTable.clear();
+    std::vector<const BNode *> queue;
+    auto ref = [&](const BNode *n) -> uint32_t {
+        if (n->axis < 0) return leafRef(n, t);
+        queue.push_back(n);
+        return (uint32_t) queue.size() - 1; /* node index = BFS position */
+    };
+    auto splitBits = [](float f) {
+        uint32_t b;
+        std::memcpy(&b, &f, 4);
+        return b;
+    };
+    if (root->axis < 0) {
+        /* single-leaf tree: a node whose top split sends every ray to one side */
+        HptNode4 nd{};
+        nd.w[0] = splitBits(std::numeric_limits<float>::infinity());
+        nd.w[4] = nd.w[5] = nd.w[6] = nd.w[7] = leafRef(root, t);
+        t.nodes4.push_back(nd);
+        return;
+    }
+    queue.push_back(root);
+    for (size_t qi = 0; qi < queue.size(); ++qi) {
+        const BNode *n = queue[qi];
+        HptNode4 nd{};
+        nd.w[0] = splitBits(n->split);
+        uint32_t flags = (uint32_t) n->axis;
+        for (int k = 0; k < 2; ++k) {
+            const BNode *c = n->kid[k].get();
+            if (c->axis >= 0) {
+                nd.w[1 + k] = splitBits(c->split);
+                flags |= ((uint32_t) c->axis << (2 + 2 * k)) | (1u << (6 + k));
+                nd.w[4 + 2 * k] = ref(c->kid[0].get());
+                nd.w[5 + 2 * k] = ref(c->kid[1].get());
+            } else {
+                nd.w[4 + 2 * k] = nd.w[5 + 2 * k] = leafRef(c, t);
+            }
+        }
+        nd.w[3] = flags;
+        t.nodes4.push_back(nd);
+    }
+    if (t.leafTable.empty()) t.leafTable.push_back(0), t.leafTable.push_back(0);
 }
 
 } // namespace
@@ -522,6 +584,7 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
     std::unique_ptr<BNode> tree = b.build(std::move(refs), root, 0, 0);
     t.nodes.reserve(2 * S);
     layoutTreelets(tree.get(), t);
+    buildNode4(tree.get(), t);
     /* leaf-ordered fp32 pre-test records */
     t.leafF.resize(t.prims.size());
     for (size_t e = 0; e < t.prims.size(); ++e) {

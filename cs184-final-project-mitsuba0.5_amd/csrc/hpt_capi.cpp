@@ -438,6 +438,8 @@ int hpt_prepare(hpt_context *c) {
     setupCamera(d, sc.cam);
     int r = 0;
     r |= upload(c, c->tree.nodes.data(), c->tree.nodes.size() * sizeof(HptNode), (const void **) &sc.nodes);
+    r |= upload(c, c->tree.nodes4.data(), c->tree.nodes4.size() * sizeof(HptNode4), (const void **) &sc.nodes4);
+    r |= upload(c, c->tree.leafTable.data(), c->tree.leafTable.size() * 4, (const void **) &sc.leafTable);
     r |= upload(c, c->tree.leafF.data(), c->tree.leafF.size() * sizeof(HptSegF), (const void **) &sc.leafF);
     r |= upload(c, c->tree.segs.data(), c->tree.segs.size() * sizeof(HptSegment), (const void **) &sc.segs);
     for (int i = 0; i < 3; ++i) {

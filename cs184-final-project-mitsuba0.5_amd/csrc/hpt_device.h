@@ -62,6 +62,19 @@ struct HptNode {
     uint32_t w0, w1;
 };
 
+/* Two-level kd node (32 bytes): a binary node fused with its two children,
+ * so the device descent fetches once per two levels.
+ *   w[0] split of the top node, w[1]/w[2] splits of its left/right child
+ *   w[3] axis_top | axis_L << 2 | axis_R << 4 | L_inner << 6 | R_inner << 7
+ *   w[4..7] grandchild refs LL, LR, RL, RR (a leaf child fills both of its
+ *   slots with its own ref).  A ref is a node index (bit 31 clear) or a
+ *   leaf: 0x80000000 | count << 24 | first primitive, with count ==
+ *   HPT_LEAF_INLINE_MAX meaning "look up (first, end) in leafTable[index]". */
+#define HPT_LEAF_INLINE_MAX 127u
+struct HptNode4 {
+    uint32_t w[8];
+};
+
 struct HptCamera {
     float s2c[16];      /* sampleToCamera, row-major (perspective.cpp:155) */
     float toWorld[16];  /* camera-to-world, row-major */
@@ -102,6 +115,8 @@ struct HptEnvMap {
 struct HptScene {
     HptCamera cam;
     const HptNode *nodes;
+    const HptNode4 *nodes4;
+    const uint32_t *leafTable;
     const HptSegF *leafF;       /* leaf primitive list (fp32 pre-test records) */
     const HptSegment *segs;
     float aabbMin[3], aabbMax[3];

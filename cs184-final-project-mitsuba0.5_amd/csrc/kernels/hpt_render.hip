@@ -33,6 +33,9 @@
 
 using namespace hk;
 
+#ifndef HPT_NODE4
+#define HPT_NODE4 1 /* 1: descend over two-level nodes (HptNode4); 0: binary HptNode */
+#endif
 #ifndef HPT_LEAF_MODE
 #define HPT_LEAF_MODE 2 /* 0 prefetch next record, 1 no prefetch, 2 mask then exact (fastest) */
 #endif
@@ -285,6 +288,99 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     const V3 o = r.o, d = r.d, rcp = r.rcp;
     /* hard bound so every wave drains even on a malformed tree */
     if (++r.leaves > (1 << 18)) return true;
+#if HPT_NODE4
+    /* descent over two-level nodes (HptNode4): one 32-byte fetch decides the
+       top split and the split of each child the ray interval reaches; the
+       binary traversal's front-to-back order and intervals are kept exactly
+       (the second side's children are pushed as the binary traversal would
+       push that side and later split it) */
+    const uint4 *__restrict__ nodes4 = reinterpret_cast<const uint4 *>(sc.nodes4);
+    uint32_t ref = r.node;
+    auto push = [&](uint32_t what, float tmaxOf) {
+        stk[(r.top & (STACK - 1)) * stride] = make_uint2(what, __float_as_uint(tmaxOf));
+        r.lost = r.lost | (r.sp == STACK);
+        r.top += 1u;
+        r.sp += (r.sp < STACK) ? 1 : 0;
+    };
+    while (!(ref & 0x80000000u)) {
+        if (STATS) {
+            ++tc.nodes;
+            if (waveLeader()) tc.nodeSlots += 64;
+        }
+        const uint4 na = nodes4[2 * ref], nb = nodes4[2 * ref + 1];
+        const uint32_t flags = na.w;
+        /* top split */
+        const uint32_t ax0 = flags & 3u;
+        const float sp0 = __uint_as_float(na.x);
+        const float oa0 = ax0 == 0 ? o.x : (ax0 == 1 ? o.y : o.z);
+        const float da0 = ax0 == 0 ? d.x : (ax0 == 1 ? d.y : d.z);
+        const float ra0 = ax0 == 0 ? rcp.x : (ax0 == 1 ? rcp.y : rcp.z);
+        const float ts0 = (sp0 - oa0) * ra0;
+        const bool below0 = (oa0 < sp0) | ((oa0 == sp0) & (da0 <= 0.0f));
+        const bool near0 = !(ts0 <= r.tmax) | (ts0 <= 0.0f);
+        const bool far0 = !near0 & (ts0 < r.tmin);
+        const bool both0 = !(near0 | far0);
+        const uint32_t firstSide = below0 ? 0u : 1u;
+        const uint32_t sideA = far0 ? (firstSide ^ 1u) : firstSide, sideB = firstSide ^ 1u;
+        const float tA = both0 ? ts0 : r.tmax;
+        /* side B (visited after side A) is pushed first */
+        if (both0) {
+            const bool innerB = (flags >> (6 + sideB)) & 1u;
+            const uint32_t rB0 = sideB ? nb.z : nb.x, rB1 = sideB ? nb.w : nb.y;
+            if (innerB) {
+                const uint32_t ax = (flags >> (2 + 2 * sideB)) & 3u;
+                const float spl = __uint_as_float(sideB ? na.z : na.y);
+                const float oa = ax == 0 ? o.x : (ax == 1 ? o.y : o.z);
+                const float da = ax == 0 ? d.x : (ax == 1 ? d.y : d.z);
+                const float ra = ax == 0 ? rcp.x : (ax == 1 ? rcp.y : rcp.z);
+                const float ts = (spl - oa) * ra;
+                const bool below = (oa < spl) | ((oa == spl) & (da <= 0.0f));
+                const uint32_t f = below ? rB0 : rB1, sc2 = below ? rB1 : rB0;
+                const bool nearB = !(ts <= r.tmax) | (ts <= 0.0f);
+                const bool farB = !nearB & (ts < ts0);
+                if (!(nearB | farB)) {
+                    push(sc2, r.tmax);
+                    push(f, ts);
+                } else {
+                    push(farB ? sc2 : f, r.tmax);
+                }
+            } else {
+                push(rB0, r.tmax);
+            }
+        }
+        /* side A, over [tmin, tA] */
+        const bool innerA = (flags >> (6 + sideA)) & 1u;
+        const uint32_t rA0 = sideA ? nb.z : nb.x, rA1 = sideA ? nb.w : nb.y;
+        if (innerA) {
+            const uint32_t ax = (flags >> (2 + 2 * sideA)) & 3u;
+            const float spl = __uint_as_float(sideA ? na.z : na.y);
+            const float oa = ax == 0 ? o.x : (ax == 1 ? o.y : o.z);
+            const float da = ax == 0 ? d.x : (ax == 1 ? d.y : d.z);
+            const float ra = ax == 0 ? rcp.x : (ax == 1 ? rcp.y : rcp.z);
+            const float ts = (spl - oa) * ra;
+            const bool below = (oa < spl) | ((oa == spl) & (da <= 0.0f));
+            const uint32_t f = below ? rA0 : rA1, sc2 = below ? rA1 : rA0;
+            const bool nearA = !(ts <= tA) | (ts <= 0.0f);
+            const bool farA = !nearA & (ts < r.tmin);
+            const bool bothA = !(nearA | farA);
+            if (bothA) push(sc2, tA);
+            ref = farA ? sc2 : f;
+            r.tmax = bothA ? ts : tA;
+        } else {
+            ref = rA0;
+            r.tmax = tA;
+        }
+    }
+    if (STATS) {
+        ++tc.nodes;
+        if (waveLeader()) tc.nodeSlots += 64;
+    }
+    uint32_t leafFirst = ref & 0x00ffffffu, leafLast = leafFirst + ((ref >> 24) & 0x7fu);
+    if (((ref >> 24) & 0x7fu) == HPT_LEAF_INLINE_MAX) {
+        leafLast = sc.leafTable[2 * leafFirst + 1];
+        leafFirst = sc.leafTable[2 * leafFirst];
+    }
+#else
     HptNode nd = nodes[r.node];
     while (!(nd.w0 & 0x80000000u)) {
         if (STATS) {
@@ -317,12 +413,14 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
         ++tc.nodes;
         if (waveLeader()) tc.nodeSlots += 64;
     }
+    const uint32_t leafFirst = nd.w0 & 0x7fffffffu, leafLast = nd.w1;
+#endif
 #if HPT_LEAF_MODE == 2
     /* leaf, two passes: the fp32 pre-test marks candidates in a bit mask
        (32 records per chunk), then the exact fp64 test runs on the marked
        ones -- the prefetched records are dead by then, so the fp64 test's
        registers do not stack on top of them */
-    const uint32_t first = nd.w0 & 0x7fffffffu, last = nd.w1;
+    const uint32_t first = leafFirst, last = leafLast;
     const double r2 = (double) (sc.radius * sc.radius); /* Float product (hair.cpp:500) */
     for (uint32_t c0 = first; c0 < last; c0 += 32) {
         const uint32_t c1 = min(last, c0 + 32);
@@ -358,7 +456,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
 #else
     /* leaf: records are contiguous; the next one is fetched before the
        current one is tested, so the loads of a leaf overlap */
-    const uint32_t first = nd.w0 & 0x7fffffffu, last = nd.w1;
+    const uint32_t first = leafFirst, last = leafLast;
     float4 na = make_float4(0, 0, 0, 0), nb = na;
     if (first < last) {
         na = leafF[2 * first];
