@@ -61,6 +61,28 @@ HD float sobolSample(const HptScene &sc, uint64_t index, uint32_t dim) {
     return fminr((float) result * (1.0f / 4294967296.0f), kOneMinusEps);
 }
 
+/* sobolSample for a dimension that is the same across the wave (k_shade /
+   k_post: all paths of a bounce have consumed the same number of dimensions,
+   path.cpp's sampler->next1D/next2D order).  The dimension's 52 direction
+   numbers are then read once for the wave and every index bit is applied
+   with a select, instead of a per-lane loop of dependent table loads.  Falls
+   back to sobolSample when the wave disagrees.  Same XOR of the same
+   matrix rows as sobolseq.h:43-58. */
+HD float sobolSampleUniform(const HptScene &sc, uint64_t index, uint32_t dim) {
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(dim);
+    if (__ballot(dim != d0) != 0) return sobolSample(sc, index, dim);
+    const uint32_t *__restrict__ m = sc.sobol + d0 * HPT_SOBOL_BITS;
+    const uint32_t lo = (uint32_t) index, hi = (uint32_t) (index >> 32);
+    uint32_t result = 0;
+#pragma unroll
+    for (int i = 0; i < 32; ++i) result ^= ((lo >> i) & 1u) ? m[i] : 0u;
+    if (__ballot(hi != 0) != 0) {
+#pragma unroll
+        for (int i = 32; i < HPT_SOBOL_BITS; ++i) result ^= ((hi >> (i - 32)) & 1u) ? m[i] : 0u;
+    }
+    return fminr((float) result * (1.0f / 4294967296.0f), kOneMinusEps);
+}
+
 HD uint64_t sobolLookUp(const HptScene &sc, uint32_t m, uint32_t frame, uint32_t px, uint32_t py) {
     uint64_t index = (uint64_t) frame << (m << 1);
     uint64_t delta = 0;
@@ -1232,7 +1254,7 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade(HptScene sc, Hp
             float4 thr = P.thr[id];
             V3 T = v3(thr.x, thr.y, thr.z);
             /* ---- direct illumination (scene.cpp:828-852, envmap.cpp:516-543) ---- */
-            float nx = sobolSample(sc, sidx, dim), ny = sobolSample(sc, sidx, dim + 1);
+            float nx = sobolSampleUniform(sc, sidx, dim), ny = sobolSampleUniform(sc, sidx, dim + 1);
             dim += 2;
             {
                 V3 dl, value;
@@ -1256,7 +1278,7 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade(HptScene sc, Hp
                 }
             }
             /* ---- BSDF sampling ---- */
-            float bx = sobolSample(sc, sidx, dim), by = sobolSample(sc, sidx, dim + 1);
+            float bx = sobolSampleUniform(sc, sidx, dim), by = sobolSampleUniform(sc, sidx, dim + 1);
             dim += 2;
             V3 woL;
             float bpdf = 0.0f;
@@ -1328,7 +1350,7 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_post(HptScene sc, Hpt
                     alive = false;
                 } else if ((int) depth >= sc.rrDepth) {
                     float q = fminr(maxc(T) * 1.0f * 1.0f, 0.95f);
-                    float u = sobolSample(sc, P.sobol[id], dim);
+                    float u = sobolSampleUniform(sc, P.sobol[id], dim);
                     dim += 1;
                     if (u >= q) alive = false;
                     else T = divs(T, q);
