@@ -78,6 +78,7 @@ struct SceneDesc {
     bool specularGiven = false;
     float exponent = 30.0f;
     bool nonlinear = false;
+    bool sampleVisible = true, ensureEnergyConservation = true;
     /* emitter */
     std::string emitter = "";
     std::string envFile;
@@ -144,6 +145,17 @@ struct MarschnerHost {
 bool precomputeMarschner(const SceneDesc &d, const std::string &dataDir, MarschnerHost &out,
                          std::string &err);
 void configureKajiyaKay(const SceneDesc &d, HptKajiyaKay &out);
+
+/* roughplastic (roughplastic.cpp:197-299): device parameters + the 1-D external transmittance slice */
+struct RoughPlasticHost {
+    HptRoughPlastic p{};
+    std::vector<float> trans;
+};
+bool configureRoughPlastic(const SceneDesc &d, const std::string &dataDir, RoughPlasticHost &out, std::string &err);
+/* RoughTransmittance (rtrans.h) for one distribution: the external 1-D slice at (eta, alphaSlice) and
+ * Fdr = 1 - internal (1/eta) diffuse transmittance at alphaDiffuse */
+bool roughTransmittance(const std::string &dataDir, const std::string &distribution, float eta, float alphaSlice,
+                        float alphaDiffuse, std::vector<float> &trans, float &fdr, std::string &err);
 
 struct EnvHost {
     int w = 0, h = 0;

@@ -335,28 +335,90 @@ bool precomputeMarschner(const SceneDesc &d, const std::string &dataDir, Marschn
     out.invEta2 = 1.0f / (eta * eta);
     for (int i = 0; i < 3; ++i) out.diffuse[i] = d.diffuse[i];
     /* rough transmittance slices (rtrans.h) */
+    float alpha = std::max(d.alpha, 1e-4f);
+    if (eta < 1) { err = "marschner: eta < 1 is not supported by the transmittance tables"; return false; }
+    return roughTransmittance(dataDir, d.distribution, eta, alpha, alpha, out.trans, out.fdr, err);
+}
+
+bool roughTransmittance(const std::string &dataDir, const std::string &distribution, float eta, float alphaSlice,
+                        float alphaDiffuse, std::vector<float> &trans, float &fdr, std::string &err) {
     RTrans rt;
-    std::string path = dataDir + "/microfacet/" + d.distribution + ".dat";
+    std::string path = dataDir + "/microfacet/" + distribution + ".dat";
     if (!rt.load(path)) {
         err = "cannot load rough transmittance data \"" + path + "\"";
         return false;
     }
-    float alpha = std::max(d.alpha, 1e-4f);
-    if (eta < 1) { err = "marschner: eta < 1 is not supported by the transmittance tables"; return false; }
-    if (alpha < rt.alphaMin || alpha > rt.alphaMax) {
-        err = "marschner: alpha outside the precomputed range";
+    /* checkEta / checkAlpha (rtrans.h:390-407) */
+    float etaC = eta < 1 ? 1 / eta : eta;
+    if (etaC < rt.etaMin || etaC > rt.etaMax) {
+        err = "the requested relative index of refraction eta=" + std::to_string(eta) +
+              " is outside of the supported range";
+        return false;
+    }
+    if (alphaSlice < rt.alphaMin || alphaSlice > rt.alphaMax) {
+        err = "the requested roughness value alpha=" + std::to_string(alphaSlice) +
+              " is outside of the supported range";
         return false;
     }
     std::vector<float> ext2, extD, int2, intD;
     rt.sliceEta(eta, ext2, extD);
     rt.sliceEta(1 / eta, int2, intD);
-    float wa = std::pow((alpha - rt.alphaMin) / (rt.alphaMax - rt.alphaMin), (float) 0.25f);
-    out.trans.resize(rt.nTheta);
+    /* setAlpha (rtrans.h:353-388) on the external copy */
+    float wa = std::pow((alphaSlice - rt.alphaMin) / (rt.alphaMax - rt.alphaMin), (float) 0.25f);
+    trans.resize(rt.nTheta);
     float dT = 1.0f / (rt.nTheta - 1);
-    for (size_t i = 0; i < rt.nTheta; ++i) out.trans[i] = cubic2D(i * dT, wa, ext2.data(), rt.nTheta, rt.nAlpha);
-    float internalDiffuse = cubic1D(wa, intD.data(), rt.nAlpha, 0.0f, 1.0f);
+    for (size_t i = 0; i < rt.nTheta; ++i) trans[i] = cubic2D(i * dT, wa, ext2.data(), rt.nTheta, rt.nAlpha);
+    /* evalDiffuse(alpha) (rtrans.h:249-260) on the internal 2D copy */
+    float wd = std::pow((alphaDiffuse - rt.alphaMin) / (rt.alphaMax - rt.alphaMin), (float) 0.25f);
+    float internalDiffuse = cubic1D(wd, intD.data(), rt.nAlpha, 0.0f, 1.0f);
     internalDiffuse = std::min(1.0f, std::max(0.0f, internalDiffuse));
-    out.fdr = 1 - internalDiffuse;
+    fdr = 1 - internalDiffuse;
+    return true;
+}
+
+bool configureRoughPlastic(const SceneDesc &d, const std::string &dataDir, RoughPlasticHost &out, std::string &err) {
+    /* RoughPlastic(props) + configure (roughplastic.cpp:197-299) */
+    const float eta = d.intIOR / d.extIOR;
+    if (d.intIOR < 0 || d.extIOR < 0 || d.intIOR == d.extIOR) {
+        err = "roughplastic: the interior and exterior indices of refraction must be positive and differ";
+        return false;
+    }
+    HptRoughPlastic &rp = out.p;
+    rp.type = d.distribution == "beckmann" ? 0 : d.distribution == "ggx" ? 1 : 2;
+    rp.sampleVisible = rp.type == 2 ? 0 : (d.sampleVisible ? 1 : 0);
+    rp.nonlinear = d.nonlinear ? 1 : 0;
+    /* m_alpha = ConstantFloatTexture(distr.getAlpha()); every use reads eval().average() (spectrum.h:481-486)
+     * and a MicrofacetDistribution built from it clamps to 1e-4 again (microfacet.h:67-75) */
+    const float a0 = std::max(d.alpha, 1e-4f);
+    const float aAvg = (((0.0f + a0) + a0) + a0) * (1.0f / 3);
+    rp.alpha = std::max(aAvg, 1e-4f);
+    rp.exponent = std::max(2.0f / (rp.alpha * rp.alpha) - 2.0f, 0.0f); /* computePhongExponent (:701-704) */
+    rp.eta = eta;
+    rp.invEta2 = 1.0f / (eta * eta);
+    float spec[3] = {d.specular[0], d.specular[1], d.specular[2]};
+    float diff[3] = {d.diffuse[0], d.diffuse[1], d.diffuse[2]};
+    if (d.ensureEnergyConservation) { /* bsdf.cpp:88-113, max = 1 */
+        for (float *v : {spec, diff}) {
+            float mx = std::max(std::max(v[0], v[1]), v[2]);
+            if (mx > 1.0f) {
+                float s = 0.99f * (1.0f / mx);
+                for (int i = 0; i < 3; ++i) v[i] *= s;
+            }
+        }
+    }
+    float dAvg = diff[0] * 0.212671f + diff[1] * 0.715160f + diff[2] * 0.072169f;
+    float sAvg = spec[0] * 0.212671f + spec[1] * 0.715160f + spec[2] * 0.072169f;
+    rp.specularSamplingWeight = sAvg / (dAvg + sAvg);
+    for (int i = 0; i < 3; ++i) {
+        rp.diffuse[i] = diff[i];
+        rp.specular[i] = spec[i];
+    }
+    if (!roughTransmittance(dataDir, d.distribution, eta, aAvg, rp.alpha, out.trans, rp.fdr, err)) {
+        err = "roughplastic: " + err;
+        return false;
+    }
+    rp.trans = nullptr;
+    rp.transSize = (int) out.trans.size();
     return true;
 }
 

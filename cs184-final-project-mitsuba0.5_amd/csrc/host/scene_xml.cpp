@@ -367,9 +367,45 @@ void parseBSDF(const Ctx &c, const XNode &b, SceneDesc &d) {
             d.specular[0] = d.specular[1] = d.specular[2] = 0.2f;
         }
         d.exponent = num1(p, "exponent", 30.0f);
+    } else if (type == "roughplastic") {
+        /* roughplastic.cpp:197-227 + MicrofacetDistribution(props) (microfacet.h:99-144) */
+        d.intIOR = lookupIOR(c, b, p, "intIOR", "polypropylene");
+        d.extIOR = lookupIOR(c, b, p, "extIOR", "air");
+        if (d.intIOR < 0 || d.extIOR < 0 || d.intIOR == d.extIOR)
+            fail(c.file, b.line, "The interior and exterior indices of refraction must be positive and differ!");
+        d.distribution = "beckmann";
+        if (p.str.count("distribution")) {
+            std::string v = p.str["distribution"];
+            for (auto &ch : v) ch = (char) std::tolower((unsigned char) ch);
+            if (v == "as") v = "phong";
+            if (v != "beckmann" && v != "ggx" && v != "phong")
+                fail(c.file, b.line, "Specified an invalid distribution \"" + v +
+                                         "\", must be \"beckmann\", \"ggx\", or \"phong\"/\"as\"!");
+            d.distribution = v;
+        }
+        const bool hasA = p.num.count("alpha") != 0, hasU = p.num.count("alphaU") != 0,
+                   hasV = p.num.count("alphaV") != 0;
+        d.alpha = 0.1f;
+        if (hasA) {
+            if (hasU || hasV) fail(c.file, b.line, "Microfacet model: please specify either 'alpha' or 'alphaU'/'alphaV'.");
+            d.alpha = num1(p, "alpha", 0.1f);
+        } else if (hasU || hasV) {
+            if (!(hasU && hasV)) fail(c.file, b.line, "Microfacet model: both 'alphaU' and 'alphaV' must be specified.");
+            d.alpha = num1(p, "alphaU", 0.1f);
+            if (std::max(num1(p, "alphaU", 0.1f), 1e-4f) != std::max(num1(p, "alphaV", 0.1f), 1e-4f))
+                fail(c.file, b.line, "The 'roughplastic' plugin currently does not support anisotropic "
+                                     "microfacet distributions!");
+        }
+        d.sampleVisible = num1(p, "sampleVisible", 1.0f) != 0.0f;
+        d.nonlinear = num1(p, "nonlinear", 0.0f) != 0.0f;
+        d.ensureEnergyConservation = num1(p, "ensureEnergyConservation", 1.0f) != 0.0f;
+        for (int i = 0; i < 3; ++i) {
+            d.diffuse[i] = p.num.count("diffuseReflectance") ? p.num["diffuseReflectance"][i] : 0.5f;
+            d.specular[i] = p.num.count("specularReflectance") ? p.num["specularReflectance"][i] : 1.0f;
+        }
     } else {
         fail(c.file, b.line, "BSDF plugin \"" + type +
-                                 "\" is outside the hair hot path (supported: marschner, kajiyakay)");
+                                 "\" is outside the hair hot path (supported: marschner, kajiyakay, roughplastic)");
     }
 }
 

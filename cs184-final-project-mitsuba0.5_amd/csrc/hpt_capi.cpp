@@ -51,6 +51,7 @@ struct hpt_context {
     KDTreeHost tree;
     MarschnerHost mar;
     HptKajiyaKay kk;
+    RoughPlasticHost rp;
     EnvHost env;
     bool envFromSunsky = false;
     SunSkyTables sunsky;
@@ -346,6 +347,29 @@ int hpt_set_bsdf_marschner(hpt_context *c, float int_ior, float ext_ior, int dis
     return HPT_OK;
 }
 
+int hpt_set_bsdf_roughplastic(hpt_context *c, float int_ior, float ext_ior, int distribution, float alpha,
+                              int sample_visible, int nonlinear, const float diffuse[3], const float specular[3]) {
+    if (!c || distribution < 0 || distribution > 2) return setErr(c, HPT_EINVAL, "bad roughplastic params");
+    if (int_ior < 0 || ext_ior < 0 || int_ior == ext_ior)
+        return setErr(c, HPT_EINVAL, "The interior and exterior indices of refraction must be positive and differ!");
+    static const char *names[3] = {"beckmann", "ggx", "phong"};
+    c->desc.bsdf = "roughplastic";
+    c->desc.intIOR = int_ior;
+    c->desc.extIOR = ext_ior;
+    c->desc.distribution = names[distribution];
+    c->desc.alpha = alpha;
+    c->desc.sampleVisible = sample_visible != 0;
+    c->desc.nonlinear = nonlinear != 0;
+    c->desc.ensureEnergyConservation = true;
+    for (int i = 0; i < 3; ++i) {
+        c->desc.diffuse[i] = diffuse ? diffuse[i] : 0.5f;
+        c->desc.specular[i] = specular ? specular[i] : 1.0f;
+    }
+    c->haveBSDF = true;
+    c->prepared = false;
+    return HPT_OK;
+}
+
 int hpt_set_bsdf_kajiyakay(hpt_context *c, const float kd[3], const float ks[3], float exponent) {
     if (!c || !kd) return HPT_EINVAL;
     c->desc.bsdf = "kajiyakay";
@@ -418,6 +442,9 @@ int hpt_prepare(hpt_context *c) {
             if (!precomputeMarschner(d, c->dataDir, c->mar, err)) return setErr(c, HPT_EIO, err);
         } else if (d.bsdf == "kajiyakay") {
             configureKajiyaKay(d, c->kk);
+        } else if (d.bsdf == "roughplastic") {
+            std::string err;
+            if (!configureRoughPlastic(d, c->dataDir, c->rp, err)) return setErr(c, HPT_EINVAL, err);
         } else {
             return setErr(c, HPT_EINVAL, "unsupported bsdf " + d.bsdf);
         }
@@ -447,7 +474,7 @@ int hpt_prepare(hpt_context *c) {
         sc.aabbMax[i] = c->tree.aabbMax[i];
     }
     sc.radius = c->hair.radius;
-    sc.bsdfKind = d.bsdf == "marschner" ? 0 : 1;
+    sc.bsdfKind = d.bsdf == "marschner" ? 0 : d.bsdf == "kajiyakay" ? 1 : 2;
     if (sc.bsdfKind == 0) {
         for (int l = 0; l < 3; ++l) {
             r |= upload(c, c->mar.table[l].data(), c->mar.table[l].size() * 16, (const void **) &sc.mar.table[l]);
@@ -464,6 +491,9 @@ int hpt_prepare(hpt_context *c) {
         sc.mar.vTRT = c->mar.vTRT;
         sc.mar.scaleAngleRad = c->mar.scaleAngleRad;
         for (int i = 0; i < 3; ++i) sc.mar.diffuse[i] = c->mar.diffuse[i];
+    } else if (sc.bsdfKind == 2) {
+        sc.rp = c->rp.p;
+        r |= upload(c, c->rp.trans.data(), c->rp.trans.size() * 4, (const void **) &sc.rp.trans);
     } else {
         sc.kk = c->kk;
     }
@@ -550,7 +580,7 @@ int hpt_get_scene_info(hpt_context *c, hpt_scene_info *o) {
     o->rr_depth = d.rrDepth;
     o->strict_normals = d.strictNormals;
     o->hide_emitters = d.hideEmitters;
-    o->bsdf = d.bsdf == "marschner" ? 0 : 1;
+    o->bsdf = d.bsdf == "marschner" ? 0 : d.bsdf == "kajiyakay" ? 1 : 2;
     o->vertices = c->hair.vertexCount();
     o->segments = c->tree.segs.size();
     o->kd_nodes = c->tree.nodes.size();

@@ -100,6 +100,19 @@ struct HptKajiyaKay {
     float exponent, specularSamplingWeight;
 };
 
+/* roughplastic (roughplastic.cpp:196-296): isotropic microfacet coating over
+ * a diffuse base, constant textures */
+struct HptRoughPlastic {
+    int type;                   /* 0 beckmann, 1 ggx, 2 phong (microfacet.h:48-58) */
+    int sampleVisible, nonlinear;
+    float alpha, exponent;      /* exponent: Phong (computePhongExponent) */
+    float eta, invEta2, specularSamplingWeight;
+    float diffuse[3], specular[3];
+    const float *trans;         /* external rough transmittance 1D slice (eta, alpha) */
+    int transSize;
+    float fdr;                  /* 1 - internal (1/eta) diffuse transmittance at alpha */
+};
+
 struct HptEnvMap {
     const HptF4 *texel;        /* w*h, half-rounded RGB stored as float */
     const float *cdfRows;       /* h+1 */
@@ -121,9 +134,10 @@ struct HptScene {
     const HptSegment *segs;
     float aabbMin[3], aabbMax[3];
     float radius;
-    int bsdfKind;               /* 0 = marschner, 1 = kajiyakay */
+    int bsdfKind;               /* 0 = marschner, 1 = kajiyakay, 2 = roughplastic */
     HptMarschner mar;
     HptKajiyaKay kk;
+    HptRoughPlastic rp;
     HptEnvMap env;
     const uint32_t *sobol;      /* 1024 x 52 */
     const uint64_t *vdc;        /* rows x 52 */

@@ -36,6 +36,9 @@ using namespace hk;
 #ifndef HPT_NODE4
 #define HPT_NODE4 1 /* 1: descend over two-level nodes (HptNode4); 0: binary HptNode */
 #endif
+#ifndef HPT_LEAF_BATCH
+#define HPT_LEAF_BATCH 1 /* leaf records fetched per round trip in the pre-test pass */
+#endif
 #ifndef HPT_LEAF_MODE
 #define HPT_LEAF_MODE 2 /* 0 prefetch next record, 1 no prefetch, 2 mask then exact (fastest) */
 #endif
@@ -447,6 +450,30 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     for (uint32_t c0 = first; c0 < last; c0 += 32) {
         const uint32_t c1 = min(last, c0 + 32);
         uint32_t mask = 0;
+#if HPT_LEAF_BATCH > 1
+        /* HPT_LEAF_BATCH records per round trip: their loads are issued
+           together (indices clamped into the leaf; extra lanes' results are
+           ignored), so a typical leaf costs one memory latency */
+        for (uint32_t e0 = c0; e0 < c1; e0 += HPT_LEAF_BATCH) {
+            float4 fa[HPT_LEAF_BATCH], fb[HPT_LEAF_BATCH];
+#pragma unroll
+            for (int k = 0; k < HPT_LEAF_BATCH; ++k) {
+                const uint32_t e = min(e0 + (uint32_t) k, c1 - 1u);
+                fa[k] = leafF[2 * e];
+                fb[k] = leafF[2 * e + 1];
+            }
+#pragma unroll
+            for (int k = 0; k < HPT_LEAF_BATCH; ++k) {
+                if (e0 + (uint32_t) k < c1) {
+                    if (STATS) {
+                        ++tc.prims;
+                        if (waveLeader()) tc.primSlots += 64;
+                    }
+                    if (segMayHit(fa[k], fb[k], o, d, sc.radius)) mask |= 1u << (e0 + (uint32_t) k - c0);
+                }
+            }
+        }
+#else
         float4 na = leafF[2 * c0], nb = leafF[2 * c0 + 1];
         for (uint32_t e = c0; e < c1; ++e) {
             const float4 fa = na, fb = nb;
@@ -460,6 +487,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
             }
             if (segMayHit(fa, fb, o, d, sc.radius)) mask |= 1u << (e - c0);
         }
+#endif
         while (mask) {
             const uint32_t e = c0 + (uint32_t) (__ffs(mask) - 1);
             mask &= mask - 1;
@@ -738,17 +766,17 @@ HD float azSample(const float *__restrict__ cdfs, float cosThetaD, float xi) {
 }
 
 /* rtrans.h:183-199 (eta and alpha fixed) + spline.cpp:23-61 */
-HD float roughTrans(const HptMarschner &m, float cosTheta) {
+HD float roughTransSlice(const float *__restrict__ trans, int transSize, float cosTheta) {
     float w = powf(fabsf(cosTheta), 0.25f);
     if (!(cosTheta >= 0)) return 0.f;
     float result;
     if (!(w >= 0.0f && w <= 1.0f)) {
         result = 0.0f;
     } else {
-        const size_t size = (size_t) m.transSize;
+        const size_t size = (size_t) transSize;
         float t = ((w - 0.0f) * (size - 1)) / (1.0f - 0.0f);
         size_t k = (size_t) t < size - 2 ? (size_t) t : size - 2;
-        const float *val = m.trans;
+        const float *val = trans;
         float f0 = val[k], f1 = val[k + 1], d0, d1;
         d0 = (k > 0) ? 0.5f * (val[k + 1] - val[k - 1]) : val[k + 1] - val[k];
         d1 = (k + 2 < size) ? 0.5f * (val[k + 2] - val[k]) : val[k + 1] - val[k];
@@ -758,6 +786,7 @@ HD float roughTrans(const HptMarschner &m, float cosTheta) {
     }
     return fminr(1.0f, fmaxr(0.0f, result));
 }
+HD float roughTrans(const HptMarschner &m, float cosTheta) { return roughTransSlice(m.trans, m.transSize, cosTheta); }
 
 /* MarschnerDiffuse::eval (:377-482), hasDiffuse = true */
 HD V3 marschnerEval(const HptMarschner &m, V3 wi, V3 wo) {
@@ -891,15 +920,287 @@ HD V3 kkSample(const HptKajiyaKay &k, V3 wi, float sx, float sy, V3 &wo, float &
     return divs(kkEval(k, wi, wo), pdf);
 }
 
+/* ------------------------------------------------------------------ */
+/* roughplastic (roughplastic.cpp:196-506) over the isotropic            */
+/* MicrofacetDistribution (microfacet.h:67-720); constant textures.       */
+/* math::fastexp/fastlog are double exp/log on Linux x86_64 (math.h:185). */
+/* ------------------------------------------------------------------ */
+HD float fastexpf(float v) { return (float) exp((double) v); }
+HD float fastlogf(float v) { return (float) log((double) v); }
+
+HD float mtsErf(float x) { /* math.cpp:55-72 */
+    const float a1 = 0.254829592f, a2 = -0.284496736f, a3 = 1.421413741f, a4 = -1.453152027f,
+                a5 = 1.061405429f, p = 0.3275911f;
+    const float sign = copysignf(1.0f, x);
+    x = fabsf(x);
+    const float t = 1.0f / (1.0f + p * x);
+    const float y = 1.0f - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * fastexpf(-x * x);
+    return sign * y;
+}
+HD float mtsErfinv(float x) { /* math.cpp:25-53 (Giles) */
+    float w = -fastlogf((1.0f - x) * (1.0f + x));
+    float p;
+    if (w < 5.0f) {
+        w = w - 2.5f;
+        p = 2.81022636e-08f;
+        p = 3.43273939e-07f + p * w;
+        p = -3.5233877e-06f + p * w;
+        p = -4.39150654e-06f + p * w;
+        p = 0.00021858087f + p * w;
+        p = -0.00125372503f + p * w;
+        p = -0.00417768164f + p * w;
+        p = 0.246640727f + p * w;
+        p = 1.50140941f + p * w;
+    } else {
+        w = sqrtf(w) - 3.0f;
+        p = -0.000200214257f;
+        p = 0.000100950558f + p * w;
+        p = 0.00134934322f + p * w;
+        p = -0.00367342844f + p * w;
+        p = 0.00573950773f + p * w;
+        p = -0.0076224613f + p * w;
+        p = 0.00943887047f + p * w;
+        p = 1.00167406f + p * w;
+        p = 2.83297682f + p * w;
+    }
+    return p * x;
+}
+HD float hypot2f(float a, float b) { /* math.cpp:74-86 */
+    float r;
+    if (fabsf(a) > fabsf(b)) {
+        r = b / a;
+        r = fabsf(a) * sqrtf(1.0f + r * r);
+    } else if (b != 0.0f) {
+        r = a / b;
+        r = fabsf(b) * sqrtf(1.0f + r * r);
+    } else {
+        r = 0.0f;
+    }
+    return r;
+}
+
+/* MicrofacetDistribution::eval (isotropic) */
+HD float mfEval(const HptRoughPlastic &m, V3 h) {
+    if (h.z <= 0) return 0.0f;
+    const float cosTheta2 = h.z * h.z;
+    const float a = m.alpha;
+    const float beckmannExponent = ((h.x * h.x) / (a * a) + (h.y * h.y) / (a * a)) / cosTheta2;
+    float result;
+    /* M_PI is a double: the denominators and the divisions run in double */
+    if (m.type == 0) {
+        result = (float) ((double) fastexpf(-beckmannExponent) / (M_PI * a * a * cosTheta2 * cosTheta2));
+    } else if (m.type == 1) {
+        const float root = (1.0f + beckmannExponent) * cosTheta2;
+        result = (float) (1.0 / (M_PI * a * a * root * root));
+    } else {
+        result = sqrtf((m.exponent + 2) * (m.exponent + 2)) * kInvTwoPi * powf(h.z, m.exponent);
+    }
+    if (result * h.z < 1e-20f) result = 0;
+    return result;
+}
+HD float mfSmithG1(const HptRoughPlastic &m, V3 v, V3 h) {
+    if (dot(v, h) * v.z <= 0) return 0.0f;
+    float temp = 1 - v.z * v.z;
+    float tanTheta = fabsf(temp <= 0.0f ? 0.0f : sqrtf(temp) / v.z);
+    if (tanTheta == 0.0f) return 1.0f;
+    const float alpha = m.alpha; /* projectRoughness, isotropic */
+    if (m.type == 1) {
+        const float root = alpha * tanTheta;
+        return 2.0f / (1.0f + hypot2f(1.0f, root));
+    }
+    const float a = 1.0f / (alpha * tanTheta);
+    if (a >= 1.6f) return 1.0f;
+    const float aSqr = a * a;
+    return (3.535f * a + 2.181f * aSqr) / (1.0f + 2.276f * a + 2.577f * aSqr);
+}
+HD float mfPdf(const HptRoughPlastic &m, V3 wi, V3 h) {
+    if (m.sampleVisible) {
+        if (wi.z == 0) return 0.0f;
+        return mfSmithG1(m, wi, h) * fabsf(dot(wi, h)) * mfEval(m, h) / fabsf(wi.z);
+    }
+    return mfEval(m, h) * h.z;
+}
+/* sampleVisible11 (microfacet.h:567-686), isotropic Beckmann / GGX */
+HD void mfSampleVisible11(const HptRoughPlastic &m, float thetaI, float sx, float sy, float &slopeX, float &slopeY) {
+    const float SQRT_PI_INV = (float) (1 / sqrt(M_PI));
+    if (m.type == 0) {
+        if (thetaI < 1e-4f) {
+            const float r = sqrtf(-fastlogf(1.0f - sx));
+            const float ang = (float) (2 * M_PI * sy);
+            slopeX = r * cosf(ang);
+            slopeY = r * sinf(ang);
+            return;
+        }
+        const float tanThetaI = tanf(thetaI), cotThetaI = 1 / tanThetaI;
+        float a = -1, c = mtsErf(cotThetaI);
+        const float sample_x = fmaxr(sx, 1e-6f);
+        const float fit = 1 + thetaI * (-0.876f + thetaI * (0.4265f - 0.0594f * thetaI));
+        float b = c - (1 + c) * powf(1 - sample_x, fit);
+        const float normalization = 1 / (1 + c + SQRT_PI_INV * tanThetaI * expf(-cotThetaI * cotThetaI));
+        int it = 0;
+        while (++it < 10) {
+            if (!(b >= a && b <= c)) b = 0.5f * (a + c);
+            const float invErf = mtsErfinv(b);
+            const float value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * expf(-invErf * invErf)) - sample_x;
+            const float derivative = normalization * (1 - invErf * tanThetaI);
+            if (fabsf(value) < 1e-5f) break;
+            if (value > 0) c = b;
+            else a = b;
+            b -= value / derivative;
+        }
+        slopeX = mtsErfinv(b);
+        slopeY = mtsErfinv(2.0f * fmaxr(sy, 1e-6f) - 1.0f);
+        return;
+    }
+    /* GGX */
+    if (thetaI < 1e-4f) {
+        const float r = sqrtf(fmaxr(0.0f, sx / (1 - sx)));
+        const float ang = (float) (2 * M_PI * sy);
+        slopeX = r * cosf(ang);
+        slopeY = r * sinf(ang);
+        return;
+    }
+    const float tanThetaI = tanf(thetaI);
+    const float a = 1 / tanThetaI;
+    const float G1 = 2.0f / (1.0f + sqrtf(fmaxr(0.0f, 1.0f + 1.0f / (a * a))));
+    float A = 2.0f * sx / G1 - 1.0f;
+    if (fabsf(A) == 1) A -= copysignf(1.0f, A) * kEpsilon;
+    const float tmp = 1.0f / (A * A - 1.0f);
+    const float B = tanThetaI;
+    const float D = sqrtf(fmaxr(0.0f, B * B * tmp * tmp - (A * A - B * B) * tmp));
+    const float slope_x_1 = B * tmp - D, slope_x_2 = B * tmp + D;
+    slopeX = (A < 0.0f || slope_x_2 > 1.0f / tanThetaI) ? slope_x_1 : slope_x_2;
+    float S;
+    if (sy > 0.5f) {
+        S = 1.0f;
+        sy = 2.0f * (sy - 0.5f);
+    } else {
+        S = -1.0f;
+        sy = 2.0f * (0.5f - sy);
+    }
+    const float z = (sy * (sy * (sy * (-0.365728915865723f) + 0.790235037209296f) - 0.424965825137544f) +
+                     0.000152998850436920f) /
+                    (sy * (sy * (sy * (sy * 0.169507819808272f - 0.397203533833404f) - 0.232500544458471f) + 1.0f) -
+                     0.539825872510702f);
+    slopeY = S * z * sqrtf(1.0f + slopeX * slopeX);
+}
+/* MicrofacetDistribution::sample(wi, sample) without pdf */
+HD V3 mfSample(const HptRoughPlastic &m, V3 wiIn, float sx, float sy) {
+    if (m.sampleVisible) {
+        const V3 wi = normalize(v3(m.alpha * wiIn.x, m.alpha * wiIn.y, wiIn.z));
+        float theta = 0, phi = 0;
+        if (wi.z < 0.99999f) {
+            theta = acosf(wi.z);
+            phi = atan2f(wi.y, wi.x);
+        }
+        const float sinPhi = sinf(phi), cosPhi = cosf(phi);
+        float slx, sly;
+        mfSampleVisible11(m, theta, sx, sy, slx, sly);
+        const float rx = cosPhi * slx - sinPhi * sly, ry = sinPhi * slx + cosPhi * sly;
+        const float ux = rx * m.alpha, uy = ry * m.alpha;
+        const float normalization = 1.0f / sqrtf(ux * ux + uy * uy + 1.0f);
+        return v3(-ux * normalization, -uy * normalization, normalization);
+    }
+    /* sampleAll, isotropic */
+    float cosThetaM, sinPhiM, cosPhiM;
+    if (m.type == 2) {
+        const float phiM = (float) ((2.0 * M_PI) * sy);
+        sinPhiM = sinf(phiM);
+        cosPhiM = cosf(phiM);
+        cosThetaM = powf(sx, 1.0f / (m.exponent + 2.0f));
+    } else {
+        const float ang = (float) ((2.0f * M_PI) * sy);
+        sinPhiM = sinf(ang);
+        cosPhiM = cosf(ang);
+        const float alphaSqr = m.alpha * m.alpha;
+        const float tanThetaMSqr = (m.type == 0) ? alphaSqr * -fastlogf(1.0f - sx) : alphaSqr * sx / (1.0f - sx);
+        cosThetaM = 1.0f / sqrtf(1.0f + tanThetaMSqr);
+    }
+    const float sinThetaM = sqrtf(fmaxr(0.0f, 1 - cosThetaM * cosThetaM));
+    return v3(sinThetaM * cosPhiM, sinThetaM * sinPhiM, cosThetaM);
+}
+
+/* RoughPlastic::eval (:296-360) */
+HD V3 rpEval(const HptRoughPlastic &m, V3 wi, V3 wo) {
+    if (wi.z <= 0 || wo.z <= 0) return v3(0, 0, 0);
+    V3 result = v3(0, 0, 0);
+    {
+        const V3 H = normalize(wo + wi);
+        const float D = mfEval(m, H);
+        const float F = fresnelDielectricExt(dot(wi, H), m.eta);
+        const float G = mfSmithG1(m, wi, H) * mfSmithG1(m, wo, H);
+        const float value = F * D * G / (4.0f * wi.z);
+        result = result + v3(m.specular[0], m.specular[1], m.specular[2]) * value;
+    }
+    {
+        V3 diff = v3(m.diffuse[0], m.diffuse[1], m.diffuse[2]);
+        const float T12 = roughTransSlice(m.trans, m.transSize, wi.z);
+        const float T21 = roughTransSlice(m.trans, m.transSize, wo.z);
+        const float Fdr = m.fdr;
+        if (m.nonlinear) diff = v3(diff.x / (1.0f - diff.x * Fdr), diff.y / (1.0f - diff.y * Fdr), diff.z / (1.0f - diff.z * Fdr));
+        else diff = divs(diff, 1 - Fdr);
+        result = result + diff * (kInvPi * wo.z * T12 * T21 * m.invEta2);
+    }
+    return result;
+}
+/* RoughPlastic::pdf (:362-436) */
+HD float rpPdf(const HptRoughPlastic &m, V3 wi, V3 wo) {
+    if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+    const V3 H = normalize(wo + wi);
+    float probSpecular = 1 - roughTransSlice(m.trans, m.transSize, wi.z);
+    probSpecular = (probSpecular * m.specularSamplingWeight) /
+                   (probSpecular * m.specularSamplingWeight + (1 - probSpecular) * (1 - m.specularSamplingWeight));
+    const float probDiffuse = 1 - probSpecular;
+    const float dwh_dwo = 1.0f / (4.0f * dot(wo, H));
+    const float prob = mfPdf(m, wi, H);
+    float result = prob * dwh_dwo * probSpecular;
+    result += probDiffuse * (kInvPi * wo.z);
+    return result;
+}
+/* RoughPlastic::sample (:438-506) */
+HD V3 rpSample(const HptRoughPlastic &m, V3 wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
+    pdf = 0.0f;
+    type = 0;
+    wo = v3(0, 0, 0);
+    if (wi.z <= 0) return v3(0, 0, 0);
+    bool choseSpecular = true;
+    float probSpecular = 1 - roughTransSlice(m.trans, m.transSize, wi.z);
+    probSpecular = (probSpecular * m.specularSamplingWeight) /
+                   (probSpecular * m.specularSamplingWeight + (1 - probSpecular) * (1 - m.specularSamplingWeight));
+    if (sy < probSpecular) {
+        sy /= probSpecular;
+    } else {
+        sy = (sy - probSpecular) / (1 - probSpecular);
+        choseSpecular = false;
+    }
+    if (choseSpecular) {
+        const V3 mn = mfSample(m, wi, sx, sy);
+        wo = mn * (2 * dot(wi, mn)) - wi; /* reflect (:281-283) */
+        type = HPT_EGLOSSY_REFLECTION;
+        if (wo.z <= 0) return v3(0, 0, 0);
+    } else {
+        type = HPT_EDIFFUSE_REFLECTION;
+        wo = squareToCosineHemisphere(sx, sy);
+    }
+    pdf = rpPdf(m, wi, wo);
+    if (pdf == 0) return v3(0, 0, 0);
+    return divs(rpEval(m, wi, wo), pdf);
+}
+
 HD V3 bsdfEval(const HptScene &sc, V3 wi, V3 wo) {
+    if (sc.bsdfKind == 2) return rpEval(sc.rp, wi, wo);
     return sc.bsdfKind == 0 ? marschnerEval(sc.mar, wi, wo) : kkEval(sc.kk, wi, wo);
 }
-HD float bsdfPdf(const HptScene &sc, V3 wi, V3 wo) { return sc.bsdfKind == 0 ? 1.0f : kkPdf(sc.kk, wi, wo); }
+HD float bsdfPdf(const HptScene &sc, V3 wi, V3 wo) {
+    if (sc.bsdfKind == 2) return rpPdf(sc.rp, wi, wo);
+    return sc.bsdfKind == 0 ? 1.0f : kkPdf(sc.kk, wi, wo);
+}
 HD V3 bsdfSample(const HptScene &sc, V3 wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
     if (sc.bsdfKind == 0) {
         pdf = 1.0f;
         return marschnerSample(sc.mar, wi, sx, sy, wo, type);
     }
+    if (sc.bsdfKind == 2) return rpSample(sc.rp, wi, sx, sy, wo, pdf, type);
     return kkSample(sc.kk, wi, sx, sy, wo, pdf, type);
 }
 

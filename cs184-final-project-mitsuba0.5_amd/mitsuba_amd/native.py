@@ -64,6 +64,8 @@ SIGNATURES = {
     "hpt_set_hair_vertices": (C.c_int, [C.c_void_p, _f, _u8, C.c_uint64, C.c_float]),
     "hpt_set_bsdf_marschner": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_int, C.c_float, _f, _f]),
     "hpt_set_bsdf_kajiyakay": (C.c_int, [C.c_void_p, _f, _f, C.c_float]),
+    "hpt_set_bsdf_roughplastic": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_int, C.c_float, C.c_int, C.c_int,
+                                            _f, _f]),
     "hpt_set_envmap_rgb": (C.c_int, [C.c_void_p, _f, C.c_int, C.c_int, C.c_float, _f]),
     "hpt_set_sunsky": (C.c_int, [C.c_void_p, _f, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int]),
     "hpt_prepare": (C.c_int, [C.c_void_p]),
@@ -178,6 +180,14 @@ class Renderer:
         a = _f32(kd)
         b = _f32(ks)
         self._check(self.lib.hpt_set_bsdf_kajiyakay(self.h, _p(a, _f), _p(b, _f), exponent))
+
+    def set_roughplastic(self, int_ior=1.49, ext_ior=1.000277, distribution=0, alpha=0.1, sample_visible=True,
+                         nonlinear=False, diffuse=(0.5, 0.5, 0.5), specular=(1.0, 1.0, 1.0)):
+        d = _f32(diffuse)
+        s = _f32(specular)
+        self._check(self.lib.hpt_set_bsdf_roughplastic(self.h, int_ior, ext_ior, distribution, alpha,
+                                                       int(bool(sample_visible)), int(bool(nonlinear)),
+                                                       _p(d, _f), _p(s, _f)))
 
     def set_envmap(self, rgb, scale=1.0):
         rgb = _f32(rgb)

@@ -48,7 +48,7 @@ int hpt_set_data_dir(hpt_context *ctx, const char *dir);
 
 /* Parse a Mitsuba scene XML (src/librender/scenehandler.cpp) with -D style
    defines: integrator "path", sensor "perspective" + sampler "sobol" + film,
-   shape "hair", bsdf "marschner"/"kajiyakay", emitter "sunsky"/"envmap". */
+   shape "hair", bsdf "marschner"/"kajiyakay"/"roughplastic", emitter "sunsky"/"envmap". */
 int hpt_load_scene_xml(hpt_context *ctx, const char *path, int n_defines, const char *const *keys,
                        const char *const *values);
 
@@ -73,11 +73,18 @@ int hpt_set_bsdf_marschner(hpt_context *ctx, float int_ior, float ext_ior, int d
                            const float diffuse[3], const float specular[3]);
 /* KajiyaKay(Properties) (src/bsdfs/kajiyakay.cpp:60-69) */
 int hpt_set_bsdf_kajiyakay(hpt_context *ctx, const float kd[3], const float ks[3], float exponent);
+/* RoughPlastic(Properties) (src/bsdfs/roughplastic.cpp:197-227) with constant
+   textures; distribution 0 = beckmann, 1 = ggx, 2 = phong (sample_visible is
+   forced off for phong, microfacet.h:139-143); diffuse/specular may be NULL
+   (defaults 0.5 / 1.0).  The reference's anisotropic case is an error there
+   and is not expressible here. */
+int hpt_set_bsdf_roughplastic(hpt_context *ctx, float int_ior, float ext_ior, int distribution, float alpha,
+                              int sample_visible, int nonlinear, const float diffuse[3], const float specular[3]);
 /* EnvironmentMap from a bitmap (src/emitters/envmap.cpp:105-189); rgb is w*h*3
    linear floats, to_world may be NULL */
 int hpt_set_envmap_rgb(hpt_context *ctx, const float *rgb, int w, int h, float scale, const float *to_world);
-/* SunSkyEmitter (src/emitters/sunsky.cpp:100-240) -- round-1 stand-in sky
-   rasteriser with the same bitmap geometry */
+/* SunSkyEmitter (src/emitters/sunsky.cpp:100-240): Hosek-Wilkie sky + Preetham
+   sun rasterised into the envmap bitmap (sun_direction given explicitly) */
 int hpt_set_sunsky(hpt_context *ctx, const float sun_direction[3], float turbidity, float sky_scale,
                    float sun_scale, float sun_radius_scale, int resolution);
 
@@ -87,7 +94,7 @@ int hpt_prepare(hpt_context *ctx);
 
 typedef struct hpt_scene_info {
     int width, height, spp, max_depth, rr_depth, strict_normals, hide_emitters;
-    int bsdf;                      /* 0 marschner, 1 kajiyakay */
+    int bsdf;                      /* 0 marschner, 1 kajiyakay, 2 roughplastic */
     uint64_t vertices, segments, kd_nodes, kd_indices;
     int kd_depth;
     double kd_build_seconds;

@@ -768,6 +768,315 @@ struct KajiyaKay {
 };
 
 /* ------------------------------------------------------------------ */
+/* microfacet.h:36-720 -- MicrofacetDistribution (isotropic instances)  */
+/* ------------------------------------------------------------------ */
+namespace mathx {
+inline float fastexp(float v) { return (float) ::exp((double) v); } /* math.h:185-199 (Linux) */
+inline float fastlog(float v) { return (float) ::log((double) v); }
+inline float signum(float v) { return std::copysign(1.0f, v); }     /* math.h:270-276 */
+float erfinv(float x) { /* math.cpp:25-53 */
+    float w = -fastlog((1.0f - x) * (1.0f + x)), p;
+    if (w < 5.0f) {
+        w = w - 2.5f;
+        p = 2.81022636e-08f;
+        p = 3.43273939e-07f + p * w;
+        p = -3.5233877e-06f + p * w;
+        p = -4.39150654e-06f + p * w;
+        p = 0.00021858087f + p * w;
+        p = -0.00125372503f + p * w;
+        p = -0.00417768164f + p * w;
+        p = 0.246640727f + p * w;
+        p = 1.50140941f + p * w;
+    } else {
+        w = std::sqrt(w) - 3.0f;
+        p = -0.000200214257f;
+        p = 0.000100950558f + p * w;
+        p = 0.00134934322f + p * w;
+        p = -0.00367342844f + p * w;
+        p = 0.00573950773f + p * w;
+        p = -0.0076224613f + p * w;
+        p = 0.00943887047f + p * w;
+        p = 1.00167406f + p * w;
+        p = 2.83297682f + p * w;
+    }
+    return p * x;
+}
+float erf(float x) { /* math.cpp:55-72 (A&S 7.1.26) */
+    const float a1 = 0.254829592f, a2 = -0.284496736f, a3 = 1.421413741f;
+    const float a4 = -1.453152027f, a5 = 1.061405429f, p = 0.3275911f;
+    float sign = signum(x);
+    x = std::abs(x);
+    float t = 1.0f / (1.0f + p * x);
+    float y = 1.0f - (((((a5 * t + a4) * t) + a3) * t + a2) * t + a1) * t * fastexp(-x * x);
+    return sign * y;
+}
+float hypot2(float a, float b) { /* math.cpp:74-86 */
+    float r;
+    if (std::abs(a) > std::abs(b)) {
+        r = b / a;
+        r = std::abs(a) * std::sqrt(1.0f + r * r);
+    } else if (b != 0.0f) {
+        r = a / b;
+        r = std::abs(b) * std::sqrt(1.0f + r * r);
+    } else {
+        r = 0.0f;
+    }
+    return r;
+}
+} // namespace mathx
+
+struct Microfacet {
+    enum EType { EBeckmann = 0, EGGX = 1, EPhong = 2 };
+    int type = EBeckmann;
+    float alpha = 0.1f, exponent = 0.0f;
+    bool sampleVisible = true;
+
+    Microfacet() {}
+    Microfacet(int t, float a, bool sv) : type(t), alpha(std::max(a, 1e-4f)), sampleVisible(sv) { /* :67-75 */
+        if (type == EPhong) exponent = std::max(2.0f / (alpha * alpha) - 2.0f, 0.0f); /* :701-704 */
+    }
+    float eval(const V3 &m) const { /* :190-237 */
+        if (m.z <= 0) return 0.0f;
+        float cosTheta2 = m.z * m.z;
+        float beckmannExponent = ((m.x * m.x) / (alpha * alpha) + (m.y * m.y) / (alpha * alpha)) / cosTheta2;
+        float result;
+        if (type == EBeckmann) {
+            result = mathx::fastexp(-beckmannExponent) / (M_PI * alpha * alpha * cosTheta2 * cosTheta2);
+        } else if (type == EGGX) {
+            float root = (1.0f + beckmannExponent) * cosTheta2;
+            result = 1.0f / (M_PI * alpha * alpha * root * root);
+        } else {
+            result = std::sqrt((exponent + 2) * (exponent + 2)) * kInvTwoPi * std::pow(m.z, exponent);
+        }
+        if (result * m.z < 1e-20f) result = 0;
+        return result;
+    }
+    float smithG1(const V3 &v, const V3 &m) const { /* :451-484 */
+        if (dot(v, m) * v.z <= 0) return 0.0f;
+        float temp = 1 - v.z * v.z;
+        float tanTheta = std::abs(temp <= 0.0f ? 0.0f : std::sqrt(temp) / v.z);
+        if (tanTheta == 0.0f) return 1.0f;
+        if (type == EGGX) {
+            float root = alpha * tanTheta;
+            return 2.0f / (1.0f + mathx::hypot2(1.0f, root));
+        }
+        float a = 1.0f / (alpha * tanTheta);
+        if (a >= 1.6f) return 1.0f;
+        float aSqr = a * a;
+        return (3.535f * a + 2.181f * aSqr) / (1.0f + 2.276f * a + 2.577f * aSqr);
+    }
+    float pdf(const V3 &wi, const V3 &m) const { /* :275-280, :436-441, :396-400 */
+        if (sampleVisible) {
+            if (wi.z == 0) return 0.0f;
+            return smithG1(wi, m) * absDot(wi, m) * eval(m) / std::abs(wi.z);
+        }
+        return eval(m) * m.z;
+    }
+    void sampleVisible11(float thetaI, float sx, float sy, float &slx, float &sly) const { /* :567-686 */
+        const float SQRT_PI_INV = 1 / std::sqrt(M_PI);
+        if (type == EBeckmann) {
+            if (thetaI < 1e-4f) {
+                float r = std::sqrt(-mathx::fastlog(1.0f - sx));
+                float ang = 2 * M_PI * sy;
+                slx = r * std::cos(ang);
+                sly = r * std::sin(ang);
+                return;
+            }
+            float tanThetaI = std::tan(thetaI), cotThetaI = 1 / tanThetaI;
+            float a = -1, c = mathx::erf(cotThetaI);
+            float sample_x = std::max(sx, 1e-6f);
+            float fit = 1 + thetaI * (-0.876f + thetaI * (0.4265f - 0.0594f * thetaI));
+            float b = c - (1 + c) * std::pow(1 - sample_x, fit);
+            float normalization = 1 / (1 + c + SQRT_PI_INV * tanThetaI * std::exp(-cotThetaI * cotThetaI));
+            for (int it = 1; it < 10; ++it) {
+                if (!(b >= a && b <= c)) b = 0.5f * (a + c);
+                float invErf = mathx::erfinv(b);
+                float value = normalization * (1 + b + SQRT_PI_INV * tanThetaI * std::exp(-invErf * invErf)) - sample_x;
+                float derivative = normalization * (1 - invErf * tanThetaI);
+                if (std::abs(value) < 1e-5f) break;
+                if (value > 0) c = b;
+                else a = b;
+                b -= value / derivative;
+            }
+            slx = mathx::erfinv(b);
+            sly = mathx::erfinv(2.0f * std::max(sy, 1e-6f) - 1.0f);
+            return;
+        }
+        if (thetaI < 1e-4f) {
+            float r = safe_sqrt(sx / (1 - sx));
+            float ang = 2 * M_PI * sy;
+            slx = r * std::cos(ang);
+            sly = r * std::sin(ang);
+            return;
+        }
+        float tanThetaI = std::tan(thetaI), a = 1 / tanThetaI;
+        float G1 = 2.0f / (1.0f + safe_sqrt(1.0f + 1.0f / (a * a)));
+        float A = 2.0f * sx / G1 - 1.0f;
+        if (std::abs(A) == 1) A -= mathx::signum(A) * kEpsilon;
+        float tmp = 1.0f / (A * A - 1.0f), B = tanThetaI;
+        float D = safe_sqrt(B * B * tmp * tmp - (A * A - B * B) * tmp);
+        float x1 = B * tmp - D, x2 = B * tmp + D;
+        slx = (A < 0.0f || x2 > 1.0f / tanThetaI) ? x1 : x2;
+        float S;
+        if (sy > 0.5f) {
+            S = 1.0f;
+            sy = 2.0f * (sy - 0.5f);
+        } else {
+            S = -1.0f;
+            sy = 2.0f * (0.5f - sy);
+        }
+        float z = (sy * (sy * (sy * -0.365728915865723f + 0.790235037209296f) - 0.424965825137544f) +
+                   0.000152998850436920f) /
+                  (sy * (sy * (sy * (sy * 0.169507819808272f - 0.397203533833404f) - 0.232500544458471f) + 1.0f) -
+                   0.539825872510702f);
+        sly = S * z * std::sqrt(1.0f + slx * slx);
+    }
+    V3 sample(const V3 &wi_, float sx, float sy) const { /* :258-269 */
+        if (sampleVisible) { /* sampleVisible :355-393 */
+            V3 wi = normalize(V3(alpha * wi_.x, alpha * wi_.y, wi_.z));
+            float theta = 0, phi = 0;
+            if (wi.z < 0.99999f) {
+                theta = std::acos(wi.z);
+                phi = std::atan2(wi.y, wi.x);
+            }
+            float sinPhi = std::sin(phi), cosPhi = std::cos(phi);
+            float slx, sly;
+            sampleVisible11(theta, sx, sy, slx, sly);
+            float rx = cosPhi * slx - sinPhi * sly, ry = sinPhi * slx + cosPhi * sly;
+            rx *= alpha;
+            ry *= alpha;
+            float normalization = 1.0f / std::sqrt(rx * rx + ry * ry + 1.0f);
+            return V3(-rx * normalization, -ry * normalization, normalization);
+        }
+        /* sampleAll (:291-385), isotropic */
+        float cosThetaM, sinPhiM, cosPhiM;
+        if (type == EPhong) {
+            float phiM = (2.0f * M_PI) * sy;
+            sinPhiM = std::sin(phiM);
+            cosPhiM = std::cos(phiM);
+            cosThetaM = std::pow(sx, 1.0f / (exponent + 2.0f));
+        } else {
+            float ang = (2.0f * M_PI) * sy;
+            sinPhiM = std::sin(ang);
+            cosPhiM = std::cos(ang);
+            float alphaSqr = alpha * alpha;
+            float tanThetaMSqr = type == EBeckmann ? alphaSqr * -mathx::fastlog(1.0f - sx)
+                                                   : alphaSqr * sx / (1.0f - sx);
+            cosThetaM = 1.0f / std::sqrt(1.0f + tanThetaMSqr);
+        }
+        float sinThetaM = std::sqrt(std::max(0.0f, 1 - cosThetaM * cosThetaM));
+        return V3(sinThetaM * cosPhiM, sinThetaM * sinPhiM, cosThetaM);
+    }
+};
+
+/* ------------------------------------------------------------------ */
+/* roughplastic.cpp:197-506 (constant textures, both components)       */
+/* ------------------------------------------------------------------ */
+struct RoughPlastic {
+    int type = 0;
+    bool sampleVisible = true, nonlinear = false;
+    float alphaTex = 0.1f; /* ConstantFloatTexture(distr.getAlpha()) */
+    float eta = 1.49f, invEta2 = 0, specularSamplingWeight = 0;
+    Spec diffuse{0.5f}, specular{1.0f};
+    RoughTransmittance ext, internal;
+
+    float alphaEval() const { return Spec(alphaTex).average(); } /* m_alpha->eval(its).average() */
+
+    bool configure(const std::string &datDir, std::string &err) { /* :268-299 */
+        float mx = specular.max();
+        if (mx > 1.0f) specular *= 0.99f * (1.0f / mx);
+        mx = diffuse.max();
+        if (mx > 1.0f) diffuse *= 0.99f * (1.0f / mx);
+        float dAvg = diffuse.getLuminance(), sAvg = specular.getLuminance();
+        specularSamplingWeight = sAvg / (dAvg + sAvg);
+        invEta2 = 1.0f / (eta * eta);
+        const char *names[3] = {"beckmann", "ggx", "phong"};
+        std::string path = datDir + "/" + names[type] + ".dat";
+        if (!ext.load(path)) { err = "cannot load " + path; return false; }
+        float etaC = eta < 1 ? 1 / eta : eta;
+        if (etaC < ext.etaMin || etaC > ext.etaMax) { err = "eta outside the supported range"; return false; }
+        if (alphaEval() < ext.alphaMin || alphaEval() > ext.alphaMax) {
+            err = "alpha outside the supported range";
+            return false;
+        }
+        internal = ext;
+        ext.setEta(eta);
+        internal.setEta(1 / eta);
+        ext.setAlpha(alphaEval());
+        return true;
+    }
+    Microfacet distr() const { return Microfacet(type, alphaEval(), sampleVisible); }
+
+    Spec eval(const V3 &wi, const V3 &wo) const { /* :305-360 */
+        if (wi.z <= 0 || wo.z <= 0) return Spec(0.0f);
+        Microfacet d = distr();
+        Spec result(0.0f);
+        {
+            V3 H = normalize(wo + wi);
+            float D = d.eval(H);
+            float F = fresnelDielectricExt(dot(wi, H), eta);
+            float G = d.smithG1(wi, H) * d.smithG1(wo, H);
+            float value = F * D * G / (4.0f * wi.z);
+            result += specular * value;
+        }
+        {
+            Spec diff = diffuse;
+            float T12 = ext.eval(wi.z), T21 = ext.eval(wo.z);
+            float Fdr = 1 - internal.evalDiffuse(d.alpha);
+            if (nonlinear) {
+                for (int i = 0; i < 3; ++i) diff.s[i] /= 1.0f - diff.s[i] * Fdr;
+            } else {
+                diff /= 1 - Fdr;
+            }
+            result += diff * (kInvPi * wo.z * T12 * T21 * invEta2);
+        }
+        return result;
+    }
+    float pdf(const V3 &wi, const V3 &wo) const { /* :362-436 */
+        if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+        Microfacet d = distr();
+        V3 H = normalize(wo + wi);
+        float probSpecular = 1 - ext.eval(wi.z);
+        probSpecular = (probSpecular * specularSamplingWeight) /
+                       (probSpecular * specularSamplingWeight + (1 - probSpecular) * (1 - specularSamplingWeight));
+        float probDiffuse = 1 - probSpecular;
+        float dwh_dwo = 1.0f / (4.0f * dot(wo, H));
+        float prob = d.pdf(wi, H);
+        float result = prob * dwh_dwo * probSpecular;
+        result += probDiffuse * (kInvPi * wo.z);
+        return result;
+    }
+    Spec sample(const V3 &wi, float sx, float sy, V3 &wo, float &pdfOut, uint32_t &type_) const { /* :438-499 */
+        pdfOut = 0;
+        type_ = 0;
+        if (wi.z <= 0) return Spec(0.0f);
+        bool choseSpecular = true;
+        Microfacet d = distr();
+        float probSpecular = 1 - ext.eval(wi.z);
+        probSpecular = (probSpecular * specularSamplingWeight) /
+                       (probSpecular * specularSamplingWeight + (1 - probSpecular) * (1 - specularSamplingWeight));
+        if (sy < probSpecular) {
+            sy /= probSpecular;
+        } else {
+            sy = (sy - probSpecular) / (1 - probSpecular);
+            choseSpecular = false;
+        }
+        if (choseSpecular) {
+            V3 m = d.sample(wi, sx, sy);
+            wo = 2 * dot(wi, m) * m - wi;
+            type_ = EGlossyReflection;
+            if (wo.z <= 0) return Spec(0.0f);
+        } else {
+            type_ = EDiffuseReflection;
+            wo = squareToCosineHemisphere(sx, sy);
+        }
+        pdfOut = pdf(wi, wo);
+        if (pdfOut == 0) return Spec(0.0f);
+        return eval(wi, wo) / pdfOut;
+    }
+};
+
+/* ------------------------------------------------------------------ */
 /* Hair shape: hair.cpp                                                 */
 /* ------------------------------------------------------------------ */
 struct HairGeom {
@@ -1132,9 +1441,10 @@ struct orc_scene {
     HairGeom hair;
     KDTree tree;
     AABB aabb;
-    int bsdfKind = -1; /* 0 marschner, 1 kajiyakay */
+    int bsdfKind = -1; /* 0 marschner, 1 kajiyakay, 2 roughplastic */
     Marschner marschner;
     KajiyaKay kk;
+    RoughPlastic rp;
     EnvMap env;
     bool hasEnv = false;
     int maxDepth = -1, rrDepth = 5;
@@ -1470,12 +1780,15 @@ inline float miWeight(float pdfA, float pdfB) { /* path.cpp:296-300 */
 }
 
 Spec bsdfEval(const orc_scene *s, const V3 &wi, const V3 &wo) {
+    if (s->bsdfKind == 2) return s->rp.eval(wi, wo);
     return s->bsdfKind == 0 ? s->marschner.eval(wi, wo) : s->kk.eval(wi, wo);
 }
 float bsdfPdf(const orc_scene *s, const V3 &wi, const V3 &wo) {
+    if (s->bsdfKind == 2) return s->rp.pdf(wi, wo);
     return s->bsdfKind == 0 ? s->marschner.pdf() : s->kk.pdf(wi, wo);
 }
 Spec bsdfSample(const orc_scene *s, const V3 &wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
+    if (s->bsdfKind == 2) return s->rp.sample(wi, sx, sy, wo, pdf, type);
     return s->bsdfKind == 0 ? s->marschner.sample(wi, sx, sy, wo, pdf, type)
                             : s->kk.sample(wi, sx, sy, wo, pdf, type);
 }
@@ -1870,6 +2183,22 @@ int orc_set_kajiyakay(orc_scene *s, const float kd[3], const float ks[3], float 
     s->kk.exponent = exponent;
     s->kk.configure();
     return 0;
+}
+
+int orc_set_roughplastic(orc_scene *s, float eta, int distribution, float alpha, int sample_visible,
+                         int nonlinear, const float diffuse[3], const float specular[3], const char *dat_dir) {
+    if (distribution < 0 || distribution > 2) { s->err = "bad distribution"; return -1; }
+    s->bsdfKind = 2;
+    RoughPlastic &r = s->rp;
+    r = RoughPlastic();
+    r.type = distribution;
+    r.eta = eta;
+    r.alphaTex = std::max(alpha, 1e-4f);                             /* microfacet.h:135 */
+    r.sampleVisible = distribution == 2 ? false : sample_visible != 0; /* microfacet.h:139-143 */
+    r.nonlinear = nonlinear != 0;
+    r.diffuse = Spec(diffuse[0], diffuse[1], diffuse[2]);
+    r.specular = Spec(specular[0], specular[1], specular[2]);
+    return r.configure(dat_dir, s->err) ? 0 : -1;
 }
 
 int orc_set_envmap(orc_scene *s, const float *rgb, int w, int h, float scale, const float *to_world) {

@@ -57,6 +57,10 @@ int orc_set_marschner(orc_scene *s, float eta, int distribution, float alpha,
                       const char *microfacet_dat_dir);
 /* kajiyakay.cpp */
 int orc_set_kajiyakay(orc_scene *s, const float kd[3], const float ks[3], float exponent);
+/* roughplastic.cpp (constant textures): eta = intIOR/extIOR, distribution 0=beckmann 1=ggx 2=phong */
+int orc_set_roughplastic(orc_scene *s, float eta, int distribution, float alpha, int sample_visible,
+                         int nonlinear, const float diffuse[3], const float specular[3],
+                         const char *microfacet_dat_dir);
 /* envmap.cpp: linear RGB float bitmap (w x h x 3), to_world may be NULL */
 int orc_set_envmap(orc_scene *s, const float *rgb, int w, int h, float scale,
                    const float *to_world);

@@ -102,6 +102,7 @@ struct Spec {
     float max() const { return std::max(std::max(s[0], s[1]), s[2]); }
     bool isZero() const { return s[0] == 0.0f && s[1] == 0.0f && s[2] == 0.0f; }
     float getLuminance() const { return s[0] * 0.212671f + s[1] * 0.715160f + s[2] * 0.072169f; }
+    float average() const { float r = 0.0f; for (int i = 0; i < 3; ++i) r += s[i]; return r * (1.0f / 3); } /* spectrum.h:481-486 */
 };
 inline Spec operator*(float f, const Spec &v) { return v * f; }
 

@@ -38,6 +38,8 @@ _SIG = {
     "orc_hair_aabb": (C.c_int, [C.c_void_p, _f, _f]),
     "orc_set_marschner": (C.c_int, [C.c_void_p, C.c_float, C.c_int, C.c_float, _f, _f, C.c_char_p]),
     "orc_set_kajiyakay": (C.c_int, [C.c_void_p, _f, _f, C.c_float]),
+    "orc_set_roughplastic": (C.c_int, [C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_int, C.c_int, _f, _f,
+                                       C.c_char_p]),
     "orc_set_envmap": (C.c_int, [C.c_void_p, _f, C.c_int, C.c_int, C.c_float, _f]),
     "orc_set_integrator": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
     "orc_prepare": (C.c_int, [C.c_void_p]),
@@ -131,6 +133,8 @@ class Oracle:
             dist = {"beckmann": 0, "ggx": 1, "phong": 2}[bsdf["distribution"]]
             self.check(self.lib.orc_set_marschner(self.s, bsdf["eta"], dist, bsdf["alpha"], p(dif, _f), p(spec, _f),
                                                   os.path.join(DATA, "microfacet").encode()))
+        elif kind == "roughplastic":
+            self.set_roughplastic(bsdf)
         else:
             kd = f32(bsdf["kd"])
             ks = f32(bsdf.get("ks", (0.2, 0.2, 0.2)))
@@ -138,6 +142,15 @@ class Oracle:
         env = f32(env_rgb)
         self.check(self.lib.orc_set_envmap(self.s, p(env, _f), env.shape[1], env.shape[0], 1.0, None))
         self.check(self.lib.orc_set_integrator(self.s, max_depth, rr_depth, int(strict), int(hide)))
+
+    def set_roughplastic(self, bsdf):
+        dif = f32(bsdf.get("diffuse", (0.5, 0.5, 0.5)))
+        spec = f32(bsdf.get("specular", (1.0, 1.0, 1.0)))
+        dist = {"beckmann": 0, "ggx": 1, "phong": 2}[bsdf["distribution"]]
+        self.check(self.lib.orc_set_roughplastic(self.s, bsdf["eta"], dist, bsdf["alpha"],
+                                                 int(bsdf.get("sample_visible", True)),
+                                                 int(bsdf.get("nonlinear", False)), p(dif, _f), p(spec, _f),
+                                                 os.path.join(DATA, "microfacet").encode()))
 
     def set_kdtree(self, nodes, indices):
         nodes = np.ascontiguousarray(nodes, np.uint32)

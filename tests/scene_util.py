@@ -25,6 +25,10 @@ def config_params(name):
     if "marschner" in cfg["bsdf"]:
         bsdf = {"type": "marschner", "eta": np.float32(1.55) / np.float32(1.0), "distribution": "ggx",
                 "alpha": 0.2, "diffuse": (0.143016, 0.0156076, 1.80928e-005), "specular": (0.5, 0.5, 0.5)}
+    elif "roughplastic" in cfg["bsdf"]:
+        bsdf = {"type": "roughplastic", "eta": np.float32(1.55) / np.float32(1.0), "distribution": "ggx",
+                "alpha": 0.2, "sample_visible": True, "nonlinear": False,
+                "diffuse": (0.143016, 0.0156076, 1.80928e-005), "specular": (1.0, 1.0, 1.0)}
     else:
         bsdf = {"type": "kajiyakay", "kd": (0.143016, 0.0156076, 1.80928e-005), "ks": (0.2, 0.2, 0.2),
                 "exponent": 10.0}

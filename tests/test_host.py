@@ -59,6 +59,43 @@ def test_scene_xml_parameters_and_defaults(tmp_path):
         r.render()
 
 
+def test_roughplastic_scene_xml(tmp_path):
+    """The shipped models/furball/scene.xml BSDF block (roughplastic, ggx) and
+    the plugin's errors (roughplastic.cpp:207-226, microfacet.h:104-129)."""
+    xml = scenes.make_scene("furball_roughplastic", str(tmp_path), n_strands=200)
+    r = _host(xml, {"width": 16, "height": 16, "spp": 1})
+    r.prepare()
+    assert r.info().bsdf == 2
+    src = open(xml).read()
+    block = src[src.index('<bsdf type="roughplastic"'):src.index("</bsdf>")]
+    cases = [
+        ('<float name="alpha" value="0.2"/>',
+         '<float name="alphaU" value="0.2"/><float name="alphaV" value="0.3"/>', "anisotropic"),
+        ('<float name="alpha" value="0.2"/>', '<float name="alpha" value="0.2"/><float name="alphaU" value="0.2"/>',
+         "either 'alpha'"),
+        ('<float name="extIOR" value="1"/>', '<float name="extIOR" value="1.55"/>', "must be positive and differ"),
+        ('<string name="distribution" value="ggx"/>', '<string name="distribution" value="blinn"/>',
+         "invalid distribution"),
+    ]
+    for old, new, msg in cases:
+        bad = tmp_path / "rp_bad.xml"
+        bad.write_text(src.replace(block, block.replace(old, new)))
+        with pytest.raises(native.HairPTError, match=msg):
+            rr = _host(str(bad))
+            rr.prepare()
+    # alpha outside the precomputed rough-transmittance range (rtrans.h:390-397)
+    bad.write_text(src.replace(block, block.replace('value="0.2"', 'value="9"', 1)))
+    rr = _host(str(bad))
+    with pytest.raises(native.HairPTError, match="alpha"):
+        rr.prepare()
+    # defaults: beckmann, alpha 0.1, polypropylene / air, isotropic alphaU == alphaV accepted
+    bad.write_text(src.replace(block, '<bsdf type="roughplastic" id="hair"><float name="alphaU" value="0.1"/>'
+                                      '<float name="alphaV" value="0.1"/>'))
+    rr = _host(str(bad))
+    rr.prepare()
+    assert rr.info().bsdf == 2
+
+
 def test_scene_xml_errors(tmp_path):
     bad = tmp_path / "bad.xml"
     bad.write_text('<scene version="0.6.0"><integrator type="volpath"/></scene>')
