@@ -75,6 +75,7 @@ struct SceneDesc {
     float alpha = 0.1f;                            /* microfacet.h:99-140 defaults */
     float diffuse[3] = {0.5f, 0.5f, 0.5f};
     float specular[3] = {0.5f, 0.5f, 0.5f};        /* marschner default 0.5 */
+    float transmittance[3] = {0.1f, 0.1f, 0.1f};   /* marschnerdielectric specularTransmittance */
     bool specularGiven = false;
     float exponent = 30.0f;
     bool nonlinear = false;
@@ -145,6 +146,7 @@ struct MarschnerHost {
 bool precomputeMarschner(const SceneDesc &d, const std::string &dataDir, MarschnerHost &out,
                          std::string &err);
 void configureKajiyaKay(const SceneDesc &d, HptKajiyaKay &out);
+void configureMarschnerDielectric(const SceneDesc &d, HptMarschnerDielectric &out);
 
 /* roughplastic (roughplastic.cpp:197-299): device parameters + the 1-D external transmittance slice */
 struct RoughPlasticHost {

@@ -422,6 +422,30 @@ bool configureRoughPlastic(const SceneDesc &d, const std::string &dataDir, Rough
     return true;
 }
 
+void configureMarschnerDielectric(const SceneDesc &d, HptMarschnerDielectric &out) {
+    /* MarschnerDielectric(props) + configure (marschnerdielectric.cpp:147-211) */
+    out.eta = d.intIOR / d.extIOR;
+    float sr[3] = {d.specular[0], d.specular[1], d.specular[2]};
+    float st[3] = {d.transmittance[0], d.transmittance[1], d.transmittance[2]};
+    if (d.ensureEnergyConservation) { /* bsdf.cpp:88-113, each texture separately, max = 1 */
+        for (float *v : {sr, st}) {
+            float mx = std::max(std::max(v[0], v[1]), v[2]);
+            if (mx > 1.0f) {
+                float s = 0.99f * (1.0f / mx);
+                for (int i = 0; i < 3; ++i) v[i] *= s;
+            }
+        }
+    }
+    float dAvg = d.diffuse[0] * 0.212671f + d.diffuse[1] * 0.715160f + d.diffuse[2] * 0.072169f;
+    float sAvg = sr[0] * 0.212671f + sr[1] * 0.715160f + sr[2] * 0.072169f;
+    float tAvg = st[0] * 0.212671f + st[1] * 0.715160f + st[2] * 0.072169f;
+    out.specularSamplingWeight = (sAvg + tAvg) / (dAvg + sAvg + tAvg);
+    for (int i = 0; i < 3; ++i) {
+        out.specR[i] = sr[i];
+        out.specT[i] = st[i];
+    }
+}
+
 void configureKajiyaKay(const SceneDesc &d, HptKajiyaKay &out) {
     float kd[3] = {d.diffuse[0], d.diffuse[1], d.diffuse[2]};
     float ks[3] = {d.specular[0], d.specular[1], d.specular[2]};

@@ -403,9 +403,23 @@ void parseBSDF(const Ctx &c, const XNode &b, SceneDesc &d) {
             d.diffuse[i] = p.num.count("diffuseReflectance") ? p.num["diffuseReflectance"][i] : 0.5f;
             d.specular[i] = p.num.count("specularReflectance") ? p.num["specularReflectance"][i] : 1.0f;
         }
+    } else if (type == "marschnerdielectric") {
+        /* marschnerdielectric.cpp:147-169 */
+        d.intIOR = lookupIOR(c, b, p, "intIOR", "benzene");
+        d.extIOR = lookupIOR(c, b, p, "extIOR", "air");
+        if (d.intIOR < 0 || d.extIOR < 0)
+            fail(c.file, b.line, "The interior and exterior indices of refraction must be positive!");
+        for (int i = 0; i < 3; ++i) {
+            d.diffuse[i] = p.num.count("diffuseReflectance") ? p.num["diffuseReflectance"][i] : 0.5f;
+            d.specular[i] = p.num.count("specularReflectance") ? p.num["specularReflectance"][i] : 0.1f;
+            d.transmittance[i] = p.num.count("specularTransmittance") ? p.num["specularTransmittance"][i] : 0.1f;
+        }
+        d.exponent = num1(p, "exponent", 30.0f); /* read by the plugin, unused on every evaluated branch */
+        d.ensureEnergyConservation = num1(p, "ensureEnergyConservation", 1.0f) != 0.0f;
     } else {
         fail(c.file, b.line, "BSDF plugin \"" + type +
-                                 "\" is outside the hair hot path (supported: marschner, kajiyakay, roughplastic)");
+                                 "\" is outside the hair hot path (supported: marschner, kajiyakay, roughplastic, "
+                                 "marschnerdielectric)");
     }
 }
 

@@ -52,6 +52,7 @@ struct hpt_context {
     MarschnerHost mar;
     HptKajiyaKay kk;
     RoughPlasticHost rp;
+    HptMarschnerDielectric md;
     EnvHost env;
     bool envFromSunsky = false;
     SunSkyTables sunsky;
@@ -73,6 +74,10 @@ struct hpt_context {
 };
 
 namespace {
+/* HptScene::bsdfKind / hpt_scene_info::bsdf numbering */
+int bsdfKindOf(const std::string &b) {
+    return b == "marschner" ? 0 : b == "kajiyakay" ? 1 : b == "roughplastic" ? 2 : 3;
+}
 
 int setErr(hpt_context *c, int code, const std::string &m) {
     if (c) c->err = m;
@@ -370,6 +375,25 @@ int hpt_set_bsdf_roughplastic(hpt_context *c, float int_ior, float ext_ior, int 
     return HPT_OK;
 }
 
+int hpt_set_bsdf_marschnerdielectric(hpt_context *c, float int_ior, float ext_ior, const float diffuse[3],
+                                     const float specular_reflectance[3], const float specular_transmittance[3]) {
+    if (!c) return HPT_EINVAL;
+    if (int_ior < 0 || ext_ior < 0)
+        return setErr(c, HPT_EINVAL, "The interior and exterior indices of refraction must be positive!");
+    c->desc.bsdf = "marschnerdielectric";
+    c->desc.intIOR = int_ior;
+    c->desc.extIOR = ext_ior;
+    c->desc.ensureEnergyConservation = true;
+    for (int i = 0; i < 3; ++i) {
+        c->desc.diffuse[i] = diffuse ? diffuse[i] : 0.5f;
+        c->desc.specular[i] = specular_reflectance ? specular_reflectance[i] : 0.1f;
+        c->desc.transmittance[i] = specular_transmittance ? specular_transmittance[i] : 0.1f;
+    }
+    c->haveBSDF = true;
+    c->prepared = false;
+    return HPT_OK;
+}
+
 int hpt_set_bsdf_kajiyakay(hpt_context *c, const float kd[3], const float ks[3], float exponent) {
     if (!c || !kd) return HPT_EINVAL;
     c->desc.bsdf = "kajiyakay";
@@ -442,6 +466,8 @@ int hpt_prepare(hpt_context *c) {
             if (!precomputeMarschner(d, c->dataDir, c->mar, err)) return setErr(c, HPT_EIO, err);
         } else if (d.bsdf == "kajiyakay") {
             configureKajiyaKay(d, c->kk);
+        } else if (d.bsdf == "marschnerdielectric") {
+            configureMarschnerDielectric(d, c->md);
         } else if (d.bsdf == "roughplastic") {
             std::string err;
             if (!configureRoughPlastic(d, c->dataDir, c->rp, err)) return setErr(c, HPT_EINVAL, err);
@@ -474,7 +500,7 @@ int hpt_prepare(hpt_context *c) {
         sc.aabbMax[i] = c->tree.aabbMax[i];
     }
     sc.radius = c->hair.radius;
-    sc.bsdfKind = d.bsdf == "marschner" ? 0 : d.bsdf == "kajiyakay" ? 1 : 2;
+    sc.bsdfKind = bsdfKindOf(d.bsdf);
     if (sc.bsdfKind == 0) {
         for (int l = 0; l < 3; ++l) {
             r |= upload(c, c->mar.table[l].data(), c->mar.table[l].size() * 16, (const void **) &sc.mar.table[l]);
@@ -491,6 +517,8 @@ int hpt_prepare(hpt_context *c) {
         sc.mar.vTRT = c->mar.vTRT;
         sc.mar.scaleAngleRad = c->mar.scaleAngleRad;
         for (int i = 0; i < 3; ++i) sc.mar.diffuse[i] = c->mar.diffuse[i];
+    } else if (sc.bsdfKind == 3) {
+        sc.md = c->md;
     } else if (sc.bsdfKind == 2) {
         sc.rp = c->rp.p;
         r |= upload(c, c->rp.trans.data(), c->rp.trans.size() * 4, (const void **) &sc.rp.trans);
@@ -580,7 +608,7 @@ int hpt_get_scene_info(hpt_context *c, hpt_scene_info *o) {
     o->rr_depth = d.rrDepth;
     o->strict_normals = d.strictNormals;
     o->hide_emitters = d.hideEmitters;
-    o->bsdf = d.bsdf == "marschner" ? 0 : d.bsdf == "kajiyakay" ? 1 : 2;
+    o->bsdf = bsdfKindOf(d.bsdf);
     o->vertices = c->hair.vertexCount();
     o->segments = c->tree.segs.size();
     o->kd_nodes = c->tree.nodes.size();

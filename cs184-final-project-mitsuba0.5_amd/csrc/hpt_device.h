@@ -102,6 +102,14 @@ struct HptKajiyaKay {
 
 /* roughplastic (roughplastic.cpp:196-296): isotropic microfacet coating over
  * a diffuse base, constant textures */
+/* marschnerdielectric (marschnerdielectric.cpp:145-659): a thin dielectric
+ * sheet -- delta reflection about the fiber, straight pass-through (ENull) and
+ * a diffuse component whose solid-angle eval is identically zero there */
+struct HptMarschnerDielectric {
+    float eta, specularSamplingWeight;
+    float specR[3], specT[3];
+};
+
 struct HptRoughPlastic {
     int type;                   /* 0 beckmann, 1 ggx, 2 phong (microfacet.h:48-58) */
     int sampleVisible, nonlinear;
@@ -134,10 +142,11 @@ struct HptScene {
     const HptSegment *segs;
     float aabbMin[3], aabbMax[3];
     float radius;
-    int bsdfKind;               /* 0 = marschner, 1 = kajiyakay, 2 = roughplastic */
+    int bsdfKind;               /* 0 marschner, 1 kajiyakay, 2 roughplastic, 3 marschnerdielectric */
     HptMarschner mar;
     HptKajiyaKay kk;
     HptRoughPlastic rp;
+    HptMarschnerDielectric md;
     HptEnvMap env;
     const uint32_t *sobol;      /* 1024 x 52 */
     const uint64_t *vdc;        /* rows x 52 */

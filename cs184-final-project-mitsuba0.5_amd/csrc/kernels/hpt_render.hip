@@ -1187,12 +1187,53 @@ HD V3 rpSample(const HptRoughPlastic &m, V3 wi, float sx, float sy, V3 &wo, floa
     return divs(rpEval(m, wi, wo), pdf);
 }
 
+/* ------------------------------------------------------------------ */
+/* marschnerdielectric (marschnerdielectric.cpp:226-529), typeMask EAll.  */
+/* eval() and pdf() are called with ESolidAngle by the integrator, where  */
+/* the specular branches require EDiscrete: eval is 0 for every pair and  */
+/* pdf is the cosine-hemisphere density (:232-240, :285-335).             */
+/* ------------------------------------------------------------------ */
+HD V3 mdEval(const HptMarschnerDielectric &, V3, V3) { return v3(0, 0, 0); }
+HD float mdPdf(const HptMarschnerDielectric &, V3 wi, V3 wo) {
+    if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+    return kInvPi * wo.z;
+}
+HD V3 mdSample(const HptMarschnerDielectric &m, V3 wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
+    bool choseSpecular = true;
+    if (sx <= m.specularSamplingWeight) {
+        sx /= m.specularSamplingWeight;
+    } else {
+        sx = (sx - m.specularSamplingWeight) / (1 - m.specularSamplingWeight);
+        choseSpecular = false;
+    }
+    if (choseSpecular) {
+        float R = fresnelDielectricExt(fabsf(wi.z), m.eta), T = 1 - R;
+        if (R < 1) R += T * T * R / (1 - R * R); /* R + TRT + TR^3T + .. */
+        if (sx <= R) {
+            type = HPT_EDELTA_REFLECTION;
+            wo = v3(-wi.x, -wi.y, wi.z);
+            pdf = R;
+            return v3(m.specR[0], m.specR[1], m.specR[2]);
+        }
+        type = HPT_ENULL;
+        wo = v3(-wi.x, -wi.y, -wi.z);
+        pdf = 1 - R;
+        return v3(m.specT[0], m.specT[1], m.specT[2]);
+    }
+    wo = squareToCosineHemisphere(sx, sy);
+    type = HPT_EDIFFUSE_REFLECTION;
+    pdf = mdPdf(m, wi, wo);
+    return v3(0, 0, 0); /* eval / pdf with eval == 0 (or pdf == 0) */
+}
+
 HD V3 bsdfEval(const HptScene &sc, V3 wi, V3 wo) {
     if (sc.bsdfKind == 2) return rpEval(sc.rp, wi, wo);
+    if (sc.bsdfKind == 3) return mdEval(sc.md, wi, wo);
     return sc.bsdfKind == 0 ? marschnerEval(sc.mar, wi, wo) : kkEval(sc.kk, wi, wo);
 }
 HD float bsdfPdf(const HptScene &sc, V3 wi, V3 wo) {
     if (sc.bsdfKind == 2) return rpPdf(sc.rp, wi, wo);
+    if (sc.bsdfKind == 3) return mdPdf(sc.md, wi, wo);
     return sc.bsdfKind == 0 ? 1.0f : kkPdf(sc.kk, wi, wo);
 }
 HD V3 bsdfSample(const HptScene &sc, V3 wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
@@ -1201,6 +1242,7 @@ HD V3 bsdfSample(const HptScene &sc, V3 wi, float sx, float sy, V3 &wo, float &p
         return marschnerSample(sc.mar, wi, sx, sy, wo, type);
     }
     if (sc.bsdfKind == 2) return rpSample(sc.rp, wi, sx, sy, wo, pdf, type);
+    if (sc.bsdfKind == 3) return mdSample(sc.md, wi, sx, sy, wo, pdf, type);
     return kkSample(sc.kk, wi, sx, sy, wo, pdf, type);
 }
 
@@ -1593,7 +1635,8 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade(HptScene sc, Hp
                     P.rd[id] = make_float4(wo.x, wo.y, wo.z, finf());
                     P.bw[id] = make_float4(w.x, w.y, w.z, bpdf);
                     cont = true;
-                    st = (st & 0x00ffffffu) | (type << 24);
+                    /* bits 24-30: sampled type; bit 31: 'scattered' (path.cpp:205) */
+                    st = (st & 0x80ffffffu) | (type << 24) | (type != HPT_ENULL ? 0x80000000u : 0u);
                 }
             }
             if (shadow && !cont) P.ro[id] = make_float4(p.x, p.y, p.z, kEpsilon);
@@ -1616,7 +1659,8 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_post(HptScene sc, Hpt
     if (tid < n) {
         id = traceQ[tid];
         uint32_t st = P.state[id];
-        uint32_t dim = st & 0xffffu, depth = (st >> 16) & 0xffu, type = st >> 24;
+        uint32_t dim = st & 0xffffu, depth = (st >> 16) & 0xffu, type = (st >> 24) & 0x7fu;
+        const bool scattered = (st >> 31) != 0;
         float4 h = P.hit[id], bw = P.bw[id], thr = P.thr[id], rd = P.rd[id];
         bool hit = __float_as_int(h.x) >= 0;
         V3 T = v3(thr.x, thr.y, thr.z);
@@ -1624,12 +1668,12 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_post(HptScene sc, Hpt
         V3 value = v3(0, 0, 0);
         V3 d = v3(rd.x, rd.y, rd.z);
         if (!hit) {
-            /* path.cpp:239: 'hideEmitters && !scattered' never holds here -- every
-               sampled type of marschner / kajiyakay differs from ENull */
+            /* path.cpp:238-240: only a pass-through (ENull) chain from the camera is unscattered */
             value = envEval(sc.env, d);
             float4 ro = P.ro[id];
             float nearT, farT;
-            if (!bsphereIntersect(sc.env, v3(ro.x, ro.y, ro.z), d, nearT, farT) || nearT > 0 || farT < 0) {
+            if ((sc.hideEmitters && !scattered) ||
+                !bsphereIntersect(sc.env, v3(ro.x, ro.y, ro.z), d, nearT, farT) || nearT > 0 || farT < 0) {
                 done = true;
                 hitEmitter = false;
             } else {

@@ -66,6 +66,7 @@ SIGNATURES = {
     "hpt_set_bsdf_kajiyakay": (C.c_int, [C.c_void_p, _f, _f, C.c_float]),
     "hpt_set_bsdf_roughplastic": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_int, C.c_float, C.c_int, C.c_int,
                                             _f, _f]),
+    "hpt_set_bsdf_marschnerdielectric": (C.c_int, [C.c_void_p, C.c_float, C.c_float, _f, _f, _f]),
     "hpt_set_envmap_rgb": (C.c_int, [C.c_void_p, _f, C.c_int, C.c_int, C.c_float, _f]),
     "hpt_set_sunsky": (C.c_int, [C.c_void_p, _f, C.c_float, C.c_float, C.c_float, C.c_float, C.c_int]),
     "hpt_prepare": (C.c_int, [C.c_void_p]),
@@ -188,6 +189,12 @@ class Renderer:
         self._check(self.lib.hpt_set_bsdf_roughplastic(self.h, int_ior, ext_ior, distribution, alpha,
                                                        int(bool(sample_visible)), int(bool(nonlinear)),
                                                        _p(d, _f), _p(s, _f)))
+
+    def set_marschnerdielectric(self, int_ior=1.501, ext_ior=1.000277, diffuse=(0.5, 0.5, 0.5),
+                                specular_reflectance=(0.1, 0.1, 0.1), specular_transmittance=(0.1, 0.1, 0.1)):
+        d, r, t = _f32(diffuse), _f32(specular_reflectance), _f32(specular_transmittance)
+        self._check(self.lib.hpt_set_bsdf_marschnerdielectric(self.h, int_ior, ext_ior, _p(d, _f), _p(r, _f),
+                                                              _p(t, _f)))
 
     def set_envmap(self, rgb, scale=1.0):
         rgb = _f32(rgb)

@@ -48,7 +48,7 @@ int hpt_set_data_dir(hpt_context *ctx, const char *dir);
 
 /* Parse a Mitsuba scene XML (src/librender/scenehandler.cpp) with -D style
    defines: integrator "path", sensor "perspective" + sampler "sobol" + film,
-   shape "hair", bsdf "marschner"/"kajiyakay"/"roughplastic", emitter "sunsky"/"envmap". */
+   shape "hair", bsdf "marschner"/"kajiyakay"/"roughplastic"/"marschnerdielectric", emitter "sunsky"/"envmap". */
 int hpt_load_scene_xml(hpt_context *ctx, const char *path, int n_defines, const char *const *keys,
                        const char *const *values);
 
@@ -80,6 +80,10 @@ int hpt_set_bsdf_kajiyakay(hpt_context *ctx, const float kd[3], const float ks[3
    and is not expressible here. */
 int hpt_set_bsdf_roughplastic(hpt_context *ctx, float int_ior, float ext_ior, int distribution, float alpha,
                               int sample_visible, int nonlinear, const float diffuse[3], const float specular[3]);
+/* MarschnerDielectric(Properties) (src/bsdfs/marschnerdielectric.cpp:147-169);
+   NULL colours take the plugin defaults (0.5 / 0.1 / 0.1) */
+int hpt_set_bsdf_marschnerdielectric(hpt_context *ctx, float int_ior, float ext_ior, const float diffuse[3],
+                                     const float specular_reflectance[3], const float specular_transmittance[3]);
 /* EnvironmentMap from a bitmap (src/emitters/envmap.cpp:105-189); rgb is w*h*3
    linear floats, to_world may be NULL */
 int hpt_set_envmap_rgb(hpt_context *ctx, const float *rgb, int w, int h, float scale, const float *to_world);
@@ -94,7 +98,7 @@ int hpt_prepare(hpt_context *ctx);
 
 typedef struct hpt_scene_info {
     int width, height, spp, max_depth, rr_depth, strict_normals, hide_emitters;
-    int bsdf;                      /* 0 marschner, 1 kajiyakay, 2 roughplastic */
+    int bsdf;                      /* 0 marschner, 1 kajiyakay, 2 roughplastic, 3 marschnerdielectric */
     uint64_t vertices, segments, kd_nodes, kd_indices;
     int kd_depth;
     double kd_build_seconds;

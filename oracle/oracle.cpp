@@ -1077,6 +1077,104 @@ struct RoughPlastic {
 };
 
 /* ------------------------------------------------------------------ */
+/* marschnerdielectric.cpp:145-529 -- thin-sheet "MarschnerDielectric"  */
+/* Restated with its measure / component gates; the integrator calls     */
+/* eval/pdf with ESolidAngle, typeMask EAll, component -1.               */
+/* ------------------------------------------------------------------ */
+struct MarschnerDielectric {
+    enum EMeasure { ESolidAngle = 1, EDiscrete = 3 };
+    float eta = 1.501f, specularSamplingWeight = 0;
+    Spec diffuse{0.5f}, specR{0.1f}, specT{0.1f};
+    float exponent = 30.0f;
+    static constexpr float DeltaEpsilon = 1e-3f;                /* constants.h:31 */
+
+    void configure() { /* :189-211 */
+        float mx = specR.max();
+        if (mx > 1.0f) specR *= 0.99f * (1.0f / mx);
+        mx = specT.max();
+        if (mx > 1.0f) specT *= 0.99f * (1.0f / mx);
+        float dAvg = diffuse.getLuminance(), sAvg = specR.getLuminance(), tAvg = specT.getLuminance();
+        specularSamplingWeight = (sAvg + tAvg) / (dAvg + sAvg + tAvg);
+    }
+    static V3 reflect(const V3 &wi) { return V3(-wi.x, -wi.y, wi.z); }
+    static V3 transmit(const V3 &wi) { return V3(-wi.x, -wi.y, -wi.z); }
+    float fresnelR(const V3 &wi) const {
+        float R = fresnelDielectricExt(std::abs(wi.z), eta), T = 1 - R;
+        if (R < 1) R += T * T * R / (1 - R * R);
+        return R;
+    }
+    Spec eval(const V3 &wi, const V3 &wo, EMeasure measure = ESolidAngle) const { /* :232-283 */
+        const bool sampleReflection = measure == EDiscrete, sampleTransmission = measure == EDiscrete;
+        const bool hasDiffuse = true;
+        if (wi.z <= 0 || wo.z <= 0 || measure != ESolidAngle) return Spec(0.0f);
+        Spec result(0.0f);
+        float R = fresnelR(wi);
+        if (wi.z * wo.z >= 0) {
+            if (!sampleReflection || std::abs(dot(reflect(wi), wo) - 1) > DeltaEpsilon) return Spec(0.0f);
+            float tl = std::abs(wi.x), te = std::abs(wo.x);
+            float alpha = tl * te + std::sqrt(1 - tl * tl) * std::sqrt(1 - te * te);
+            if (alpha > 0.0f && wi.x * wo.x < 0)
+                result += 0.15f * specR * ((exponent + 2) * kInvFourPi * std::pow(alpha, exponent));
+        } else {
+            if (!sampleTransmission || std::abs(dot(transmit(wi), wo) - 1) > DeltaEpsilon) return Spec(0.0f);
+            result += specT * (1 - R);
+        }
+        if (hasDiffuse) result += diffuse * kInvPi;
+        return result * wo.z;
+    }
+    float pdf(const V3 &wi, const V3 &wo, EMeasure measure = ESolidAngle) const { /* :285-358 */
+        const bool sampleReflection = measure == EDiscrete, sampleTransmission = measure == EDiscrete;
+        const bool hasDiffuse = true;
+        if (measure != ESolidAngle || wi.z <= 0 || wo.z <= 0 ||
+            (!sampleReflection && !sampleTransmission && !hasDiffuse))
+            return 0.0f;
+        float diffuseProb = kInvPi * wo.z, specProb = 0.0f;
+        if (sampleReflection) {
+            float alpha = dot(wo, reflect(wi));
+            if (alpha > 0) specProb = std::pow(alpha, exponent) * (exponent + 1.0f) / (2.0f * kPi);
+        }
+        float R = fresnelR(wi), tProb = 0.0f, rProb = 0.0f;
+        if (wi.z * wo.z >= 0) {
+            if (!sampleReflection || std::abs(dot(reflect(wi), wo) - 1) > DeltaEpsilon) return diffuseProb;
+            tProb = sampleTransmission ? R : 1.0f;
+        } else {
+            if (!sampleTransmission || std::abs(dot(transmit(wi), wo) - 1) > DeltaEpsilon) return diffuseProb;
+            rProb = sampleReflection ? 1 - R : 1.0f;
+        }
+        if (sampleReflection) return specularSamplingWeight * specProb * rProb + (1 - specularSamplingWeight) * diffuseProb;
+        if (sampleTransmission) return specularSamplingWeight * specProb * tProb + (1 - specularSamplingWeight) * diffuseProb;
+        return diffuseProb;
+    }
+    Spec sample(const V3 &wi, float sx, float sy, V3 &wo, float &pdfOut, uint32_t &type) const { /* :424-500 */
+        bool choseSpecular = true;
+        if (sx <= specularSamplingWeight) {
+            sx /= specularSamplingWeight;
+        } else {
+            sx = (sx - specularSamplingWeight) / (1 - specularSamplingWeight);
+            choseSpecular = false;
+        }
+        if (choseSpecular) {
+            float R = fresnelR(wi);
+            if (sx <= R) {
+                type = EDeltaReflection;
+                wo = reflect(wi);
+                pdfOut = R;
+                return specR;
+            }
+            type = ENull;
+            wo = transmit(wi);
+            pdfOut = 1 - R;
+            return specT;
+        }
+        wo = squareToCosineHemisphere(sx, sy);
+        type = EDiffuseReflection;
+        pdfOut = pdf(wi, wo);
+        if (pdfOut == 0) return Spec(0.0f);
+        return eval(wi, wo) / pdfOut;
+    }
+};
+
+/* ------------------------------------------------------------------ */
 /* Hair shape: hair.cpp                                                 */
 /* ------------------------------------------------------------------ */
 struct HairGeom {
@@ -1441,10 +1539,11 @@ struct orc_scene {
     HairGeom hair;
     KDTree tree;
     AABB aabb;
-    int bsdfKind = -1; /* 0 marschner, 1 kajiyakay, 2 roughplastic */
+    int bsdfKind = -1; /* 0 marschner, 1 kajiyakay, 2 roughplastic, 3 marschnerdielectric */
     Marschner marschner;
     KajiyaKay kk;
     RoughPlastic rp;
+    MarschnerDielectric md;
     EnvMap env;
     bool hasEnv = false;
     int maxDepth = -1, rrDepth = 5;
@@ -1781,14 +1880,17 @@ inline float miWeight(float pdfA, float pdfB) { /* path.cpp:296-300 */
 
 Spec bsdfEval(const orc_scene *s, const V3 &wi, const V3 &wo) {
     if (s->bsdfKind == 2) return s->rp.eval(wi, wo);
+    if (s->bsdfKind == 3) return s->md.eval(wi, wo);
     return s->bsdfKind == 0 ? s->marschner.eval(wi, wo) : s->kk.eval(wi, wo);
 }
 float bsdfPdf(const orc_scene *s, const V3 &wi, const V3 &wo) {
     if (s->bsdfKind == 2) return s->rp.pdf(wi, wo);
+    if (s->bsdfKind == 3) return s->md.pdf(wi, wo);
     return s->bsdfKind == 0 ? s->marschner.pdf() : s->kk.pdf(wi, wo);
 }
 Spec bsdfSample(const orc_scene *s, const V3 &wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
     if (s->bsdfKind == 2) return s->rp.sample(wi, sx, sy, wo, pdf, type);
+    if (s->bsdfKind == 3) return s->md.sample(wi, sx, sy, wo, pdf, type);
     return s->bsdfKind == 0 ? s->marschner.sample(wi, sx, sy, wo, pdf, type)
                             : s->kk.sample(wi, sx, sy, wo, pdf, type);
 }
@@ -2199,6 +2301,19 @@ int orc_set_roughplastic(orc_scene *s, float eta, int distribution, float alpha,
     r.diffuse = Spec(diffuse[0], diffuse[1], diffuse[2]);
     r.specular = Spec(specular[0], specular[1], specular[2]);
     return r.configure(dat_dir, s->err) ? 0 : -1;
+}
+
+int orc_set_marschnerdielectric(orc_scene *s, float eta, const float diffuse[3], const float spec_r[3],
+                                const float spec_t[3]) {
+    s->bsdfKind = 3;
+    MarschnerDielectric &m = s->md;
+    m = MarschnerDielectric();
+    m.eta = eta;
+    m.diffuse = Spec(diffuse[0], diffuse[1], diffuse[2]);
+    m.specR = Spec(spec_r[0], spec_r[1], spec_r[2]);
+    m.specT = Spec(spec_t[0], spec_t[1], spec_t[2]);
+    m.configure();
+    return 0;
 }
 
 int orc_set_envmap(orc_scene *s, const float *rgb, int w, int h, float scale, const float *to_world) {

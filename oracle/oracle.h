@@ -61,6 +61,9 @@ int orc_set_kajiyakay(orc_scene *s, const float kd[3], const float ks[3], float 
 int orc_set_roughplastic(orc_scene *s, float eta, int distribution, float alpha, int sample_visible,
                          int nonlinear, const float diffuse[3], const float specular[3],
                          const char *microfacet_dat_dir);
+/* marschnerdielectric.cpp: eta = intIOR/extIOR */
+int orc_set_marschnerdielectric(orc_scene *s, float eta, const float diffuse[3], const float spec_r[3],
+                                const float spec_t[3]);
 /* envmap.cpp: linear RGB float bitmap (w x h x 3), to_world may be NULL */
 int orc_set_envmap(orc_scene *s, const float *rgb, int w, int h, float scale,
                    const float *to_world);

@@ -38,6 +38,7 @@ _SIG = {
     "orc_hair_aabb": (C.c_int, [C.c_void_p, _f, _f]),
     "orc_set_marschner": (C.c_int, [C.c_void_p, C.c_float, C.c_int, C.c_float, _f, _f, C.c_char_p]),
     "orc_set_kajiyakay": (C.c_int, [C.c_void_p, _f, _f, C.c_float]),
+    "orc_set_marschnerdielectric": (C.c_int, [C.c_void_p, C.c_float, _f, _f, _f]),
     "orc_set_roughplastic": (C.c_int, [C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_int, C.c_int, _f, _f,
                                        C.c_char_p]),
     "orc_set_envmap": (C.c_int, [C.c_void_p, _f, C.c_int, C.c_int, C.c_float, _f]),
@@ -133,6 +134,8 @@ class Oracle:
             dist = {"beckmann": 0, "ggx": 1, "phong": 2}[bsdf["distribution"]]
             self.check(self.lib.orc_set_marschner(self.s, bsdf["eta"], dist, bsdf["alpha"], p(dif, _f), p(spec, _f),
                                                   os.path.join(DATA, "microfacet").encode()))
+        elif kind == "marschnerdielectric":
+            self.set_marschnerdielectric(bsdf)
         elif kind == "roughplastic":
             self.set_roughplastic(bsdf)
         else:
@@ -142,6 +145,12 @@ class Oracle:
         env = f32(env_rgb)
         self.check(self.lib.orc_set_envmap(self.s, p(env, _f), env.shape[1], env.shape[0], 1.0, None))
         self.check(self.lib.orc_set_integrator(self.s, max_depth, rr_depth, int(strict), int(hide)))
+
+    def set_marschnerdielectric(self, bsdf):
+        dif = f32(bsdf.get("diffuse", (0.5, 0.5, 0.5)))
+        sr = f32(bsdf.get("specular", (0.1, 0.1, 0.1)))
+        st = f32(bsdf.get("transmittance", (0.1, 0.1, 0.1)))
+        self.check(self.lib.orc_set_marschnerdielectric(self.s, bsdf["eta"], p(dif, _f), p(sr, _f), p(st, _f)))
 
     def set_roughplastic(self, bsdf):
         dif = f32(bsdf.get("diffuse", (0.5, 0.5, 0.5)))

@@ -22,9 +22,13 @@ WORK = os.environ.get("HPT_TEST_WORK", os.path.join(tempfile.gettempdir(), "hpt_
 def config_params(name):
     cfg = scenes.CONFIGS[name]
     cam = np.array([float(x) for x in cfg["cam"].split()], np.float32)
-    if "marschner" in cfg["bsdf"]:
+    if 'type="marschner"' in cfg["bsdf"]:
         bsdf = {"type": "marschner", "eta": np.float32(1.55) / np.float32(1.0), "distribution": "ggx",
                 "alpha": 0.2, "diffuse": (0.143016, 0.0156076, 1.80928e-005), "specular": (0.5, 0.5, 0.5)}
+    elif "marschnerdielectric" in cfg["bsdf"]:
+        c = (0.143016, 0.0156076, 1.80928e-005)
+        bsdf = {"type": "marschnerdielectric", "eta": np.float32(1.55) / np.float32(1.0), "diffuse": c,
+                "specular": c, "transmittance": c}
     elif "roughplastic" in cfg["bsdf"]:
         bsdf = {"type": "roughplastic", "eta": np.float32(1.55) / np.float32(1.0), "distribution": "ggx",
                 "alpha": 0.2, "sample_visible": True, "nonlinear": False,

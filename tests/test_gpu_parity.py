@@ -113,6 +113,12 @@ def test_trace_bit_exact(fixture, kind, request):
 
 
 @pytest.fixture(scope="module")
+def straight_md():
+    xml, r, o = scene_util.make("straight_dielectric", 1500, 48, 40, 8, device=0)
+    return xml, r, o
+
+
+@pytest.fixture(scope="module")
 def furball_rp():
     xml, r, o = scene_util.make("furball_roughplastic", 3000, 48, 40, 8, device=0)
     return xml, r, o
@@ -129,7 +135,7 @@ def _dirs(rng, n):
     return (v / np.linalg.norm(v, axis=1, keepdims=True)).astype(np.float32)
 
 
-@pytest.mark.parametrize("fixture", ["furball", "straight", "furball_rp"])
+@pytest.mark.parametrize("fixture", ["furball", "straight", "furball_rp", "straight_md"])
 def test_bsdf_matches_oracle(fixture, request):
     _, r, o = request.getfixturevalue(fixture)
     rng = np.random.default_rng(7)
@@ -192,6 +198,30 @@ def test_roughplastic_variants_match_oracle(dist):
         assert close[agree].mean() > 0.999, (dist, sv, nl)
 
 
+def test_hide_emitters_with_pass_through(straight_md):
+    """hideEmitters with a BSDF that has an ENull component: a camera path that
+    only passed straight through fibers is still 'unscattered' and must not
+    see the environment (path.cpp:205, 238-240); after any reflection it must."""
+    _, r, o = straight_md
+    si = r.info()
+    try:
+        r.set_integrator(si.max_depth, si.rr_depth, True, True)
+        r.prepare()
+        o.lib.orc_set_integrator(o.s, si.max_depth, si.rr_depth, 1, 1)
+        film = r.render(0, si.spp)
+        ofilm, _ = o.render(0, si.spp, width=si.width, height=si.height)
+        a, b = native.develop(film), native.develop(ofilm)
+        m = scene_util.l2_metrics(b, a)
+        print("hideEmitters gpu vs oracle", m)
+        assert m["rmse"] < 1e-3, m
+        same = np.all(np.abs(a - b) <= 1e-5 * np.abs(b) + 1e-7, axis=-1)
+        assert same.mean() > 0.85
+    finally:
+        r.set_integrator(si.max_depth, si.rr_depth, True, False)
+        r.prepare()
+        o.lib.orc_set_integrator(o.s, si.max_depth, si.rr_depth, 1, 0)
+
+
 def test_envmap_matches_oracle(furball):
     _, r, o = furball
     rng = np.random.default_rng(9)
@@ -216,11 +246,11 @@ def test_envmap_matches_oracle(furball):
 
 def _reference_flags_floor(fixture, r, si):
     name, n = {"furball": ("furball_marschner", 3000), "straight": ("straight_kk", 1500),
-               "furball_rp": ("furball_roughplastic", 3000)}[fixture]
+               "furball_rp": ("furball_roughplastic", 3000), "straight_md": ("straight_dielectric", 1500)}[fixture]
     return scene_util.reference_flags_floor(name, n, r, si.width, si.height, si.spp)
 
 
-@pytest.mark.parametrize("fixture", ["furball", "straight", "furball_rp"])
+@pytest.mark.parametrize("fixture", ["furball", "straight", "furball_rp", "straight_md"])
 def test_render_matches_oracle(fixture, request):
     """Full wavefront render vs the oracle's MIPathTracer::Li restatement."""
     _, r, o = request.getfixturevalue(fixture)

@@ -96,6 +96,24 @@ def test_roughplastic_scene_xml(tmp_path):
     assert rr.info().bsdf == 2
 
 
+def test_marschnerdielectric_scene_xml(tmp_path):
+    """models/straight-hair/scene_dielectric.xml's BSDF parses to kind 3; the
+    shipped scene_dielectric2.xml (an unclosed <float name="m_exponent">) is
+    malformed XML and is refused, as the reference's XML parser refuses it."""
+    xml = scenes.make_scene("straight_dielectric", str(tmp_path), n_strands=100)
+    r = _host(xml, {"width": 16, "height": 16, "spp": 1})
+    r.prepare()
+    assert r.info().bsdf == 3
+    src = open(xml).read()
+    bad = tmp_path / "md_bad.xml"
+    bad.write_text(src.replace('<float name="exponent" value="5.0"/>', '<float name="m_exponent" value="10.0">'))
+    with pytest.raises(native.HairPTError):
+        _host(str(bad))
+    bad.write_text(src.replace('<float name="intIOR" value="1.55"/>', '<float name="intIOR" value="-1"/>'))
+    with pytest.raises(native.HairPTError, match="positive"):
+        _host(str(bad))
+
+
 def test_scene_xml_errors(tmp_path):
     bad = tmp_path / "bad.xml"
     bad.write_text('<scene version="0.6.0"><integrator type="volpath"/></scene>')

@@ -134,3 +134,44 @@ def test_roughplastic_energy_and_reciprocity():
         f_ba, _ = o.bsdf_eval(b, a)
         # eval includes cos(theta_o): f(a,b)/cos_b == f(b,a)/cos_a
         np.testing.assert_allclose(f_ab / b[:, 2:3], f_ba / a[:, 2:3], rtol=1e-5, atol=1e-7)
+
+
+def test_marschnerdielectric_lobe_probabilities():
+    """marschnerdielectric (models/straight-hair/scene_dielectric.xml): the
+    integrator's solid-angle eval is zero everywhere, the pdf is the cosine
+    density, and sample() picks reflect / pass-through / diffuse with
+    probabilities w*R', w*(1-R'), 1-w where R' = R + T^2 R / (1 - R^2)
+    (marschnerdielectric.cpp:226-283, 424-500)."""
+    o = oracle_lib.Oracle()
+    c = (0.143016, 0.0156076, 1.80928e-005)
+    o.set_marschnerdielectric({"eta": np.float32(1.55), "diffuse": c, "specular": c, "transmittance": c})
+    rng = np.random.default_rng(3)
+    a = rng.normal(size=(5000, 3))
+    a = (a / np.linalg.norm(a, axis=1, keepdims=True)).astype(np.float32)
+    b = rng.normal(size=(5000, 3))
+    b = (b / np.linalg.norm(b, axis=1, keepdims=True)).astype(np.float32)
+    ev, pdf = o.bsdf_eval(a, b)
+    assert np.all(ev == 0)
+    ok = (a[:, 2] > 0) & (b[:, 2] > 0)
+    np.testing.assert_allclose(pdf[ok], np.float32(1 / np.pi) * b[ok, 2], rtol=1e-6)
+    assert np.all(pdf[~ok] == 0)
+    wi = np.array([0.3, 0.2, 0.9327], np.float32)
+    wi /= np.linalg.norm(wi)
+    n = 400000
+    u = rng.random((n, 2)).astype(np.float32)
+    wo, w, p, t = o.bsdf_sample(np.repeat(wi[None], n, 0), u)
+    lum = lambda v: v[0] * 0.212671 + v[1] * 0.715160 + v[2] * 0.072169
+    sw = 2 * lum(c) / (3 * lum(c))
+    cos = float(wi[2])
+    eta = 1.55
+    st2 = (1 - cos * cos) / eta ** 2
+    ct = np.sqrt(1 - st2)
+    R = 0.5 * (((cos - eta * ct) / (cos + eta * ct)) ** 2 + ((eta * cos - ct) / (eta * cos + ct)) ** 2)
+    R = R + (1 - R) ** 2 * R / (1 - R * R)
+    refl, null, diff = (t == 0x20), (t == 0x1), (t == 0x2)
+    assert abs(refl.mean() - sw * R) < 4e-3 and abs(null.mean() - sw * (1 - R)) < 4e-3
+    assert abs(diff.mean() - (1 - sw)) < 4e-3
+    np.testing.assert_allclose(wo[refl], np.repeat([[-wi[0], -wi[1], wi[2]]], refl.sum(), 0), rtol=1e-6)
+    np.testing.assert_allclose(wo[null], np.repeat([-wi], null.sum(), 0), rtol=1e-6)
+    assert np.all(w[diff] == 0)
+    np.testing.assert_allclose(w[null], np.repeat([np.float32(c)], null.sum(), 0), rtol=1e-6)
