@@ -61,15 +61,16 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(args, cfg, xml_defines, hair_file, env_rgb, nodes, idx):
+def cpu_baseline(args, cfg, xml_defines, hair_src, env_rgb, nodes, idx):
     """Oracle built with the reference's flags (liboracle_ref.so), bounded sample on host cores."""
     import oracle_lib
     import scene_util
 
-    _, cam, bsdf = scene_util.config_params(args.config)
+    _, cam, _ = scene_util.config_params(args.config)
     o = oracle_lib.Oracle(variant="ref")
     W, H = xml_defines["width"], xml_defines["height"]
-    o.setup(cam, 35.0, W, H, hair_file, float(cfg["radius"]), bsdf, env_rgb, xml_defines["maxDepth"])
+    o.setup(cam, 35.0, W, H, scene_util.oracle_shapes(args.config, hair_src[1], hair_src[0]), None, None, env_rgb,
+            xml_defines["maxDepth"])
     o.set_kdtree(nodes, idx)
     o.prepare()
     threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
@@ -102,7 +103,7 @@ def main():
     xml = scenes.make_scene(args.config, workdir, n_strands=n)
     if args.kd:
         xml = scenes.with_kd_params(xml, dict(kv.split("=") for kv in args.kd.split(",") if kv))
-    hair_file = os.path.join(workdir, "%s_%d.mitshair" % (cfg["geom"], n))
+    hair_src = (workdir, n)  # the oracle re-reads the same hair file(s)
 
     r = native.Renderer(device=local)
     r.load_scene_xml(xml, defines)
@@ -171,7 +172,7 @@ def main():
         cpu = None
         if args.cpu_baseline == "auto" and world == 1:
             nodes, idx, _ = r.kdtree()
-            cpu = cpu_baseline(args, cfg, defines, hair_file, r.envmap(), nodes, idx)
+            cpu = cpu_baseline(args, cfg, defines, hair_src, r.envmap(), nodes, idx)
         img = native.develop(film.cpu().numpy())
         out = {
             "metric": "Mpaths/sec + achieved HBM GB/s, furball Marschner 512² @ 256spp",

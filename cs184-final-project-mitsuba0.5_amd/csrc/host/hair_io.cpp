@@ -174,9 +174,31 @@ HairData loadHair(const std::string &path, float radius, float angleThresholdDeg
     }
     out.starts.push_back(1);
     out.radius = radius;
+    out.shapeRadius = {radius};
     out.nDegenerate = b.nDegenerate;
     out.nSkipped = b.nSkipped;
     return out;
+}
+
+void appendHair(HairData &a, const HairData &b) {
+    /* several HairShapes in one scene (ShapeKDTree over shapes, skdtree.cpp):
+       concatenated vertex arrays; a shape's first vertex always starts a
+       fiber, so no segment or miter spans two shapes */
+    if (a.shapeRadius.empty()) {
+        a = b;
+        if (a.shapeRadius.empty()) a.shapeRadius = {a.radius};
+        a.shapeFirst = {0};
+        return;
+    }
+    const uint32_t base = (uint32_t) a.vertexCount();
+    a.xyz.insert(a.xyz.end(), b.xyz.begin(), b.xyz.end());
+    a.starts.pop_back(); /* a's terminator */
+    a.starts.insert(a.starts.end(), b.starts.begin(), b.starts.end());
+    if (b.vertexCount()) a.starts[base] = 1;
+    a.shapeFirst.push_back(base);
+    a.shapeRadius.push_back(b.radius);
+    a.nDegenerate += b.nDegenerate;
+    a.nSkipped += b.nSkipped;
 }
 
 } // namespace hpt

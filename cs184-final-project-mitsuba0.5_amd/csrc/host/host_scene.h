@@ -9,6 +9,7 @@
  */
 #ifndef HPT_HOST_SCENE_H
 #define HPT_HOST_SCENE_H
+#include <algorithm>
 #include <cstdint>
 #include <map>
 #include <memory>
@@ -43,6 +44,29 @@ struct KDBuildParams {
     int threads = 0;               /* 0 = hardware concurrency */
 };
 
+/* ---- one BSDF instance (constant textures) ---- */
+struct BsdfDesc {
+    std::string type = "diffuse";                  /* Shape::configure default (shape.cpp:99-110) */
+    float intIOR = 1.5046f, extIOR = 1.000277f;   /* ior.h: bk7 / air defaults */
+    std::string distribution = "beckmann";
+    float alpha = 0.1f;                            /* microfacet.h:99-140 defaults */
+    float diffuse[3] = {0.5f, 0.5f, 0.5f};
+    float specular[3] = {0.5f, 0.5f, 0.5f};        /* marschner default 0.5 */
+    float transmittance[3] = {0.1f, 0.1f, 0.1f};   /* marschnerdielectric / thindielectric specularTransmittance */
+    float exponent = 30.0f;
+    bool nonlinear = false;
+    bool sampleVisible = true, ensureEnergyConservation = true;
+};
+
+/* ---- one hair shape ---- */
+struct HairShapeDesc {
+    std::string file;
+    float radius = 0.025f, angleThreshold = 1.0f, reduction = 0.0f;
+    float toWorld[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    bool hasToWorld = false;
+    int bsdf = 0;                                  /* index into SceneDesc::bsdfs */
+};
+
 /* ---- parsed scene description (subset of the Mitsuba 0.5 scene schema) ---- */
 struct SceneDesc {
     /* integrator (integrator.cpp:190-203, path.cpp) */
@@ -62,24 +86,10 @@ struct SceneDesc {
     float gamma = -1.0f;
     std::string fileFormat;
     std::string rfilter = "tent";
-    /* hair shape (hair.cpp:609-640) */
-    std::string hairFile;
-    float radius = 0.025f, angleThreshold = 1.0f, reduction = 0.0f;
-    float hairToWorld[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
-    bool hairHasToWorld = false;
-    KDBuildParams kd;
-    /* bsdf */
-    std::string bsdf = "";
-    float intIOR = 1.5046f, extIOR = 1.000277f;   /* ior.h: bk7 / air defaults */
-    std::string distribution = "beckmann";
-    float alpha = 0.1f;                            /* microfacet.h:99-140 defaults */
-    float diffuse[3] = {0.5f, 0.5f, 0.5f};
-    float specular[3] = {0.5f, 0.5f, 0.5f};        /* marschner default 0.5 */
-    float transmittance[3] = {0.1f, 0.1f, 0.1f};   /* marschnerdielectric specularTransmittance */
-    bool specularGiven = false;
-    float exponent = 30.0f;
-    bool nonlinear = false;
-    bool sampleVisible = true, ensureEnergyConservation = true;
+    /* hair shapes (hair.cpp:609-640), each referencing one of bsdfs */
+    std::vector<HairShapeDesc> shapes;
+    std::vector<BsdfDesc> bsdfs;
+    KDBuildParams kd;                              /* from the first hair shape */
     /* emitter */
     std::string emitter = "";
     std::string envFile;
@@ -107,7 +117,14 @@ SceneDesc parseSceneXML(const std::string &path, const std::map<std::string, std
 struct HairData {
     std::vector<float> xyz;         /* 3 per vertex */
     std::vector<uint8_t> starts;    /* n + 1 entries, last = 1 */
-    float radius = 0.025f;
+    float radius = 0.025f;          /* radius of a single-shape set (== shapeRadius[0]) */
+    /* merged hair shapes: shape k owns vertices [shapeFirst[k], shapeFirst[k+1]) */
+    std::vector<uint32_t> shapeFirst{0};
+    std::vector<float> shapeRadius;
+    uint32_t shapeOf(uint32_t iv) const {
+        return (uint32_t) (std::upper_bound(shapeFirst.begin(), shapeFirst.end(), iv) - shapeFirst.begin() - 1);
+    }
+    float radiusOf(uint32_t iv) const { return shapeRadius.empty() ? radius : shapeRadius[shapeOf(iv)]; }
     size_t nDegenerate = 0, nSkipped = 0;
     size_t vertexCount() const { return xyz.size() / 3; }
 };
@@ -132,6 +149,8 @@ struct KDTreeHost {
 };
 
 KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params);
+/* append shape b to a (a's first vertex of b starts a fiber) */
+void appendHair(HairData &a, const HairData &b);
 
 /* ---- precomputation ---- */
 struct MarschnerHost {
@@ -143,17 +162,19 @@ struct MarschnerHost {
     float diffuse[3];
 };
 
-bool precomputeMarschner(const SceneDesc &d, const std::string &dataDir, MarschnerHost &out,
+bool precomputeMarschner(const BsdfDesc &d, const std::string &dataDir, MarschnerHost &out,
                          std::string &err);
-void configureKajiyaKay(const SceneDesc &d, HptKajiyaKay &out);
-void configureMarschnerDielectric(const SceneDesc &d, HptMarschnerDielectric &out);
+void configureKajiyaKay(const BsdfDesc &d, HptKajiyaKay &out);
+void configureMarschnerDielectric(const BsdfDesc &d, HptMarschnerDielectric &out);
+void configureThinDielectric(const BsdfDesc &d, HptMarschnerDielectric &out);
+void configureDiffuse(const BsdfDesc &d, HptDiffuse &out);
 
 /* roughplastic (roughplastic.cpp:197-299): device parameters + the 1-D external transmittance slice */
 struct RoughPlasticHost {
     HptRoughPlastic p{};
     std::vector<float> trans;
 };
-bool configureRoughPlastic(const SceneDesc &d, const std::string &dataDir, RoughPlasticHost &out, std::string &err);
+bool configureRoughPlastic(const BsdfDesc &d, const std::string &dataDir, RoughPlasticHost &out, std::string &err);
 /* RoughTransmittance (rtrans.h) for one distribution: the external 1-D slice at (eta, alphaSlice) and
  * Fdr = 1 - internal (1/eta) diffuse transmittance at alphaDiffuse */
 bool roughTransmittance(const std::string &dataDir, const std::string &distribution, float eta, float alphaSlice,

@@ -158,7 +158,7 @@ struct SegGeom {
         for (int end = 0; end < 2; ++end) {
             V p = end == 0 ? vtx(iv) : vtx(iv + 1);
             V n = end == 0 ? firstMiter(iv) : secondMiter(iv);
-            if (!cylPlane(p, n, p, tangent(iv), h.radius * (1 - kEps), c, ax, l)) {
+            if (!cylPlane(p, n, p, tangent(iv), h.radiusOf(iv) * (1 - kEps), c, ax, l)) {
                 l[0] = l[1] = 0;
                 c = p;
             }
@@ -174,14 +174,14 @@ struct SegGeom {
     }
 
     /* hair.cpp:289-343 */
-    Box cylFace(int axis, V mn, V mx, V cylPt, V cylD) const {
+    Box cylFace(int axis, V mn, V mx, V cylPt, V cylD, float radius) const {
         int a1 = (axis + 1) % 3, a2 = (axis + 2) % 3;
         V n{0, 0, 0};
         n[axis] = 1;
         V c, ax[2];
         float l[2];
         Box out;
-        if (!cylPlane(mn, n, cylPt, cylD, h.radius * (1 + kEps), c, ax, l)) return out;
+        if (!cylPlane(mn, n, cylPt, cylD, radius * (1 + kEps), c, ax, l)) return out;
         for (int i = 0; i < 4; ++i) {
             V p1, p2;
             p1[axis] = p2[axis] = mn[axis];
@@ -222,14 +222,15 @@ struct SegGeom {
         base.clip(box);
         if (!base.valid()) return base;
         V cp = vtx(iv), cd = tangent(iv);
+        const float rad = h.radiusOf(iv);
         Box r;
         const V &a = base.mn, &b = base.mx;
-        r.expand(cylFace(0, {a.x, a.y, a.z}, {a.x, b.y, b.z}, cp, cd));
-        r.expand(cylFace(0, {b.x, a.y, a.z}, {b.x, b.y, b.z}, cp, cd));
-        r.expand(cylFace(1, {a.x, a.y, a.z}, {b.x, a.y, b.z}, cp, cd));
-        r.expand(cylFace(1, {a.x, b.y, a.z}, {b.x, b.y, b.z}, cp, cd));
-        r.expand(cylFace(2, {a.x, a.y, a.z}, {b.x, b.y, a.z}, cp, cd));
-        r.expand(cylFace(2, {a.x, a.y, b.z}, {b.x, b.y, b.z}, cp, cd));
+        r.expand(cylFace(0, {a.x, a.y, a.z}, {a.x, b.y, b.z}, cp, cd, rad));
+        r.expand(cylFace(0, {b.x, a.y, a.z}, {b.x, b.y, b.z}, cp, cd, rad));
+        r.expand(cylFace(1, {a.x, a.y, a.z}, {b.x, a.y, b.z}, cp, cd, rad));
+        r.expand(cylFace(1, {a.x, b.y, a.z}, {b.x, b.y, b.z}, cp, cd, rad));
+        r.expand(cylFace(2, {a.x, a.y, a.z}, {b.x, b.y, a.z}, cp, cd, rad));
+        r.expand(cylFace(2, {a.x, a.y, b.z}, {b.x, b.y, b.z}, cp, cd, rad));
         r.clip(base);
         return r;
     }
@@ -557,7 +558,7 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
             r.v2[k] = v2[k];
         }
         r.iv = iv;
-        r.pad = 0;
+        r.shape = hair.shapeOf(iv);
     }
 
     /* primitive bounds + tree AABB (gkdtree.h:990-994) */
@@ -595,7 +596,7 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
             f.axis[k] = (float) t.segs[s].axis[k];
         }
         f.seg = s;
-        f.pad = 0;
+        f.radius = hair.radiusOf(segIv[s]);
     }
     t.buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return t;

@@ -244,7 +244,7 @@ void buildIDist(std::vector<float> w, int size, int nd, std::vector<float> &cdf,
 
 } // namespace
 
-bool precomputeMarschner(const SceneDesc &d, const std::string &dataDir, MarschnerHost &out, std::string &err) {
+bool precomputeMarschner(const BsdfDesc &d, const std::string &dataDir, MarschnerHost &out, std::string &err) {
     const float eta = d.intIOR / d.extIOR;
     const float betaR = 0.1f, betaTT = betaR * 0.5f, betaTRT = betaR * 2.0f;
     const F3 sigmaA{0.5f, 0.5f, 0.5f};
@@ -376,7 +376,7 @@ bool roughTransmittance(const std::string &dataDir, const std::string &distribut
     return true;
 }
 
-bool configureRoughPlastic(const SceneDesc &d, const std::string &dataDir, RoughPlasticHost &out, std::string &err) {
+bool configureRoughPlastic(const BsdfDesc &d, const std::string &dataDir, RoughPlasticHost &out, std::string &err) {
     /* RoughPlastic(props) + configure (roughplastic.cpp:197-299) */
     const float eta = d.intIOR / d.extIOR;
     if (d.intIOR < 0 || d.extIOR < 0 || d.intIOR == d.extIOR) {
@@ -422,7 +422,7 @@ bool configureRoughPlastic(const SceneDesc &d, const std::string &dataDir, Rough
     return true;
 }
 
-void configureMarschnerDielectric(const SceneDesc &d, HptMarschnerDielectric &out) {
+void configureMarschnerDielectric(const BsdfDesc &d, HptMarschnerDielectric &out) {
     /* MarschnerDielectric(props) + configure (marschnerdielectric.cpp:147-211) */
     out.eta = d.intIOR / d.extIOR;
     float sr[3] = {d.specular[0], d.specular[1], d.specular[2]};
@@ -446,7 +446,39 @@ void configureMarschnerDielectric(const SceneDesc &d, HptMarschnerDielectric &ou
     }
 }
 
-void configureKajiyaKay(const SceneDesc &d, HptKajiyaKay &out) {
+void configureThinDielectric(const BsdfDesc &d, HptMarschnerDielectric &out) {
+    /* ThinDielectric(props) + configure (thindielectric.cpp:73-125) */
+    out.eta = d.intIOR / d.extIOR;
+    out.specularSamplingWeight = 1.0f; /* no diffuse component: the sample is never split */
+    float sr[3] = {d.specular[0], d.specular[1], d.specular[2]};
+    float st[3] = {d.transmittance[0], d.transmittance[1], d.transmittance[2]};
+    if (d.ensureEnergyConservation) {
+        for (float *v : {sr, st}) {
+            float mx = std::max(std::max(v[0], v[1]), v[2]);
+            if (mx > 1.0f) {
+                float s = 0.99f * (1.0f / mx);
+                for (int i = 0; i < 3; ++i) v[i] *= s;
+            }
+        }
+    }
+    for (int i = 0; i < 3; ++i) {
+        out.specR[i] = sr[i];
+        out.specT[i] = st[i];
+    }
+}
+
+void configureDiffuse(const BsdfDesc &d, HptDiffuse &out) {
+    /* SmoothDiffuse::configure (diffuse.cpp:77-88) */
+    float v[3] = {d.diffuse[0], d.diffuse[1], d.diffuse[2]};
+    float mx = std::max(std::max(v[0], v[1]), v[2]);
+    if (d.ensureEnergyConservation && mx > 1.0f) {
+        float s = 0.99f * (1.0f / mx);
+        for (int i = 0; i < 3; ++i) v[i] *= s;
+    }
+    for (int i = 0; i < 3; ++i) out.refl[i] = v[i];
+}
+
+void configureKajiyaKay(const BsdfDesc &d, HptKajiyaKay &out) {
     float kd[3] = {d.diffuse[0], d.diffuse[1], d.diffuse[2]};
     float ks[3] = {d.specular[0], d.specular[1], d.specular[2]};
     float mx = std::max(std::max(ks[0] + kd[0], ks[1] + kd[1]), ks[2] + kd[2]);

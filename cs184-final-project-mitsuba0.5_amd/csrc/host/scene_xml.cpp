@@ -136,6 +136,7 @@ struct Ctx {
     std::string file;
     std::map<std::string, std::string> defines;
     std::map<std::string, const XNode *> ids;
+    std::map<const XNode *, int> bsdfIndex; /* one instance per <bsdf> element, shared by its refs */
 };
 
 std::string subst(const Ctx &c, const XNode &nd, const std::string &v) {
@@ -318,11 +319,11 @@ float lookupIOR(const Ctx &c, const XNode &nd, const Props &p, const char *key, 
     fail(c.file, nd.line, "Unable to find an IOR value for \"" + name + "\"");
 }
 
-void parseBSDF(const Ctx &c, const XNode &b, SceneDesc &d) {
+void parseBSDF(const Ctx &c, const XNode &b, BsdfDesc &d) {
     std::string type = attrS(c, b, "type");
     Props p;
     collectProps(c, b, p);
-    d.bsdf = type;
+    d.type = type;
     if (type == "marschner") {
         /* marschner_diffuse.cpp:113-160 (plugin "marschner", SConscript:38) */
         d.intIOR = lookupIOR(c, b, p, "intIOR", "bk7");
@@ -416,10 +417,26 @@ void parseBSDF(const Ctx &c, const XNode &b, SceneDesc &d) {
         }
         d.exponent = num1(p, "exponent", 30.0f); /* read by the plugin, unused on every evaluated branch */
         d.ensureEnergyConservation = num1(p, "ensureEnergyConservation", 1.0f) != 0.0f;
+    } else if (type == "thindielectric") {
+        /* thindielectric.cpp:73-89 */
+        d.intIOR = lookupIOR(c, b, p, "intIOR", "bk7");
+        d.extIOR = lookupIOR(c, b, p, "extIOR", "air");
+        if (d.intIOR < 0 || d.extIOR < 0)
+            fail(c.file, b.line, "The interior and exterior indices of refraction must be positive!");
+        for (int i = 0; i < 3; ++i) {
+            d.specular[i] = p.num.count("specularReflectance") ? p.num["specularReflectance"][i] : 1.0f;
+            d.transmittance[i] = p.num.count("specularTransmittance") ? p.num["specularTransmittance"][i] : 1.0f;
+        }
+        d.ensureEnergyConservation = num1(p, "ensureEnergyConservation", 1.0f) != 0.0f;
+    } else if (type == "diffuse") {
+        /* diffuse.cpp:62-69: 'reflectance' or 'diffuseReflectance' */
+        const char *key = p.num.count("reflectance") ? "reflectance" : "diffuseReflectance";
+        for (int i = 0; i < 3; ++i) d.diffuse[i] = p.num.count(key) ? p.num[key][i] : 0.5f;
+        d.ensureEnergyConservation = num1(p, "ensureEnergyConservation", 1.0f) != 0.0f;
     } else {
         fail(c.file, b.line, "BSDF plugin \"" + type +
                                  "\" is outside the hair hot path (supported: marschner, kajiyakay, roughplastic, "
-                                 "marschnerdielectric)");
+                                 "marschnerdielectric, thindielectric, diffuse)");
     }
 }
 
@@ -474,7 +491,8 @@ void parseObject(Ctx &c, const XNode &nd, SceneDesc &d) {
     } else if (tag == "bsdf") {
         std::string id = attrS(c, nd, "id", false);
         if (!id.empty()) c.ids[id] = &nd;
-        else parseBSDF(c, nd, d);
+        BsdfDesc unused; /* instantiated (and validated) even when no shape refers to it */
+        parseBSDF(c, nd, unused);
     } else if (tag == "shape") {
         std::string type = attrS(c, nd, "type");
         if (type != "hair")
@@ -482,32 +500,53 @@ void parseObject(Ctx &c, const XNode &nd, SceneDesc &d) {
         Props p;
         collectProps(c, nd, p);
         if (!p.str.count("filename")) fail(c.file, nd.line, "hair shape needs a filename");
-        d.hairFile = p.str["filename"];
-        d.radius = num1(p, "radius", 0.025f);
-        d.angleThreshold = num1(p, "angleThreshold", 1.0f);
-        d.reduction = num1(p, "reduction", 0.0f);
-        d.kd.queryCost = num1(p, "kdIntersectionCost", d.kd.queryCost);
-        d.kd.traversalCost = num1(p, "kdTraversalCost", d.kd.traversalCost);
-        d.kd.emptySpaceBonus = num1(p, "kdEmptySpaceBonus", d.kd.emptySpaceBonus);
-        d.kd.stopPrims = (int) num1(p, "kdStopPrims", (float) d.kd.stopPrims);
-        d.kd.maxDepth = (int) num1(p, "kdMaxDepth", (float) d.kd.maxDepth);
-        d.kd.maxBadRefines = (int) num1(p, "kdMaxBadRefines", (float) d.kd.maxBadRefines);
-        d.kd.clip = num1(p, "kdClip", d.kd.clip ? 1.0f : 0.0f) != 0.0f;
-        if (p.xform.count("toWorld")) {
-            parseTransform(c, *p.xform["toWorld"], d.hairToWorld);
-            d.hairHasToWorld = true;
+        HairShapeDesc h;
+        h.file = p.str["filename"];
+        if (!h.file.empty() && h.file[0] != '/') h.file = d.sceneDir + "/" + h.file;
+        h.radius = num1(p, "radius", 0.025f);
+        h.angleThreshold = num1(p, "angleThreshold", 1.0f);
+        h.reduction = num1(p, "reduction", 0.0f);
+        if (d.shapes.empty()) { /* one kd-tree over every hair shape: the first shape's build parameters */
+            d.kd.queryCost = num1(p, "kdIntersectionCost", d.kd.queryCost);
+            d.kd.traversalCost = num1(p, "kdTraversalCost", d.kd.traversalCost);
+            d.kd.emptySpaceBonus = num1(p, "kdEmptySpaceBonus", d.kd.emptySpaceBonus);
+            d.kd.stopPrims = (int) num1(p, "kdStopPrims", (float) d.kd.stopPrims);
+            d.kd.maxDepth = (int) num1(p, "kdMaxDepth", (float) d.kd.maxDepth);
+            d.kd.maxBadRefines = (int) num1(p, "kdMaxBadRefines", (float) d.kd.maxBadRefines);
+            d.kd.clip = num1(p, "kdClip", d.kd.clip ? 1.0f : 0.0f) != 0.0f;
         }
+        if (p.xform.count("toWorld")) {
+            parseTransform(c, *p.xform["toWorld"], h.toWorld);
+            h.hasToWorld = true;
+        }
+        const XNode *bn = nullptr;
         for (auto &kp : nd.kids) {
             const XNode &k = *kp;
             if (k.tag == "ref") {
                 std::string id = attrS(c, k, "id");
                 auto it = c.ids.find(id);
                 if (it == c.ids.end()) fail(c.file, k.line, "unknown reference \"" + id + "\"");
-                parseBSDF(c, *it->second, d);
+                bn = it->second;
             } else if (k.tag == "bsdf") {
-                parseBSDF(c, k, d);
+                bn = &k;
             }
         }
+        if (bn) {
+            auto it = c.bsdfIndex.find(bn);
+            if (it == c.bsdfIndex.end()) {
+                BsdfDesc b;
+                parseBSDF(c, *bn, b);
+                d.bsdfs.push_back(b);
+                it = c.bsdfIndex.emplace(bn, (int) d.bsdfs.size() - 1).first;
+            }
+            h.bsdf = it->second;
+        } else {
+            /* Shape::configure (shape.cpp:48-64): a 0.5 Lambertian BRDF */
+            d.bsdfs.push_back(BsdfDesc());
+            h.bsdf = (int) d.bsdfs.size() - 1;
+        }
+        if (d.shapes.size() >= HPT_MAX_SHAPES) fail(c.file, nd.line, "too many hair shapes");
+        d.shapes.push_back(h);
     } else if (tag == "emitter") {
         std::string type = attrS(c, nd, "type");
         Props p;
@@ -580,9 +619,7 @@ SceneDesc parseSceneXML(const std::string &path, const std::map<std::string, std
     size_t slash = path.find_last_of('/');
     d.sceneDir = slash == std::string::npos ? "." : path.substr(0, slash);
     for (auto &kp : root->kids) parseObject(c, *kp, d);
-    if (d.hairFile.empty()) fail(path, root->line, "scene has no hair shape");
-    if (d.bsdf.empty()) fail(path, root->line, "hair shape has no BSDF");
-    if (!d.hairFile.empty() && d.hairFile[0] != '/') d.hairFile = d.sceneDir + "/" + d.hairFile;
+    if (d.shapes.empty()) fail(path, root->line, "scene has no hair shape");
     if (!d.envFile.empty() && d.envFile[0] != '/') d.envFile = d.sceneDir + "/" + d.envFile;
     if (d.emitter.empty()) {
         /* scene.cpp:358-372: no emitter -> default sun & sky */

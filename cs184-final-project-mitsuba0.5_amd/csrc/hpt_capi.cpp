@@ -42,17 +42,13 @@ struct hpt_context {
     std::string dataDir;
     SceneDesc desc;
     bool haveCamera = false, haveHair = false, haveBSDF = false, haveEnv = false, prepared = false;
-    bool hairFromFile = false;
-    std::string hairPath;
-    float hairRadius = 0.025f, hairAngle = 1.0f;
-    float hairToWorld[16];
-    bool hairHasToWorld = false;
-    HairData hair;
+    bool hairFromFile = false;     /* desc.shapes are loaded from files at prepare */
+    HairData hair;                 /* every hair shape, merged */
     KDTreeHost tree;
-    MarschnerHost mar;
-    HptKajiyaKay kk;
-    RoughPlasticHost rp;
-    HptMarschnerDielectric md;
+    /* per BSDF of desc.bsdfs: host tables and the device record */
+    std::vector<MarschnerHost> mar;
+    std::vector<RoughPlasticHost> rp;
+    std::vector<HptBsdf> bsdfRec;
     EnvHost env;
     bool envFromSunsky = false;
     SunSkyTables sunsky;
@@ -74,9 +70,22 @@ struct hpt_context {
 };
 
 namespace {
-/* HptScene::bsdfKind / hpt_scene_info::bsdf numbering */
+/* HptBsdf::kind / hpt_scene_info::bsdf numbering */
 int bsdfKindOf(const std::string &b) {
-    return b == "marschner" ? 0 : b == "kajiyakay" ? 1 : b == "roughplastic" ? 2 : 3;
+    if (b == "marschner") return HPT_BSDF_MARSCHNER;
+    if (b == "kajiyakay") return HPT_BSDF_KAJIYAKAY;
+    if (b == "roughplastic") return HPT_BSDF_ROUGHPLASTIC;
+    if (b == "marschnerdielectric") return HPT_BSDF_MARSCHNERDIELECTRIC;
+    if (b == "thindielectric") return HPT_BSDF_THINDIELECTRIC;
+    if (b == "diffuse") return HPT_BSDF_DIFFUSE;
+    return -1;
+}
+/* the low-level setters describe a single BSDF used by every shape */
+BsdfDesc &singleBsdf(SceneDesc &d, const char *type) {
+    d.bsdfs.assign(1, BsdfDesc());
+    for (auto &h : d.shapes) h.bsdf = 0;
+    d.bsdfs[0].type = type;
+    return d.bsdfs[0];
 }
 
 int setErr(hpt_context *c, int code, const std::string &m) {
@@ -192,7 +201,6 @@ int hpt_context_create(int device, hpt_context **out) {
         c->dataDir = defaultDataDir();
         std::memset(&c->sc, 0, sizeof(c->sc));
         std::memset(&c->stats, 0, sizeof(c->stats));
-        for (int i = 0; i < 16; ++i) c->hairToWorld[i] = (i % 5 == 0) ? 1.0f : 0.0f;
         *out = c;
         return HPT_OK;
     }
@@ -212,7 +220,6 @@ int hpt_context_create(int device, hpt_context **out) {
     c->dataDir = defaultDataDir();
     std::memset(&c->sc, 0, sizeof(c->sc));
     std::memset(&c->stats, 0, sizeof(c->stats));
-    for (int i = 0; i < 16; ++i) c->hairToWorld[i] = (i % 5 == 0) ? 1.0f : 0.0f;
     *out = c;
     return HPT_OK;
 }
@@ -254,11 +261,6 @@ int hpt_load_scene_xml(hpt_context *c, const char *path, int n_defines, const ch
     const SceneDesc &d = c->desc;
     c->haveCamera = true;
     c->hairFromFile = true;
-    c->hairPath = d.hairFile;
-    c->hairRadius = d.radius;
-    c->hairAngle = d.angleThreshold;
-    c->hairHasToWorld = d.hairHasToWorld;
-    std::memcpy(c->hairToWorld, d.hairToWorld, sizeof(c->hairToWorld));
     c->haveHair = true;
     c->haveBSDF = true;
     c->haveEnv = true;
@@ -310,11 +312,13 @@ int hpt_set_integrator(hpt_context *c, int max_depth, int rr_depth, int strict_n
 int hpt_set_hair_file(hpt_context *c, const char *path, float radius, float angle, const float *to_world) {
     if (!c || !path) return HPT_EINVAL;
     c->hairFromFile = true;
-    c->hairPath = path;
-    c->hairRadius = radius;
-    c->hairAngle = angle;
-    c->hairHasToWorld = to_world != nullptr;
-    if (to_world) std::memcpy(c->hairToWorld, to_world, sizeof(c->hairToWorld));
+    HairShapeDesc h;
+    h.file = path;
+    h.radius = radius;
+    h.angleThreshold = angle;
+    h.hasToWorld = to_world != nullptr;
+    if (to_world) std::memcpy(h.toWorld, to_world, sizeof(h.toWorld));
+    c->desc.shapes.assign(1, h);
     c->haveHair = true;
     c->prepared = false;
     return HPT_OK;
@@ -329,6 +333,11 @@ int hpt_set_hair_vertices(hpt_context *c, const float *xyz, const uint8_t *start
     c->hair.starts.push_back(1);
     if (n) c->hair.starts[0] = 1;
     c->hair.radius = radius;
+    c->hair.shapeRadius = {radius};
+    c->hair.shapeFirst = {0};
+    HairShapeDesc h;
+    h.radius = radius;
+    c->desc.shapes.assign(1, h);
     c->haveHair = true;
     c->prepared = false;
     return HPT_OK;
@@ -338,14 +347,14 @@ int hpt_set_bsdf_marschner(hpt_context *c, float int_ior, float ext_ior, int dis
                            const float diffuse[3], const float specular[3]) {
     if (!c || distribution < 0 || distribution > 2 || !diffuse) return setErr(c, HPT_EINVAL, "bad marschner params");
     static const char *names[3] = {"beckmann", "ggx", "phong"};
-    c->desc.bsdf = "marschner";
-    c->desc.intIOR = int_ior;
-    c->desc.extIOR = ext_ior;
-    c->desc.distribution = names[distribution];
-    c->desc.alpha = alpha;
+    BsdfDesc &b = singleBsdf(c->desc, "marschner");
+    b.intIOR = int_ior;
+    b.extIOR = ext_ior;
+    b.distribution = names[distribution];
+    b.alpha = alpha;
     for (int i = 0; i < 3; ++i) {
-        c->desc.diffuse[i] = diffuse[i];
-        c->desc.specular[i] = specular ? specular[i] : 0.5f;
+        b.diffuse[i] = diffuse[i];
+        b.specular[i] = specular ? specular[i] : 0.5f;
     }
     c->haveBSDF = true;
     c->prepared = false;
@@ -358,17 +367,16 @@ int hpt_set_bsdf_roughplastic(hpt_context *c, float int_ior, float ext_ior, int 
     if (int_ior < 0 || ext_ior < 0 || int_ior == ext_ior)
         return setErr(c, HPT_EINVAL, "The interior and exterior indices of refraction must be positive and differ!");
     static const char *names[3] = {"beckmann", "ggx", "phong"};
-    c->desc.bsdf = "roughplastic";
-    c->desc.intIOR = int_ior;
-    c->desc.extIOR = ext_ior;
-    c->desc.distribution = names[distribution];
-    c->desc.alpha = alpha;
-    c->desc.sampleVisible = sample_visible != 0;
-    c->desc.nonlinear = nonlinear != 0;
-    c->desc.ensureEnergyConservation = true;
+    BsdfDesc &b = singleBsdf(c->desc, "roughplastic");
+    b.intIOR = int_ior;
+    b.extIOR = ext_ior;
+    b.distribution = names[distribution];
+    b.alpha = alpha;
+    b.sampleVisible = sample_visible != 0;
+    b.nonlinear = nonlinear != 0;
     for (int i = 0; i < 3; ++i) {
-        c->desc.diffuse[i] = diffuse ? diffuse[i] : 0.5f;
-        c->desc.specular[i] = specular ? specular[i] : 1.0f;
+        b.diffuse[i] = diffuse ? diffuse[i] : 0.5f;
+        b.specular[i] = specular ? specular[i] : 1.0f;
     }
     c->haveBSDF = true;
     c->prepared = false;
@@ -380,14 +388,13 @@ int hpt_set_bsdf_marschnerdielectric(hpt_context *c, float int_ior, float ext_io
     if (!c) return HPT_EINVAL;
     if (int_ior < 0 || ext_ior < 0)
         return setErr(c, HPT_EINVAL, "The interior and exterior indices of refraction must be positive!");
-    c->desc.bsdf = "marschnerdielectric";
-    c->desc.intIOR = int_ior;
-    c->desc.extIOR = ext_ior;
-    c->desc.ensureEnergyConservation = true;
+    BsdfDesc &b = singleBsdf(c->desc, "marschnerdielectric");
+    b.intIOR = int_ior;
+    b.extIOR = ext_ior;
     for (int i = 0; i < 3; ++i) {
-        c->desc.diffuse[i] = diffuse ? diffuse[i] : 0.5f;
-        c->desc.specular[i] = specular_reflectance ? specular_reflectance[i] : 0.1f;
-        c->desc.transmittance[i] = specular_transmittance ? specular_transmittance[i] : 0.1f;
+        b.diffuse[i] = diffuse ? diffuse[i] : 0.5f;
+        b.specular[i] = specular_reflectance ? specular_reflectance[i] : 0.1f;
+        b.transmittance[i] = specular_transmittance ? specular_transmittance[i] : 0.1f;
     }
     c->haveBSDF = true;
     c->prepared = false;
@@ -396,12 +403,12 @@ int hpt_set_bsdf_marschnerdielectric(hpt_context *c, float int_ior, float ext_io
 
 int hpt_set_bsdf_kajiyakay(hpt_context *c, const float kd[3], const float ks[3], float exponent) {
     if (!c || !kd) return HPT_EINVAL;
-    c->desc.bsdf = "kajiyakay";
+    BsdfDesc &b = singleBsdf(c->desc, "kajiyakay");
     for (int i = 0; i < 3; ++i) {
-        c->desc.diffuse[i] = kd[i];
-        c->desc.specular[i] = ks ? ks[i] : 0.2f;
+        b.diffuse[i] = kd[i];
+        b.specular[i] = ks ? ks[i] : 0.2f;
     }
-    c->desc.exponent = exponent;
+    b.exponent = exponent;
     c->haveBSDF = true;
     c->prepared = false;
     return HPT_OK;
@@ -458,22 +465,48 @@ int hpt_prepare(hpt_context *c) {
                 !readFile(dir + "vdc.u64", c->vdc) || !readFile(dir + "vdc_inv.u64", c->vdcInv))
                 return setErr(c, HPT_EIO, "cannot read Sobol tables from " + dir);
         }
-        if (c->hairFromFile)
-            c->hair = loadHair(c->hairPath, c->hairRadius, c->hairAngle, 0.0f, c->hairHasToWorld ? c->hairToWorld : nullptr);
-        c->tree = buildHairKDTree(c->hair, d.kd);
-        if (d.bsdf == "marschner") {
-            std::string err;
-            if (!precomputeMarschner(d, c->dataDir, c->mar, err)) return setErr(c, HPT_EIO, err);
-        } else if (d.bsdf == "kajiyakay") {
-            configureKajiyaKay(d, c->kk);
-        } else if (d.bsdf == "marschnerdielectric") {
-            configureMarschnerDielectric(d, c->md);
-        } else if (d.bsdf == "roughplastic") {
-            std::string err;
-            if (!configureRoughPlastic(d, c->dataDir, c->rp, err)) return setErr(c, HPT_EINVAL, err);
-        } else {
-            return setErr(c, HPT_EINVAL, "unsupported bsdf " + d.bsdf);
+        if (c->hairFromFile) {
+            c->hair = HairData();
+            c->hair.shapeRadius.clear();
+            for (const HairShapeDesc &h : d.shapes)
+                appendHair(c->hair, loadHair(h.file, h.radius, h.angleThreshold, h.reduction,
+                                             h.hasToWorld ? h.toWorld : nullptr));
         }
+        c->tree = buildHairKDTree(c->hair, d.kd);
+        const size_t nb = d.bsdfs.size();
+        c->mar.assign(nb, MarschnerHost());
+        c->rp.assign(nb, RoughPlasticHost());
+        c->bsdfRec.assign(nb, HptBsdf());
+        for (size_t i = 0; i < nb; ++i) {
+            const BsdfDesc &b = d.bsdfs[i];
+            HptBsdf &rec = c->bsdfRec[i];
+            std::memset(&rec, 0, sizeof(rec));
+            rec.kind = bsdfKindOf(b.type);
+            rec.smooth = 1;
+            std::string err;
+            switch (rec.kind) {
+            case HPT_BSDF_MARSCHNER:
+                if (!precomputeMarschner(b, c->dataDir, c->mar[i], err)) return setErr(c, HPT_EIO, err);
+                break;
+            case HPT_BSDF_KAJIYAKAY: configureKajiyaKay(b, rec.kk); break;
+            case HPT_BSDF_ROUGHPLASTIC:
+                if (!configureRoughPlastic(b, c->dataDir, c->rp[i], err)) return setErr(c, HPT_EINVAL, err);
+                rec.rp = c->rp[i].p;
+                break;
+            case HPT_BSDF_MARSCHNERDIELECTRIC: configureMarschnerDielectric(b, rec.md); break;
+            case HPT_BSDF_THINDIELECTRIC:
+                configureThinDielectric(b, rec.md);
+                rec.smooth = 0; /* EDeltaReflection | ENull only */
+                break;
+            case HPT_BSDF_DIFFUSE:
+                configureDiffuse(b, rec.df);
+                /* no component at all when the reflectance is 0 (diffuse.cpp:81-84) */
+                rec.smooth = std::max(std::max(rec.df.refl[0], rec.df.refl[1]), rec.df.refl[2]) > 0 ? 1 : 0;
+                break;
+            default: return setErr(c, HPT_EINVAL, "unsupported bsdf " + b.type);
+            }
+        }
+        if (d.shapes.empty() || nb == 0) return setErr(c, HPT_ESTATE, "no hair shape / bsdf");
         if (c->envFromSunsky) {
             if (c->sunsky.hosek.empty()) {
                 std::string err;
@@ -499,31 +532,45 @@ int hpt_prepare(hpt_context *c) {
         sc.aabbMin[i] = c->tree.aabbMin[i];
         sc.aabbMax[i] = c->tree.aabbMax[i];
     }
-    sc.radius = c->hair.radius;
-    sc.bsdfKind = bsdfKindOf(d.bsdf);
-    if (sc.bsdfKind == 0) {
-        for (int l = 0; l < 3; ++l) {
-            r |= upload(c, c->mar.table[l].data(), c->mar.table[l].size() * 16, (const void **) &sc.mar.table[l]);
-            r |= upload(c, c->mar.cdf[l].data(), c->mar.cdf[l].size() * 4, (const void **) &sc.mar.cdf[l]);
-            r |= upload(c, c->mar.sums[l].data(), c->mar.sums[l].size() * 4, (const void **) &sc.mar.sums[l]);
+    /* BSDF records: device tables first, then the records themselves */
+    for (size_t i = 0; i < c->bsdfRec.size(); ++i) {
+        HptBsdf &rec = c->bsdfRec[i];
+        if (rec.kind == HPT_BSDF_MARSCHNER) {
+            const MarschnerHost &m = c->mar[i];
+            for (int l = 0; l < 3; ++l) {
+                r |= upload(c, m.table[l].data(), m.table[l].size() * 16, (const void **) &rec.mar.table[l]);
+                r |= upload(c, m.cdf[l].data(), m.cdf[l].size() * 4, (const void **) &rec.mar.cdf[l]);
+                r |= upload(c, m.sums[l].data(), m.sums[l].size() * 4, (const void **) &rec.mar.sums[l]);
+            }
+            r |= upload(c, m.trans.data(), m.trans.size() * 4, (const void **) &rec.mar.trans);
+            rec.mar.transSize = (int) m.trans.size();
+            rec.mar.fdr = m.fdr;
+            rec.mar.invEta2 = m.invEta2;
+            rec.mar.specularSamplingWeight = m.specularSamplingWeight;
+            rec.mar.vR = m.vR;
+            rec.mar.vTT = m.vTT;
+            rec.mar.vTRT = m.vTRT;
+            rec.mar.scaleAngleRad = m.scaleAngleRad;
+            for (int k = 0; k < 3; ++k) rec.mar.diffuse[k] = m.diffuse[k];
+        } else if (rec.kind == HPT_BSDF_ROUGHPLASTIC) {
+            r |= upload(c, c->rp[i].trans.data(), c->rp[i].trans.size() * 4, (const void **) &rec.rp.trans);
         }
-        r |= upload(c, c->mar.trans.data(), c->mar.trans.size() * 4, (const void **) &sc.mar.trans);
-        sc.mar.transSize = (int) c->mar.trans.size();
-        sc.mar.fdr = c->mar.fdr;
-        sc.mar.invEta2 = c->mar.invEta2;
-        sc.mar.specularSamplingWeight = c->mar.specularSamplingWeight;
-        sc.mar.vR = c->mar.vR;
-        sc.mar.vTT = c->mar.vTT;
-        sc.mar.vTRT = c->mar.vTRT;
-        sc.mar.scaleAngleRad = c->mar.scaleAngleRad;
-        for (int i = 0; i < 3; ++i) sc.mar.diffuse[i] = c->mar.diffuse[i];
-    } else if (sc.bsdfKind == 3) {
-        sc.md = c->md;
-    } else if (sc.bsdfKind == 2) {
-        sc.rp = c->rp.p;
-        r |= upload(c, c->rp.trans.data(), c->rp.trans.size() * 4, (const void **) &sc.rp.trans);
-    } else {
-        sc.kk = c->kk;
+    }
+    const size_t nShapes = std::max<size_t>(1, c->hair.shapeRadius.size());
+    if (nShapes > HPT_MAX_SHAPES) return setErr(c, HPT_EINVAL, "too many hair shapes");
+    std::vector<HptShape> shapes(nShapes);
+    for (size_t k = 0; k < nShapes; ++k) {
+        shapes[k].radius = c->hair.shapeRadius.empty() ? c->hair.radius : c->hair.shapeRadius[k];
+        shapes[k].bsdf = k < d.shapes.size() ? d.shapes[k].bsdf : 0;
+    }
+    sc.nShapes = (int) nShapes;
+    sc.radius = shapes[0].radius;
+    sc.maxRadius = 0.0f;
+    for (const HptShape &h : shapes) sc.maxRadius = std::max(sc.maxRadius, h.radius);
+    sc.bsdf = c->bsdfRec[shapes[0].bsdf];
+    if (nShapes > 1) {
+        r |= upload(c, shapes.data(), shapes.size() * sizeof(HptShape), (const void **) &sc.shapes);
+        r |= upload(c, c->bsdfRec.data(), c->bsdfRec.size() * sizeof(HptBsdf), (const void **) &sc.bsdfs);
     }
     /* environment (envmap.cpp) + scene bounding sphere (scene.cpp:386-412, envmap.cpp:336-347) */
     HptEnvMap &E = sc.env;
@@ -608,7 +655,8 @@ int hpt_get_scene_info(hpt_context *c, hpt_scene_info *o) {
     o->rr_depth = d.rrDepth;
     o->strict_normals = d.strictNormals;
     o->hide_emitters = d.hideEmitters;
-    o->bsdf = bsdfKindOf(d.bsdf);
+    o->bsdf = d.bsdfs.empty() ? -1 : bsdfKindOf(d.bsdfs[d.shapes.empty() ? 0 : d.shapes[0].bsdf].type);
+    o->n_shapes = (int) std::max<size_t>(1, c->hair.shapeRadius.size());
     o->vertices = c->hair.vertexCount();
     o->segments = c->tree.segs.size();
     o->kd_nodes = c->tree.nodes.size();
@@ -833,18 +881,20 @@ int hpt_get_envmap(hpt_context *c, float *rgb, int *w, int *h) {
 
 int hpt_get_marschner_tables(hpt_context *c, float *nR, float *nTT, float *nTRT, float *fdr, float *trans,
                              float *specw) {
-    if (!c || c->sc.bsdfKind != 0 || !c->prepared) return setErr(c, HPT_ESTATE, "no marschner bsdf prepared");
+    if (!c || !c->prepared || c->sc.bsdf.kind != HPT_BSDF_MARSCHNER)
+        return setErr(c, HPT_ESTATE, "no marschner bsdf prepared");
+    const MarschnerHost &m = c->mar[c->desc.shapes.empty() ? 0 : c->desc.shapes[0].bsdf];
     float *outs[3] = {nR, nTT, nTRT};
     for (int l = 0; l < 3; ++l)
         if (outs[l])
-            for (size_t i = 0; i < c->mar.table[l].size(); ++i) {
-                outs[l][3 * i] = c->mar.table[l][i].x;
-                outs[l][3 * i + 1] = c->mar.table[l][i].y;
-                outs[l][3 * i + 2] = c->mar.table[l][i].z;
+            for (size_t i = 0; i < m.table[l].size(); ++i) {
+                outs[l][3 * i] = m.table[l][i].x;
+                outs[l][3 * i + 1] = m.table[l][i].y;
+                outs[l][3 * i + 2] = m.table[l][i].z;
             }
-    if (fdr) *fdr = c->mar.fdr;
-    if (trans) std::memcpy(trans, c->mar.trans.data(), std::min<size_t>(100, c->mar.trans.size()) * 4);
-    if (specw) *specw = c->mar.specularSamplingWeight;
+    if (fdr) *fdr = m.fdr;
+    if (trans) std::memcpy(trans, m.trans.data(), std::min<size_t>(100, m.trans.size()) * 4);
+    if (specw) *specw = m.specularSamplingWeight;
     return HPT_OK;
 }
 

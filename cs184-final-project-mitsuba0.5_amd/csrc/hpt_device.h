@@ -38,7 +38,7 @@ struct HptSegment {
     double n2[3];
     double v2[3];
     uint32_t iv;   /* first vertex index (reference prim id, for parity) */
-    uint32_t pad;
+    uint32_t shape;/* hair shape the segment belongs to */
 };
 
 /* fp32 shadow of a segment for the conservative pre-test (32 bytes), stored
@@ -52,7 +52,7 @@ struct HptSegF {
     float v1[3];
     float axis[3];
     uint32_t seg;  /* segment index (into HptScene::segs) */
-    uint32_t pad;
+    float radius;  /* its shape's radius */
 };
 
 /* kd-tree node, 8 bytes (gkdtree.h:452-583 layout with absolute child index):
@@ -100,16 +100,23 @@ struct HptKajiyaKay {
     float exponent, specularSamplingWeight;
 };
 
-/* roughplastic (roughplastic.cpp:196-296): isotropic microfacet coating over
- * a diffuse base, constant textures */
 /* marschnerdielectric (marschnerdielectric.cpp:145-659): a thin dielectric
  * sheet -- delta reflection about the fiber, straight pass-through (ENull) and
- * a diffuse component whose solid-angle eval is identically zero there */
+ * a diffuse component whose solid-angle eval is identically zero there.
+ * thindielectric (thindielectric.cpp:70-252) is the same sampler without the
+ * diffuse choice (specularSamplingWeight = 1) and without NEE. */
 struct HptMarschnerDielectric {
     float eta, specularSamplingWeight;
     float specR[3], specT[3];
 };
 
+/* diffuse (diffuse.cpp:60-140) */
+struct HptDiffuse {
+    float refl[3];
+};
+
+/* roughplastic (roughplastic.cpp:196-296): isotropic microfacet coating over
+ * a diffuse base, constant textures */
 struct HptRoughPlastic {
     int type;                   /* 0 beckmann, 1 ggx, 2 phong (microfacet.h:48-58) */
     int sampleVisible, nonlinear;
@@ -119,6 +126,31 @@ struct HptRoughPlastic {
     const float *trans;         /* external rough transmittance 1D slice (eta, alpha) */
     int transSize;
     float fdr;                  /* 1 - internal (1/eta) diffuse transmittance at alpha */
+};
+
+/* One BSDF instance.  kind: 0 marschner, 1 kajiyakay, 2 roughplastic,
+ * 3 marschnerdielectric, 4 thindielectric, 5 diffuse.  smooth: the combined
+ * type has an ESmooth component, so path.cpp:175 samples the emitter (and
+ * consumes two sample dimensions) before the BSDF. */
+#define HPT_BSDF_MARSCHNER 0
+#define HPT_BSDF_KAJIYAKAY 1
+#define HPT_BSDF_ROUGHPLASTIC 2
+#define HPT_BSDF_MARSCHNERDIELECTRIC 3
+#define HPT_BSDF_THINDIELECTRIC 4
+#define HPT_BSDF_DIFFUSE 5
+#define HPT_MAX_SHAPES 64
+struct HptBsdf {
+    int kind, smooth;
+    HptMarschner mar;
+    HptKajiyaKay kk;
+    HptRoughPlastic rp;
+    HptMarschnerDielectric md;
+    HptDiffuse df;
+};
+
+struct HptShape {
+    float radius;
+    int bsdf;
 };
 
 struct HptEnvMap {
@@ -141,12 +173,15 @@ struct HptScene {
     const HptSegF *leafF;       /* leaf primitive list (fp32 pre-test records) */
     const HptSegment *segs;
     float aabbMin[3], aabbMax[3];
-    float radius;
-    int bsdfKind;               /* 0 marschner, 1 kajiyakay, 2 roughplastic, 3 marschnerdielectric */
-    HptMarschner mar;
-    HptKajiyaKay kk;
-    HptRoughPlastic rp;
-    HptMarschnerDielectric md;
+    float radius;               /* shape 0's radius (every shape's when nShapes == 1) */
+    float maxRadius;            /* largest shape radius: bound for the conservative fp32 pre-test */
+    HptBsdf bsdf;               /* shape 0's BSDF */
+    /* several hair shapes (hair-curl): HptSegment::shape indexes shapes[],
+       which gives the radius and the entry of bsdfs[] (both in HBM: a kernel
+       argument indexed per lane would be copied to scratch) */
+    int nShapes;
+    const HptShape *shapes;
+    const HptBsdf *bsdfs;
     HptEnvMap env;
     const uint32_t *sobol;      /* 1024 x 52 */
     const uint64_t *vdc;        /* rows x 52 */

@@ -203,6 +203,11 @@ HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, V3 of, V3 
    most 11u |w|_1 and r|n| by at most 12u r; the test keeps a 4x margin on
    both (3e-6 (r + |w|_1)) and never divides by |n|, so it holds for rays
    of any direction, near-parallel ones included. */
+/* radius of segment s's hair shape (uniform branch: one shape in every shipped scene but hair-curl) */
+HD float segRadius(const HptScene &sc, uint32_t s) {
+    return sc.nShapes > 1 ? sc.shapes[sc.segs[s].shape].radius : sc.radius;
+}
+
 HD bool segMayHit(const float4 a, const float4 b, V3 o, V3 d, float r) {
     const float wx = o.x - a.x, wy = o.y - a.y, wz = o.z - a.z;
     const float ax = a.w, ay = b.x, az = b.y; /* axis */
@@ -446,7 +451,6 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
        ones -- the prefetched records are dead by then, so the fp64 test's
        registers do not stack on top of them */
     const uint32_t first = leafFirst, last = leafLast;
-    const double r2 = (double) (sc.radius * sc.radius); /* Float product (hair.cpp:500) */
     for (uint32_t c0 = first; c0 < last; c0 += 32) {
         const uint32_t c1 = min(last, c0 + 32);
         uint32_t mask = 0;
@@ -469,7 +473,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
                         ++tc.prims;
                         if (waveLeader()) tc.primSlots += 64;
                     }
-                    if (segMayHit(fa[k], fb[k], o, d, sc.radius)) mask |= 1u << (e0 + (uint32_t) k - c0);
+                    if (segMayHit(fa[k], fb[k], o, d, sc.maxRadius)) mask |= 1u << (e0 + (uint32_t) k - c0);
                 }
             }
         }
@@ -485,13 +489,15 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
                 ++tc.prims;
                 if (waveLeader()) tc.primSlots += 64;
             }
-            if (segMayHit(fa, fb, o, d, sc.radius)) mask |= 1u << (e - c0);
+            if (segMayHit(fa, fb, o, d, sc.maxRadius)) mask |= 1u << (e - c0);
         }
 #endif
         while (mask) {
             const uint32_t e = c0 + (uint32_t) (__ffs(mask) - 1);
             mask &= mask - 1;
             const uint32_t s = __float_as_uint(leafF[2 * e + 1].z);
+            const float rad = segRadius(sc, s);
+            const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
             if (STATS) ++tc.exact;
             float t;
             V3 p;
@@ -512,7 +518,6 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
         na = leafF[2 * first];
         nb = leafF[2 * first + 1];
     }
-    const double r2 = (double) (sc.radius * sc.radius); /* Float product (hair.cpp:500) */
     for (uint32_t e = first; e < last; ++e) {
 #if HPT_LEAF_MODE == 1
         const float4 fa = leafF[2 * e], fb = leafF[2 * e + 1];
@@ -527,8 +532,10 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
             ++tc.prims;
             if (waveLeader()) tc.primSlots += 64;
         }
-        if (!segMayHit(fa, fb, o, d, sc.radius)) continue;
+        if (!segMayHit(fa, fb, o, d, sc.maxRadius)) continue;
         const uint32_t s = __float_as_uint(fb.z);
+        const float rad = segRadius(sc, s);
+        const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
         if (STATS) ++tc.exact;
         float t;
         V3 p;
@@ -568,7 +575,8 @@ HD V3 hitPoint(const HptScene &sc, const TraceRay &r) {
     if (!r.found) return v3(0.0f, 0.0f, 0.0f);
     float t;
     V3 p = v3(0.0f, 0.0f, 0.0f);
-    const double r2 = (double) (sc.radius * sc.radius);
+    const float radius = segRadius(sc, r.segHit);
+    const double r2 = (double) (radius * radius);
     segIntersect(sc.segs, r.segHit, r.o, r.d, r2, r.mint, finf(), t, p);
     return p;
 }
@@ -1226,24 +1234,71 @@ HD V3 mdSample(const HptMarschnerDielectric &m, V3 wi, float sx, float sy, V3 &w
     return v3(0, 0, 0); /* eval / pdf with eval == 0 (or pdf == 0) */
 }
 
-HD V3 bsdfEval(const HptScene &sc, V3 wi, V3 wo) {
-    if (sc.bsdfKind == 2) return rpEval(sc.rp, wi, wo);
-    if (sc.bsdfKind == 3) return mdEval(sc.md, wi, wo);
-    return sc.bsdfKind == 0 ? marschnerEval(sc.mar, wi, wo) : kkEval(sc.kk, wi, wo);
-}
-HD float bsdfPdf(const HptScene &sc, V3 wi, V3 wo) {
-    if (sc.bsdfKind == 2) return rpPdf(sc.rp, wi, wo);
-    if (sc.bsdfKind == 3) return mdPdf(sc.md, wi, wo);
-    return sc.bsdfKind == 0 ? 1.0f : kkPdf(sc.kk, wi, wo);
-}
-HD V3 bsdfSample(const HptScene &sc, V3 wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
-    if (sc.bsdfKind == 0) {
-        pdf = 1.0f;
-        return marschnerSample(sc.mar, wi, sx, sy, wo, type);
+/* thindielectric (thindielectric.cpp:138-252): no ESmooth component, so the
+   integrator never evaluates it in solid angle (eval/pdf are 0 there) */
+HD V3 tdSample(const HptMarschnerDielectric &m, V3 wi, float sx, V3 &wo, float &pdf, uint32_t &type) {
+    float R = fresnelDielectricExt(fabsf(wi.z), m.eta), T = 1 - R;
+    if (R < 1) R += T * T * R / (1 - R * R);
+    if (sx <= R) {
+        type = HPT_EDELTA_REFLECTION;
+        wo = v3(-wi.x, -wi.y, wi.z);
+        pdf = R;
+        return v3(m.specR[0], m.specR[1], m.specR[2]);
     }
-    if (sc.bsdfKind == 2) return rpSample(sc.rp, wi, sx, sy, wo, pdf, type);
-    if (sc.bsdfKind == 3) return mdSample(sc.md, wi, sx, sy, wo, pdf, type);
-    return kkSample(sc.kk, wi, sx, sy, wo, pdf, type);
+    type = HPT_ENULL;
+    wo = v3(-wi.x, -wi.y, -wi.z);
+    pdf = 1 - R;
+    return v3(m.specT[0], m.specT[1], m.specT[2]);
+}
+
+/* diffuse (diffuse.cpp:111-140) */
+HD V3 dfEval(const HptDiffuse &m, V3 wi, V3 wo) {
+    if (wi.z <= 0 || wo.z <= 0) return v3(0, 0, 0);
+    return v3(m.refl[0], m.refl[1], m.refl[2]) * (kInvPi * wo.z);
+}
+HD float dfPdf(V3 wi, V3 wo) {
+    if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+    return kInvPi * wo.z;
+}
+HD V3 dfSample(const HptDiffuse &m, V3 wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
+    pdf = 0.0f;
+    type = 0;
+    wo = v3(0, 0, 0);
+    if (wi.z <= 0) return v3(0, 0, 0);
+    wo = squareToCosineHemisphere(sx, sy);
+    type = HPT_EDIFFUSE_REFLECTION;
+    pdf = kInvPi * wo.z;
+    return v3(m.refl[0], m.refl[1], m.refl[2]);
+}
+
+HD V3 bsdfEval(const HptBsdf &b, V3 wi, V3 wo) {
+    switch (b.kind) {
+    case HPT_BSDF_MARSCHNER: return marschnerEval(b.mar, wi, wo);
+    case HPT_BSDF_KAJIYAKAY: return kkEval(b.kk, wi, wo);
+    case HPT_BSDF_ROUGHPLASTIC: return rpEval(b.rp, wi, wo);
+    case HPT_BSDF_DIFFUSE: return dfEval(b.df, wi, wo);
+    default: return v3(0, 0, 0); /* marschnerdielectric (:232-240), thindielectric */
+    }
+}
+HD float bsdfPdf(const HptBsdf &b, V3 wi, V3 wo) {
+    switch (b.kind) {
+    case HPT_BSDF_MARSCHNER: return 1.0f;
+    case HPT_BSDF_KAJIYAKAY: return kkPdf(b.kk, wi, wo);
+    case HPT_BSDF_ROUGHPLASTIC: return rpPdf(b.rp, wi, wo);
+    case HPT_BSDF_MARSCHNERDIELECTRIC: return mdPdf(b.md, wi, wo);
+    case HPT_BSDF_DIFFUSE: return dfPdf(wi, wo);
+    default: return 0.0f;
+    }
+}
+HD V3 bsdfSample(const HptBsdf &b, V3 wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
+    switch (b.kind) {
+    case HPT_BSDF_MARSCHNER: pdf = 1.0f; return marschnerSample(b.mar, wi, sx, sy, wo, type);
+    case HPT_BSDF_KAJIYAKAY: return kkSample(b.kk, wi, sx, sy, wo, pdf, type);
+    case HPT_BSDF_ROUGHPLASTIC: return rpSample(b.rp, wi, sx, sy, wo, pdf, type);
+    case HPT_BSDF_MARSCHNERDIELECTRIC: return mdSample(b.md, wi, sx, sy, wo, pdf, type);
+    case HPT_BSDF_THINDIELECTRIC: return tdSample(b.md, wi, sx, wo, pdf, type);
+    default: return dfSample(b.df, wi, sx, sy, wo, pdf, type);
+    }
 }
 
 /* ------------------------------------------------------------------ */
@@ -1534,7 +1589,8 @@ HD void fillIts(const HptScene &sc, uint32_t seg, V3 hp, V3 rayD, V3 &p, Frame &
     geo.n = normalize(rel - axis * dot(axis, rel));
     geo.t = cross(geo.n, geo.s);
     V3 local = geo.toLocal(rel);
-    p = hp + geo.n * (sc.radius - sqrtf(local.y * local.y + local.z * local.z));
+    const float radius = segRadius(sc, seg);
+    p = hp + geo.n * (radius - sqrtf(local.y * local.y + local.z * local.z));
     sh.n = geo.n;
     sh.s = normalize(geo.s - sh.n * dot(sh.n, geo.s));
     sh.t = cross(sh.n, sh.s);
@@ -1566,12 +1622,14 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
     qpushBlock<HPT_QBLOCK>(alive, id, shadeQ, &counters[HPT_Q_SHADE_OUT]);
 }
 
-/* one bounce of shading: path.cpp:145-232 up to the continuation ray cast */
-extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade(HptScene sc, HptPaths P,
-                                                           const uint32_t *__restrict__ shadeQ,
-                                                           uint32_t *__restrict__ traceQ,
-                                                           uint32_t *__restrict__ shadowQ,
-                                                           uint32_t *__restrict__ counters) {
+/* one bounce of shading: path.cpp:145-232 up to the continuation ray cast.
+   MULTI: several hair shapes, the hit shape's BSDF comes from sc.bsdfs (a
+   separate kernel, so the single-shape one never mixes a kernel-argument
+   pointer with a global one -- that would copy the scene to scratch) */
+template <bool MULTI>
+__device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
+                                            uint32_t *__restrict__ traceQ, uint32_t *__restrict__ shadowQ,
+                                            uint32_t *__restrict__ counters) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = counters[HPT_Q_SHADE_IN];
     bool cont = false, shadow = false;
@@ -1584,7 +1642,8 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade(HptScene sc, Hp
         V3 rayD = v3(rd.x, rd.y, rd.z);
         V3 p, wi;
         Frame geo, sh;
-        fillIts(sc, (uint32_t) __float_as_int(h.x), v3(hp.x, hp.y, hp.z), rayD, p, geo, sh, wi);
+        const uint32_t seg = (uint32_t) __float_as_int(h.x);
+        fillIts(sc, seg, v3(hp.x, hp.y, hp.z), rayD, p, geo, sh, wi);
         bool stop = ((int) depth >= sc.maxDepth && sc.maxDepth > 0) ||
                     (sc.strictNormals && dot(rayD, geo.n) * wi.z >= 0);
         if (!stop && dim + 3 >= HPT_SOBOL_DIMS) {
@@ -1592,14 +1651,17 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade(HptScene sc, Hp
             atomicOr(&counters[HPT_Q_ERROR], 1u);
             stop = true;
         }
-        if (!stop) {
+        /* one inlined copy per BSDF source: the scene's own (kernel
+           argument, scalar loads) or, with several hair shapes, the hit
+           shape's entry of sc.bsdfs */
+        auto shadeWith = [&](const HptBsdf &B) {
             const uint64_t sidx = P.sobol[id];
             float4 thr = P.thr[id];
             V3 T = v3(thr.x, thr.y, thr.z);
-            /* ---- direct illumination (scene.cpp:828-852, envmap.cpp:516-543) ---- */
-            float nx = sobolSampleUniform(sc, sidx, dim), ny = sobolSampleUniform(sc, sidx, dim + 1);
-            dim += 2;
-            {
+            /* ---- direct illumination (path.cpp:175, scene.cpp:828-852, envmap.cpp:516-543) ---- */
+            if (B.smooth) {
+                float nx = sobolSampleUniform(sc, sidx, dim), ny = sobolSampleUniform(sc, sidx, dim + 1);
+                dim += 2;
                 V3 dl, value;
                 float pdf;
                 envSampleDir(sc.env, nx, ny, dl, value, pdf);
@@ -1609,9 +1671,9 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade(HptScene sc, Hp
                       farT <= 0)) {
                     V3 val = divs(value, pdf);
                     V3 wo = sh.toLocal(dW);
-                    V3 bsdfVal = bsdfEval(sc, wi, wo);
+                    V3 bsdfVal = bsdfEval(B, wi, wo);
                     if (!isZero(bsdfVal) && (!sc.strictNormals || dot(geo.n, dW) * wo.z > 0)) {
-                        float bp = bsdfPdf(sc, wi, wo);
+                        float bp = bsdfPdf(B, wi, wo);
                         float weight = miWeight(pdf, bp);
                         V3 c = mul(mul(T, val), bsdfVal) * weight;
                         P.sdir[id] = make_float4(dW.x, dW.y, dW.z, farT * (1 - kShadowEpsilon));
@@ -1626,7 +1688,7 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade(HptScene sc, Hp
             V3 woL;
             float bpdf = 0.0f;
             uint32_t type = 0;
-            V3 w = bsdfSample(sc, wi, bx, by, woL, bpdf, type);
+            V3 w = bsdfSample(B, wi, bx, by, woL, bpdf, type);
             if (!isZero(w)) {
                 V3 wo = sh.toWorld(woL);
                 float woDotGeoN = dot(geo.n, wo);
@@ -1640,11 +1702,29 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade(HptScene sc, Hp
                 }
             }
             if (shadow && !cont) P.ro[id] = make_float4(p.x, p.y, p.z, kEpsilon);
+        };
+        if (!stop) {
+            if (MULTI) shadeWith(sc.bsdfs[sc.shapes[sc.segs[seg].shape].bsdf]);
+            else shadeWith(sc.bsdf);
         }
         P.state[id] = (st & 0xffff0000u) | dim;
     }
     qpushBlock<HPT_QBLOCK>(cont, id, traceQ, &counters[HPT_Q_TRACE]);
     qpushBlock<HPT_QBLOCK>(shadow, id, shadowQ, &counters[HPT_Q_SHADOW]);
+}
+extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade(HptScene sc, HptPaths P,
+                                                           const uint32_t *__restrict__ shadeQ,
+                                                           uint32_t *__restrict__ traceQ,
+                                                           uint32_t *__restrict__ shadowQ,
+                                                           uint32_t *__restrict__ counters) {
+    shadeBounce<false>(sc, P, shadeQ, traceQ, shadowQ, counters);
+}
+extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade_multi(HptScene sc, HptPaths P,
+                                                                 const uint32_t *__restrict__ shadeQ,
+                                                                 uint32_t *__restrict__ traceQ,
+                                                                 uint32_t *__restrict__ shadowQ,
+                                                                 uint32_t *__restrict__ counters) {
+    shadeBounce<true>(sc, P, shadeQ, traceQ, shadowQ, counters);
 }
 
 /* continuation result: path.cpp:225-286 */
@@ -1864,15 +1944,15 @@ extern "C" __global__ void k_bsdf_batch(HptScene sc, int n, const float *wi, con
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     V3 a = v3(wi[3 * i], wi[3 * i + 1], wi[3 * i + 2]), b = v3(wo[3 * i], wo[3 * i + 1], wo[3 * i + 2]);
-    V3 e = bsdfEval(sc, a, b);
+    V3 e = bsdfEval(sc.bsdf, a, b);
     outEval[3 * i] = e.x;
     outEval[3 * i + 1] = e.y;
     outEval[3 * i + 2] = e.z;
-    outPdf[i] = bsdfPdf(sc, a, b);
+    outPdf[i] = bsdfPdf(sc.bsdf, a, b);
     V3 so;
     float pdf = 0;
     uint32_t type = 0;
-    V3 w = bsdfSample(sc, a, u[2 * i], u[2 * i + 1], so, pdf, type);
+    V3 w = bsdfSample(sc.bsdf, a, u[2 * i], u[2 * i + 1], so, pdf, type);
     outWo[3 * i] = so.x;
     outWo[3 * i + 1] = so.y;
     outWo[3 * i + 2] = so.z;
@@ -1973,8 +2053,12 @@ hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint3
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *traceQ,
                             uint32_t *shadowQ, uint32_t *counters, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_shade, dim3(blocksFor(maxItems, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, P, shadeQ, traceQ, shadowQ,
-                       counters);
+    if (sc.nShapes > 1)
+        hipLaunchKernelGGL(k_shade_multi, dim3(blocksFor(maxItems, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, P, shadeQ,
+                           traceQ, shadowQ, counters);
+    else
+        hipLaunchKernelGGL(k_shade, dim3(blocksFor(maxItems, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, P, shadeQ,
+                           traceQ, shadowQ, counters);
     return hipGetLastError();
 }
 hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,

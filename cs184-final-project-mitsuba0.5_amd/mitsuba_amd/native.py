@@ -32,7 +32,7 @@ class SceneInfo(C.Structure):
                 ("vertices", C.c_uint64), ("segments", C.c_uint64), ("kd_nodes", C.c_uint64),
                 ("kd_indices", C.c_uint64), ("kd_depth", C.c_int), ("kd_build_seconds", C.c_double),
                 ("aabb_min", C.c_float * 3), ("aabb_max", C.c_float * 3), ("bsphere_center", C.c_float * 3),
-                ("bsphere_radius", C.c_float)]
+                ("bsphere_radius", C.c_float), ("n_shapes", C.c_int)]
 
 
 class RenderParams(C.Structure):

@@ -10,6 +10,8 @@ numbers from models/*/scene*.xml) with synthetic hair written next to it:
   curly_marschner  models/curly-hair/scene.xml + marschner     1024^2 @ 256
   furball_roughplastic models/furball/scene.xml as shipped (roughplastic) 512^2 @ 256
   straight_dielectric models/straight-hair/scene_dielectric.xml (marschnerdielectric) 1024^2 @ 128
+  haircurl_roughplastic / haircurl_kk  models/hair-curl/{scene,kkay_scene}.xml: four hair
+                   shapes with one BSDF each, 1200x1000 @ 64
   furball_1m       furball scaled to ~1M segments              1024^2 @ 1024, maxDepth 64
 Resolution / spp / maxDepth are $-parameters (-D width=..., spp=...).
 """
@@ -58,6 +60,33 @@ MARSCHNER_DIELECTRIC = """  <bsdf type="marschnerdielectric" id="hair">
     <rgb name="diffuseReflectance" value="%s"/>
   </bsdf>""" % (HAIR_DIFFUSE, HAIR_DIFFUSE, HAIR_DIFFUSE)          # models/straight-hair/scene_dielectric.xml:31-38
 
+THIN_DIELECTRIC = """  <bsdf type="thindielectric" id="hair">
+    <float name="intIOR" value="1.55"/>
+    <float name="extIOR" value="1"/>
+    <float name="exponent" value="5.0"/>
+    <rgb name="specularTransmittance" value="%s"/>
+    <rgb name="specularReflectance" value="%s"/>
+  </bsdf>""" % (HAIR_DIFFUSE, HAIR_DIFFUSE)                        # models/straight-hair/scene_thindielectric.xml:31-37
+
+HAIRCURL_CAM = ("-1 4.24672e-010 1.50958e-007 -0.055286 1.11022e-016 0.999996 -0.00281317 5.92976 "
+                "-1.50959e-007 -0.00281317 -0.999996 17.0651 0 0 0 1")      # models/hair-curl/scene.xml:12
+HAIRCURL_COLOURS = [("black_hair", "6.344e-006, 7.62186e-012, 6.53751e-030"),
+                    ("red_hair", "0.0112431, 6.77287e-005, 1.13705e-011"),
+                    ("brown_hair", "0.143016, 0.0156076, 1.80928e-005"),
+                    ("blonde_hair", "0.592384, 0.32628, 0.0528657")]      # models/hair-curl/*.xml:31-65
+HAIRCURL_RP = "\n".join("""  <bsdf type="roughplastic" id="%s">
+    <float name="alpha" value="0.3"/>
+    <string name="distribution" value="ggx"/>
+    <float name="intIOR" value="1.55"/>
+    <float name="extIOR" value="1"/>
+    <boolean name="nonlinear" value="false"/>
+    <rgb name="diffuseReflectance" value="%s"/>
+  </bsdf>""" % c for c in HAIRCURL_COLOURS)                           # models/hair-curl/scene.xml
+HAIRCURL_KK = "\n".join("""  <bsdf type="kajiyakay" id="%s">
+    <float name="exponent" value="10"/>
+    <rgb name="diffuseReflectance" value="%s"/>
+  </bsdf>""" % c for c in HAIRCURL_COLOURS)                           # models/hair-curl/kkay_scene.xml
+
 CONFIGS = {
     # name: (camera, bsdf, radius, sun direction, width, height, spp, maxDepth, geometry, geometry args)
     "straight_kk": dict(cam=STRAIGHT_CAM, bsdf=KAJIYAKAY, radius="0.00566563", sun="0.19033 0.758426 -0.623349",
@@ -72,6 +101,16 @@ CONFIGS = {
     "straight_dielectric": dict(cam=STRAIGHT_CAM, bsdf=MARSCHNER_DIELECTRIC, radius="0.00566563",
                                 sun="0.19033 0.758426 -0.623349", width=1024, height=1024, spp=128, max_depth=65,
                                 geom="straight", n=10000),
+    # four hair shapes, one BSDF each (models/hair-curl: 1200x1000 @ 64 spp, radius 0.000444)
+    "haircurl_roughplastic": dict(cam=HAIRCURL_CAM, bsdf=HAIRCURL_RP, radius="0.000444",
+                                  sun="-0.376047 0.758426 0.532333", width=1200, height=1000, spp=64, max_depth=65,
+                                  geom="curl4", n=6000, shapes=[c[0] for c in HAIRCURL_COLOURS]),
+    "haircurl_kk": dict(cam=HAIRCURL_CAM, bsdf=HAIRCURL_KK, radius="0.000444", sun="-0.376047 0.758426 0.532333",
+                        width=1200, height=1000, spp=64, max_depth=65, geom="curl4", n=6000,
+                        shapes=[c[0] for c in HAIRCURL_COLOURS]),
+    "straight_thindielectric": dict(cam=STRAIGHT_CAM, bsdf=THIN_DIELECTRIC, radius="0.00566563",
+                                    sun="0.19033 0.758426 -0.623349", width=1024, height=1024, spp=128, max_depth=65,
+                                    geom="straight", n=10000),
     "furball_1m": dict(cam=FURBALL_CAM, bsdf=MARSCHNER, radius="0.00216667", sun="-0.376047 0.758426 0.532333",
                        width=1024, height=1024, spp=1024, max_depth=64, geom="furball", n=125000),
 }
@@ -83,8 +122,7 @@ XML = """<?xml version="1.0" encoding="utf-8"?>
   <default name="width" value="{width}"/>
   <default name="height" value="{height}"/>
   <default name="maxDepth" value="{max_depth}"/>
-  <default name="hairfile" value="{hairfile}"/>
-  <integrator type="path">
+{hairdefaults}  <integrator type="path">
     <integer name="maxDepth" value="$maxDepth"/>
     <boolean name="strictNormals" value="true"/>
   </integrator>
@@ -107,11 +145,7 @@ XML = """<?xml version="1.0" encoding="utf-8"?>
     </film>
   </sensor>
 {bsdf}
-  <shape type="hair">
-    <float name="radius" value="{radius}"/>
-    <string name="filename" value="$hairfile"/>
-    <ref id="hair"/>
-  </shape>
+{shapes}
   <emitter type="sunsky">
     <float name="turbidity" value="3"/>
     <vector name="sunDirection" x="{sx}" y="{sy}" z="{sz}"/>
@@ -133,21 +167,48 @@ def hair_strands(geom: str, n: int):
     raise ValueError(geom)
 
 
+SHAPE = """  <shape type="hair">
+    <float name="radius" value="{radius}"/>
+    <string name="filename" value="${var}"/>
+    <ref id="{ref}"/>
+  </shape>"""
+
+
+def hair_files(name: str, workdir: str, n_strands: int | None = None):
+    """Hair file path(s) of a config (one per hair shape), written if missing."""
+    cfg = CONFIGS[name]
+    n = int(n_strands if n_strands is not None else cfg["n"])
+    os.makedirs(workdir, exist_ok=True)
+    if cfg["geom"] == "curl4":
+        items = [("curl4_%d_%d.mitshair" % (k, n), lambda k=k: synth_hair.curl_lock(n, k)) for k in range(4)]
+    else:
+        items = [("%s_%d.mitshair" % (cfg["geom"], n), lambda: hair_strands(cfg["geom"], n))]
+    out = []
+    for fname, gen in items:
+        path = os.path.join(workdir, fname)
+        if not os.path.exists(path):
+            tmp = path + ".tmp%d" % os.getpid()
+            synth_hair.write_binary_hair(tmp, gen())
+            os.replace(tmp, path)
+        out.append(path)
+    return out
+
+
 def make_scene(name: str, workdir: str, n_strands: int | None = None, **override) -> str:
-    """Write <workdir>/<name>.xml (+ hair file, cached) and return the XML path."""
+    """Write <workdir>/<name>_<n>.xml (+ hair files, cached) and return the XML path."""
     cfg = dict(CONFIGS[name])
     cfg.update(override)
     n = int(n_strands if n_strands is not None else cfg["n"])
-    os.makedirs(workdir, exist_ok=True)
-    hairfile = os.path.join(workdir, "%s_%d.mitshair" % (cfg["geom"], n))
-    if not os.path.exists(hairfile):
-        tmp = hairfile + ".tmp%d" % os.getpid()
-        synth_hair.write_binary_hair(tmp, hair_strands(cfg["geom"], n))
-        os.replace(tmp, hairfile)
+    files = hair_files(name, workdir, n)
+    refs = cfg.get("shapes", ["hair"])
+    var = ["hairfile"] if len(files) == 1 else ["hairfile%d" % k for k in range(len(files))]
+    defaults = "".join('  <default name="%s" value="%s"/>\n' % (v, os.path.basename(f)) for v, f in zip(var, files))
+    radii = cfg.get("radii") or [cfg["radius"]] * len(files)   # per-shape radii (tests)
+    shapes = "\n".join(SHAPE.format(radius=rad, var=v, ref=r) for v, r, rad in zip(var, refs, radii))
     sx, sy, sz = cfg["sun"].split()
     xml = XML.format(name=name, spp=cfg["spp"], width=cfg["width"], height=cfg["height"],
-                     max_depth=cfg["max_depth"], hairfile=os.path.basename(hairfile), cam=cfg["cam"],
-                     bsdf=cfg["bsdf"], radius=cfg["radius"], sx=sx, sy=sy, sz=sz)
+                     max_depth=cfg["max_depth"], hairdefaults=defaults, cam=cfg["cam"],
+                     bsdf=cfg["bsdf"], shapes=shapes, sx=sx, sy=sy, sz=sz)
     path = os.path.join(workdir, "%s_%d.xml" % (name, n))
     with open(path, "w") as f:
         f.write(xml)

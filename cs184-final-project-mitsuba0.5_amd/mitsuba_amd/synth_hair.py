@@ -109,6 +109,29 @@ def curly(n_strands: int, nseg: int = 270, seed: int = 3):
     return list(pts)
 
 
+def curl_lock(n_strands: int, lock: int, nseg: int = 60, seed: int = 4):
+    """One of the four hanging curly locks of models/hair-curl (black, red,
+    brown, blonde; the camera at z = 17 looks down -z at y ~ 5.9): lock k
+    hangs at x = -3.6 + 2.4 k from y ~ 9.5 down to y ~ 2.5, helical curls of
+    radius 0.08-0.2 around a slightly swaying axis."""
+    rng = np.random.default_rng(seed * 16 + lock)
+    cx = -3.6 + 2.4 * lock
+    roots = np.stack([cx + rng.uniform(-0.7, 0.7, n_strands), 9.5 + rng.uniform(-0.15, 0.15, n_strands),
+                      rng.uniform(-0.5, 0.5, n_strands)], -1)
+    radius = rng.uniform(0.08, 0.2, size=n_strands)
+    turns = rng.uniform(5.0, 9.0, size=n_strands)
+    length = rng.uniform(5.5, 7.0, size=n_strands)
+    phase = rng.uniform(0, 2 * math.pi, size=n_strands)
+    sway = rng.uniform(-0.3, 0.3, size=(n_strands, 2))
+    k = np.arange(nseg + 1)[None, :] / nseg
+    ang = phase[:, None] + 2 * math.pi * turns[:, None] * k
+    pts = np.empty((n_strands, nseg + 1, 3))
+    pts[..., 0] = roots[:, 0:1] + sway[:, 0:1] * k ** 2 + radius[:, None] * np.cos(ang)
+    pts[..., 1] = roots[:, 1:2] - length[:, None] * k
+    pts[..., 2] = roots[:, 2:3] + sway[:, 1:2] * k ** 2 + radius[:, None] * np.sin(ang)
+    return list(pts)
+
+
 def write_binary_hair(path: str, strands) -> int:
     """Write strands (iterable of (n_i, 3) arrays) as BINARY_HAIR; returns vertex count."""
     nvert = sum(len(s) for s in strands)

@@ -48,7 +48,8 @@ int hpt_set_data_dir(hpt_context *ctx, const char *dir);
 
 /* Parse a Mitsuba scene XML (src/librender/scenehandler.cpp) with -D style
    defines: integrator "path", sensor "perspective" + sampler "sobol" + film,
-   shape "hair", bsdf "marschner"/"kajiyakay"/"roughplastic"/"marschnerdielectric", emitter "sunsky"/"envmap". */
+   shape "hair", bsdf "marschner"/"kajiyakay"/"roughplastic"/"marschnerdielectric"/"thindielectric"/"diffuse"
+   (one per hair shape; several shapes per scene), emitter "sunsky"/"envmap". */
 int hpt_load_scene_xml(hpt_context *ctx, const char *path, int n_defines, const char *const *keys,
                        const char *const *values);
 
@@ -98,12 +99,14 @@ int hpt_prepare(hpt_context *ctx);
 
 typedef struct hpt_scene_info {
     int width, height, spp, max_depth, rr_depth, strict_normals, hide_emitters;
-    int bsdf;                      /* 0 marschner, 1 kajiyakay, 2 roughplastic, 3 marschnerdielectric */
+    int bsdf;                      /* first shape's: 0 marschner, 1 kajiyakay, 2 roughplastic,
+                                      3 marschnerdielectric, 4 thindielectric, 5 diffuse */
     uint64_t vertices, segments, kd_nodes, kd_indices;
     int kd_depth;
     double kd_build_seconds;
     float aabb_min[3], aabb_max[3];
     float bsphere_center[3], bsphere_radius;
+    int n_shapes;                  /* hair shapes (merged into one kd-tree, each with its BSDF) */
 } hpt_scene_info;
 int hpt_get_scene_info(hpt_context *ctx, hpt_scene_info *out);
 

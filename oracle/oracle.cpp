@@ -1175,12 +1175,127 @@ struct MarschnerDielectric {
 };
 
 /* ------------------------------------------------------------------ */
+/* thindielectric.cpp:70-252 (constant textures)                       */
+/* ------------------------------------------------------------------ */
+struct ThinDielectric {
+    float eta = 1.5046f;
+    Spec specR{1.0f}, specT{1.0f};
+    void configure() { /* :110-125 */
+        float mx = specR.max();
+        if (mx > 1.0f) specR *= 0.99f * (1.0f / mx);
+        mx = specT.max();
+        if (mx > 1.0f) specT *= 0.99f * (1.0f / mx);
+    }
+    float fresnelR(const V3 &wi) const {
+        float R = fresnelDielectricExt(std::abs(wi.z), eta), T = 1 - R;
+        if (R < 1) R += T * T * R / (1 - R * R);
+        return R;
+    }
+    /* eval / pdf need EDiscrete for both components (:151-201): zero for the
+       integrator's solid-angle queries, which it never makes (no ESmooth) */
+    Spec eval(const V3 &, const V3 &) const { return Spec(0.0f); }
+    float pdf(const V3 &, const V3 &) const { return 0.0f; }
+    Spec sample(const V3 &wi, float sx, float, V3 &wo, float &pdfOut, uint32_t &type) const { /* :203-232 */
+        float R = fresnelR(wi);
+        if (sx <= R) {
+            type = EDeltaReflection;
+            wo = V3(-wi.x, -wi.y, wi.z);
+            pdfOut = R;
+            return specR;
+        }
+        type = ENull;
+        wo = V3(-wi.x, -wi.y, -wi.z);
+        pdfOut = 1 - R;
+        return specT;
+    }
+};
+
+/* ------------------------------------------------------------------ */
+/* diffuse.cpp:60-140 (SmoothDiffuse, constant reflectance)            */
+/* ------------------------------------------------------------------ */
+struct SmoothDiffuse {
+    Spec reflectance{0.5f};
+    void configure() {
+        float mx = reflectance.max();
+        if (mx > 1.0f) reflectance *= 0.99f * (1.0f / mx);
+    }
+    Spec eval(const V3 &wi, const V3 &wo) const {
+        if (wi.z <= 0 || wo.z <= 0) return Spec(0.0f);
+        return reflectance * (kInvPi * wo.z);
+    }
+    float pdf(const V3 &wi, const V3 &wo) const {
+        if (wi.z <= 0 || wo.z <= 0) return 0.0f;
+        return kInvPi * wo.z;
+    }
+    Spec sample(const V3 &wi, float sx, float sy, V3 &wo, float &pdfOut, uint32_t &type) const {
+        pdfOut = 0;
+        type = 0;
+        if (wi.z <= 0) return Spec(0.0f);
+        wo = squareToCosineHemisphere(sx, sy);
+        type = EDiffuseReflection;
+        pdfOut = kInvPi * wo.z;
+        return reflectance;
+    }
+};
+
+/* One BSDF instance of a hair shape (the default is Shape::configure's 0.5
+   Lambertian, shape.cpp:57-64) */
+struct BsdfInst {
+    int kind = 5; /* 0 marschner, 1 kajiyakay, 2 roughplastic, 3 marschnerdielectric, 4 thindielectric, 5 diffuse */
+    Marschner marschner;
+    KajiyaKay kk;
+    RoughPlastic rp;
+    MarschnerDielectric md;
+    ThinDielectric td;
+    SmoothDiffuse df;
+    /* the combined type has an ESmooth component (path.cpp:175 gate) */
+    bool smooth() const { return kind != 4 && !(kind == 5 && df.reflectance.max() <= 0); }
+    Spec eval(const V3 &wi, const V3 &wo) const {
+        switch (kind) {
+        case 0: return marschner.eval(wi, wo);
+        case 1: return kk.eval(wi, wo);
+        case 2: return rp.eval(wi, wo);
+        case 3: return md.eval(wi, wo);
+        case 4: return td.eval(wi, wo);
+        default: return df.eval(wi, wo);
+        }
+    }
+    float pdf(const V3 &wi, const V3 &wo) const {
+        switch (kind) {
+        case 0: return marschner.pdf();
+        case 1: return kk.pdf(wi, wo);
+        case 2: return rp.pdf(wi, wo);
+        case 3: return md.pdf(wi, wo);
+        case 4: return td.pdf(wi, wo);
+        default: return df.pdf(wi, wo);
+        }
+    }
+    Spec sample(const V3 &wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) const {
+        switch (kind) {
+        case 0: return marschner.sample(wi, sx, sy, wo, pdf, type);
+        case 1: return kk.sample(wi, sx, sy, wo, pdf, type);
+        case 2: return rp.sample(wi, sx, sy, wo, pdf, type);
+        case 3: return md.sample(wi, sx, sy, wo, pdf, type);
+        case 4: return td.sample(wi, sx, sy, wo, pdf, type);
+        default: return df.sample(wi, sx, sy, wo, pdf, type);
+        }
+    }
+};
+
+/* ------------------------------------------------------------------ */
 /* Hair shape: hair.cpp                                                 */
 /* ------------------------------------------------------------------ */
 struct HairGeom {
     std::vector<V3> v;
     std::vector<uint8_t> start; /* size n+1, last = 1 */
-    float radius = 0.025f;
+    /* several HairShapes, concatenated: shape k owns vertices [shapeFirst[k], shapeFirst[k+1]) */
+    std::vector<uint32_t> shapeFirst;
+    std::vector<float> shapeRadius;
+    std::vector<int> shapeBsdf;
+    uint32_t shapeOf(uint32_t iv) const {
+        return (uint32_t) (std::upper_bound(shapeFirst.begin(), shapeFirst.end(), iv) - shapeFirst.begin() - 1);
+    }
+    float radius(uint32_t iv) const { return shapeRadius[shapeOf(iv)]; }
 
     V3 firstVertex(uint32_t iv) const { return v[iv]; }
     V3 secondVertex(uint32_t iv) const { return v[iv + 1]; }
@@ -1249,9 +1364,9 @@ struct HairGeom {
         for (int end = 0; end < 2; ++end) {
             bool ok = end == 0
                           ? intersectCylPlane(firstVertex(iv), firstMiterNormal(iv), firstVertex(iv),
-                                              tangent(iv), radius * (1 - kEpsilon), center, axes, lengths)
+                                              tangent(iv), radius(iv) * (1 - kEpsilon), center, axes, lengths)
                           : intersectCylPlane(secondVertex(iv), secondMiterNormal(iv), secondVertex(iv),
-                                              tangent(iv), radius * (1 - kEpsilon), center, axes, lengths);
+                                              tangent(iv), radius(iv) * (1 - kEpsilon), center, axes, lengths);
             (void) ok;
             axes[0] *= lengths[0];
             axes[1] *= lengths[1];
@@ -1274,7 +1389,8 @@ struct HairGeom {
         V3d projDirection = rayD - dot(axis, rayD) * axis;
         const double A = projDirection.lengthSquared();
         const double B = 2 * dot(projOrigin, projDirection);
-        const double C = projOrigin.lengthSquared() - radius * radius;
+        const float r = radius(iv);
+        const double C = projOrigin.lengthSquared() - r * r;
         double nearT, farT;
         if (!solveQuadraticDouble(A, B, C, nearT, farT))
             return false;
@@ -1539,11 +1655,7 @@ struct orc_scene {
     HairGeom hair;
     KDTree tree;
     AABB aabb;
-    int bsdfKind = -1; /* 0 marschner, 1 kajiyakay, 2 roughplastic, 3 marschnerdielectric */
-    Marschner marschner;
-    KajiyaKay kk;
-    RoughPlastic rp;
-    MarschnerDielectric md;
+    std::vector<BsdfInst> bsdfs; /* one per hair shape (orc_set_* sets the last loaded shape's) */
     EnvMap env;
     bool hasEnv = false;
     int maxDepth = -1, rrDepth = 5;
@@ -1848,6 +1960,7 @@ bool sceneOccluded(const orc_scene *s, const Ray &ray, Stats *st, bool brute = f
 
 struct Intersection {
     float t;
+    uint32_t iv; /* segment (its first vertex) -> shape -> BSDF */
     V3 p;
     Frame geoFrame, shFrame;
     V3 wi;
@@ -1858,6 +1971,7 @@ struct Intersection {
 /* hair.cpp:825-862 + skdtree.h:422-427 */
 void fillIntersection(const orc_scene *s, const Ray &ray, const Hit &hit, Intersection &its) {
     its.t = hit.t;
+    its.iv = hit.iv;
     its.p = hit.p;
     const V3 axis = s->hair.tangent(hit.iv);
     its.geoFrame.s = axis;
@@ -1865,7 +1979,7 @@ void fillIntersection(const orc_scene *s, const Ray &ray, const Hit &hit, Inters
     its.geoFrame.n = normalize(relHitPoint - dot(axis, relHitPoint) * axis);
     its.geoFrame.t = cross(its.geoFrame.n, its.geoFrame.s);
     const V3 local = its.geoFrame.toLocal(relHitPoint);
-    its.p += its.geoFrame.n * (s->hair.radius - std::sqrt(local.y * local.y + local.z * local.z));
+    its.p += its.geoFrame.n * (s->hair.radius(hit.iv) - std::sqrt(local.y * local.y + local.z * local.z));
     its.shFrame = its.geoFrame;
     V3 dpdu = its.geoFrame.s;
     computeShadingFrame(its.shFrame.n, dpdu, its.shFrame);
@@ -1878,21 +1992,16 @@ inline float miWeight(float pdfA, float pdfB) { /* path.cpp:296-300 */
     return pdfA / (pdfA + pdfB);
 }
 
-Spec bsdfEval(const orc_scene *s, const V3 &wi, const V3 &wo) {
-    if (s->bsdfKind == 2) return s->rp.eval(wi, wo);
-    if (s->bsdfKind == 3) return s->md.eval(wi, wo);
-    return s->bsdfKind == 0 ? s->marschner.eval(wi, wo) : s->kk.eval(wi, wo);
+/* the BSDF of the shape a hit belongs to; the batch entry points use the last loaded shape's */
+const BsdfInst &bsdfOf(const orc_scene *s, uint32_t iv) { return s->bsdfs[s->hair.shapeBsdf[s->hair.shapeOf(iv)]]; }
+BsdfInst &lastBsdf(orc_scene *s) {
+    if (s->bsdfs.empty()) s->bsdfs.emplace_back();
+    return s->bsdfs.back();
 }
-float bsdfPdf(const orc_scene *s, const V3 &wi, const V3 &wo) {
-    if (s->bsdfKind == 2) return s->rp.pdf(wi, wo);
-    if (s->bsdfKind == 3) return s->md.pdf(wi, wo);
-    return s->bsdfKind == 0 ? s->marschner.pdf() : s->kk.pdf(wi, wo);
-}
+Spec bsdfEval(const orc_scene *s, const V3 &wi, const V3 &wo) { return s->bsdfs.back().eval(wi, wo); }
+float bsdfPdf(const orc_scene *s, const V3 &wi, const V3 &wo) { return s->bsdfs.back().pdf(wi, wo); }
 Spec bsdfSample(const orc_scene *s, const V3 &wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
-    if (s->bsdfKind == 2) return s->rp.sample(wi, sx, sy, wo, pdf, type);
-    if (s->bsdfKind == 3) return s->md.sample(wi, sx, sy, wo, pdf, type);
-    return s->bsdfKind == 0 ? s->marschner.sample(wi, sx, sy, wo, pdf, type)
-                            : s->kk.sample(wi, sx, sy, wo, pdf, type);
+    return s->bsdfs.back().sample(wi, sx, sy, wo, pdf, type);
 }
 
 /* envmap.cpp:516-543 + scene.cpp:828-852; returns value (0 if occluded/failed) */
@@ -1952,18 +2061,19 @@ Spec Li(const orc_scene *s, const CamRay &cr, Sampler &sampler, Stats *st, int *
             (s->strictNormals && dot(ray.d, its.geoFrame.n) * its.wi.z >= 0))
             break;
         if (st) st->bounces++;
-        /* direct illumination (both BSDFs have ESmooth components) */
+        const BsdfInst &bsdf = bsdfOf(s, its.iv);
+        /* direct illumination, only for BSDFs with an ESmooth component (path.cpp:175) */
         float nx, ny;
-        sampler.next2D(nx, ny);
-        if (s->hasEnv) {
+        if (bsdf.smooth()) sampler.next2D(nx, ny);
+        if (bsdf.smooth() && s->hasEnv) {
             V3 dRecD;
             float dRecPdf;
             Spec value = sampleEmitterDirect(s, its.p, nx, ny, dRecD, dRecPdf, st);
             if (!value.isZero()) {
                 V3 wo = its.toLocal(dRecD);
-                const Spec bsdfVal = bsdfEval(s, its.wi, wo);
+                const Spec bsdfVal = bsdf.eval(its.wi, wo);
                 if (!bsdfVal.isZero() && (!s->strictNormals || dot(its.geoFrame.n, dRecD) * wo.z > 0)) {
-                    float bp = bsdfPdf(s, its.wi, wo);
+                    float bp = bsdf.pdf(its.wi, wo);
                     float weight = miWeight(dRecPdf, bp);
                     Li += throughput * value * bsdfVal * weight;
                 }
@@ -1975,7 +2085,7 @@ Spec Li(const orc_scene *s, const CamRay &cr, Sampler &sampler, Stats *st, int *
         float bsdfPdfV = 0;
         uint32_t sampledType = 0;
         V3 woLocal;
-        Spec bsdfWeight = bsdfSample(s, its.wi, bx, by, woLocal, bsdfPdfV, sampledType);
+        Spec bsdfWeight = bsdf.sample(its.wi, bx, by, woLocal, bsdfPdfV, sampledType);
         if (bsdfWeight.isZero())
             break;
         scattered |= sampledType != ENull;
@@ -2232,9 +2342,16 @@ int orc_load_hair(orc_scene *s, const char *path, float radius, float angle_thre
         }
     }
     starts.push_back(1);
-    s->hair.v.swap(vertices);
-    s->hair.start.swap(starts);
-    s->hair.radius = radius;
+    /* another HairShape of the scene: appended; its first vertex starts a fiber */
+    HairGeom &H = s->hair;
+    if (!H.start.empty()) H.start.pop_back();
+    const uint32_t base = (uint32_t) H.v.size();
+    H.v.insert(H.v.end(), vertices.begin(), vertices.end());
+    H.start.insert(H.start.end(), starts.begin(), starts.end());
+    H.shapeFirst.push_back(base);
+    H.shapeRadius.push_back(radius);
+    s->bsdfs.emplace_back(); /* Shape::configure default until orc_set_* */
+    H.shapeBsdf.push_back((int) s->bsdfs.size() - 1);
     return 0;
 }
 
@@ -2268,30 +2385,35 @@ int orc_hair_aabb(orc_scene *s, float out_min[3], float out_max[3]) {
 
 int orc_set_marschner(orc_scene *s, float eta, int distribution, float alpha, const float diffuse[3],
                       const float specular[3], const char *dat_dir) {
-    s->bsdfKind = 0;
-    s->marschner.eta = eta;
-    s->marschner.alpha = std::max(alpha, (float) 1e-4f); /* microfacet.h:131-132 */
-    s->marschner.diffuse = Spec(diffuse[0], diffuse[1], diffuse[2]);
-    s->marschner.specular = Spec(specular[0], specular[1], specular[2]);
-    if (!s->marschner.configure(distribution, dat_dir, s->err))
+    BsdfInst &b = lastBsdf(s);
+    b.kind = 0;
+    b.marschner = Marschner();
+    b.marschner.eta = eta;
+    b.marschner.alpha = std::max(alpha, (float) 1e-4f); /* microfacet.h:131-132 */
+    b.marschner.diffuse = Spec(diffuse[0], diffuse[1], diffuse[2]);
+    b.marschner.specular = Spec(specular[0], specular[1], specular[2]);
+    if (!b.marschner.configure(distribution, dat_dir, s->err))
         return -1;
     return 0;
 }
 
 int orc_set_kajiyakay(orc_scene *s, const float kd[3], const float ks[3], float exponent) {
-    s->bsdfKind = 1;
-    s->kk.kd = Spec(kd[0], kd[1], kd[2]);
-    s->kk.ks = Spec(ks[0], ks[1], ks[2]);
-    s->kk.exponent = exponent;
-    s->kk.configure();
+    BsdfInst &b = lastBsdf(s);
+    b.kind = 1;
+    b.kk = KajiyaKay();
+    b.kk.kd = Spec(kd[0], kd[1], kd[2]);
+    b.kk.ks = Spec(ks[0], ks[1], ks[2]);
+    b.kk.exponent = exponent;
+    b.kk.configure();
     return 0;
 }
 
 int orc_set_roughplastic(orc_scene *s, float eta, int distribution, float alpha, int sample_visible,
                          int nonlinear, const float diffuse[3], const float specular[3], const char *dat_dir) {
     if (distribution < 0 || distribution > 2) { s->err = "bad distribution"; return -1; }
-    s->bsdfKind = 2;
-    RoughPlastic &r = s->rp;
+    BsdfInst &b = lastBsdf(s);
+    b.kind = 2;
+    RoughPlastic &r = b.rp;
     r = RoughPlastic();
     r.type = distribution;
     r.eta = eta;
@@ -2305,14 +2427,35 @@ int orc_set_roughplastic(orc_scene *s, float eta, int distribution, float alpha,
 
 int orc_set_marschnerdielectric(orc_scene *s, float eta, const float diffuse[3], const float spec_r[3],
                                 const float spec_t[3]) {
-    s->bsdfKind = 3;
-    MarschnerDielectric &m = s->md;
+    BsdfInst &b = lastBsdf(s);
+    b.kind = 3;
+    MarschnerDielectric &m = b.md;
     m = MarschnerDielectric();
     m.eta = eta;
     m.diffuse = Spec(diffuse[0], diffuse[1], diffuse[2]);
     m.specR = Spec(spec_r[0], spec_r[1], spec_r[2]);
     m.specT = Spec(spec_t[0], spec_t[1], spec_t[2]);
     m.configure();
+    return 0;
+}
+
+int orc_set_thindielectric(orc_scene *s, float eta, const float spec_r[3], const float spec_t[3]) {
+    BsdfInst &b = lastBsdf(s);
+    b.kind = 4;
+    b.td = ThinDielectric();
+    b.td.eta = eta;
+    b.td.specR = Spec(spec_r[0], spec_r[1], spec_r[2]);
+    b.td.specT = Spec(spec_t[0], spec_t[1], spec_t[2]);
+    b.td.configure();
+    return 0;
+}
+
+int orc_set_diffuse(orc_scene *s, const float reflectance[3]) {
+    BsdfInst &b = lastBsdf(s);
+    b.kind = 5;
+    b.df = SmoothDiffuse();
+    b.df.reflectance = Spec(reflectance[0], reflectance[1], reflectance[2]);
+    b.df.configure();
     return 0;
 }
 
@@ -2366,7 +2509,7 @@ int orc_set_integrator(orc_scene *s, int max_depth, int rr_depth, int strict_nor
 int orc_prepare(orc_scene *s) {
     if (s->m32.empty()) { s->err = "sobol tables not set"; return -1; }
     if (s->width <= 0) { s->err = "camera not set"; return -1; }
-    if (s->bsdfKind < 0) { s->err = "bsdf not set"; return -1; }
+    if (s->hair.shapeFirst.empty()) { s->err = "no hair shape"; return -1; }
     prepareScene(s);
     return 0;
 }
@@ -2546,8 +2689,9 @@ void orc_bsdf_sample(orc_scene *s, int n, const float *wi, const float *u, float
 
 int orc_marschner_tables(orc_scene *s, float *nR, float *nTT, float *nTRT, float *out_fdr,
                          float *out_trans100, float *out_spec_weight) {
-    if (s->bsdfKind != 0) return -1;
-    const Azimuthal *lobes[3] = {s->marschner.nR.get(), s->marschner.nTT.get(), s->marschner.nTRT.get()};
+    if (s->bsdfs.empty() || s->bsdfs.back().kind != 0) return -1;
+    const Marschner &mar = s->bsdfs.back().marschner;
+    const Azimuthal *lobes[3] = {mar.nR.get(), mar.nTT.get(), mar.nTRT.get()};
     float *outs[3] = {nR, nTT, nTRT};
     for (int l = 0; l < 3; ++l)
         for (int i = 0; i < kAzRes * kAzRes; ++i) {
@@ -2555,9 +2699,9 @@ int orc_marschner_tables(orc_scene *s, float *nR, float *nTT, float *nTRT, float
             outs[l][3 * i + 1] = lobes[l]->table[i].y;
             outs[l][3 * i + 2] = lobes[l]->table[i].z;
         }
-    *out_fdr = s->marschner.Fdr;
-    for (size_t i = 0; i < s->marschner.ext.trans.size() && i < 100; ++i) out_trans100[i] = s->marschner.ext.trans[i];
-    *out_spec_weight = s->marschner.specularSamplingWeight;
+    *out_fdr = mar.Fdr;
+    for (size_t i = 0; i < mar.ext.trans.size() && i < 100; ++i) out_trans100[i] = mar.ext.trans[i];
+    *out_spec_weight = mar.specularSamplingWeight;
     return 0;
 }
 

@@ -39,7 +39,10 @@ int orc_set_sobol(orc_scene *s, const uint32_t *m32, const uint64_t *vdc, int vd
 /* perspective.cpp:125-165: toWorld row-major 4x4, x field of view in degrees */
 int orc_set_camera(orc_scene *s, const float to_world[16], float fov_x_deg, int width,
                    int height, float near_clip, float far_clip);
-/* hair.cpp:609-785 loader restatement (BINARY_HAIR or ASCII); to_world may be NULL */
+/* hair.cpp:609-785 loader restatement (BINARY_HAIR or ASCII); to_world may be NULL.
+   Each call adds one HairShape (vertices appended after the previous shapes'),
+   with the default 0.5 diffuse BSDF; the orc_set_<bsdf> calls below set the
+   BSDF of the most recently added shape. */
 int orc_load_hair(orc_scene *s, const char *path, float radius, float angle_threshold_deg,
                   const float *to_world);
 int64_t orc_hair_vertex_count(orc_scene *s);
@@ -64,6 +67,9 @@ int orc_set_roughplastic(orc_scene *s, float eta, int distribution, float alpha,
 /* marschnerdielectric.cpp: eta = intIOR/extIOR */
 int orc_set_marschnerdielectric(orc_scene *s, float eta, const float diffuse[3], const float spec_r[3],
                                 const float spec_t[3]);
+/* thindielectric.cpp / diffuse.cpp */
+int orc_set_thindielectric(orc_scene *s, float eta, const float spec_r[3], const float spec_t[3]);
+int orc_set_diffuse(orc_scene *s, const float reflectance[3]);
 /* envmap.cpp: linear RGB float bitmap (w x h x 3), to_world may be NULL */
 int orc_set_envmap(orc_scene *s, const float *rgb, int w, int h, float scale,
                    const float *to_world);

@@ -39,6 +39,8 @@ _SIG = {
     "orc_set_marschner": (C.c_int, [C.c_void_p, C.c_float, C.c_int, C.c_float, _f, _f, C.c_char_p]),
     "orc_set_kajiyakay": (C.c_int, [C.c_void_p, _f, _f, C.c_float]),
     "orc_set_marschnerdielectric": (C.c_int, [C.c_void_p, C.c_float, _f, _f, _f]),
+    "orc_set_thindielectric": (C.c_int, [C.c_void_p, C.c_float, _f, _f]),
+    "orc_set_diffuse": (C.c_int, [C.c_void_p, _f]),
     "orc_set_roughplastic": (C.c_int, [C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_int, C.c_int, _f, _f,
                                        C.c_char_p]),
     "orc_set_envmap": (C.c_int, [C.c_void_p, _f, C.c_int, C.c_int, C.c_float, _f]),
@@ -126,7 +128,16 @@ class Oracle:
         cam = f32(cam).reshape(16)
         self.check(self.lib.orc_set_sample_count(self.s, spp))
         self.check(self.lib.orc_set_camera(self.s, p(cam, _f), fov, width, height, near, far))
-        self.check(self.lib.orc_load_hair(self.s, hair_file.encode(), radius, 1.0, None))
+        shapes = hair_file if isinstance(hair_file, list) else [(hair_file, radius, bsdf)]
+        for path, rad, b in shapes:
+            self.check(self.lib.orc_load_hair(self.s, path.encode(), rad, 1.0, None))
+            self.set_bsdf(b)
+        env = f32(env_rgb)
+        self.check(self.lib.orc_set_envmap(self.s, p(env, _f), env.shape[1], env.shape[0], 1.0, None))
+        self.check(self.lib.orc_set_integrator(self.s, max_depth, rr_depth, int(strict), int(hide)))
+
+    def set_bsdf(self, bsdf):
+        """Set the BSDF of the most recently loaded hair shape."""
         kind = bsdf["type"]
         if kind == "marschner":
             dif = f32(bsdf["diffuse"])
@@ -138,13 +149,15 @@ class Oracle:
             self.set_marschnerdielectric(bsdf)
         elif kind == "roughplastic":
             self.set_roughplastic(bsdf)
+        elif kind == "thindielectric":
+            self.check(self.lib.orc_set_thindielectric(self.s, bsdf["eta"], p(f32(bsdf.get("specular", (1, 1, 1))), _f),
+                                                       p(f32(bsdf.get("transmittance", (1, 1, 1))), _f)))
+        elif kind == "diffuse":
+            self.check(self.lib.orc_set_diffuse(self.s, p(f32(bsdf.get("diffuse", (0.5, 0.5, 0.5))), _f)))
         else:
             kd = f32(bsdf["kd"])
             ks = f32(bsdf.get("ks", (0.2, 0.2, 0.2)))
             self.check(self.lib.orc_set_kajiyakay(self.s, p(kd, _f), p(ks, _f), bsdf["exponent"]))
-        env = f32(env_rgb)
-        self.check(self.lib.orc_set_envmap(self.s, p(env, _f), env.shape[1], env.shape[0], 1.0, None))
-        self.check(self.lib.orc_set_integrator(self.s, max_depth, rr_depth, int(strict), int(hide)))
 
     def set_marschnerdielectric(self, bsdf):
         dif = f32(bsdf.get("diffuse", (0.5, 0.5, 0.5)))

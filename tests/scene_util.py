@@ -9,6 +9,7 @@ checks them against a brute-force intersection (tests/test_host.py).
 from __future__ import annotations
 
 import os
+import re
 import tempfile
 
 import numpy as np
@@ -19,56 +20,99 @@ from mitsuba_amd import native, scenes
 WORK = os.environ.get("HPT_TEST_WORK", os.path.join(tempfile.gettempdir(), "hpt_test_work"))
 
 
+def _bsdf_blocks(xml_text):
+    """{id: oracle BSDF dict} from the <bsdf> blocks of a config, with each
+    plugin's defaults (marschner_diffuse.cpp:113-160, kajiyakay.cpp:60-69,
+    roughplastic.cpp:197-227, marschnerdielectric.cpp:147-169,
+    thindielectric.cpp:73-89, diffuse.cpp:62-69)."""
+    out = {}
+    for m in re.finditer(r'<bsdf type="(\w+)" id="(\w+)"\s*>(.*?)</bsdf>', xml_text, re.S):
+        kind, bid, body = m.groups()
+        props = {}
+        for k, name, val in re.findall(r'<(float|rgb|string|boolean)\s+name="(\w+)"\s+value="([^"]*)"', body):
+            if k == "rgb":
+                v = [float(x) for x in val.replace(",", " ").split()]
+                props[name] = tuple(v * 3 if len(v) == 1 else v)
+            elif k == "float":
+                props[name] = float(val)
+            elif k == "boolean":
+                props[name] = val.lower() == "true"
+            else:
+                props[name] = val
+        eta = np.float32(props.get("intIOR", 1.5046)) / np.float32(props.get("extIOR", 1.000277))
+        if kind == "marschner":
+            b = {"type": kind, "eta": eta, "distribution": props.get("distribution", "beckmann"),
+                 "alpha": props.get("alpha", 0.1), "diffuse": props.get("diffuseReflectance", (0.5,) * 3),
+                 "specular": props.get("specularReflectance", (0.5,) * 3)}
+        elif kind == "kajiyakay":
+            b = {"type": kind, "kd": props.get("diffuseReflectance", (0.5,) * 3),
+                 "ks": props.get("specularReflectance", (0.2,) * 3), "exponent": props.get("exponent", 30.0)}
+        elif kind == "roughplastic":
+            eta = np.float32(props.get("intIOR", 1.49)) / np.float32(props.get("extIOR", 1.000277))
+            b = {"type": kind, "eta": eta, "distribution": props.get("distribution", "beckmann"),
+                 "alpha": props.get("alpha", 0.1), "sample_visible": props.get("sampleVisible", True),
+                 "nonlinear": props.get("nonlinear", False), "diffuse": props.get("diffuseReflectance", (0.5,) * 3),
+                 "specular": props.get("specularReflectance", (1.0,) * 3)}
+        elif kind == "marschnerdielectric":
+            eta = np.float32(props.get("intIOR", 1.501)) / np.float32(props.get("extIOR", 1.000277))
+            b = {"type": kind, "eta": eta, "diffuse": props.get("diffuseReflectance", (0.5,) * 3),
+                 "specular": props.get("specularReflectance", (0.1,) * 3),
+                 "transmittance": props.get("specularTransmittance", (0.1,) * 3)}
+        elif kind == "thindielectric":
+            b = {"type": kind, "eta": eta, "specular": props.get("specularReflectance", (1.0,) * 3),
+                 "transmittance": props.get("specularTransmittance", (1.0,) * 3)}
+        else:
+            b = {"type": "diffuse", "diffuse": props.get("reflectance", props.get("diffuseReflectance", (0.5,) * 3))}
+        out[bid] = b
+    return out
+
+
 def config_params(name):
+    """(config, camera matrix, BSDF of the first shape) -- single-shape callers."""
     cfg = scenes.CONFIGS[name]
     cam = np.array([float(x) for x in cfg["cam"].split()], np.float32)
-    if 'type="marschner"' in cfg["bsdf"]:
-        bsdf = {"type": "marschner", "eta": np.float32(1.55) / np.float32(1.0), "distribution": "ggx",
-                "alpha": 0.2, "diffuse": (0.143016, 0.0156076, 1.80928e-005), "specular": (0.5, 0.5, 0.5)}
-    elif "marschnerdielectric" in cfg["bsdf"]:
-        c = (0.143016, 0.0156076, 1.80928e-005)
-        bsdf = {"type": "marschnerdielectric", "eta": np.float32(1.55) / np.float32(1.0), "diffuse": c,
-                "specular": c, "transmittance": c}
-    elif "roughplastic" in cfg["bsdf"]:
-        bsdf = {"type": "roughplastic", "eta": np.float32(1.55) / np.float32(1.0), "distribution": "ggx",
-                "alpha": 0.2, "sample_visible": True, "nonlinear": False,
-                "diffuse": (0.143016, 0.0156076, 1.80928e-005), "specular": (1.0, 1.0, 1.0)}
-    else:
-        bsdf = {"type": "kajiyakay", "kd": (0.143016, 0.0156076, 1.80928e-005), "ks": (0.2, 0.2, 0.2),
-                "exponent": 10.0}
-    return cfg, cam, bsdf
+    blocks = _bsdf_blocks(cfg["bsdf"])
+    return cfg, cam, blocks[cfg.get("shapes", ["hair"])[0]]
 
 
-def make(name, n_strands, width, height, spp, max_depth=None, device=native.HOST_ONLY):
+def oracle_shapes(name, n_strands, workdir=None, radii=None):
+    """[(hair file, radius, oracle BSDF dict)] per hair shape of a config."""
+    cfg = scenes.CONFIGS[name]
+    files = scenes.hair_files(name, workdir or WORK, n_strands)
+    blocks = _bsdf_blocks(cfg["bsdf"])
+    radii = radii or [cfg["radius"]] * len(files)
+    return [(f, float(rad), blocks[ref]) for f, ref, rad in zip(files, cfg.get("shapes", ["hair"]), radii)]
+
+
+def make(name, n_strands, width, height, spp, max_depth=None, device=native.HOST_ONLY, radii=None):
     """Return (xml_path, product Renderer (prepared), Oracle (prepared, with product kd-tree))."""
-    cfg, cam, bsdf = config_params(name)
+    cfg, cam, _ = config_params(name)
     max_depth = cfg["max_depth"] if max_depth is None else max_depth
-    xml = scenes.make_scene(name, WORK, n_strands=n_strands)
+    xml = scenes.make_scene(name, WORK, n_strands=n_strands, **({"radii": radii} if radii else {}))
     r = native.Renderer(device=device)
     r.load_scene_xml(xml, {"width": width, "height": height, "spp": spp, "maxDepth": max_depth})
     r.prepare()
     env = r.envmap()
     nodes, idx, _ = r.kdtree()
     o = oracle_lib.Oracle()
-    hair_file = os.path.join(WORK, "%s_%d.mitshair" % (cfg["geom"], n_strands))
-    o.setup(cam, 35.0, width, height, hair_file, float(cfg["radius"]), bsdf, env, max_depth, spp=spp)
+    o.setup(cam, 35.0, width, height, oracle_shapes(name, n_strands, radii=radii), None, None, env, max_depth,
+            spp=spp)
     o.set_kdtree(nodes, idx)
     o.prepare()
     return xml, r, o
 
 
-def reference_flags_floor(name, n_strands, r, width, height, spp):
+def reference_flags_floor(name, n_strands, r, width, height, spp, radii=None):
     """L2 between the strict oracle and the oracle built with the reference's
     own compiler flags (liboracle_ref.so): the float-nondeterminism floor that
     any re-implementation of the path inherits (SURVEY.md 7 'Hard parts' i)."""
-    cfg, cam, bsdf = config_params(name)
-    hair_file = os.path.join(WORK, "%s_%d.mitshair" % (cfg["geom"], n_strands))
+    cfg, cam, _ = config_params(name)
+    shapes = oracle_shapes(name, n_strands, radii=radii)
     films = []
     nodes, idx, _ = r.kdtree()
     for variant in ("parity", "ref"):
         o = oracle_lib.Oracle(variant=variant)
-        o.setup(cam, 35.0, width, height, hair_file, float(cfg["radius"]), bsdf, r.envmap(), cfg["max_depth"],
-                spp=spp)
+        o.setup(cam, 35.0, width, height, shapes, None, None, r.envmap(), cfg["max_depth"], spp=spp)
         o.set_kdtree(nodes, idx)
         o.prepare()
         films.append(native.develop(o.render(0, spp, threads=16, width=width, height=height)[0]))

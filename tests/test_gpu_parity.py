@@ -46,13 +46,13 @@ def test_sobol_bit_exact(furball):
     np.testing.assert_array_equal(gv, o.sobol_sample(oi, dim))
 
 
-def _rays(o, n, seed, width=48, height=40):
+def _rays(o, n, seed, width=48, height=40, centre=(0.0, 12.3, 0.0), spread=2.0):
     rng = np.random.default_rng(seed)
     pos = np.stack([rng.uniform(0, width, n // 2), rng.uniform(0, height, n // 2)], 1)
     co, cd, cmin, cmax = o.camera_rays(pos)
-    centre = np.array([0.0, 12.3, 0.0])
-    a = centre + rng.normal(0, 2.0, (n // 2, 3))
-    b = centre + rng.normal(0, 2.0, (n // 2, 3))
+    centre = np.array(centre)
+    a = centre + rng.normal(0, spread, (n // 2, 3))
+    b = centre + rng.normal(0, spread, (n // 2, 3))
     d = (b - a) / np.linalg.norm(b - a, axis=1, keepdims=True)
     orig = np.concatenate([co, a]).astype(np.float32)
     dirs = np.concatenate([cd, d]).astype(np.float32)
@@ -61,7 +61,7 @@ def _rays(o, n, seed, width=48, height=40):
     return orig, dirs, mint, maxt
 
 
-def _grazing_rays(r, n, seed, radius):
+def _grazing_rays(r, n, seed, radius, vrange=None):
     """Rays whose line passes the axis of a random segment at radius * (1 +- 1e-4),
     from origins 0.05..40 units away: the worst case for the fp32 pre-test
     (HptSegF in hpt_device.h), which must never reject a segment the exact
@@ -69,6 +69,8 @@ def _grazing_rays(r, n, seed, radius):
     rng = np.random.default_rng(seed)
     xyz, st = r.hair()
     segs = np.nonzero(st[1:len(xyz)] == 0)[0]
+    if vrange is not None:  # segments of one hair shape
+        segs = segs[(segs >= vrange[0]) & (segs < vrange[1])]
     s = rng.choice(segs, n)
     v1, v2 = xyz[s].astype(np.float64), xyz[s + 1].astype(np.float64)
     axis = (v2 - v1) / np.linalg.norm(v2 - v1, axis=1, keepdims=True)
@@ -87,12 +89,24 @@ def _grazing_rays(r, n, seed, radius):
     return orig, d.astype(np.float32), np.full(n, 1e-4, np.float32), np.full(n, np.inf, np.float32)
 
 
-@pytest.mark.parametrize("fixture", ["furball", "straight"])
+@pytest.mark.parametrize("fixture", ["furball", "straight", "haircurl"])
 @pytest.mark.parametrize("kind", ["mixed", "grazing"])
 def test_trace_bit_exact(fixture, kind, request):
     _, r, o = request.getfixturevalue(fixture)
     if kind == "mixed":
-        orig, dirs, mint, maxt = _rays(o, 40000, 3)
+        orig, dirs, mint, maxt = (_rays(o, 40000, 3, centre=(0.0, 6.0, 0.0), spread=3.0) if fixture == "haircurl"
+                                  else _rays(o, 40000, 3))
+    elif fixture == "haircurl":
+        # grazing rays at each shape's own radius: the shapes' vertex ranges in the merged set
+        counts = []
+        for path, rad, _ in scene_util.oracle_shapes("haircurl_roughplastic", 300, radii=HAIRCURL_RADII):
+            oo = oracle_lib.Oracle()
+            oo.check(oo.lib.orc_load_hair(oo.s, path.encode(), rad, 1.0, None))
+            counts.append(int(oo.lib.orc_hair_vertex_count(oo.s)))
+        first = np.concatenate([[0], np.cumsum(counts)])
+        parts = [_grazing_rays(r, 10000, 5 + k, rad, vrange=(first[k], first[k + 1]))
+                 for k, rad in enumerate(HAIRCURL_RADII)]
+        orig, dirs, mint, maxt = (np.concatenate([p[i] for p in parts]) for i in range(4))
     else:
         name = {"furball": "furball_marschner", "straight": "straight_kk"}[fixture]
         orig, dirs, mint, maxt = _grazing_rays(r, 40000, 5, float(scene_util.scenes.CONFIGS[name]["radius"]))
@@ -110,6 +124,23 @@ def test_trace_bit_exact(fixture, kind, request):
     np.testing.assert_array_equal(tiv, oiv)
     np.testing.assert_array_equal(tt, ot)
     np.testing.assert_array_equal(r.trace(orig, dirs, mint, sm, shadow=True, tiny_stack=True), osh)
+
+
+HAIRCURL_RADII = [0.02, 0.035, 0.05, 0.028]
+
+
+@pytest.fixture(scope="module")
+def haircurl():
+    """models/hair-curl: four hair shapes with their own roughplastic BSDFs
+    (and, here, distinct radii so the per-shape radius path is exercised)."""
+    xml, r, o = scene_util.make("haircurl_roughplastic", 300, 48, 40, 8, device=0, radii=HAIRCURL_RADII)
+    return xml, r, o
+
+
+@pytest.fixture(scope="module")
+def straight_td():
+    xml, r, o = scene_util.make("straight_thindielectric", 1500, 48, 40, 8, device=0)
+    return xml, r, o
 
 
 @pytest.fixture(scope="module")
@@ -135,7 +166,7 @@ def _dirs(rng, n):
     return (v / np.linalg.norm(v, axis=1, keepdims=True)).astype(np.float32)
 
 
-@pytest.mark.parametrize("fixture", ["furball", "straight", "furball_rp", "straight_md"])
+@pytest.mark.parametrize("fixture", ["furball", "straight", "furball_rp", "straight_md", "straight_td"])
 def test_bsdf_matches_oracle(fixture, request):
     _, r, o = request.getfixturevalue(fixture)
     rng = np.random.default_rng(7)
@@ -246,11 +277,13 @@ def test_envmap_matches_oracle(furball):
 
 def _reference_flags_floor(fixture, r, si):
     name, n = {"furball": ("furball_marschner", 3000), "straight": ("straight_kk", 1500),
-               "furball_rp": ("furball_roughplastic", 3000), "straight_md": ("straight_dielectric", 1500)}[fixture]
-    return scene_util.reference_flags_floor(name, n, r, si.width, si.height, si.spp)
+               "furball_rp": ("furball_roughplastic", 3000), "straight_md": ("straight_dielectric", 1500),
+               "straight_td": ("straight_thindielectric", 1500), "haircurl": ("haircurl_roughplastic", 300)}[fixture]
+    return scene_util.reference_flags_floor(name, n, r, si.width, si.height, si.spp,
+                                            radii=HAIRCURL_RADII if fixture == "haircurl" else None)
 
 
-@pytest.mark.parametrize("fixture", ["furball", "straight", "furball_rp", "straight_md"])
+@pytest.mark.parametrize("fixture", ["furball", "straight", "furball_rp", "straight_md", "straight_td", "haircurl"])
 def test_render_matches_oracle(fixture, request):
     """Full wavefront render vs the oracle's MIPathTracer::Li restatement."""
     _, r, o = request.getfixturevalue(fixture)

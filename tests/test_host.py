@@ -186,18 +186,25 @@ def test_aabb_and_marschner_tables_match_oracle():
     assert np.all(ot[0][:, 0] >= 0) and ot[0][:, 0].max() > 0.1
 
 
-def test_kdtree_traversal_equals_brute_force():
+HAIRCURL_RADII = [0.02, 0.035, 0.05, 0.028]  # distinct per-shape radii exercise the per-segment radius
+
+
+@pytest.mark.parametrize("name,n,radii,centre,spread", [
+    ("furball_marschner", 2000, None, (0.0, 12.3, 0.0), 2.0),
+    ("haircurl_kk", 150, HAIRCURL_RADII, (0.0, 6.0, 0.0), 3.0)])
+def test_kdtree_traversal_equals_brute_force(name, n, radii, centre, spread):
     """Oracle Havran traversal (sahkdtree3.h:178-308) over the product's tree
-    finds exactly the brute-force closest hit and any-hit."""
-    _, r, o = scene_util.make("furball_marschner", 2000, 32, 32, 4)
+    finds exactly the brute-force closest hit and any-hit -- also over four
+    merged hair shapes of different radii (models/hair-curl)."""
+    _, r, o = scene_util.make(name, n, 32, 32, 4, radii=radii)
     rng = np.random.default_rng(11)
     n = 4000
     # camera rays and random chords through the hair volume
     pos = rng.uniform(0, 32, (n // 2, 2))
     co, cd, cmin, cmax = o.camera_rays(pos)
-    centre = np.array([0.0, 12.3, 0.0])
-    a = centre + rng.normal(0, 2.0, (n // 2, 3))
-    b = centre + rng.normal(0, 2.0, (n // 2, 3))
+    centre = np.array(centre)
+    a = centre + rng.normal(0, spread, (n // 2, 3))
+    b = centre + rng.normal(0, spread, (n // 2, 3))
     d2 = (b - a) / np.linalg.norm(b - a, axis=1, keepdims=True)
     orig = np.concatenate([co, a]).astype(np.float32)
     dirs = np.concatenate([cd, d2]).astype(np.float32)
@@ -212,6 +219,32 @@ def test_kdtree_traversal_equals_brute_force():
     s1 = o.trace(orig, dirs, mint, np.minimum(maxt, 5.0), shadow=True)
     s2 = o.trace(orig, dirs, mint, np.minimum(maxt, 5.0), shadow=True, brute=True)
     np.testing.assert_array_equal(s1, s2)
+
+
+def test_multi_shape_scene_matches_oracle():
+    """models/hair-curl: four hair shapes, one BSDF each.  The shapes are
+    merged (each shape's first vertex starts a fiber) exactly like the oracle
+    appends HairShapes; the scene AABB and per-shape info agree."""
+    _, r, o = scene_util.make("haircurl_roughplastic", 120, 24, 20, 2, radii=HAIRCURL_RADII)
+    si = r.info()
+    assert si.n_shapes == 4 and si.bsdf == 2
+    pxyz, pst = r.hair()
+    oxyz, ost = o.hair()
+    np.testing.assert_array_equal(pxyz, oxyz)
+    np.testing.assert_array_equal(pst, ost)
+    _, _, aabb = r.kdtree()
+    mn, mx = o.aabb()
+    np.testing.assert_array_equal(aabb[:3], mn)
+    np.testing.assert_array_equal(aabb[3:], mx)
+    # a shape without a BSDF gets Shape::configure's 0.5 diffuse (shape.cpp:57-64)
+    src = open(scene_util.scenes.make_scene("haircurl_kk", scene_util.WORK, n_strands=120)).read()
+    bad = src.replace('<ref id="black_hair"/>', "")
+    path = os.path.join(scene_util.WORK, "haircurl_nobsdf.xml")
+    with open(path, "w") as f:
+        f.write(bad)
+    rr = _host(path)
+    rr.prepare()
+    assert rr.info().bsdf == 5 and rr.info().n_shapes == 4
 
 
 def test_kdtree_structure():
