@@ -108,11 +108,22 @@ int main(int argc, char **argv) {
             std::fprintf(stderr, "Error while parsing \"%s\": %s\n", scene.c_str(), e.what());
             return 2;
         }
-        bool ldr = desc.film == "ldrfilm" || desc.fileFormat == "png";
+        /* output name: -o, else the scene file without its extension; the film
+           appends its own extension (ldrfilm.cpp:335-345, hdrfilm.cpp:508-519) */
+        const hpt::FilmDesc &fd = desc.film;
+        const std::string ext = fd.type == "ldrfilm" ? ".png" : fd.fileFormat == "openexr" ? ".exr"
+                                                           : fd.fileFormat == "rgbe"    ? ".rgbe"
+                                                                                        : ".pfm";
         std::string out = o.out;
         if (out.empty()) {
-            size_t dot = scene.find_last_of('.');
-            out = (dot == std::string::npos ? scene : scene.substr(0, dot)) + (ldr ? ".png" : ".pfm");
+            size_t dot = scene.find_last_of('.'), slash = scene.find_last_of('/');
+            out = (dot == std::string::npos || (slash != std::string::npos && dot < slash)) ? scene : scene.substr(0, dot);
+        }
+        {
+            size_t dot = out.find_last_of('.'), slash = out.find_last_of('/');
+            std::string cur = (dot != std::string::npos && (slash == std::string::npos || dot > slash)) ? out.substr(dot) : "";
+            for (auto &ch : cur) ch = (char) std::tolower((unsigned char) ch);
+            if (cur != ext) out = (cur.empty() ? out : out.substr(0, dot)) + ext;
         }
         if (o.skipExisting && exists(out)) {
             if (!o.quiet) std::printf("Skipping \"%s\": output exists\n", scene.c_str());
@@ -167,17 +178,18 @@ int main(int argc, char **argv) {
         double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         for (int g = 0; g < G; ++g)
             if (rcs[g]) { std::fprintf(stderr, "render failed on device %d: %s\n", o.device + g, hpt_last_error(ctx[g])); return 4; }
-        /* film combine (renderproc.cpp:142-145) + develop (ldrfilm.cpp:300-330) */
-        std::vector<float> rgb((size_t) W * H * 3, 0.0f);
-        for (size_t i = 0; i < (size_t) W * H; ++i) {
-            float acc[4] = {0, 0, 0, 0};
-            for (int g = 0; g < G; ++g)
-                for (int k = 0; k < 4; ++k) acc[k] += films[g][4 * i + k];
-            float inv = acc[3] != 0 ? 1.0f / acc[3] : 0.0f;
-            for (int k = 0; k < 3; ++k) rgb[3 * i + k] = acc[k] * inv;
+        /* film combine (renderproc.cpp:142-145) + develop (Film::develop) */
+        std::vector<float> sum((size_t) W * H * 4, 0.0f);
+        for (int g = 0; g < G; ++g)
+            for (size_t i = 0; i < sum.size(); ++i) sum[i] += films[g][i];
+        hpt_film_params fp;
+        hpt_get_film_params(ctx[0], &fp);
+        char written[4096];
+        if (hpt_write_film(ctx[0], out.c_str(), sum.data(), W, H, &fp, written, sizeof(written))) {
+            std::fprintf(stderr, "%s\n", hpt_last_error(ctx[0]));
+            return 5;
         }
-        bool ok = ldr ? hpt::writePNG8(out, rgb.data(), W, H, desc.gamma) : hpt::writePFM(out, rgb.data(), W, H);
-        if (!ok) { std::fprintf(stderr, "cannot write %s\n", out.c_str()); return 5; }
+        out = written;
         if (!o.quiet) {
             double paths = (double) W * H * spp;
             std::printf("Rendering finished (took %.3f s, %.2f Mpaths/s on %d GPU%s) -> %s\n", sec, paths / sec * 1e-6, G,

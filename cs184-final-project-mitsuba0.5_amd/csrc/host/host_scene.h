@@ -44,6 +44,17 @@ struct KDBuildParams {
     int threads = 0;               /* 0 = hardware concurrency */
 };
 
+/* ---- film development (ldrfilm.cpp:132-190, 300-351; hdrfilm.cpp:205-340, 480-537) ---- */
+struct FilmDesc {
+    std::string type = "hdrfilm";                  /* sensor.cpp: the default film */
+    std::string fileFormat;                        /* "" = the film's default (png / openexr) */
+    std::string pixelFormat = "rgb";               /* luminance | rgb (alpha is not recorded) */
+    std::string componentFormat = "float16";       /* hdrfilm: float16 | float32 | uint32 */
+    std::string tonemapMethod = "gamma";           /* ldrfilm: gamma | reinhard */
+    float gamma = -1.0f, exposure = 0.0f, key = 0.18f, burn = 0.0f;
+    bool banner = true;
+};
+
 /* ---- one BSDF instance (constant textures) ---- */
 struct BsdfDesc {
     std::string type = "diffuse";                  /* Shape::configure default (shape.cpp:99-110) */
@@ -81,10 +92,8 @@ struct SceneDesc {
     std::string sampler = "sobol";
     int spp = 4;
     /* film */
-    std::string film = "hdrfilm";
     int width = 768, height = 576;
-    float gamma = -1.0f;
-    std::string fileFormat;
+    FilmDesc film;
     std::string rfilter = "tent";
     /* hair shapes (hair.cpp:609-640), each referencing one of bsdfs */
     std::vector<HairShapeDesc> shapes;
@@ -213,8 +222,19 @@ uint16_t floatToHalf(float f);
 float halfToFloat(uint16_t h);
 
 /* image output (ldrfilm.cpp:300-330 / hdrfilm.cpp:214-227) */
-bool writePFM(const std::string &path, const float *rgb, int w, int h);
-bool writePNG8(const std::string &path, const float *rgb, int w, int h, float gamma);
+/* film.cpp: ImageBlock (R, G, B, W per pixel) -> developed bitmap -> file */
+struct FilmImage {
+    int width = 0, height = 0, channels = 0;
+    int component = 0;                             /* 0 uint8, 1 float16, 2 float32, 3 uint32 */
+    std::vector<uint8_t> bytes;                    /* row-major, top row first */
+};
+bool checkFilm(FilmDesc &f, std::string &err);    /* validate + resolve defaults (constructors) */
+bool developFilm(const float *rgbw, int w, int h, const FilmDesc &f, const std::string &dataDir, FilmImage &out,
+                 std::string &err);
+/* writes f's format; the extension is replaced by the proper one like the films do;
+   returns the path written */
+bool writeFilm(const std::string &path, const FilmImage &img, const FilmDesc &f, std::string &written,
+               std::string &err);
 
 } // namespace hpt
 #endif

@@ -692,87 +692,4 @@ void setupTent(float *lut, float &scale) {
     for (int i = 0; i < R; ++i) lut[i] *= norm;
 }
 
-/* ---------------- image output ---------------- */
-bool writePFM(const std::string &path, const float *rgb, int w, int h) {
-    std::ofstream f(path, std::ios::binary);
-    if (!f) return false;
-    f << "PF\n" << w << " " << h << "\n-1.0\n";
-    for (int y = h - 1; y >= 0; --y) f.write((const char *) &rgb[(size_t) y * w * 3], (std::streamsize) ((size_t) w * 12));
-    return (bool) f;
-}
-
-namespace {
-uint32_t crc32(const unsigned char *p, size_t n, uint32_t c = 0xffffffffu) {
-    static uint32_t table[256];
-    static bool init = false;
-    if (!init) {
-        for (uint32_t i = 0; i < 256; ++i) {
-            uint32_t v = i;
-            for (int k = 0; k < 8; ++k) v = (v & 1) ? 0xedb88320u ^ (v >> 1) : v >> 1;
-            table[i] = v;
-        }
-        init = true;
-    }
-    for (size_t i = 0; i < n; ++i) c = table[(c ^ p[i]) & 0xff] ^ (c >> 8);
-    return c;
-}
-void be32(std::vector<unsigned char> &v, uint32_t x) {
-    v.push_back((unsigned char) (x >> 24)); v.push_back((unsigned char) (x >> 16));
-    v.push_back((unsigned char) (x >> 8)); v.push_back((unsigned char) x);
-}
-void chunk(std::ofstream &f, const char *type, const std::vector<unsigned char> &data) {
-    std::vector<unsigned char> buf;
-    be32(buf, (uint32_t) data.size());
-    std::vector<unsigned char> td(type, type + 4);
-    td.insert(td.end(), data.begin(), data.end());
-    buf.insert(buf.end(), td.begin(), td.end());
-    be32(buf, crc32(td.data(), td.size()) ^ 0xffffffffu);
-    f.write((const char *) buf.data(), (std::streamsize) buf.size());
-}
-} // namespace
-
-/* ldrfilm.cpp:300-330 develop: gamma (sRGB curve when gamma == -1), 8-bit, stored-deflate PNG */
-bool writePNG8(const std::string &path, const float *rgb, int w, int h, float gamma) {
-    std::ofstream f(path, std::ios::binary);
-    if (!f) return false;
-    const unsigned char sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
-    f.write((const char *) sig, 8);
-    std::vector<unsigned char> ihdr;
-    be32(ihdr, (uint32_t) w);
-    be32(ihdr, (uint32_t) h);
-    ihdr.insert(ihdr.end(), {8, 2, 0, 0, 0});
-    chunk(f, "IHDR", ihdr);
-    std::vector<unsigned char> raw;
-    raw.reserve((size_t) h * (1 + 3 * (size_t) w));
-    for (int y = 0; y < h; ++y) {
-        raw.push_back(0);
-        for (int x = 0; x < 3 * w; ++x) {
-            float v = std::max(0.0f, rgb[(size_t) y * w * 3 + x]);
-            if (gamma == -1.0f)
-                v = v <= 0.0031308f ? 12.92f * v : 1.055f * std::pow(v, 1.0f / 2.4f) - 0.055f;
-            else
-                v = std::pow(v, 1.0f / gamma);
-            raw.push_back((unsigned char) std::min(255, (int) (v * 255.0f + 0.5f)));
-        }
-    }
-    std::vector<unsigned char> z = {0x78, 0x01};
-    size_t pos = 0;
-    uint32_t a = 1, b = 0;
-    for (unsigned char c : raw) { a = (a + c) % 65521; b = (b + a) % 65521; }
-    while (pos < raw.size() || pos == 0) {
-        size_t n = std::min((size_t) 65535, raw.size() - pos);
-        bool last = pos + n >= raw.size();
-        z.push_back(last ? 1 : 0);
-        z.push_back((unsigned char) (n & 0xff)); z.push_back((unsigned char) (n >> 8));
-        z.push_back((unsigned char) (~n & 0xff)); z.push_back((unsigned char) ((~n >> 8) & 0xff));
-        z.insert(z.end(), raw.begin() + pos, raw.begin() + pos + n);
-        pos += n;
-        if (last) break;
-    }
-    be32(z, (b << 16) | a);
-    chunk(f, "IDAT", z);
-    chunk(f, "IEND", {});
-    return (bool) f;
-}
-
 } // namespace hpt

@@ -473,13 +473,25 @@ void parseObject(Ctx &c, const XNode &nd, SceneDesc &d) {
                 collectProps(c, k, sp);
                 d.spp = (int) num1(sp, "sampleCount", 4);
             } else if (k.tag == "film") {
-                d.film = attrS(c, k, "type");
+                FilmDesc &fd = d.film;
+                fd.type = attrS(c, k, "type");
+                if (fd.type != "ldrfilm" && fd.type != "hdrfilm")
+                    fail(c.file, k.line, "film \"" + fd.type + "\" is not supported (ldrfilm, hdrfilm)");
                 Props fp;
                 collectProps(c, k, fp);
                 d.width = (int) num1(fp, "width", 768);
                 d.height = (int) num1(fp, "height", 576);
-                d.gamma = num1(fp, "gamma", -1.0f);
-                if (fp.str.count("fileFormat")) d.fileFormat = fp.str["fileFormat"];
+                fd.gamma = num1(fp, "gamma", -1.0f);
+                fd.exposure = num1(fp, "exposure", 0.0f);
+                fd.key = num1(fp, "key", 0.18f);
+                fd.burn = num1(fp, "burn", 0.0f);
+                fd.banner = num1(fp, "banner", 1.0f) != 0.0f;
+                if (fp.str.count("fileFormat")) fd.fileFormat = fp.str["fileFormat"];
+                if (fp.str.count("pixelFormat")) fd.pixelFormat = fp.str["pixelFormat"];
+                if (fp.str.count("componentFormat")) fd.componentFormat = fp.str["componentFormat"];
+                if (fp.str.count("tonemapMethod")) fd.tonemapMethod = fp.str["tonemapMethod"];
+                std::string err;
+                if (!checkFilm(fd, err)) fail(c.file, k.line, err);
                 for (auto &fk : k.kids)
                     if (fk->tag == "rfilter") {
                         d.rfilter = attrS(c, *fk, "type");

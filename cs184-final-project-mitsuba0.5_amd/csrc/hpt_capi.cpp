@@ -644,6 +644,57 @@ int hpt_prepare(hpt_context *c) {
     return HPT_OK;
 }
 
+int hpt_get_film_params(hpt_context *c, hpt_film_params *o) {
+    if (!c || !o) return HPT_EINVAL;
+    const FilmDesc &f = c->desc.film;
+    std::memset(o, 0, sizeof(*o));
+    o->ldr = f.type == "ldrfilm";
+    o->file_format = o->ldr ? HPT_FILE_PNG
+                     : f.fileFormat == "rgbe" ? HPT_FILE_RGBE
+                     : f.fileFormat == "pfm"  ? HPT_FILE_PFM
+                                              : HPT_FILE_OPENEXR;
+    o->luminance = f.pixelFormat == "luminance";
+    o->component_format = f.componentFormat == "float32" ? HPT_COMPONENT_FLOAT32
+                          : f.componentFormat == "uint32" ? HPT_COMPONENT_UINT32
+                                                          : HPT_COMPONENT_FLOAT16;
+    o->reinhard = f.tonemapMethod == "reinhard";
+    o->gamma = f.gamma;
+    o->exposure = f.exposure;
+    o->key = f.key;
+    o->burn = f.burn;
+    o->banner = f.banner;
+    return HPT_OK;
+}
+
+int hpt_write_film(hpt_context *c, const char *path, const float *rgbw, int w, int h, const hpt_film_params *p,
+                   char *written, int cap) {
+    if (!c || !path || !rgbw || !p || w <= 0 || h <= 0) return setErr(c, HPT_EINVAL, "bad film arguments");
+    FilmDesc f;
+    f.type = p->ldr ? "ldrfilm" : "hdrfilm";
+    static const char *files[4] = {"png", "openexr", "rgbe", "pfm"};
+    static const char *comps[3] = {"float16", "float32", "uint32"};
+    if (p->file_format < 0 || p->file_format > 3 || p->component_format < 0 || p->component_format > 2)
+        return setErr(c, HPT_EINVAL, "bad film format");
+    f.fileFormat = files[p->file_format];
+    f.pixelFormat = p->luminance ? "luminance" : "rgb";
+    f.componentFormat = comps[p->component_format];
+    f.tonemapMethod = p->reinhard ? "reinhard" : "gamma";
+    f.gamma = p->gamma;
+    f.exposure = p->exposure;
+    f.key = p->key;
+    f.burn = p->burn;
+    f.banner = p->banner != 0;
+    std::string err, out;
+    FilmImage img;
+    if (!checkFilm(f, err) || !developFilm(rgbw, w, h, f, c->dataDir, img, err) || !writeFilm(path, img, f, out, err))
+        return setErr(c, HPT_EIO, err);
+    if (written && cap > 0) {
+        std::strncpy(written, out.c_str(), (size_t) cap - 1);
+        written[cap - 1] = 0;
+    }
+    return HPT_OK;
+}
+
 int hpt_get_scene_info(hpt_context *c, hpt_scene_info *o) {
     if (!c || !o) return HPT_EINVAL;
     std::memset(o, 0, sizeof(*o));

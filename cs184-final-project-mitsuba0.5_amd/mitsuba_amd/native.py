@@ -35,6 +35,16 @@ class SceneInfo(C.Structure):
                 ("bsphere_radius", C.c_float), ("n_shapes", C.c_int)]
 
 
+class FilmParams(C.Structure):
+    _fields_ = [("ldr", C.c_int), ("file_format", C.c_int), ("luminance", C.c_int), ("component_format", C.c_int),
+                ("reinhard", C.c_int), ("gamma", C.c_float), ("exposure", C.c_float), ("key", C.c_float),
+                ("burn", C.c_float), ("banner", C.c_int)]
+
+
+FILE_PNG, FILE_OPENEXR, FILE_RGBE, FILE_PFM = 0, 1, 2, 3
+COMPONENT_FLOAT16, COMPONENT_FLOAT32, COMPONENT_UINT32 = 0, 1, 2
+
+
 class RenderParams(C.Structure):
     _fields_ = [("spp_begin", C.c_int), ("spp_end", C.c_int), ("shard", C.c_int), ("n_shards", C.c_int),
                 ("max_wave_paths", C.c_uint64), ("collect_stats", C.c_int)]
@@ -74,6 +84,9 @@ SIGNATURES = {
     "hpt_render": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), _f]),
     "hpt_render_device": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]),
     "hpt_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
+    "hpt_get_film_params": (C.c_int, [C.c_void_p, C.POINTER(FilmParams)]),
+    "hpt_write_film": (C.c_int, [C.c_void_p, C.c_char_p, _f, C.c_int, C.c_int, C.POINTER(FilmParams), C.c_char_p,
+                                 C.c_int]),
     "hpt_get_hair": (C.c_int64, [C.c_void_p, _f, _u8]),
     "hpt_get_kdtree": (C.c_int, [C.c_void_p, _u32, _i64, _u32, _i64, _f]),
     "hpt_get_envmap": (C.c_int, [C.c_void_p, _f, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
@@ -246,6 +259,21 @@ class Renderer:
         st = np.zeros(n + 1, np.uint8)
         self.lib.hpt_get_hair(self.h, _p(xyz, _f), _p(st, _u8))
         return xyz, st
+
+    def film_params(self) -> FilmParams:
+        p = FilmParams()
+        self._check(self.lib.hpt_get_film_params(self.h, C.byref(p)))
+        return p
+
+    def write_film(self, path, film, params: FilmParams | None = None) -> str:
+        """Develop an accumulated (H, W, 4) film like the scene's ldrfilm / hdrfilm
+        and write it; returns the path written (extension fixed by the format)."""
+        film = _f32(film)
+        h, w = film.shape[:2]
+        p = params or self.film_params()
+        buf = C.create_string_buffer(4096)
+        self._check(self.lib.hpt_write_film(self.h, str(path).encode(), _p(film, _f), w, h, C.byref(p), buf, 4096))
+        return buf.value.decode()
 
     def kdtree(self):
         nn = C.c_int64()

@@ -141,6 +141,35 @@ typedef struct hpt_stats {
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 
+/* ---- film development (Film::develop) ----
+   ldrfilm (src/films/ldrfilm.cpp:132-190, 300-351) / hdrfilm
+   (src/films/hdrfilm.cpp:205-340, 480-537) applied to an accumulated
+   film_rgbw (as filled by hpt_render). */
+#define HPT_FILE_PNG 0
+#define HPT_FILE_OPENEXR 1
+#define HPT_FILE_RGBE 2
+#define HPT_FILE_PFM 3
+#define HPT_COMPONENT_FLOAT16 0
+#define HPT_COMPONENT_FLOAT32 1
+#define HPT_COMPONENT_UINT32 2
+typedef struct hpt_film_params {
+    int ldr;                       /* 1 ldrfilm, 0 hdrfilm */
+    int file_format;               /* HPT_FILE_* (ldrfilm: PNG; JPEG is not supported) */
+    int luminance;                 /* pixelFormat: 1 luminance, 0 rgb (no alpha channel on this path) */
+    int component_format;          /* hdrfilm: HPT_COMPONENT_* (RGBE / PFM force float32) */
+    int reinhard;                  /* ldrfilm tonemapMethod: 0 gamma, 1 reinhard */
+    float gamma;                   /* ldrfilm: -1 = sRGB */
+    float exposure, key, burn;     /* ldrfilm exposure (gamma method), Reinhard key / burn */
+    int banner;                    /* the films' "banner" property (default 1) */
+} hpt_film_params;
+/* the scene's <film> after hpt_load_scene_xml */
+int hpt_get_film_params(hpt_context *ctx, hpt_film_params *out);
+/* develop + write; the file extension is replaced by the format's own (.png,
+   .exr, .rgbe, .pfm) like the films do.  written (may be NULL) receives the
+   path actually written.  ctx is used for the data directory and errors. */
+int hpt_write_film(hpt_context *ctx, const char *path, const float *film_rgbw, int width, int height,
+                   const hpt_film_params *params, char *written, int written_capacity);
+
 /* ---- exports used by the parity tests ---- */
 /* vertex count is returned; pass NULL buffers to query the size */
 int64_t hpt_get_hair(hpt_context *ctx, float *xyz, uint8_t *starts_fiber /* n+1 */);

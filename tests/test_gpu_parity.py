@@ -9,6 +9,8 @@ Tolerances:
   - Rendered film: per-pixel L2 on linear HDR RGB, RMSE < 1e-3 relative to
     mean luminance (north_star "per-pixel L2 error < 1e-3").
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -363,3 +365,29 @@ def test_full_size_headline_frame():
     assert m["rmse"] < 1e-3
     assert m["rmse"] <= 3.0 * floor["rmse"] + 1e-6
     assert same.mean() >= floor_same - 0.05
+
+
+def test_cli_renders_and_develops(tmp_path):
+    """bin/mitsuba (mitsuba.cpp:52-400 options) on a scene: -D defines, -o with a
+    wrong extension (the ldrfilm replaces it), -x skip; the PNG equals the film
+    developed through hpt_write_film from a library render of the same scene."""
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
+    import film as ref
+    root = os.path.dirname(native.__file__)
+    cli = os.path.join(root, "..", "bin", "mitsuba")
+    xml = scene_util.scenes.make_scene("furball_marschner", str(tmp_path), n_strands=800)
+    cmd = [cli, "-D", "spp=4", "-D", "width=64", "-D", "height=48", "-o", str(tmp_path / "out.jpg"), xml]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr
+    png = tmp_path / "out.png"
+    assert png.exists()
+    r = native.Renderer(device=0)
+    r.load_scene_xml(xml, {"spp": 4, "width": 64, "height": 48})
+    r.prepare()
+    film = r.render(0, 4)
+    out = r.write_film(tmp_path / "lib.png", film)
+    np.testing.assert_array_equal(ref.read_png(str(png)), ref.read_png(out))
+    res = subprocess.run(cmd + ["-x"], capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0 and "Skipping" in res.stdout
