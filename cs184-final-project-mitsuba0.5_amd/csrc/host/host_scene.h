@@ -41,6 +41,8 @@ struct KDBuildParams {
     int maxDepth = 0;              /* 0 = automatic: min(8 + 1.3 log2 N, 48) */
     int bins = 128;                /* min-max bins */
     bool clip = true;              /* perfect splits via getClippedAABB */
+    int clipMinPrims = 0;          /* nodes with fewer primitives split boxes without clipping */
+    int exactSweepMax = 256;       /* nodes up to this size sweep every bound event, larger ones bin */
     int threads = 0;               /* 0 = hardware concurrency */
 };
 

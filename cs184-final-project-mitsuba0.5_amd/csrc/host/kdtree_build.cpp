@@ -26,6 +26,8 @@
 #include <array>
 #include <chrono>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <future>
 #include <limits>
@@ -217,8 +219,12 @@ struct SegGeom {
         return out;
     }
 
-    Box clipped(uint32_t iv, const Box &box) const {
-        Box base = aabb(iv);
+    /* getClippedAABB (hair.cpp:381-444) starting from the primitive's current
+       bounds instead of its full AABB: those already contain the segment's
+       part inside the parent cell, so the result stays conservative and
+       each level avoids re-deriving the miter ellipses */
+    Box clipped(uint32_t iv, const Box &cur, const Box &box) const {
+        Box base = cur;
         base.clip(box);
         if (!base.valid()) return base;
         V cp = vtx(iv), cd = tangent(iv);
@@ -241,6 +247,25 @@ struct Ref {
     Box b;
 };
 
+/* f(begin, end, chunk) over [0, n) in contiguous chunks, one thread each;
+   chunk order is index order, so per-chunk outputs concatenated in chunk
+   order equal the serial result */
+template <class F> void parallelChunks(size_t n, int threads, size_t minPerThread, F f) {
+    threads = (int) std::min<size_t>((size_t) std::max(1, threads), std::max<size_t>(1, n / minPerThread));
+    if (threads <= 1) {
+        f((size_t) 0, n, 0);
+        return;
+    }
+    const size_t chunk = (n + threads - 1) / threads;
+    std::vector<std::thread> th;
+    for (int t = 1; t < threads; ++t) {
+        size_t b = t * chunk, e = std::min(n, b + chunk);
+        if (b < e) th.emplace_back(f, b, e, t);
+    }
+    f((size_t) 0, std::min(n, chunk), 0);
+    for (auto &x : th) x.join();
+}
+
 struct BNode {
     int axis = -1;
     float split = 0;
@@ -254,6 +279,7 @@ struct Builder {
     const std::vector<uint32_t> &segIv;
     KDBuildParams P;
     int maxDepth;
+    int hwThreads;
 
     struct Split {
         float cost = kInf;
@@ -262,7 +288,7 @@ struct Builder {
         size_t nl = 0, nr = 0;
     };
 
-    Split findSplit(const std::vector<Ref> &refs, const Box &bounds) const {
+    Split findSplit(const std::vector<Ref> &refs, const Box &bounds, int threads) const {
         Split best;
         const size_t N = refs.size();
         const float invSA = 1.0f / bounds.area();
@@ -277,7 +303,7 @@ struct Builder {
                 if (nl == 0 || nr == 0) c *= P.emptySpaceBonus;
                 return c;
             };
-            if (N <= 256) {
+            if ((int) N <= P.exactSweepMax) {
                 /* exact sweep over primitive bound events */
                 std::vector<std::pair<float, int>> ev;
                 ev.reserve(2 * N);
@@ -306,13 +332,27 @@ struct Builder {
                 const int B = P.bins;
                 std::vector<uint32_t> minB(B, 0), maxB(B, 0);
                 float scale = B / ext;
-                for (auto &r : refs) {
-                    int a = (int) ((r.b.mn[axis] - lo) * scale), b = (int) ((r.b.mx[axis] - lo) * scale);
-                    a = std::min(std::max(a, 0), B - 1);
-                    b = std::min(std::max(b, 0), B - 1);
-                    minB[a]++;
-                    maxB[b]++;
-                }
+                /* per-chunk histograms (integer counts: the sum is order independent) */
+                const int T = std::max(1, threads);
+                std::vector<std::vector<uint32_t>> hMin(T), hMax(T);
+                parallelChunks(N, T, 1u << 16, [&](size_t b0, size_t e0, int t) {
+                    std::vector<uint32_t> &mnB = hMin[t], &mxB = hMax[t];
+                    mnB.assign(B, 0);
+                    mxB.assign(B, 0);
+                    for (size_t k = b0; k < e0; ++k) {
+                        const Ref &r = refs[k];
+                        int a = (int) ((r.b.mn[axis] - lo) * scale), b = (int) ((r.b.mx[axis] - lo) * scale);
+                        a = std::min(std::max(a, 0), B - 1);
+                        b = std::min(std::max(b, 0), B - 1);
+                        mnB[a]++;
+                        mxB[b]++;
+                    }
+                });
+                for (int t = 0; t < T; ++t)
+                    for (int i = 0; i < B && !hMin[t].empty(); ++i) {
+                        minB[i] += hMin[t][i];
+                        maxB[i] += hMax[t][i];
+                    }
                 size_t nl = 0, nEndedLeft = 0;
                 for (int i = 0; i < B - 1; ++i) {
                     nl += minB[i];
@@ -338,7 +378,10 @@ struct Builder {
         };
         if ((int) N <= P.stopPrims || depth >= maxDepth) return makeLeaf();
         float leafCost = P.queryCost * (float) N;
-        Split s = findSplit(refs, bounds);
+        /* threads for the data-parallel passes of this node: the top levels see
+           most of the primitives while few subtrees run concurrently */
+        const int threads = depth < 3 ? std::max(1, hwThreads >> depth) : 1;
+        Split s = findSplit(refs, bounds, threads);
         if (s.axis < 0) return makeLeaf();
         if (s.cost >= leafCost) {
             if ((s.cost > 4 * leafCost && N < 16) || badRefines >= P.maxBadRefines) return makeLeaf();
@@ -347,27 +390,44 @@ struct Builder {
         Box lb = bounds, rb = bounds;
         lb.mx[s.axis] = s.pos;
         rb.mn[s.axis] = s.pos;
-        std::vector<Ref> L, R;
-        L.reserve(s.nl);
-        R.reserve(s.nr);
-        for (auto &r : refs) {
-            float a = r.b.mn[s.axis], b = r.b.mx[s.axis];
-            if (b <= s.pos && !(a == b && b == s.pos)) {
-                L.push_back(r);
-            } else if (a >= s.pos) {
-                R.push_back(r);
-            } else {
-                Box cl = r.b, cr = r.b;
-                if (P.clip) {
-                    cl = g.clipped(segIv[r.seg], lb);
-                    cr = g.clipped(segIv[r.seg], rb);
+        /* partition (straddling primitives are clipped to both halves); per-chunk
+           outputs concatenated in chunk order == the serial order */
+        std::vector<std::vector<Ref>> cL(std::max(1, threads)), cR(std::max(1, threads));
+        parallelChunks(N, threads, 1u << 15, [&](size_t b0, size_t e0, int t) {
+            std::vector<Ref> &LL = cL[t], &RR = cR[t];
+            for (size_t k = b0; k < e0; ++k) {
+                const Ref &r = refs[k];
+                float a = r.b.mn[s.axis], b = r.b.mx[s.axis];
+                if (b <= s.pos && !(a == b && b == s.pos)) {
+                    LL.push_back(r);
+                } else if (a >= s.pos) {
+                    RR.push_back(r);
                 } else {
-                    cl.clip(lb);
-                    cr.clip(rb);
+                    Box cl = r.b, cr = r.b;
+                    if (P.clip && (int) N >= P.clipMinPrims) {
+                        cl = g.clipped(segIv[r.seg], r.b, lb);
+                        cr = g.clipped(segIv[r.seg], r.b, rb);
+                    } else {
+                        cl.clip(lb);
+                        cr.clip(rb);
+                    }
+                    if (cl.valid()) LL.push_back({r.seg, cl});
+                    if (cr.valid()) RR.push_back({r.seg, cr});
                 }
-                if (cl.valid()) L.push_back({r.seg, cl});
-                if (cr.valid()) R.push_back({r.seg, cr});
             }
+        });
+        std::vector<Ref> L, R;
+        if (cL.size() == 1) {
+            L.swap(cL[0]);
+            R.swap(cR[0]);
+        } else {
+            size_t nl = 0, nr = 0;
+            for (auto &v : cL) nl += v.size();
+            for (auto &v : cR) nr += v.size();
+            L.reserve(nl);
+            R.reserve(nr);
+            for (auto &v : cL) L.insert(L.end(), v.begin(), v.end());
+            for (auto &v : cR) R.insert(R.end(), v.begin(), v.end());
         }
         std::vector<Ref>().swap(refs);
         node->axis = s.axis;
@@ -564,10 +624,15 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
     /* primitive bounds + tree AABB (gkdtree.h:990-994) */
     std::vector<Ref> refs(S);
     Box root;
-    for (size_t s = 0; s < S; ++s) {
-        refs[s].seg = (uint32_t) s;
-        refs[s].b = g.aabb(segIv[s]);
-        root.expand(refs[s].b);
+    {
+        const int hw0 = params.threads > 0 ? params.threads : (int) std::max(1u, std::thread::hardware_concurrency());
+        parallelChunks(S, std::min(hw0, 64), 1u << 14, [&](size_t b0, size_t e0, int) {
+            for (size_t s = b0; s < e0; ++s) {
+                refs[s].seg = (uint32_t) s;
+                refs[s].b = g.aabb(segIv[s]);
+            }
+        });
+        for (size_t s = 0; s < S; ++s) root.expand(refs[s].b);
     }
     for (int i = 0; i < 3; ++i) {
         t.aabbMin[i] = root.mn[i];
@@ -581,11 +646,18 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
     int lg = 0;
     while ((S >> (lg + 1)) != 0) lg++;
     const int autoDepth = std::min((int) (8 + 1.3f * lg), 48);
-    Builder b{g, segIv, params, params.maxDepth > 0 ? std::min(params.maxDepth, 64) : autoDepth};
+    const int hw = params.threads > 0 ? params.threads : (int) std::max(1u, std::thread::hardware_concurrency());
+    Builder b{g, segIv, params, params.maxDepth > 0 ? std::min(params.maxDepth, 64) : autoDepth, std::min(hw, 64)};
+    auto tb = std::chrono::steady_clock::now();
     std::unique_ptr<BNode> tree = b.build(std::move(refs), root, 0, 0);
+    auto tl = std::chrono::steady_clock::now();
     t.nodes.reserve(2 * S);
     layoutTreelets(tree.get(), t);
     buildNode4(tree.get(), t);
+    if (std::getenv("HPT_KD_TIMING"))
+        std::fprintf(stderr, "kd: bounds %.3f s, build %.3f s, layout %.3f s\n",
+                     std::chrono::duration<double>(tb - t0).count(), std::chrono::duration<double>(tl - tb).count(),
+                     std::chrono::duration<double>(std::chrono::steady_clock::now() - tl).count());
     /* leaf-ordered fp32 pre-test records */
     t.leafF.resize(t.prims.size());
     for (size_t e = 0; e < t.prims.size(); ++e) {

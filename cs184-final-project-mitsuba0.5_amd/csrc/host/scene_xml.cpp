@@ -526,6 +526,9 @@ void parseObject(Ctx &c, const XNode &nd, SceneDesc &d) {
             d.kd.maxDepth = (int) num1(p, "kdMaxDepth", (float) d.kd.maxDepth);
             d.kd.maxBadRefines = (int) num1(p, "kdMaxBadRefines", (float) d.kd.maxBadRefines);
             d.kd.clip = num1(p, "kdClip", d.kd.clip ? 1.0f : 0.0f) != 0.0f;
+            /* build-speed knobs of this builder (no reference counterpart) */
+            d.kd.clipMinPrims = (int) num1(p, "kdClipMinPrims", (float) d.kd.clipMinPrims);
+            d.kd.exactSweepMax = (int) num1(p, "kdExactSweepMax", (float) d.kd.exactSweepMax);
         }
         if (p.xform.count("toWorld")) {
             parseTransform(c, *p.xform["toWorld"], h.toWorld);

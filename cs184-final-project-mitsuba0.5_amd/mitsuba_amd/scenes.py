@@ -215,7 +215,7 @@ def make_scene(name: str, workdir: str, n_strands: int | None = None, **override
     return path
 
 
-_KD_INT = ("kdStopPrims", "kdMaxDepth", "kdMaxBadRefines")
+_KD_INT = ("kdStopPrims", "kdMaxDepth", "kdMaxBadRefines", "kdClipMinPrims", "kdExactSweepMax")
 
 
 def with_kd_params(xml: str, kd: dict, tag: str = "kd") -> str:
