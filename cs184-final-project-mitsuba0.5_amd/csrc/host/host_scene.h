@@ -93,6 +93,7 @@ struct SceneDesc {
     /* sampler */
     std::string sampler = "sobol";
     int spp = 4;
+    uint64_t scramble = 0;                         /* sobol "scramble" property */
     /* film */
     int width = 768, height = 576;
     FilmDesc film;

@@ -471,6 +471,9 @@ void parseObject(Ctx &c, const XNode &nd, SceneDesc &d) {
                     fail(c.file, k.line, "sampler \"" + d.sampler + "\" is not supported (only \"sobol\")");
                 Props sp;
                 collectProps(c, k, sp);
+                for (auto &sk : k.kids) /* an exact 64-bit integer (Properties::getSize) */
+                    if (sk->tag == "integer" && attrS(c, *sk, "name") == "scramble")
+                        d.scramble = std::stoull(attrS(c, *sk, "value"));
                 d.spp = (int) num1(sp, "sampleCount", 4);
             } else if (k.tag == "film") {
                 FilmDesc &fd = d.film;

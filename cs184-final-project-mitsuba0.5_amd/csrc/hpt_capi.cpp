@@ -298,6 +298,13 @@ int hpt_set_sampler(hpt_context *c, int spp) {
     return HPT_OK;
 }
 
+int hpt_set_sampler_scramble(hpt_context *c, uint64_t scramble) {
+    if (!c) return HPT_EINVAL;
+    c->desc.scramble = scramble;
+    c->prepared = false;
+    return HPT_OK;
+}
+
 int hpt_set_integrator(hpt_context *c, int max_depth, int rr_depth, int strict_normals, int hide_emitters) {
     if (!c) return HPT_EINVAL;
     if (max_depth > 250) return setErr(c, HPT_EINVAL, "maxDepth > 250 exceeds the Sobol dimension table");
@@ -627,6 +634,16 @@ int hpt_prepare(hpt_context *c) {
         E.bsRadius = std::max(1e-4f, radius * 1.5f);
     }
     r |= upload(c, c->sobol32.data(), c->sobol32.size() * 4, (const void **) &sc.sobol);
+    sc.scramble = 0;
+    if (d.scramble) { /* sobol.cpp:96-102: sampleTEA of the two 32-bit halves (qmc.h:146-156) */
+        uint32_t v0 = (uint32_t) d.scramble, v1 = (uint32_t) (d.scramble >> 32), sum = 0;
+        for (int i = 0; i < 4; ++i) {
+            sum += 0x9e3779b9u;
+            v0 += ((v1 << 4) + 0xA341316Cu) ^ (v1 + sum) ^ ((v1 >> 5) + 0xC8013EA4u);
+            v1 += ((v0 << 4) + 0xAD90777Du) ^ (v0 + sum) ^ ((v0 >> 5) + 0x7E95761Eu);
+        }
+        sc.scramble = v0; /* sampleSingle / look_up use the low 32 bits */
+    }
     r |= upload(c, c->vdc.data(), c->vdc.size() * 8, (const void **) &sc.vdc);
     r |= upload(c, c->vdcInv.data(), c->vdcInv.size() * 8, (const void **) &sc.vdcInv);
     if (r) return HPT_EDEVICE;

@@ -184,6 +184,7 @@ struct HptScene {
     const HptBsdf *bsdfs;
     HptEnvMap env;
     const uint32_t *sobol;      /* 1024 x 52 */
+    uint32_t scramble;          /* low 32 bits of sampleTEA(scramble) (sobol.cpp:92-102), 0 = off */
     const uint64_t *vdc;        /* rows x 52 */
     const uint64_t *vdcInv;     /* rows x 52 */
     float tent[HPT_FILTER_RES + 1];

@@ -54,7 +54,7 @@ namespace {
 /* sobol.cpp:204-250 (setSampleIndex / next1D / next2D)                 */
 /* ------------------------------------------------------------------ */
 HD float sobolSample(const HptScene &sc, uint64_t index, uint32_t dim) {
-    uint32_t result = 0;
+    uint32_t result = sc.scramble;
     const uint32_t *m = sc.sobol + dim * HPT_SOBOL_BITS;
     uint32_t lo = (uint32_t) index, hi = (uint32_t) (index >> 32);
     for (int i = 0; lo; lo >>= 1, ++i)
@@ -76,7 +76,7 @@ HD float sobolSampleUniform(const HptScene &sc, uint64_t index, uint32_t dim) {
     if (__ballot(dim != d0) != 0) return sobolSample(sc, index, dim);
     const uint32_t *__restrict__ m = sc.sobol + d0 * HPT_SOBOL_BITS;
     const uint32_t lo = (uint32_t) index, hi = (uint32_t) (index >> 32);
-    uint32_t result = 0;
+    uint32_t result = sc.scramble;
 #pragma unroll
     for (int i = 0; i < 32; ++i) result ^= ((lo >> i) & 1u) ? m[i] : 0u;
     if (__ballot(hi != 0) != 0) {
@@ -93,7 +93,8 @@ HD uint64_t sobolLookUp(const HptScene &sc, uint32_t m, uint32_t frame, uint32_t
     const uint64_t *inv = sc.vdcInv + (m - 1) * HPT_SOBOL_BITS;
     for (uint32_t c = 0; frame; frame >>= 1, ++c)
         if (frame & 1u) delta ^= vdc[c];
-    uint64_t b = (((uint64_t) px << m) | py) ^ delta;
+    const uint32_t sm = sc.scramble >> (32 - m); /* (scramble & 0xFFFFFFFF) >> (32 - m), m >= 1 */
+    uint64_t b = (((uint64_t) (px ^ sm) << m) | (py ^ sm)) ^ delta;
     for (uint32_t c = 0; b; b >>= 1, ++c)
         if (b & 1u) index ^= inv[c];
     return index;

@@ -69,6 +69,7 @@ SIGNATURES = {
     "hpt_load_scene_xml": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]),
     "hpt_set_camera": (C.c_int, [C.c_void_p, _f, C.c_float, C.c_int, C.c_int, C.c_float, C.c_float]),
     "hpt_set_sampler": (C.c_int, [C.c_void_p, C.c_int]),
+    "hpt_set_sampler_scramble": (C.c_int, [C.c_void_p, C.c_uint64]),
     "hpt_set_integrator": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
     "hpt_set_hair_file": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_float, _f]),
     "hpt_set_hair_vertices": (C.c_int, [C.c_void_p, _f, _u8, C.c_uint64, C.c_float]),
@@ -172,6 +173,9 @@ class Renderer:
 
     def set_sampler(self, spp):
         self._check(self.lib.hpt_set_sampler(self.h, spp))
+
+    def set_scramble(self, scramble: int):
+        self._check(self.lib.hpt_set_sampler_scramble(self.h, scramble))
 
     def set_integrator(self, max_depth, rr_depth=5, strict_normals=True, hide_emitters=False):
         self._check(self.lib.hpt_set_integrator(self.h, max_depth, rr_depth, int(strict_normals), int(hide_emitters)))

@@ -59,6 +59,8 @@ int hpt_set_camera(hpt_context *ctx, const float to_world[16], float fov_x_deg, 
                    float near_clip, float far_clip);
 /* SobolSampler sampleCount (src/samplers/sobol.cpp:80-106) */
 int hpt_set_sampler(hpt_context *ctx, int sample_count);
+/* SobolSampler "scramble" (sobol.cpp:92-102); 0 = unscrambled (the default) */
+int hpt_set_sampler_scramble(hpt_context *ctx, uint64_t scramble);
 /* MonteCarloIntegrator params (src/librender/integrator.cpp:190-203) */
 int hpt_set_integrator(hpt_context *ctx, int max_depth, int rr_depth, int strict_normals, int hide_emitters);
 /* HairShape(Properties) (src/shapes/hair.cpp:609-785); to_world may be NULL */

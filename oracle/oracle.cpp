@@ -1640,6 +1640,7 @@ struct orc_scene {
     std::string err;
     /* sobol */
     std::vector<uint32_t> m32;
+    uint64_t scramble = 0; /* after sampleTEA */
     std::vector<uint64_t> vdc, vdcInv;
     int vdcRows = 0, invRows = 0;
     /* camera */
@@ -1668,7 +1669,7 @@ namespace {
 
 /* ---------------- Sobol: sobolseq.h:43-58, 99-131; sobol.cpp:204-250 ---------------- */
 inline float sobolSample(const orc_scene *s, uint64_t index, uint32_t dim) {
-    uint32_t result = 0;
+    uint32_t result = (uint32_t) s->scramble; /* sobolseq.h:43-58 with (uint32_t) scramble */
     for (uint32_t i = dim * 52; index; index >>= 1, ++i)
         if (index & 1)
             result ^= s->m32[i];
@@ -1682,7 +1683,7 @@ inline uint64_t sobolLookUp(const orc_scene *s, uint32_t m, uint32_t frame, uint
     for (uint32_t c = 0; frame; frame >>= 1, ++c)
         if (frame & 1)
             delta ^= s->vdc[(m - 1) * 52 + c];
-    uint64_t scramble = 0;
+    uint64_t scramble = (s->scramble & 0xFFFFFFFF) >> (32 - m); /* sobolseq.h:119-123 */
     uint64_t b = (((uint64_t) (px ^ scramble) << m) | (py ^ scramble)) ^ delta;
     for (uint32_t c = 0; b; b >>= 1, ++c)
         if (b & 1)
@@ -2234,6 +2235,25 @@ int orc_set_sobol(orc_scene *s, const uint32_t *m32, const uint64_t *vdc, int vd
     s->vdcInv.assign(vdc_inv, vdc_inv + (size_t) inv_rows * 52);
     s->vdcRows = vdc_rows;
     s->invRows = inv_rows;
+    return 0;
+}
+
+int orc_set_sobol_scramble(orc_scene *s, uint64_t scramble) { /* sobol.cpp:92-102 */
+    s->scramble = 0;
+    if (scramble) {
+        union {
+            uint64_t ui64;
+            uint32_t v[2];
+        } u = {scramble};
+        /* qmc.h:146-156 sampleTEA(v0, v1, 4) */
+        uint32_t v0 = u.v[0], v1 = u.v[1], sum = 0;
+        for (int i = 0; i < 4; ++i) {
+            sum += 0x9e3779b9;
+            v0 += ((v1 << 4) + 0xA341316C) ^ (v1 + sum) ^ ((v1 >> 5) + 0xC8013EA4);
+            v1 += ((v0 << 4) + 0xAD90777D) ^ (v0 + sum) ^ ((v0 >> 5) + 0x7E95761E);
+        }
+        s->scramble = ((uint64_t) v1 << 32) + v0;
+    }
     return 0;
 }
 

@@ -37,6 +37,8 @@ const char *orc_last_error(orc_scene *s);
 int orc_set_sobol(orc_scene *s, const uint32_t *m32, const uint64_t *vdc, int vdc_rows,
                   const uint64_t *vdc_inv, int inv_rows);
 /* perspective.cpp:125-165: toWorld row-major 4x4, x field of view in degrees */
+/* sobol.cpp:92-102: the sampler's raw "scramble" property (TEA applied inside) */
+int orc_set_sobol_scramble(orc_scene *s, uint64_t scramble);
 int orc_set_camera(orc_scene *s, const float to_world[16], float fov_x_deg, int width,
                    int height, float near_clip, float far_clip);
 /* hair.cpp:609-785 loader restatement (BINARY_HAIR or ASCII); to_world may be NULL.

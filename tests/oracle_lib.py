@@ -41,6 +41,7 @@ _SIG = {
     "orc_set_marschnerdielectric": (C.c_int, [C.c_void_p, C.c_float, _f, _f, _f]),
     "orc_set_thindielectric": (C.c_int, [C.c_void_p, C.c_float, _f, _f]),
     "orc_set_diffuse": (C.c_int, [C.c_void_p, _f]),
+    "orc_set_sobol_scramble": (C.c_int, [C.c_void_p, C.c_uint64]),
     "orc_set_roughplastic": (C.c_int, [C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_int, C.c_int, _f, _f,
                                        C.c_char_p]),
     "orc_set_envmap": (C.c_int, [C.c_void_p, _f, C.c_int, C.c_int, C.c_float, _f]),

@@ -391,3 +391,34 @@ def test_cli_renders_and_develops(tmp_path):
     np.testing.assert_array_equal(ref.read_png(str(png)), ref.read_png(out))
     res = subprocess.run(cmd + ["-x"], capture_output=True, text=True, timeout=300)
     assert res.returncode == 0 and "Skipping" in res.stdout
+
+
+def test_sobol_scramble_render(tmp_path):
+    """SobolSampler 'scramble' (sobol.cpp:92-102): TEA of the property, XORed
+    into every sample and into the pixel look-up (sobolseq.h:43-58, 99-131)."""
+    xml, r, o = scene_util.make("straight_kk", 800, 40, 32, 4, device=0)
+    src = open(xml).read().replace('<integer name="sampleCount" value="$spp"/>',
+                                   '<integer name="sampleCount" value="$spp"/><integer name="scramble" value="987654321987"/>')
+    path = tmp_path / "scr.xml"
+    path.write_text(src.replace('value="straight_', 'value="' + scene_util.WORK + '/straight_'))
+    r2 = native.Renderer(device=0)
+    r2.load_scene_xml(str(path), {"width": 40, "height": 32, "spp": 4})
+    r2.prepare()
+    o.check(o.lib.orc_set_sobol_scramble(o.s, 987654321987))
+    rng = np.random.default_rng(2)
+    n = 5000
+    frame = rng.integers(0, 64, n).astype(np.uint32)
+    px = rng.integers(0, 32, n).astype(np.uint32)
+    py = rng.integers(0, 32, n).astype(np.uint32)
+    dim = rng.integers(0, 300, n).astype(np.uint32)
+    gi, gv = r2.sobol(6, frame, px, py, dim)
+    oi = o.sobol_lookup(6, frame, px, py)
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_array_equal(gv, o.sobol_sample(oi, dim))
+    gi0, _ = r.sobol(6, frame, px, py, dim)
+    assert np.mean(gi0 != gi) > 0.5  # the scramble changes the sample set
+    film = r2.render(0, 4)
+    ofilm, _ = o.render(0, 4, width=40, height=32)
+    m = scene_util.l2_metrics(native.develop(ofilm), native.develop(film))
+    assert m["rmse"] < 1e-3, m
+    o.check(o.lib.orc_set_sobol_scramble(o.s, 0))
