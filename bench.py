@@ -6,7 +6,7 @@ the Marschner BSDF, 512x512 @ 256 spp, maxDepth 65, synthetic furball hair
 (40,000 strands, ~3.2e5 segments, seed 1), sunsky stand-in lighting.
 One step = one full frame: every sample of every pixel traced to
 termination (MIPathTracer::Li, path.cpp:119-294) and splatted into the film.
-With N GPUs the frame's 32x32 blocks are dealt block-cyclically to ranks and
+With N GPUs the frame's 32x32 blocks are dealt cyclically along a Hilbert curve to ranks and
 the RGBW films are summed on rank 0 with one RCCL reduce (strong scaling).
 
 Launch:  python bench.py [--gpus 1 --steps 3 --warmup 1]

@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <stdexcept>
@@ -35,8 +36,16 @@ struct DevBuf {
     size_t bytes = 0;
 };
 
+/* live paths below which a frame's remaining bounces run as one k_tail
+   launch (HPT_TAIL_PATHS overrides; 0 keeps the per-bounce launches) */
+static uint32_t defaultTailPaths() {
+    const char *v = std::getenv("HPT_TAIL_PATHS");
+    return v ? (uint32_t) std::strtoul(v, nullptr, 10) : (1u << 17);
+}
+
 struct hpt_context {
     int device = 0;
+    uint32_t tailPaths = defaultTailPaths();
     hipStream_t stream = nullptr;
     std::string err;
     std::string dataDir;
@@ -65,6 +74,10 @@ struct hpt_context {
     uint64_t *dstats = nullptr;
     float4 *partial = nullptr;     /* film splat partials: slots x 9 (k_splat -> k_gather) */
     uint64_t partialSlots = 0;
+    /* block ownership of the last render call's shard (blockOf / localOf of HptWave) */
+    uint32_t *dBlockOf = nullptr;
+    int32_t *dLocalOf = nullptr;
+    int ownW = -1, ownH = -1, ownShard = -1, ownShards = -1, ownCap = 0, ownLocal = 0;
     hpt_stats stats;
     std::vector<hipEvent_t> evPool;
 };
@@ -171,7 +184,7 @@ int ensureWave(hpt_context *c, uint64_t n) {
     r |= alloc(n * 4, (void **) &c->qShadeA);
     r |= alloc(n * 4, (void **) &c->qShadeB);
     r |= alloc(HPT_COUNTER_WORDS * 4, (void **) &c->counters);
-    r |= alloc(8 * 8, (void **) &c->dstats);
+    r |= alloc(16 * 8, (void **) &c->dstats);
     if (r) return HPT_EDEVICE;
     c->capacity = n;
     return HPT_OK;
@@ -235,6 +248,8 @@ void hpt_context_destroy(hpt_context *c) {
     freeBufs(c->sceneBufs);
     freeBufs(c->waveBufs);
     if (c->partial) (void) hipFree(c->partial);
+    if (c->dBlockOf) (void) hipFree(c->dBlockOf);
+    if (c->dLocalOf) (void) hipFree(c->dLocalOf);
     for (auto e : c->evPool) (void) hipEventDestroy(e);
     (void) hipStreamDestroy(c->stream);
     delete c;
@@ -740,6 +755,66 @@ int hpt_get_scene_info(hpt_context *c, hpt_scene_info *o) {
     return HPT_OK;
 }
 
+/* Image blocks in Hilbert-curve order over the nbx x nby grid of 32x32
+   blocks.  Shard r of N owns every N-th block of this order (r, r+N, ...):
+   N consecutive blocks of the curve are a compact patch of the image, so
+   every shard gets one block of every patch and the hair's uneven screen
+   coverage spreads evenly over the ranks (a plain b mod N deal gives
+   whole block columns to a rank whenever N divides nbx). */
+static std::vector<uint32_t> blockOrder(int nbx, int nby) {
+    uint32_t n = 1;
+    while (n < (uint32_t) std::max(nbx, nby)) n <<= 1;
+    std::vector<uint32_t> order;
+    order.reserve((size_t) nbx * nby);
+    for (uint64_t d = 0; d < (uint64_t) n * n; ++d) {
+        uint32_t x = 0, y = 0;
+        uint64_t t = d;
+        for (uint32_t sq = 1; sq < n; sq <<= 1) { /* Hilbert index -> (x, y) */
+            const uint32_t rx = 1u & (uint32_t) (t / 2), ry = 1u & (uint32_t) (t ^ rx);
+            if (ry == 0) {
+                if (rx == 1) {
+                    x = sq - 1 - x;
+                    y = sq - 1 - y;
+                }
+                std::swap(x, y);
+            }
+            x += sq * rx;
+            y += sq * ry;
+            t /= 4;
+        }
+        if ((int) x < nbx && (int) y < nby) order.push_back(y * (uint32_t) nbx + x);
+    }
+    return order;
+}
+
+/* upload this shard's block ownership tables (cached per frame shape and shard) */
+static int ensureOwnership(hpt_context *c, int W, int H, int nbx, int nby, int shard, int nShards) {
+    if (c->ownW == W && c->ownH == H && c->ownShard == shard && c->ownShards == nShards) return HPT_OK;
+    const std::vector<uint32_t> order = blockOrder(nbx, nby);
+    std::vector<uint32_t> blockOf;
+    std::vector<int32_t> localOf(order.size(), -1);
+    for (size_t i = (size_t) shard; i < order.size(); i += (size_t) nShards) {
+        localOf[order[i]] = (int32_t) blockOf.size();
+        blockOf.push_back(order[i]);
+    }
+    const int n = (int) order.size();
+    if (n > c->ownCap) {
+        if (c->dBlockOf) (void) hipFree(c->dBlockOf);
+        if (c->dLocalOf) (void) hipFree(c->dLocalOf);
+        c->dBlockOf = nullptr;
+        c->dLocalOf = nullptr;
+        c->ownCap = 0;
+        HIPCHK(c, hipMalloc((void **) &c->dBlockOf, n * sizeof(uint32_t)));
+        HIPCHK(c, hipMalloc((void **) &c->dLocalOf, n * sizeof(int32_t)));
+        c->ownCap = n;
+    }
+    if (!blockOf.empty())
+        HIPCHK(c, hipMemcpy(c->dBlockOf, blockOf.data(), blockOf.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemcpy(c->dLocalOf, localOf.data(), localOf.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    c->ownW = W, c->ownH = H, c->ownShard = shard, c->ownShards = nShards, c->ownLocal = (int) blockOf.size();
+    return HPT_OK;
+}
+
 static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFilm) {
     if (c->device == HPT_HOST_ONLY) return setErr(c, HPT_EDEVICE, "host-only context cannot render");
     if (!c->prepared) return setErr(c, HPT_ESTATE, "hpt_prepare() must succeed before rendering");
@@ -749,8 +824,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     const int nbx = (W + HPT_BLOCK - 1) / HPT_BLOCK, nby = (H + HPT_BLOCK - 1) / HPT_BLOCK;
     const int nShards = std::max(1, prm->n_shards), shard = prm->shard;
     if (shard < 0 || shard >= nShards) return setErr(c, HPT_EINVAL, "bad shard");
-    const int nBlocks = nbx * nby;
-    const int localBlocks = nBlocks > shard ? (nBlocks - shard + nShards - 1) / nShards : 0;
+    if (int r0 = ensureOwnership(c, W, H, nbx, nby, shard, nShards)) return r0;
+    const int localBlocks = c->ownLocal;
     const uint64_t slots = (uint64_t) localBlocks * 1024u;
     const int sppBegin = prm->spp_begin, sppEnd = prm->spp_end;
     if (sppEnd < sppBegin || sppBegin < 0) return setErr(c, HPT_EINVAL, "bad spp range");
@@ -772,7 +847,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     hipStream_t s = c->stream;
     const bool st = prm->collect_stats != 0;      /* HIP event timing per kernel class */
     const bool counted = prm->collect_stats >= 2; /* + traversal counters (k_trace_counted) */
-    if (counted) HIPCHK(c, hipMemsetAsync(c->dstats, 0, 64, s));
+    if (counted) HIPCHK(c, hipMemsetAsync(c->dstats, 0, 128, s));
     std::vector<std::pair<hipEvent_t, hipEvent_t>> evTrace, evOther[6];
     size_t evUsed = 0;
     auto timed = [&](int cls, auto fn) -> hipError_t {
@@ -789,6 +864,25 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     HIPCHK(c, hipHostMalloc((void **) &hostCnt, HPT_Q_COUNT * 4, hipHostMallocDefault));
     uint64_t bounces = 0;
     int maxB = 0;
+    /* HPT_TRACE_REPORT=1 with counters on: per-launch traversal counters on stderr */
+    const bool perLaunch = counted && std::getenv("HPT_TRACE_REPORT") != nullptr;
+    uint64_t prevSt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto reportLaunch = [&](const char *what) {
+        if (!perLaunch) return;
+        uint64_t hs[16];
+        if (hipMemcpyAsync(hs, c->dstats, 128, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess || hipMemsetAsync(c->dstats + 8, 0, 64, s) != hipSuccess)
+            return;
+        uint64_t d[8];
+        for (int i = 0; i < 8; ++i) d[i] = hs[i] - prevSt[i], prevSt[i] = hs[i];
+        const double rays = (double) (d[2] + d[3]);
+        std::fprintf(stderr, "[trace] %-8s closest %10llu shadow %10llu nodes/ray %6.2f prims/ray %6.2f exact/ray %5.2f "
+                     "util nodes %.3f prims %.3f | max rounds %llu max restarts %llu restarted rays %llu restarts %llu\n", what, (unsigned long long) d[2], (unsigned long long) d[3],
+                     d[0] / std::max(1.0, rays), d[1] / std::max(1.0, rays), d[5] / std::max(1.0, rays),
+                     d[0] / std::max(1.0, (double) d[6]), d[1] / std::max(1.0, (double) d[7]),
+                     (unsigned long long) hs[8], (unsigned long long) hs[9], (unsigned long long) hs[10],
+                     (unsigned long long) hs[11]);
+    };
     hipError_t e = hipSuccess;
     for (int j0 = sppBegin; j0 < sppEnd && e == hipSuccess; j0 += (int) nSpp) {
         HptWave w;
@@ -800,6 +894,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         w.nbx = nbx;
         w.shard = shard;
         w.nShards = nShards;
+        w.blockOf = c->dBlockOf;
+        w.localOf = c->dLocalOf;
         c->stats.waves++;
         HIPCHK(c, hipMemsetAsync(c->counters, 0, HPT_COUNTER_WORDS * 4, s));
         e = timed(0, [&] { return hpt_launch_camera(sc, w, c->P, c->qTrace, c->counters, s); });
@@ -809,6 +905,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                                     counted ? (uint32_t *) c->dstats : nullptr, w.nPaths, s);
         });
         if (e) break;
+        reportLaunch("camera");
         e = timed(1, [&] { return hpt_launch_primary(sc, c->P, c->qTrace, c->qShadeA, c->counters, w.nPaths, s); });
         if (e) break;
         e = hpt_launch_rotate(c->counters, s);
@@ -823,6 +920,18 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             if (n == 0) break;
             bounces += n;
             ++bounce;
+            if (n < c->tailPaths) {
+                /* few live paths: finish them all in one launch (k_tail) */
+                e = timed(5, [&] { return hpt_launch_tail(sc, c->P, shadeIn, c->counters, n, s); });
+                if (e) break;
+                e = hipMemcpyAsync(hostCnt, c->counters, HPT_Q_COUNT * 4, hipMemcpyDeviceToHost, s);
+                if (e) break;
+                e = hipStreamSynchronize(s);
+                if (e) break;
+                bounces += hostCnt[HPT_Q_TAIL_BOUNCES] - n; /* k_tail counts its first bounce too */
+                c->stats.tail_paths += n;
+                break;
+            }
             e = timed(2, [&] { return hpt_launch_shade(sc, c->P, shadeIn, c->qTrace, c->qShadow, c->counters, n, s); });
             if (e) break;
             e = timed(-1, [&] {
@@ -830,6 +939,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                                         counted ? (uint32_t *) c->dstats : nullptr, 2ull * n, s);
             });
             if (e) break;
+            reportLaunch("bounce");
             e = timed(3, [&] { return hpt_launch_post(sc, c->P, c->qTrace, shadeOut, c->counters, n, s); });
             if (e) break;
             e = hpt_launch_rotate(c->counters, s);
@@ -867,6 +977,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         c->stats.ms_shade = sumEv(evOther[2]);
         c->stats.ms_post = sumEv(evOther[3]);
         c->stats.ms_gather = sumEv(evOther[4]);
+        c->stats.ms_tail = sumEv(evOther[5]);
     }
     if (counted) {
         uint64_t hs[8];

@@ -14,6 +14,7 @@
 #define HPT_Q_SHADE_IN 2
 #define HPT_Q_SHADE_OUT 3
 #define HPT_Q_ERROR 4     /* set when a path runs out of Sobol dimensions */
+#define HPT_Q_TAIL_BOUNCES 5 /* path-bounces shaded inside k_tail */
 #define HPT_Q_COUNT 8
 /* k_trace work cursors (persistent waves claim rays from them), one per
    128-byte line, stored after the queue counters in the same buffer */
@@ -30,6 +31,8 @@ struct HptWave {
     uint32_t sppBegin, nSpp;
     int width, height, nbx;
     int shard, nShards;
+    const uint32_t *blockOf; /* this shard's k-th 32x32 block -> image block index (by * nbx + bx) */
+    const int32_t *localOf;  /* image block index -> k, or -1 when another shard owns it */
 };
 
 /* path state, structure of arrays in HBM (16-byte rows where possible) */
@@ -58,6 +61,9 @@ hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint3
                               uint32_t *counters, uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *traceQ,
                             uint32_t *shadowQ, uint32_t *counters, uint64_t maxItems, hipStream_t s);
+/* the rest of every live path (shade queue) to termination in one launch */
+hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *counters,
+                           uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
                            uint32_t *counters, uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_rotate(uint32_t *counters, hipStream_t s);

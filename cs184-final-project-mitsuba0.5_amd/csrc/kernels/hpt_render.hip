@@ -607,6 +607,15 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
     TraceRay r;
     TraceCounters tc;
     uint32_t item = 0, nC = 0, nS = 0, nU = 0;
+    uint32_t maxRounds = 0, maxRestarts = 0, restartRays = 0, restarts = 0; /* STATS: per-ray tails */
+    auto rayDone = [&](const TraceRay &q) {
+        if (STATS) {
+            maxRounds = max(maxRounds, (uint32_t) q.leaves);
+            maxRestarts = max(maxRestarts, (uint32_t) q.restarts);
+            restartRays += q.restarts > 0 ? 1u : 0u;
+            restarts += (uint32_t) q.restarts;
+        }
+    };
     bool active = false, exhausted = false;
 #if HPT_XCD_SHARDS
     /* XCD-aware claiming: the 64 shards are 8 groups of 8 contiguous
@@ -660,7 +669,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
                         nC += r.shadow ? 0u : 1u;
                         nS += r.shadow ? 1u : 0u;
                     }
-                    if (!active) nU += io.finish(sc, k, r);
+                    if (!active) nU += io.finish(sc, k, r), rayDone(r);
                 }
             }
         }
@@ -670,6 +679,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
         }
         if (active && traceRound<STACK, STATS>(sc, r, stk, (int) blockDim.x, tc)) {
             nU += io.finish(sc, item, r);
+            rayDone(r);
             active = false;
         }
     }
@@ -689,6 +699,10 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             nC += __shfl_down(nC, off);
             nS += __shfl_down(nS, off);
             nU += __shfl_down(nU, off);
+            maxRounds = max(maxRounds, (uint32_t) __shfl_down(maxRounds, off));
+            maxRestarts = max(maxRestarts, (uint32_t) __shfl_down(maxRestarts, off));
+            restartRays += __shfl_down(restartRays, off);
+            restarts += __shfl_down(restarts, off);
         }
         if (lane == 0) {
             unsigned long long *st = (unsigned long long *) stats;
@@ -700,6 +714,12 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             atomicAdd(&st[5], (unsigned long long) tc.exact);
             atomicAdd(&st[6], (unsigned long long) tc.nodeSlots);
             atomicAdd(&st[7], (unsigned long long) tc.primSlots);
+            /* [8]/[9] max rounds (leaves visited) / kd-restarts of one ray, [10] rays that
+               restarted, [11] restarts */
+            atomicMax(&st[8], (unsigned long long) maxRounds);
+            atomicMax(&st[9], (unsigned long long) maxRestarts);
+            atomicAdd(&st[10], (unsigned long long) restartRays);
+            atomicAdd(&st[11], (unsigned long long) restarts);
         }
     }
 }
@@ -1455,12 +1475,12 @@ HD void qpush(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
 /* ================================================================== */
 
 /* Decode a path id of the current wave: id = slot * nSpp + (j - sppBegin),
-   slot enumerates the 32x32 blocks owned by this shard in block order. */
+   slot = (k-th block owned by this shard) << 10 | pixel within the block. */
 HD bool decodePath(const HptWave &w, uint32_t id, int &px, int &py, uint32_t &j) {
     uint32_t slot = id / w.nSpp;
     j = w.sppBegin + (id - slot * w.nSpp);
     uint32_t lb = slot >> 10, inner = slot & 1023u;
-    uint32_t b = lb * w.nShards + w.shard;
+    uint32_t b = w.blockOf[lb];
     px = (int) ((b % w.nbx) * HPT_BLOCK + (inner & 31u));
     py = (int) ((b / w.nbx) * HPT_BLOCK + (inner >> 5));
     return px < w.width && py < w.height;
@@ -1628,15 +1648,9 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
    separate kernel, so the single-shape one never mixes a kernel-argument
    pointer with a global one -- that would copy the scene to scratch) */
 template <bool MULTI>
-__device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
-                                            uint32_t *__restrict__ traceQ, uint32_t *__restrict__ shadowQ,
-                                            uint32_t *__restrict__ counters) {
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = counters[HPT_Q_SHADE_IN];
-    bool cont = false, shadow = false;
-    uint32_t id = 0;
-    if (tid < n) {
-        id = shadeQ[tid];
+HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__restrict__ counters, bool &cont,
+                  bool &shadow) {
+    {
         uint32_t st = P.state[id];
         uint32_t dim = st & 0xffffu, depth = (st >> 16) & 0xffu;
         float4 h = P.hit[id], hp = P.hitp[id], rd = P.rd[id];
@@ -1710,6 +1724,19 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
         }
         P.state[id] = (st & 0xffff0000u) | dim;
     }
+}
+template <bool MULTI>
+__device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
+                                            uint32_t *__restrict__ traceQ, uint32_t *__restrict__ shadowQ,
+                                            uint32_t *__restrict__ counters) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = counters[HPT_Q_SHADE_IN];
+    bool cont = false, shadow = false;
+    uint32_t id = 0;
+    if (tid < n) {
+        id = shadeQ[tid];
+        shadePath<MULTI>(sc, P, id, counters, cont, shadow);
+    }
     qpushBlock<HPT_QBLOCK>(cont, id, traceQ, &counters[HPT_Q_TRACE]);
     qpushBlock<HPT_QBLOCK>(shadow, id, shadowQ, &counters[HPT_Q_SHADOW]);
 }
@@ -1728,17 +1755,10 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_shade_multi(HptScene 
     shadeBounce<true>(sc, P, shadeQ, traceQ, shadowQ, counters);
 }
 
-/* continuation result: path.cpp:225-286 */
-extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_post(HptScene sc, HptPaths P,
-                                                          const uint32_t *__restrict__ traceQ,
-                                                          uint32_t *__restrict__ shadeQ,
-                                                          uint32_t *__restrict__ counters) {
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = counters[HPT_Q_TRACE];
+/* continuation result: path.cpp:225-286; true when the path goes on */
+HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__restrict__ counters) {
     bool alive = false;
-    uint32_t id = 0;
-    if (tid < n) {
-        id = traceQ[tid];
+    {
         uint32_t st = P.state[id];
         uint32_t dim = st & 0xffffu, depth = (st >> 16) & 0xffu, type = (st >> 24) & 0x7fu;
         const bool scattered = (st >> 31) != 0;
@@ -1787,7 +1807,70 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_post(HptScene sc, Hpt
             }
         }
     }
+    return alive;
+}
+extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_post(HptScene sc, HptPaths P,
+                                                          const uint32_t *__restrict__ traceQ,
+                                                          uint32_t *__restrict__ shadeQ,
+                                                          uint32_t *__restrict__ counters) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = counters[HPT_Q_TRACE];
+    bool alive = false;
+    uint32_t id = 0;
+    if (tid < n) {
+        id = traceQ[tid];
+        alive = postPath(sc, P, id, counters);
+    }
     qpushBlock<HPT_QBLOCK>(alive, id, shadeQ, &counters[HPT_Q_SHADE_OUT]);
+}
+
+/* Tail of the frame (few live paths left, e.g. after Russian roulette
+   starts): one lane carries its path through every remaining bounce --
+   shade, shadow ray, continuation ray, post -- inside one launch, so the
+   tail costs the longest path's chain instead of one host-synchronised
+   launch sequence per bounce, each waiting on its own slowest ray.  Every
+   step is the wavefront kernels' own per-path function in the same order
+   (the shadow contribution is added before post's emitter term, as k_trace
+   finishes before k_post), so the film is bit-identical. */
+template <bool MULTI>
+__device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
+                                          uint32_t *__restrict__ counters, uint2 *stk) {
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = tid < counters[HPT_Q_SHADE_IN];
+    PathIO io{P, nullptr, nullptr, 0, 0, live ? shadeQ[tid] : 0u};
+    uint32_t nb = 0;
+    TraceCounters tc;
+    auto trace = [&](bool shadowRay) {
+        TraceRay r;
+        const float4 ro = P.ro[io.id], rd = shadowRay ? P.sdir[io.id] : P.rd[io.id];
+        if (beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(rd.x, rd.y, rd.z), shadowRay ? kEpsilon : ro.w, rd.w, shadowRay))
+            while (!traceRound<HPT_STACK, false>(sc, r, stk, (int) blockDim.x, tc)) {
+            }
+        io.finish(sc, 0, r);
+    };
+    while (live) {
+        bool cont = false, shadow = false;
+        ++nb;
+        shadePath<MULTI>(sc, P, io.id, counters, cont, shadow);
+        if (shadow) trace(true);
+        if (!cont) break;
+        trace(false);
+        if (!postPath(sc, P, io.id, counters)) break;
+    }
+    for (int off = 32; off > 0; off >>= 1) nb += __shfl_down(nb, off);
+    if (__lane_id() == 0 && nb) atomicAdd(&counters[HPT_Q_TAIL_BOUNCES], nb);
+}
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_tail(HptScene sc, HptPaths P,
+                                                               const uint32_t *__restrict__ shadeQ,
+                                                               uint32_t *__restrict__ counters) {
+    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    tailPaths<false>(sc, P, shadeQ, counters, stk + threadIdx.x);
+}
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_tail_multi(HptScene sc, HptPaths P,
+                                                                     const uint32_t *__restrict__ shadeQ,
+                                                                     uint32_t *__restrict__ counters) {
+    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    tailPaths<true>(sc, P, shadeQ, counters, stk + threadIdx.x);
 }
 
 /* Deterministic film accumulation (imageblock.h:124-204 + renderproc.cpp:
@@ -1806,7 +1889,7 @@ extern "C" __global__ __launch_bounds__(256) void k_splat(HptScene sc, HptWave w
     const uint32_t nSlots = w.nPaths / w.nSpp;
     if (slot >= nSlots) return; /* wave-uniform */
     const uint32_t lb = slot >> 10, inner = slot & 1023u;
-    const uint32_t b = lb * w.nShards + w.shard;
+    const uint32_t b = w.blockOf[lb];
     const int bx = (int) (b % w.nbx), by = (int) (b / w.nbx);
     const int px = bx * HPT_BLOCK + (int) (inner & 31u), py = by * HPT_BLOCK + (int) (inner >> 5);
     if (px >= w.width || py >= w.height) return; /* wave-uniform: never read back */
@@ -1867,8 +1950,9 @@ extern "C" __global__ __launch_bounds__(256) void k_gather(HptScene sc, HptWave 
             if (qx < 0 || qx >= w.width) continue;
             const int bx = qx / HPT_BLOCK, by = qy / HPT_BLOCK;
             const uint32_t b = (uint32_t) (by * w.nbx + bx);
-            if ((int) (b % w.nShards) != w.shard) continue;
-            const uint32_t slot = ((b / w.nShards) << 10) | ((uint32_t) (qy & 31) << 5) | (uint32_t) (qx & 31);
+            const int32_t lb = w.localOf[b];
+            if (lb < 0) continue; /* another shard's block */
+            const uint32_t slot = ((uint32_t) lb << 10) | ((uint32_t) (qy & 31) << 5) | (uint32_t) (qx & 31);
             const float4 p = partial[(size_t) slot * 9 + (y - qy + 1) * 3 + (x - qx + 1)];
             acc.x += p.x;
             acc.y += p.y;
@@ -2066,6 +2150,17 @@ hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t
                            uint32_t *counters, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
     hipLaunchKernelGGL(k_post, dim3(blocksFor(maxItems, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, P, traceQ, shadeQ, counters);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *counters,
+                           uint64_t maxItems, hipStream_t s) {
+    if (maxItems == 0) return hipSuccess;
+    if (sc.nShapes > 1)
+        hipLaunchKernelGGL(k_tail_multi, dim3(blocksFor(maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc, P,
+                           shadeQ, counters);
+    else
+        hipLaunchKernelGGL(k_tail, dim3(blocksFor(maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc, P,
+                           shadeQ, counters);
     return hipGetLastError();
 }
 hipError_t hpt_launch_rotate(uint32_t *counters, hipStream_t s) {

@@ -1,8 +1,14 @@
 """Multi-GPU frame rendering: one process per GPU (torch.distributed over RCCL).
 
 The frame's 32x32 blocks (the reference's block size, src/mitsuba/mitsuba.cpp:144)
-are dealt block-cyclically: rank r renders every sample of the blocks b with
-b % world == r.  Each rank accumulates its samples into its own
+are dealt cyclically along a Hilbert curve over the block grid: rank r renders
+every sample of the blocks at positions r, r + world, r + 2 world, ... of that
+curve (block_owner below; hpt_capi.cpp blockOrder is the renderer's own copy).
+N consecutive blocks of the curve form a compact patch, so every rank gets one
+block of every patch and the hair's uneven screen coverage is spread evenly
+(SURVEY.md 8e's plain b % world deal hands whole block columns to a rank
+whenever world divides the number of block columns: 0.73 strong-scaling
+efficiency at 8 ranks on the headline frame).  Each rank accumulates its samples into its own
 full-frame RGBW film -- the tent filter reaches one pixel into neighbouring
 blocks, so no border exchange is needed -- and one reduce(sum) to rank 0
 combines the films.  Paths never depend on which rank traces them
@@ -10,6 +16,40 @@ combines the films.  Paths never depend on which rank traces them
 equals the single-GPU frame up to floating-point summation order.
 """
 from __future__ import annotations
+
+
+def block_order(nbx: int, nby: int) -> list[int]:
+    """Image blocks (by * nbx + bx) in Hilbert-curve order over the nbx x nby grid."""
+    n = 1
+    while n < max(nbx, nby):
+        n <<= 1
+    order = []
+    for d in range(n * n):
+        x = y = 0
+        t = d
+        sq = 1
+        while sq < n:
+            rx = 1 & (t // 2)
+            ry = 1 & (t ^ rx)
+            if ry == 0:
+                if rx == 1:
+                    x, y = sq - 1 - x, sq - 1 - y
+                x, y = y, x
+            x += sq * rx
+            y += sq * ry
+            t //= 4
+            sq <<= 1
+        if x < nbx and y < nby:
+            order.append(y * nbx + x)
+    return order
+
+
+def block_owner(nbx: int, nby: int, world: int) -> list[int]:
+    """owner[b] = rank that renders 32x32 block b (hpt_render_params.shard / n_shards)."""
+    owner = [0] * (nbx * nby)
+    for k, b in enumerate(block_order(nbx, nby)):
+        owner[b] = k % world
+    return owner
 
 
 def render_frame(render_shard, film, rank: int, world: int, dist=None):

@@ -57,7 +57,8 @@ class Stats(C.Structure):
                 ("closest_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("nodes", C.c_uint64),
                 ("prims", C.c_uint64), ("bounces", C.c_uint64), ("shadow_unoccluded", C.c_uint64),
                 ("waves", C.c_uint64), ("max_bounces", C.c_int), ("prim_exact", C.c_uint64),
-                ("node_slots", C.c_uint64), ("prim_slots", C.c_uint64)]
+                ("node_slots", C.c_uint64), ("prim_slots", C.c_uint64), ("ms_tail", C.c_double),
+                ("tail_paths", C.c_uint64)]
 
 
 # every symbol declared in include/hairpt.h: (restype, argtypes)

@@ -114,7 +114,8 @@ int hpt_get_scene_info(hpt_context *ctx, hpt_scene_info *out);
 
 typedef struct hpt_render_params {
     int spp_begin, spp_end;        /* render samples [spp_begin, spp_end) of every pixel */
-    int shard, n_shards;           /* 32x32 blocks b with b % n_shards == shard (multi-GPU) */
+    int shard, n_shards;           /* the 32x32 blocks at positions shard, shard + n_shards, ... of a
+                                      Hilbert curve over the block grid (multi-GPU; hpt_capi.cpp blockOrder) */
     uint64_t max_wave_paths;       /* 0 = automatic (HBM-sized waves) */
     int collect_stats;             /* 0 none, 1 per-kernel HIP event timing,
                                       2 timing + traversal counters (slower k_trace variant) */
@@ -140,6 +141,8 @@ typedef struct hpt_stats {
     uint64_t node_slots, prim_slots; /* SIMD lanes occupied by the node / primitive loops
                                         (64 per wave iteration): nodes / node_slots is the
                                         lane utilisation */
+    double ms_tail;                /* HIP event sum of k_tail (the frame's last bounces, one launch) */
+    uint64_t tail_paths;           /* live paths handed to k_tail */
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 

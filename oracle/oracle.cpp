@@ -2540,9 +2540,33 @@ static int renderImpl(orc_scene *s, int spp_begin, int spp_end, int n_threads, i
     if (s->tree.empty()) { s->err = "kd-tree not set"; return -1; }
     const int W = s->width, H = s->height, BS = 32;
     const int nbx = (W + BS - 1) / BS, nby = (H + BS - 1) / BS, nblocks = nbx * nby;
+    /* shard ownership as the GPU renderer deals it (hpt_capi.cpp blockOrder): every
+       n_shards-th block along a Hilbert curve over the block grid */
     std::vector<int> myBlocks;
-    for (int b = 0; b < nblocks; ++b)
-        if (b % n_shards == shard) myBlocks.push_back(b);
+    {
+        int n = 1;
+        while (n < std::max(nbx, nby)) n <<= 1;
+        int k = 0;
+        for (long d = 0; d < (long) n * n; ++d) {
+            int x = 0, y = 0;
+            long t = d;
+            for (int sq = 1; sq < n; sq <<= 1) {
+                const int rx = 1 & (int) (t / 2), ry = 1 & (int) (t ^ rx);
+                if (ry == 0) {
+                    if (rx == 1) x = sq - 1 - x, y = sq - 1 - y;
+                    std::swap(x, y);
+                }
+                x += sq * rx;
+                y += sq * ry;
+                t /= 4;
+            }
+            if (x < nbx && y < nby) {
+                if (k % n_shards == shard) myBlocks.push_back(y * nbx + x);
+                ++k;
+            }
+        }
+    }
+    (void) nblocks;
     /* each block renders into a (BS+2)^2 RGBW tile with a 1-pixel border, merged in block order */
     const int TS = BS + 2;
     std::vector<float> tiles(myBlocks.size() * (size_t) TS * TS * 4, 0.0f);

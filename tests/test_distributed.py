@@ -1,6 +1,6 @@
 """World-size-2 rehearsal of the multi-GPU path on the CPU (gloo backend).
 
-Each rank renders its block-cyclic shard with the oracle (the GPU renderer's
+Each rank renders its Hilbert-cyclic shard with the oracle (the GPU renderer's
 block ownership, include/hairpt.h hpt_render_params.shard/n_shards, is the
 same rule) and mitsuba_amd.distributed.render_frame reduces the films to rank
 0, exactly as bench.py does over RCCL.  Rank 0's film must equal the
@@ -58,16 +58,32 @@ def test_two_rank_block_cyclic_frame(tmp_path):
     _, _, o = scene_util.make("furball_marschner", N, W, H, SPP)
     full, _ = o.render(0, SPP, threads=2, width=W, height=H)
     np.testing.assert_allclose(reduced, full, rtol=1e-5, atol=1e-6)
-    # ownership: 32x32 block b belongs to rank b % 2; a shard's film is zero
+    # ownership (distributed.block_owner, Hilbert-cyclic); a shard's film is zero
     # outside its blocks plus the 1-pixel tent border
     nbx = (W + 31) // 32
+    owner = distributed.block_owner(nbx, (H + 31) // 32, world)
     for rank, f in ((0, s0), (1, s1)):
         assert f[..., 3].sum() > 0
         for by in range((H + 31) // 32):
             for bx in range(nbx):
                 b = by * nbx + bx
                 core = f[by * 32 + 1:min(H, by * 32 + 31), bx * 32 + 1:min(W, bx * 32 + 31), 3]
-                if b % 2 == rank:
+                if owner[b] == rank:
                     assert core.min() > 0
                 else:
                     assert core.max() == 0
+
+
+@pytest.mark.parametrize("nbx,nby", [(16, 16), (32, 32), (38, 32), (2, 2), (1, 3), (5, 1)])
+def test_block_order_is_a_balanced_permutation(nbx, nby):
+    order = distributed.block_order(nbx, nby)
+    assert sorted(order) == list(range(nbx * nby))
+    for world in (1, 2, 4, 8):
+        owner = distributed.block_owner(nbx, nby, world)
+        counts = np.bincount(owner, minlength=world)
+        assert counts.max() - counts.min() <= 1
+    # a rank's blocks are not whole block columns (the plain b % world deal's flaw)
+    if nbx == 16 and nby == 16:
+        owner = np.array(distributed.block_owner(nbx, nby, 8)).reshape(nby, nbx)
+        for r in range(8):
+            assert len(np.unique(np.nonzero(owner == r)[1])) >= 8  # spans at least 8 columns

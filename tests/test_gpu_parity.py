@@ -16,7 +16,7 @@ import pytest
 
 import oracle_lib
 import scene_util
-from mitsuba_amd import native
+from mitsuba_amd import distributed, native
 
 pytestmark = pytest.mark.gpu
 
@@ -313,7 +313,8 @@ def test_render_matches_oracle(fixture, request):
     assert same.mean() >= floor_same - 0.05
     s = r.stats()
     assert s.paths == si.width * si.height * si.spp or s.paths >= si.width * si.height * si.spp
-    assert s.nodes > 0 and s.prims > 0 and s.trace_launches > 1
+    assert s.nodes > 0 and s.prims > 0 and s.trace_launches >= 1
+    assert s.trace_launches > 1 or s.tail_paths > 0  # later bounces ran per launch or in k_tail
 
 
 def test_render_deterministic_and_sharded(furball):
@@ -333,6 +334,37 @@ def test_render_deterministic_and_sharded(furball):
     # small waves give the same result as one wave
     d = r.render(0, si.spp, max_wave_paths=4096)
     np.testing.assert_allclose(d, a, rtol=1e-5, atol=1e-6)
+    # each shard renders exactly the blocks distributed.block_owner deals it
+    W, H = si.width, si.height
+    nbx, nby = (W + 31) // 32, (H + 31) // 32
+    for n_shards in (2, 3):
+        owner = distributed.block_owner(nbx, nby, n_shards)
+        for shard in range(n_shards):
+            f = r.render(0, 2, shard=shard, n_shards=n_shards)
+            for b, o_ in enumerate(owner):
+                bx, by = b % nbx, b // nbx
+                core = f[by * 32 + 1:min(H, by * 32 + 31), bx * 32 + 1:min(W, bx * 32 + 31), 3]
+                assert (core.min() > 0) if o_ == shard else (core.max() == 0), (n_shards, shard, b)
+
+
+@pytest.mark.parametrize("name,n,radii", [("furball_marschner", 1500, None), ("straight_kk", 400, None),
+                                          ("haircurl_roughplastic", 300, HAIRCURL_RADII)])
+def test_tail_kernel_bit_identical(name, n, radii, monkeypatch):
+    """k_tail (every remaining bounce of the few live paths in one launch)
+    runs the wavefront kernels' own per-path steps in the same order, so the
+    film is bit-identical to per-bounce launches, whichever bounce the tail
+    starts at (HPT_TAIL_PATHS: 0 = never, 1<<30 = right after the camera pass,
+    default = once fewer than 2^17 paths are live)."""
+    films = []
+    for tail in ("0", "2000", "1073741824"):
+        monkeypatch.setenv("HPT_TAIL_PATHS", tail)
+        _, r, _ = scene_util.make(name, n, 64, 48, 16, device=0, radii=radii)
+        films.append(r.render(0, 16, collect_stats=True))
+        s = r.stats()
+        assert (s.tail_paths > 0) == (tail != "0"), (tail, s.tail_paths)
+        r.close()
+    np.testing.assert_array_equal(films[0], films[1])
+    np.testing.assert_array_equal(films[0], films[2])
 
 
 def test_full_size_headline_frame():
