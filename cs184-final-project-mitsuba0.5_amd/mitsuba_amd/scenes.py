@@ -210,9 +210,17 @@ def make_scene(name: str, workdir: str, n_strands: int | None = None, **override
                      max_depth=cfg["max_depth"], hairdefaults=defaults, cam=cfg["cam"],
                      bsdf=cfg["bsdf"], shapes=shapes, sx=sx, sy=sy, sz=sz)
     path = os.path.join(workdir, "%s_%d.xml" % (name, n))
-    with open(path, "w") as f:
-        f.write(xml)
+    _write_atomic(path, xml)
     return path
+
+
+def _write_atomic(path: str, text: str) -> None:
+    """Write via a per-process temporary + rename: ranks that write the same
+    scene file concurrently never read a half-written one."""
+    tmp = path + ".tmp%d" % os.getpid()
+    with open(tmp, "w") as f:
+        f.write(text)
+    os.replace(tmp, path)
 
 
 _KD_INT = ("kdStopPrims", "kdMaxDepth", "kdMaxBadRefines", "kdClipMinPrims", "kdExactSweepMax")
@@ -230,6 +238,5 @@ def with_kd_params(xml: str, kd: dict, tag: str = "kd") -> str:
     s = open(xml).read()
     s = re.sub(r'(<shape type="hair"[^>]*>)', lambda m: m.group(1) + props, s, count=1)
     out = xml[:-4] + "_%s.xml" % tag
-    with open(out, "w") as f:
-        f.write(s)
+    _write_atomic(out, s)
     return out
