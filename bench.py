@@ -40,6 +40,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 #   node visit 32 B (two-level HptNode4); primitive test 32 B leaf-ordered fp32 pre-test record;
 #   exact fp64 test (pre-test survivors) + 128 B segment record
 BYTES_CLOSEST, BYTES_SHADOW, BYTES_UNOCC, BYTES_NODE, BYTES_PRIM, BYTES_EXACT = 68, 36, 48, 32, 32, 128
+# k_trace_packet (the camera pass, 64-ray packets over the binary kd-tree): per member lane, an 8-byte
+# HptNode per binary node visit; rays, records and exact tests as above
+BYTES_NODE2 = 8
 
 
 def parse():
@@ -129,18 +132,25 @@ def main():
     c = r.stats()
     frame = dict(nodes=c.nodes, prims=c.prims, exact=c.prim_exact, closest=c.closest_rays, shadow=c.shadow_rays,
                  unocc=c.shadow_unoccluded, bounces=c.bounces, launches=c.trace_launches,
-                 node_slots=c.node_slots, prim_slots=c.prim_slots)
+                 node_slots=c.node_slots, prim_slots=c.prim_slots,
+                 p_rays=c.packet_rays, p_nodes=c.packet_nodes, p_prims=c.packet_prims, p_exact=c.packet_exact,
+                 p_node_slots=c.packet_node_slots, p_prim_slots=c.packet_prim_slots, p_fallbacks=c.packet_fallbacks)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ms_trace = 0.0
-    launches = 0
+    ms_trace = ms_packet = 0.0
+    launches = p_launches = 0
+    ms_kernels = {}
     for _ in range(args.steps):
         step(1)  # HIP events around every kernel (on the library's stream), no counters
         s = r.stats()
         ms_trace += s.ms_trace
         launches += s.trace_launches
+        ms_packet += s.ms_trace_packet
+        p_launches += s.packet_launches
+        for k in ("camera", "trace_packet", "trace", "primary", "shade", "post", "tail", "gather"):
+            ms_kernels[k] = ms_kernels.get(k, 0.0) + getattr(s, "ms_" + k)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -158,6 +168,9 @@ def main():
     bytes_alg = (BYTES_CLOSEST * tot["closest"] + BYTES_SHADOW * tot["shadow"] + BYTES_UNOCC * tot["unocc"]
                  + BYTES_NODE * tot["nodes"] + BYTES_PRIM * tot["prims"] + BYTES_EXACT * tot["exact"])
     achieved = bytes_alg / (ms_trace * 1e-3) / 1e9 if ms_trace > 0 else 0.0
+    bytes_pk = (BYTES_CLOSEST * tot["p_rays"] + BYTES_NODE2 * tot["p_nodes"] + BYTES_PRIM * tot["p_prims"]
+                + BYTES_EXACT * tot["p_exact"])
+    achieved_pk = bytes_pk / (ms_packet * 1e-3) / 1e9 if ms_packet > 0 else 0.0
     traffic, traffic_src = None, None
     tj = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
     if os.path.exists(tj):
@@ -198,6 +211,13 @@ def main():
                          "avg_launch_ms": round(ms_trace / max(1, launches), 4), "launches": int(launches),
                          "bytes_per_step": int(bytes_alg // args.steps),
                          "rank0_trace_ms_per_step": round(ms_trace / args.steps, 3)},
+            # the camera pass's packet traversal (k_trace_packet), same byte model per member lane
+            "roofline_packet": {"bound": "hbm", "kernel": "k_trace_packet", "achieved": round(achieved_pk, 1),
+                                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_pk / HBM_PEAK_GBS, 4),
+                                "algorithmic_bytes_per_launch": int(bytes_pk // max(1, p_launches)),
+                                "avg_launch_ms": round(ms_packet / max(1, p_launches), 4),
+                                "launches": int(p_launches)},
+            "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in ms_kernels.items()},
             "cpu_baseline": cpu,
             "stats": {"bounces_per_path": round(tot["bounces"] / max(1, paths_total / world), 4),
                       "nodes_per_ray": round(tot["nodes"] / max(1, tot["closest"] + tot["shadow"]), 2),
@@ -205,6 +225,12 @@ def main():
                       "exact_tests_per_ray": round(tot["exact"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "simd_util_nodes": round(tot["nodes"] / max(1, tot["node_slots"]), 3),
                       "simd_util_prims": round(tot["prims"] / max(1, tot["prim_slots"]), 3),
+                      "camera_rays_packet": int(frame["p_rays"]),
+                      "camera_binary_nodes_per_ray": round(tot["p_nodes"] / max(1, tot["p_rays"]), 2),
+                      "camera_prims_per_ray": round(tot["p_prims"] / max(1, tot["p_rays"]), 2),
+                      "camera_packet_util_nodes": round(tot["p_nodes"] / max(1, tot["p_node_slots"]), 3),
+                      "camera_packet_util_prims": round(tot["p_prims"] / max(1, tot["p_prim_slots"]), 3),
+                      "camera_packet_fallbacks": int(frame["p_fallbacks"]),
                       "image_mean": float(img.mean()),
                       # exact-arithmetic fingerprint of the frame (sum of the RGBW film in fp64):
                       # identical for every traversal variant, since hits are bit-exact

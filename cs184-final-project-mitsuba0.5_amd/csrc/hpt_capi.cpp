@@ -43,9 +43,16 @@ static uint32_t defaultTailPaths() {
     return v ? (uint32_t) std::strtoul(v, nullptr, 10) : (1u << 17);
 }
 
+/* camera rays traced as 64-ray packets (k_trace_packet); HPT_PACKETS=0 traces them one per lane */
+static bool defaultPackets() {
+    const char *v = std::getenv("HPT_PACKETS");
+    return v ? std::atoi(v) != 0 : true;
+}
+
 struct hpt_context {
     int device = 0;
     uint32_t tailPaths = defaultTailPaths();
+    bool packets = defaultPackets();
     hipStream_t stream = nullptr;
     std::string err;
     std::string dataDir;
@@ -184,7 +191,7 @@ int ensureWave(hpt_context *c, uint64_t n) {
     r |= alloc(n * 4, (void **) &c->qShadeA);
     r |= alloc(n * 4, (void **) &c->qShadeB);
     r |= alloc(HPT_COUNTER_WORDS * 4, (void **) &c->counters);
-    r |= alloc(16 * 8, (void **) &c->dstats);
+    r |= alloc(24 * 8, (void **) &c->dstats);
     if (r) return HPT_EDEVICE;
     c->capacity = n;
     return HPT_OK;
@@ -847,8 +854,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     hipStream_t s = c->stream;
     const bool st = prm->collect_stats != 0;      /* HIP event timing per kernel class */
     const bool counted = prm->collect_stats >= 2; /* + traversal counters (k_trace_counted) */
-    if (counted) HIPCHK(c, hipMemsetAsync(c->dstats, 0, 128, s));
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> evTrace, evOther[6];
+    if (counted) HIPCHK(c, hipMemsetAsync(c->dstats, 0, 24 * 8, s));
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> evTrace, evOther[7];
     size_t evUsed = 0;
     auto timed = [&](int cls, auto fn) -> hipError_t {
         if (!st) return fn();
@@ -869,10 +876,18 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     uint64_t prevSt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     auto reportLaunch = [&](const char *what) {
         if (!perLaunch) return;
-        uint64_t hs[16];
-        if (hipMemcpyAsync(hs, c->dstats, 128, hipMemcpyDeviceToHost, s) != hipSuccess ||
-            hipStreamSynchronize(s) != hipSuccess || hipMemsetAsync(c->dstats + 8, 0, 64, s) != hipSuccess)
+        uint64_t hs[24];
+        if (hipMemcpyAsync(hs, c->dstats, 24 * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess || hipMemsetAsync(c->dstats + 8, 0, 32, s) != hipSuccess)
             return;
+        if (c->packets && std::strcmp(what, "camera") == 0) {
+            const double rays = (double) std::max<uint64_t>(1, hs[14]);
+            std::fprintf(stderr, "[trace] packets  rays %10llu binary nodes/ray %6.2f prims/ray %6.2f exact/ray %5.2f "
+                         "util nodes %.3f prims %.3f | fallbacks %llu\n", (unsigned long long) hs[14], hs[12] / rays,
+                         hs[13] / rays, hs[15] / rays, hs[12] / std::max(1.0, (double) hs[16]),
+                         hs[13] / std::max(1.0, (double) hs[17]), (unsigned long long) hs[18]);
+            return;
+        }
         uint64_t d[8];
         for (int i = 0; i < 8; ++i) d[i] = hs[i] - prevSt[i], prevSt[i] = hs[i];
         const double rays = (double) (d[2] + d[3]);
@@ -900,10 +915,14 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         HIPCHK(c, hipMemsetAsync(c->counters, 0, HPT_COUNTER_WORDS * 4, s));
         e = timed(0, [&] { return hpt_launch_camera(sc, w, c->P, c->qTrace, c->counters, s); });
         if (e) break;
-        e = timed(-1, [&] {
-            return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, c->counters,
-                                    counted ? (uint32_t *) c->dstats : nullptr, w.nPaths, s);
-        });
+        e = c->packets ? timed(6, [&] {
+            return hpt_launch_trace_packet(sc, c->P, c->qTrace, c->counters, counted ? (uint32_t *) c->dstats : nullptr,
+                                           w.nPaths, s);
+        })
+                       : timed(-1, [&] {
+                             return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, c->counters,
+                                                     counted ? (uint32_t *) c->dstats : nullptr, w.nPaths, s);
+                         });
         if (e) break;
         reportLaunch("camera");
         e = timed(1, [&] { return hpt_launch_primary(sc, c->P, c->qTrace, c->qShadeA, c->counters, w.nPaths, s); });
@@ -978,10 +997,19 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         c->stats.ms_post = sumEv(evOther[3]);
         c->stats.ms_gather = sumEv(evOther[4]);
         c->stats.ms_tail = sumEv(evOther[5]);
+        c->stats.ms_trace_packet = sumEv(evOther[6]);
+        c->stats.packet_launches = evOther[6].size();
     }
     if (counted) {
-        uint64_t hs[8];
-        HIPCHK(c, hipMemcpy(hs, c->dstats, 64, hipMemcpyDeviceToHost));
+        uint64_t hs[24];
+        HIPCHK(c, hipMemcpy(hs, c->dstats, 24 * 8, hipMemcpyDeviceToHost));
+        c->stats.packet_nodes = hs[12];
+        c->stats.packet_prims = hs[13];
+        c->stats.packet_rays = hs[14];
+        c->stats.packet_exact = hs[15];
+        c->stats.packet_node_slots = hs[16];
+        c->stats.packet_prim_slots = hs[17];
+        c->stats.packet_fallbacks = hs[18];
         c->stats.nodes = hs[0];
         c->stats.prims = hs[1];
         c->stats.closest_rays = hs[2];

@@ -725,6 +725,238 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
 }
 
 /* ------------------------------------------------------------------ */
+/* Packet traversal for coherent rays (the camera pass)                 */
+/* ------------------------------------------------------------------ */
+/* The 64 rays of a wave (camera rays: 64 samples of one pixel, one
+   origin) walk the binary kd-tree together: the node index, the stack and
+   the leaf records are wave-uniform (scalar loads), each lane keeps its own
+   ray interval and hit, and a lane takes part only in the subtrees its own
+   Havran traversal (sahkdtree3.h:178-308) would enter.  At a split every
+   member lane computes its own t and near/far/both decision exactly as
+   traceRound does; the packet enters the first child if any lane needs it
+   and stacks the second child with the masks of the lanes that need it
+   ("both" lanes also stack their own tmax).  Lanes that disagree on the
+   front-to-back order split the packet (the second group revisits the node
+   later).  A lane therefore tests the same leaves in the same order with
+   the same intervals as its own traversal, and its result is bit-identical.
+   A packet whose stack would overflow finishes lane by lane (traceRound). */
+#ifndef HPT_PACKET_STACK
+#define HPT_PACKET_STACK 24
+#endif
+struct PacketEntry {
+    uint32_t node, revisit;
+    uint64_t mBoth, mFar; /* lanes that stacked their tmax / that skipped the first child */
+};
+struct PacketLds {
+    PacketEntry ent[HPT_PACKET_STACK];
+    float saved[HPT_PACKET_STACK][64];
+};
+static_assert(sizeof(float) * HPT_PACKET_STACK * 64 >= sizeof(uint2) * 8 * 64,
+              "the fallback ring stack reuses the packet stack's LDS");
+
+/* a wave-uniform 64-bit value into scalar registers (readfirstlane returns a
+   signed int: widen through uint32_t, or lane 31's bit would smear upwards) */
+HD uint64_t uniform64(uint64_t v) {
+    return (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) v) |
+           ((uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) (v >> 32)) << 32);
+}
+
+/* returns false when the packet stack overflowed (the caller then traces each lane alone) */
+template <bool STATS>
+HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, TraceCounters &tc) {
+    const uint32_t lane = __lane_id();
+    const HptNode *__restrict__ nodes = sc.nodes;
+    const float4 *__restrict__ leafF = reinterpret_cast<const float4 *>(sc.leafF);
+    const V3 o = r.o, d = r.d, rcp = r.rcp;
+    uint64_t done = ~__ballot(valid);
+    uint64_t act = ~done;
+    if (act == 0) return true;
+#ifdef HPT_PACKET_FORCE_FALLBACK
+    return false;
+#endif
+    uint32_t node = 0;
+    int sp = 0;
+    uint32_t steps = 0;
+    while (true) {
+        /* ---- descend to a leaf ---- */
+        HptNode nd = nodes[node];
+        while (!(nd.w0 & 0x80000000u)) {
+            const bool me = (act >> lane) & 1u;
+            if (STATS) {
+                tc.nodes += me ? 1u : 0u;
+                if (lane == 0) tc.nodeSlots += 64;
+            }
+            const uint32_t axis = nd.w0 & 3u, left = nd.w0 >> 2;
+            const float split = __uint_as_float(nd.w1);
+            const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
+            const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
+            const float ra = axis == 0 ? rcp.x : (axis == 1 ? rcp.y : rcp.z);
+            const float ts = (split - oa) * ra;
+            const bool below = (oa < split) | ((oa == split) & (da <= 0.0f));
+            const bool nearOnly = !(ts <= r.tmax) | (ts <= 0.0f);
+            const bool farOnly = !nearOnly & (ts < r.tmin);
+            const bool both = !(nearOnly | farOnly);
+            const uint64_t mBelow = __ballot(me & below);
+            if (mBelow != 0 && mBelow != act) {
+                /* the lanes disagree on the front-to-back order: the others revisit this node later */
+                if (sp == HPT_PACKET_STACK) return false;
+                if (lane == 0) L.ent[sp] = PacketEntry{node, 1u, act & ~mBelow, 0ull};
+                ++sp;
+                act = mBelow;
+            }
+            const bool in = (act >> lane) & 1u;
+            const uint32_t belowG = (act & mBelow) != 0 ? 1u : 0u;
+            const uint32_t first = left + (belowG ? 0u : 1u), second = left + (belowG ? 1u : 0u);
+            const uint64_t mFirst = __ballot(in & !farOnly), mBoth = __ballot(in & both), mFar = __ballot(in & farOnly);
+            if (mFirst == 0) { /* nobody needs the first child (so no lane is "both") */
+                node = second;
+                act = mFar;
+                nd = nodes[node];
+                continue;
+            }
+            if ((mBoth | mFar) != 0) {
+                if (sp == HPT_PACKET_STACK) return false;
+                if (in & both) L.saved[sp][lane] = r.tmax;
+                if (lane == 0) L.ent[sp] = PacketEntry{second, 0u, mBoth, mFar};
+                ++sp;
+                if (in & both) r.tmax = ts;
+            }
+            node = first;
+            act = mFirst;
+            nd = nodes[node];
+        }
+        /* ---- leaf: the member lanes test its segments (pre-test, then exact) ---- */
+        const bool me = (act >> lane) & 1u;
+        if (STATS) {
+            tc.nodes += me ? 1u : 0u;
+            if (lane == 0) tc.nodeSlots += 64;
+        }
+        const uint32_t lf = nd.w0 & 0x7fffffffu, ll = nd.w1;
+        for (uint32_t e = lf; e < ll; ++e) {
+            const float4 fa = leafF[2 * e], fb = leafF[2 * e + 1];
+            if (STATS) {
+                tc.prims += me ? 1u : 0u;
+                if (lane == 0) tc.primSlots += 64;
+            }
+            if (me && segMayHit(fa, fb, o, d, sc.maxRadius)) {
+                const uint32_t sg = __float_as_uint(fb.z);
+                const float rad = segRadius(sc, sg);
+                const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
+                if (STATS) ++tc.exact;
+                float t;
+                V3 p;
+                if (HPT_SEG_TEST(sc.segs, sg, o, d, r2, r.mint, r.tHit, t, p)) {
+                    r.found = true;
+                    r.tHit = t;
+                    r.segHit = sg;
+                }
+            }
+        }
+        done |= __ballot(me && r.found && r.tHit <= r.tmax);
+        if (++steps > (1u << 20)) return false; /* malformed tree: let the lanes finish alone */
+        /* ---- pop the next subtree some unfinished lane needs ---- */
+        while (true) {
+            if (sp == 0) return true;
+            --sp;
+            const PacketEntry en = L.ent[sp];
+            const uint64_t enBoth = uniform64(en.mBoth), enFar = uniform64(en.mFar);
+            const uint32_t enNode = (uint32_t) __builtin_amdgcn_readfirstlane(en.node);
+            if (__builtin_amdgcn_readfirstlane(en.revisit)) {
+                act = enBoth & ~done;
+            } else {
+                const bool inB = ((enBoth & ~done) >> lane) & 1u;
+                if (inB) {
+                    r.tmin = r.tmax;
+                    r.tmax = L.saved[sp][lane];
+                }
+                done |= __ballot(inB && r.tmin > r.tHit);
+                act = (enBoth | enFar) & ~done;
+            }
+            if (act != 0) {
+                node = enNode;
+                break;
+            }
+        }
+    }
+}
+
+/* Persistent packet tracer: each wave claims 64 consecutive closest-hit rays
+   (the camera queue keeps a pixel's samples together), traces them as one
+   packet and writes the hits; the shard cursors are k_trace's. */
+template <bool STATS, class IO>
+__device__ __forceinline__ void tracePackets(const HptScene &sc, IO &io, uint32_t *cursors, PacketLds &L,
+                                             uint32_t *stats) {
+    const uint32_t total = io.count();
+    const uint32_t lane = __lane_id();
+    TraceCounters tc;
+    uint32_t nC = 0, fallbacks = 0;
+    uint32_t shard = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % HPT_CURSORS;
+    int tried = 0;
+    while (true) {
+        uint32_t start = 0, got = 0;
+        bool exhausted = false;
+        while (true) { /* wave-uniform */
+            const uint32_t lo = (uint32_t) ((uint64_t) total * shard / HPT_CURSORS);
+            const uint32_t size = (uint32_t) ((uint64_t) total * (shard + 1) / HPT_CURSORS) - lo;
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&cursors[shard * HPT_CURSOR_STRIDE], 64u);
+            base = __shfl(base, 0);
+            if (base < size) {
+                start = lo + base;
+                got = min(64u, size - base);
+                break;
+            }
+            if (++tried >= HPT_CURSORS) {
+                exhausted = true;
+                break;
+            }
+            shard = (shard + 1) % HPT_CURSORS;
+        }
+        if (exhausted) break;
+        const uint32_t k = start + lane;
+        TraceRay r;
+        bool valid = false;
+        r.found = false;
+        r.shadow = false;
+        if (lane < got) valid = io.begin(sc, k, r);
+        if (STATS) nC += lane < got ? 1u : 0u;
+        if (!tracePacket<STATS>(sc, r, valid, L, tc)) {
+            /* packet stack overflow: every lane re-traces its ray alone (same result) */
+            if (STATS) fallbacks += lane == 0 ? 1u : 0u;
+            uint2 *stk = reinterpret_cast<uint2 *>(&L.saved[0][0]) + lane;
+            if (lane < got && io.begin(sc, k, r))
+                while (!traceRound<8, STATS>(sc, r, stk, 64, tc)) {
+                }
+        }
+        if (lane < got) io.finish(sc, k, r);
+    }
+    if (STATS) {
+        for (int off = 32; off > 0; off >>= 1) {
+            tc.nodes += __shfl_down(tc.nodes, off);
+            tc.prims += __shfl_down(tc.prims, off);
+            tc.exact += __shfl_down(tc.exact, off);
+            tc.nodeSlots += __shfl_down(tc.nodeSlots, off);
+            tc.primSlots += __shfl_down(tc.primSlots, off);
+            nC += __shfl_down(nC, off);
+            fallbacks += __shfl_down(fallbacks, off);
+        }
+        if (lane == 0) {
+            unsigned long long *st = (unsigned long long *) stats;
+            /* the packet pass's own counters: [12] binary node visits (8-byte HptNode)
+               [13] primitive tests [14] rays [15] exact tests [16]/[17] node / primitive
+               SIMD slots [18] packets that fell back to one ray per lane */
+            atomicAdd(&st[12], (unsigned long long) tc.nodes);
+            atomicAdd(&st[13], (unsigned long long) tc.prims);
+            atomicAdd(&st[14], (unsigned long long) nC);
+            atomicAdd(&st[15], (unsigned long long) tc.exact);
+            atomicAdd(&st[16], (unsigned long long) tc.nodeSlots);
+            atomicAdd(&st[17], (unsigned long long) tc.primSlots);
+            atomicAdd(&st[18], (unsigned long long) fallbacks);
+        }
+    }
+}
+
+/* ------------------------------------------------------------------ */
 /* Marschner (marschner_diffuse.cpp)                                    */
 /* ------------------------------------------------------------------ */
 HD float trigInverse(float x) { return fminr(sqrtf(fmaxr(1.0f - x * x, 0.0f)), 1.0f); }
@@ -1599,6 +1831,25 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
     tracePersistent<HPT_STACK, true>(sc, io, cursors, stk + threadIdx.x, stats);
 }
 
+/* k_trace_packet: the camera pass's closest-hit rays as 64-ray packets */
+#ifndef HPT_PACKET_WAVES
+#define HPT_PACKET_WAVES 5
+#endif
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_PACKET_WAVES))) void
+k_trace_packet(HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, uint32_t *__restrict__ counters,
+               uint32_t *__restrict__ cursors) {
+    __shared__ PacketLds lds[HPT_TRACE_BLOCK / 64];
+    PathIO io{P, traceQ, nullptr, counters[HPT_Q_TRACE], 0, 0};
+    tracePackets<false>(sc, io, cursors, lds[threadIdx.x >> 6], nullptr);
+}
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_packet_counted(
+    HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, uint32_t *__restrict__ counters,
+    uint32_t *__restrict__ cursors, uint32_t *stats) {
+    __shared__ PacketLds lds[HPT_TRACE_BLOCK / 64];
+    PathIO io{P, traceQ, nullptr, counters[HPT_Q_TRACE], 0, 0};
+    tracePackets<true>(sc, io, cursors, lds[threadIdx.x >> 6], stats);
+}
+
 /* fill the intersection record: hair.cpp:825-862 + skdtree.h:422-427 */
 HD void fillIts(const HptScene &sc, uint32_t seg, V3 hp, V3 rayD, V3 &p, Frame &geo, Frame &sh, V3 &wi) {
     const double *rec = reinterpret_cast<const double *>(sc.segs + seg);
@@ -1981,7 +2232,8 @@ extern "C" __global__ void k_sobol_batch(HptScene sc, int m, int n, const uint32
 
 /* Batch trace through the production traversal (tracePersistent).  flags:
    bit 0 = any-hit shadow query, bit 1 = 2-entry stack (exercises the
-   kd-restart path for the parity tests) */
+   kd-restart path for the parity tests), bit 2 = closest hits through the
+   packet traversal (tracePackets, 64 consecutive rays per packet) */
 struct BatchIO {
     const float *o, *d, *mint, *maxt;
     float *outT, *outP;
@@ -2016,8 +2268,11 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptS
                                                                             float *outP, uint8_t *outHit,
                                                                             uint32_t *cursor) {
     __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    __shared__ PacketLds lds[HPT_TRACE_BLOCK / 64];
     BatchIO io{o, d, mint, maxt, outT, outP, outSeg, outHit, (uint32_t) n, (flags & 1) != 0};
-    if (flags & 2)
+    if ((flags & 4) && !(flags & 1))
+        tracePackets<false>(sc, io, cursor, lds[threadIdx.x >> 6], nullptr);
+    else if (flags & 2)
         tracePersistent<2, false>(sc, io, cursor, stk + threadIdx.x, nullptr);
     else
         tracePersistent<HPT_STACK, false>(sc, io, cursor, stk + threadIdx.x, nullptr);
@@ -2102,8 +2357,11 @@ hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPath
 /* persistent grid: as many one-wave blocks as can be resident at once
    (occupancy API x CUs), capped by the work */
 static unsigned persistentBlocks(const void *kernel, uint64_t items) {
-    static int cached[2] = {0, 0};
-    const int slot = kernel == (const void *) k_trace ? 0 : 1;
+    static const void *keys[8] = {nullptr};
+    static int cached[8] = {0};
+    int slot = 0;
+    while (slot < 7 && keys[slot] && keys[slot] != kernel) ++slot;
+    keys[slot] = kernel;
     if (cached[slot] == 0) {
         int dev = 0, perCU = 0;
         hipDeviceProp_t prop;
@@ -2127,6 +2385,17 @@ hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_
     else
         hipLaunchKernelGGL(k_trace, dim3(persistentBlocks((const void *) k_trace, maxItems)), dim3(HPT_TRACE_BLOCK),
                            0, s, sc, P, traceQ, shadowQ, counters, counters + HPT_CURSOR_OFFSET);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *counters,
+                                   uint32_t *stats, uint64_t maxItems, hipStream_t s) {
+    if (maxItems == 0) return hipSuccess;
+    if (stats)
+        hipLaunchKernelGGL(k_trace_packet_counted, dim3(persistentBlocks((const void *) k_trace_packet_counted, maxItems)),
+                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, counters, counters + HPT_CURSOR_OFFSET, stats);
+    else
+        hipLaunchKernelGGL(k_trace_packet, dim3(persistentBlocks((const void *) k_trace_packet, maxItems)),
+                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, counters, counters + HPT_CURSOR_OFFSET);
     return hipGetLastError();
 }
 hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,

@@ -58,7 +58,10 @@ class Stats(C.Structure):
                 ("prims", C.c_uint64), ("bounces", C.c_uint64), ("shadow_unoccluded", C.c_uint64),
                 ("waves", C.c_uint64), ("max_bounces", C.c_int), ("prim_exact", C.c_uint64),
                 ("node_slots", C.c_uint64), ("prim_slots", C.c_uint64), ("ms_tail", C.c_double),
-                ("tail_paths", C.c_uint64)]
+                ("tail_paths", C.c_uint64), ("ms_trace_packet", C.c_double), ("packet_launches", C.c_uint64),
+                ("packet_rays", C.c_uint64), ("packet_nodes", C.c_uint64), ("packet_prims", C.c_uint64),
+                ("packet_exact", C.c_uint64), ("packet_node_slots", C.c_uint64), ("packet_prim_slots", C.c_uint64),
+                ("packet_fallbacks", C.c_uint64)]
 
 
 # every symbol declared in include/hairpt.h: (restype, argtypes)
@@ -318,7 +321,7 @@ class Renderer:
                                              _p(oi, _u64), _p(ov, _f)))
         return oi, ov
 
-    def trace(self, o, d, mint, maxt, shadow=False, tiny_stack=False):
+    def trace(self, o, d, mint, maxt, shadow=False, tiny_stack=False, packet=False):
         o = _f32(o).reshape(-1, 3)
         d = _f32(d).reshape(-1, 3)
         n = o.shape[0]
@@ -329,7 +332,7 @@ class Renderer:
         op = np.zeros((n, 3), np.float32)
         oh = np.zeros(n, np.uint8)
         self._check(self.lib.hpt_trace_batch(self.h, n, _p(o, _f), _p(d, _f), _p(mint, _f), _p(maxt, _f),
-                                             (1 if shadow else 0) | (2 if tiny_stack else 0),
+                                             (1 if shadow else 0) | (2 if tiny_stack else 0) | (4 if packet else 0),
                                              _p(ot, _f), _p(oiv, _i32), _p(op, _f), _p(oh, _u8)))
         return oh.astype(bool) if shadow else (ot, oiv, op)
 

@@ -143,6 +143,12 @@ typedef struct hpt_stats {
                                         lane utilisation */
     double ms_tail;                /* HIP event sum of k_tail (the frame's last bounces, one launch) */
     uint64_t tail_paths;           /* live paths handed to k_tail */
+    double ms_trace_packet;        /* HIP event sum of k_trace_packet (the camera rays, 64-ray packets) */
+    uint64_t packet_launches;
+    /* the packet pass's traversal counters (counted frames), like the ones above for k_trace */
+    uint64_t packet_rays, packet_nodes /* binary-node visits per member lane */, packet_prims, packet_exact;
+    uint64_t packet_node_slots, packet_prim_slots; /* 64 per packet step: visits / slots = lane use */
+    uint64_t packet_fallbacks;     /* packets whose stack overflowed (their lanes traced alone) */
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 
@@ -193,6 +199,7 @@ int hpt_sobol_batch(hpt_context *ctx, int m, int n, const uint32_t *frame, const
    out_iv is the reference's primitive id (first vertex index of the segment) */
 #define HPT_TRACE_SHADOW 1      /* any-hit query (out_hit) instead of closest hit */
 #define HPT_TRACE_TINY_STACK 2  /* test hook: 2-entry traversal stack, forces kd-restarts */
+#define HPT_TRACE_PACKET 4      /* closest hits through the 64-ray packet traversal (camera pass) */
 int hpt_trace_batch(hpt_context *ctx, int n, const float *o, const float *d, const float *mint, const float *maxt,
                     int flags, float *out_t, int32_t *out_iv, float *out_p, uint8_t *out_hit);
 /* BSDF::eval / pdf / sample for the scene's hair BSDF (local frame) */

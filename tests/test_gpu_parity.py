@@ -121,6 +121,12 @@ def test_trace_bit_exact(fixture, kind, request):
     sm = np.minimum(maxt, 3.0).astype(np.float32)
     osh = o.trace(orig, dirs, mint, sm, shadow=True)
     np.testing.assert_array_equal(r.trace(orig, dirs, mint, sm, shadow=True), osh)
+    # packet traversal on incoherent rays: packets split on every order disagreement and
+    # overflow their stack (lanes then finish alone) -- the hits must not change
+    pt_, piv, pp = r.trace(orig, dirs, mint, maxt, packet=True)
+    np.testing.assert_array_equal(piv, oiv)
+    np.testing.assert_array_equal(pt_, ot)
+    np.testing.assert_array_equal(pp, op)
     # kd-restart path: a 2-entry stack overflows constantly and must give the same answers
     tt, tiv, tp = r.trace(orig, dirs, mint, maxt, tiny_stack=True)
     np.testing.assert_array_equal(tiv, oiv)
@@ -129,6 +135,39 @@ def test_trace_bit_exact(fixture, kind, request):
 
 
 HAIRCURL_RADII = [0.02, 0.035, 0.05, 0.028]
+
+
+def _packet_rays(r, n_groups, seed, cone):
+    """Camera-like packets: groups of 64 rays from one origin (a point 8..30 units
+    out) into a cone of half-angle `cone` around the direction to a random hair
+    vertex -- coherent like a pixel's samples, plus wider cones."""
+    rng = np.random.default_rng(seed)
+    xyz, _ = r.hair()
+    tgt = xyz[rng.integers(0, len(xyz), n_groups)].astype(np.float64)
+    q = rng.normal(size=(n_groups, 3))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    orig = tgt + q * rng.uniform(8.0, 30.0, (n_groups, 1))
+    c = (tgt - orig) / np.linalg.norm(tgt - orig, axis=1, keepdims=True)
+    d = np.repeat(c, 64, 0) + rng.normal(size=(n_groups * 64, 3)) * cone
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    o = np.repeat(orig, 64, 0).astype(np.float32)
+    n = n_groups * 64
+    return o, d.astype(np.float32), np.full(n, 1e-4, np.float32), np.full(n, np.inf, np.float32)
+
+
+@pytest.mark.parametrize("fixture", ["furball", "straight", "haircurl"])
+def test_packet_trace_bit_exact(fixture, request):
+    """k_trace_packet's traversal (the camera pass) on coherent 64-ray packets
+    gives every lane exactly its own Havran traversal's hit."""
+    _, r, o = request.getfixturevalue(fixture)
+    for cone, seed in ((2e-4, 11), (3e-3, 12), (3e-2, 13)):
+        orig, dirs, mint, maxt = _packet_rays(r, 600, seed, cone)
+        gt, giv, gp = r.trace(orig, dirs, mint, maxt, packet=True)
+        ot, oiv, op = o.trace(orig, dirs, mint, maxt)
+        assert (oiv >= 0).sum() > 500
+        np.testing.assert_array_equal(giv, oiv)
+        np.testing.assert_array_equal(gt, ot)
+        np.testing.assert_array_equal(gp, op)
 
 
 @pytest.fixture(scope="module")
@@ -313,8 +352,9 @@ def test_render_matches_oracle(fixture, request):
     assert same.mean() >= floor_same - 0.05
     s = r.stats()
     assert s.paths == si.width * si.height * si.spp or s.paths >= si.width * si.height * si.spp
-    assert s.nodes > 0 and s.prims > 0 and s.trace_launches >= 1
-    assert s.trace_launches > 1 or s.tail_paths > 0  # later bounces ran per launch or in k_tail
+    assert s.nodes + s.packet_nodes > 0 and s.prims + s.packet_prims > 0
+    assert s.trace_launches + s.packet_launches >= 1
+    assert s.trace_launches >= 1 or s.tail_paths > 0  # later bounces ran per launch or in k_tail
 
 
 def test_render_deterministic_and_sharded(furball):
