@@ -171,7 +171,7 @@ def main():
     bytes_pk = (BYTES_CLOSEST * tot["p_rays"] + BYTES_NODE2 * tot["p_nodes"] + BYTES_PRIM * tot["p_prims"]
                 + BYTES_EXACT * tot["p_exact"])
     achieved_pk = bytes_pk / (ms_packet * 1e-3) / 1e9 if ms_packet > 0 else 0.0
-    traffic, traffic_src = None, None
+    traffic, traffic_src, traffic_pk = None, None, None
     tj = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
     if os.path.exists(tj):
         # HBM-side bytes per k_trace launch from the committed rocprofv3 PMC passes
@@ -180,6 +180,8 @@ def main():
         if t.get("workload") == workload and "k_trace" in t.get("kernels", {}):
             traffic = round(t["kernels"]["k_trace"]["bytes_per_launch"])
             traffic_src = "profiles/" + os.path.basename(tj)
+            if "k_trace_packet" in t["kernels"]:
+                traffic_pk = round(t["kernels"]["k_trace_packet"]["bytes_per_launch"])
     out = None
     if rank == 0:
         cpu = None
@@ -214,6 +216,7 @@ def main():
             # the camera pass's packet traversal (k_trace_packet), same byte model per member lane
             "roofline_packet": {"bound": "hbm", "kernel": "k_trace_packet", "achieved": round(achieved_pk, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_pk / HBM_PEAK_GBS, 4),
+                                "traffic": traffic_pk,
                                 "algorithmic_bytes_per_launch": int(bytes_pk // max(1, p_launches)),
                                 "avg_launch_ms": round(ms_packet / max(1, p_launches), 4),
                                 "launches": int(p_launches)},
