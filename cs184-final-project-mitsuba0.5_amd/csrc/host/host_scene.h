@@ -196,12 +196,19 @@ struct EnvHost {
     int w = 0, h = 0;
     std::vector<float> rgb;        /* input bitmap (linear RGB) */
     std::vector<HptF4> texel;      /* half-rounded */
+    /* MIP pyramid (mipmap.h:155-302): level l is levelW[l] x levelH[l] half-rounded texels at
+       mip[levelOff[l] ...]; level 0 == texel.  sizeRatio (mipmap.h:264-266), EWA weight LUT (:296-301) */
+    std::vector<HptF4> mip;
+    std::vector<int> levelW, levelH, levelOff;
+    std::vector<float> ratioX, ratioY;
+    float ewaLut[HPT_EWA_LUT] = {};
     std::vector<float> cdfRows, cdfCols, rowWeights;
     float normalization = 0, scale = 1, pixelSizeX = 0, pixelSizeY = 0;
     float toWorld[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
 };
 
 void buildEnvMap(EnvHost &env);                           /* envmap.cpp:244-314 */
+void buildEnvMipmap(EnvHost &env);                        /* envmap.cpp:165-182, mipmap.h:155-302 */
 
 /* sunsky (sunsky.cpp): tables extracted from the reference (tools/extract_sunsky_tables.py) */
 struct SunSkyTables {

@@ -19,6 +19,8 @@
  * bits the reference's constructor would produce.
  */
 #include <algorithm>
+#include <limits>
+#include <array>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -574,6 +576,134 @@ void buildEnvMap(EnvHost &env) {
     env.pixelSizeY = kPi / h;
 }
 
+/* ---------------- MIP pyramid (envmap.cpp:165-182, mipmap.h:155-302) ---------------- */
+namespace {
+/* 2-lobed Lanczos sinc filter (lanczos.cpp:43-55) */
+float lanczos2(float x) {
+    const float radius = 2.0f;
+    x = std::abs(x);
+    if (x < 1e-4f) return 1.0f; /* Epsilon */
+    if (x > radius) return 0.0f;
+    const float x1 = (float) (M_PI * (double) x); /* M_PI is a double */
+    const float x2 = x1 / radius;
+    return (std::sin(x1) * std::sin(x2)) / (x1 * x2);
+}
+
+/* Resampler<float> (rfilter.h:107-198) resampling one axis from src to dst samples,
+   then resampleAndClamp (:232-280) on `channels` interleaved channels */
+struct AxisResampler {
+    int src, dst, taps;
+    bool repeat; /* ERepeat, else EClamp */
+    std::vector<int> start;
+    std::vector<float> weights;
+    AxisResampler(int sourceRes, int targetRes, bool rep) : src(sourceRes), dst(targetRes), repeat(rep) {
+        float filterRadius = 2.0f, scale = 1.0f, invScale = 1.0f;
+        if (targetRes < sourceRes) {
+            scale = (float) sourceRes / (float) targetRes;
+            invScale = 1 / scale;
+            filterRadius *= scale;
+        }
+        taps = (int) std::ceil(filterRadius * 2);
+        start.resize(targetRes);
+        weights.resize((size_t) taps * targetRes);
+        for (int i = 0; i < targetRes; i++) {
+            const float center = (i + 0.5f) / targetRes * sourceRes;
+            start[i] = (int) std::floor(center - filterRadius + 0.5f);
+            float sum = 0;
+            for (int j = 0; j < taps; j++) {
+                const float pos = start[i] + j + 0.5f - center;
+                const float weight = lanczos2(pos * invScale);
+                weights[(size_t) i * taps + j] = weight;
+                sum += weight;
+            }
+            const float normalization = 1.0f / sum;
+            for (int j = 0; j < taps; j++) weights[(size_t) i * taps + j] *= normalization;
+        }
+    }
+    int at(int pos) const { /* lookup (rfilter.h:437-458) */
+        if (pos < 0 || pos >= src) {
+            if (repeat) {
+                pos %= src;
+                if (pos < 0) pos += src;
+            } else {
+                pos = std::min(std::max(pos, 0), src - 1);
+            }
+        }
+        return pos;
+    }
+    /* clamp to [0, inf): min = 0, max = +infinity as MIPMap passes them (mipmap.h:261) */
+    void run(const float *source, size_t sourceStride, float *target, size_t targetStride, int channels) const {
+        const float mn = 0.0f, mx = std::numeric_limits<float>::infinity();
+        for (int i = 0; i < dst; ++i)
+            for (int ch = 0; ch < channels; ++ch) {
+                float result = 0;
+                for (int j = 0; j < taps; ++j)
+                    result += source[sourceStride * channels * (size_t) at(start[i] + j) + ch] *
+                              weights[(size_t) i * taps + j];
+                const float lo = (mn < result) ? result : mn; /* std::max(min, result) */
+                target[targetStride * channels * (size_t) i + ch] = (lo < mx) ? lo : mx; /* std::min(max, .) */
+            }
+    }
+};
+
+/* Bitmap::resample (bitmap.cpp:2230-2329): x pass (bcu = repeat) then y pass (bcv = clamp) */
+std::vector<float> resampleRGB(const std::vector<float> &in, int w, int h, int nw, int nh) {
+    std::vector<float> cur = in;
+    int cw = w;
+    if (nw != w) {
+        AxisResampler r(w, nw, true);
+        std::vector<float> tmp((size_t) nw * h * 3);
+        for (int y = 0; y < h; ++y) r.run(&cur[(size_t) y * w * 3], 1, &tmp[(size_t) y * nw * 3], 1, 3);
+        cur.swap(tmp);
+        cw = nw;
+    }
+    if (nh != h) {
+        AxisResampler r(h, nh, false);
+        std::vector<float> tmp((size_t) cw * nh * 3);
+        for (int x = 0; x < cw; ++x) r.run(&cur[(size_t) x * 3], cw, &tmp[(size_t) x * 3], cw, 3);
+        cur.swap(tmp);
+    }
+    return cur;
+}
+} // namespace
+
+void buildEnvMipmap(EnvHost &env) {
+    const int w0 = env.w, h0 = env.h;
+    /* level 0: the bitmap with negative values clamped (mipmap.h:226-240), stored as half */
+    std::vector<float> bitmap(env.rgb.size());
+    for (size_t i = 0; i < bitmap.size(); ++i) bitmap[i] = std::max(env.rgb[i], 0.0f);
+    env.mip.clear();
+    env.levelW.clear();
+    env.levelH.clear();
+    env.levelOff.clear();
+    env.ratioX.clear();
+    env.ratioY.clear();
+    auto store = [&](const std::vector<float> &b, int w, int h) {
+        env.levelW.push_back(w);
+        env.levelH.push_back(h);
+        env.levelOff.push_back((int) env.mip.size());
+        env.ratioX.push_back((float) w / (float) w0);
+        env.ratioY.push_back((float) h / (float) h0);
+        for (size_t i = 0; i < (size_t) w * h; ++i)
+            env.mip.push_back({halfToFloat(floatToHalf(b[3 * i])), halfToFloat(floatToHalf(b[3 * i + 1])),
+                               halfToFloat(floatToHalf(b[3 * i + 2])), 0.0f});
+    };
+    store(bitmap, w0, h0);
+    /* progressively downsample the float bitmap until 1x1 (mipmap.h:245-270) */
+    int w = w0, h = h0;
+    while (w > 1 || h > 1) {
+        const int nw = std::max(1, (w + 1) / 2), nh = std::max(1, (h + 1) / 2);
+        bitmap = resampleRGB(bitmap, w, h, nw, nh);
+        w = nw;
+        h = nh;
+        store(bitmap, w, h);
+    }
+    /* Gaussian weight LUT (mipmap.h:296-301); fastexp(float) = (float) exp((double) x) on Linux/x86-64 */
+    for (int i = 0; i < HPT_EWA_LUT; ++i) {
+        const float r2 = (float) i / (float) (HPT_EWA_LUT - 1);
+        env.ewaLut[i] = (float) std::exp((double) (-2.0f * r2)) - (float) std::exp((double) -2.0f);
+    }
+}
 
 bool loadEnvFile(const std::string &path, EnvHost &env, std::string &err) {
     std::ifstream f(path, std::ios::binary);
@@ -663,6 +793,24 @@ void setupCamera(const SceneDesc &d, HptCamera &cam) {
     std::memcpy(cam.toWorld, d.toWorld, sizeof(cam.toWorld));
     cam.invResX = 1.0f / (float) d.width;
     cam.invResY = 1.0f / (float) d.height;
+    /* position differentials on the near plane (perspective.cpp:160-163) */
+    auto s2c = [&](float x, float y) {
+        const float *M = cam.s2c;
+        float px = M[0] * x + M[1] * y + M[2] * 0.0f + M[3], py = M[4] * x + M[5] * y + M[6] * 0.0f + M[7];
+        float pz = M[8] * x + M[9] * y + M[10] * 0.0f + M[11], pw = M[12] * x + M[13] * y + M[14] * 0.0f + M[15];
+        if (pw != 1.0f) {
+            const float inv = 1.0f / pw;
+            px *= inv, py *= inv, pz *= inv;
+        }
+        return std::array<float, 3>{px, py, pz};
+    };
+    const auto p0 = s2c(0.0f, 0.0f), px = s2c(cam.invResX, 0.0f), py = s2c(0.0f, cam.invResY);
+    for (int k = 0; k < 3; ++k) {
+        cam.dx[k] = px[k] - p0[k];
+        cam.dy[k] = py[k] - p0[k];
+    }
+    /* sensorRay.scaleDifferential(1 / sqrt(sampleCount)) (integrator.cpp:143-144,178) */
+    cam.diffScale = 1.0f / std::sqrt((float) std::max(1, d.spp));
     cam.nearClip = d.nearClip;
     cam.farClip = d.farClip;
     cam.width = d.width;

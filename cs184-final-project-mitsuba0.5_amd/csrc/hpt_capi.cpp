@@ -545,6 +545,7 @@ int hpt_prepare(hpt_context *c) {
             rasterizeSunSky(d, c->sunsky, c->env);
         }
         buildEnvMap(c->env);
+        buildEnvMipmap(c->env);
     } catch (const std::exception &e) {
         return setErr(c, HPT_EIO, e.what());
     }
@@ -607,6 +608,16 @@ int hpt_prepare(hpt_context *c) {
     r |= upload(c, c->env.cdfRows.data(), c->env.cdfRows.size() * 4, (const void **) &E.cdfRows);
     r |= upload(c, c->env.cdfCols.data(), c->env.cdfCols.size() * 4, (const void **) &E.cdfCols);
     r |= upload(c, c->env.rowWeights.data(), c->env.rowWeights.size() * 4, (const void **) &E.rowWeights);
+    {
+        std::vector<HptMipLevel> lv(c->env.levelW.size());
+        for (size_t l = 0; l < lv.size(); ++l)
+            lv[l] = {c->env.levelW[l], c->env.levelH[l], c->env.levelOff[l], c->env.ratioX[l], c->env.ratioY[l]};
+        r |= upload(c, c->env.mip.data(), c->env.mip.size() * 16, (const void **) &E.mip);
+        r |= upload(c, lv.data(), lv.size() * sizeof(HptMipLevel), (const void **) &E.levels);
+        r |= upload(c, c->env.ewaLut, sizeof(c->env.ewaLut), (const void **) &E.ewaLut);
+        E.nLevels = (int) lv.size();
+        E.maxAnisotropy = 10.0f; /* envmap.cpp:142 */
+    }
     E.w = c->env.w;
     E.h = c->env.h;
     E.normalization = c->env.normalization;
@@ -1211,6 +1222,36 @@ int hpt_env_batch(hpt_context *c, int n, const float *refp, const float *u, cons
     fetch(oe, de, 3 * (size_t) n);
     fetch(oep, dep, n);
     return HPT_OK;
+}
+
+int hpt_env_eval_filtered(hpt_context *c, int n, const float *d, const float *rx, const float *ry, float *out_rgb) {
+    if (!c || !c->prepared) return setErr(c, HPT_ESTATE, "prepare first");
+    if (c->device == HPT_HOST_ONLY) return setErr(c, HPT_EDEVICE, "host-only context has no device");
+    HIPCHK(c, hipSetDevice(c->device));
+    Scratch S;
+    const float *a = S.in(d, 3 * (size_t) n), *b = S.in(rx, 3 * (size_t) n), *q = S.in(ry, 3 * (size_t) n);
+    float *dout = S.in<float>(nullptr, 3 * (size_t) n);
+    HIPCHK(c, hpt_launch_env_filtered_batch(c->sc, n, a, b, q, dout, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    fetch(out_rgb, dout, 3 * (size_t) n);
+    return HPT_OK;
+}
+
+int hpt_get_env_level(hpt_context *c, int level, float *rgb, int *w, int *h) {
+    if (!c || !c->prepared) return setErr(c, HPT_ESTATE, "prepare first");
+    const int n = (int) c->env.levelW.size();
+    if (level < 0 || level >= n) return n;
+    if (w) *w = c->env.levelW[level];
+    if (h) *h = c->env.levelH[level];
+    if (rgb) {
+        const HptF4 *t = &c->env.mip[c->env.levelOff[level]];
+        for (size_t i = 0; i < (size_t) c->env.levelW[level] * c->env.levelH[level]; ++i) {
+            rgb[3 * i] = t[i].x;
+            rgb[3 * i + 1] = t[i].y;
+            rgb[3 * i + 2] = t[i].z;
+        }
+    }
+    return n;
 }
 
 } /* extern "C" */

@@ -77,6 +77,8 @@ struct HptNode4 {
 
 struct HptCamera {
     float s2c[16];      /* sampleToCamera, row-major (perspective.cpp:155) */
+    float dx[3], dy[3]; /* near-plane position differentials (perspective.cpp:160-163) */
+    float diffScale;    /* 1/sqrt(sampleCount): scaleDifferential (integrator.cpp:143-144) */
     float toWorld[16];  /* camera-to-world, row-major */
     float invResX, invResY, nearClip, farClip;
     float resolution;   /* Sobol pixel resolution (sobol.cpp:147-158) */
@@ -153,8 +155,21 @@ struct HptShape {
     int bsdf;
 };
 
+/* EWA-filtered environment lookups for camera rays (envmap.cpp:391-406,
+ * mipmap.h:629-834): the MIP pyramid's levels, and the 64-entry Gaussian LUT */
+#define HPT_EWA_LUT 64
+struct HptMipLevel {
+    int w, h, off;
+    float ratioX, ratioY; /* level size / level-0 size (m_sizeRatio) */
+};
+
 struct HptEnvMap {
-    const HptF4 *texel;        /* w*h, half-rounded RGB stored as float */
+    const HptF4 *texel;        /* w*h, half-rounded RGB stored as float (= level 0 of mip) */
+    const HptF4 *mip;          /* every MIP level, level l at levels[l].off */
+    const HptMipLevel *levels;
+    const float *ewaLut;       /* HPT_EWA_LUT */
+    int nLevels;
+    float maxAnisotropy;       /* 10 (envmap.cpp:142) */
     const float *cdfRows;       /* h+1 */
     const float *cdfCols;       /* h*(w+1) */
     const float *rowWeights;    /* h */

@@ -57,6 +57,8 @@ hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPath
                              uint32_t *counters, hipStream_t s);
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             uint32_t *counters, uint32_t *stats, uint64_t maxItems, hipStream_t s);
+hipError_t hpt_launch_env_filtered_batch(const HptScene &sc, int n, const float *d, const float *rx, const float *ry,
+                                        float *out, hipStream_t s);
 /* closest-hit rays as 64-ray packets (coherent rays: the camera pass) */
 hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *counters,
                                    uint32_t *stats, uint64_t maxItems, hipStream_t s);

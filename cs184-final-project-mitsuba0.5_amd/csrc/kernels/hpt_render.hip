@@ -1592,6 +1592,140 @@ HD V3 envEval(const HptEnvMap &e, V3 dir) {
     }
     return value * e.scale;
 }
+/* ---- filtered lookups of camera rays: MIPMap::eval with EWA (mipmap.h:503-834) ---- */
+HD V3 mipTexel(const HptEnvMap &e, int level, int x, int y) { /* evalTexel (:503-563): u repeat, v clamp */
+    const HptMipLevel L = e.levels[level];
+    if (x < 0 || x >= L.w) {
+        const int r = x % L.w;
+        x = (r < 0) ? r + L.w : r;
+    }
+    if (y < 0 || y >= L.h) y = clampi(y, 0, L.h - 1);
+    const HptF4 t = e.mip[L.off + y * L.w + x];
+    return v3(t.x, t.y, t.z);
+}
+HD V3 mipBox(const HptEnvMap &e, int level, float ux, float uy) { /* evalBox (:566-569) */
+    const HptMipLevel L = e.levels[level];
+    return mipTexel(e, level, (int) floorf(ux * L.w), (int) floorf(uy * L.h));
+}
+HD V3 mipBilinear(const HptEnvMap &e, int level, float ux, float uy) { /* evalBilinear (:575-596) */
+    if (!isfinite(ux) || !isfinite(uy)) return v3(0, 0, 0);
+    if (level >= e.nLevels) return mipBox(e, e.nLevels - 1, ux, uy);
+    const HptMipLevel L = e.levels[level];
+    const float u = ux * L.w - 0.5f, v = uy * L.h - 0.5f;
+    const int xPos = (int) floorf(u), yPos = (int) floorf(v);
+    const float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = v - yPos, dy2 = 1.0f - dy1;
+    return mipTexel(e, level, xPos, yPos) * dx2 * dy2 + mipTexel(e, level, xPos, yPos + 1) * dx2 * dy1 +
+           mipTexel(e, level, xPos + 1, yPos) * dx1 * dy2 + mipTexel(e, level, xPos + 1, yPos + 1) * dx1 * dy1;
+}
+/* evalEWA (:764-834) */
+HD V3 mipEWA(const HptEnvMap &e, int level, float ux, float uy, float A, float B, float C) {
+    if (!isfinite(A + B + C + ux + uy)) return v3(0, 0, 0);
+    if (level >= e.nLevels) return mipBox(e, e.nLevels - 1, ux, uy);
+    const HptMipLevel L = e.levels[level];
+    const float u = ux * L.w - 0.5f, v = uy * L.h - 0.5f;
+    A /= L.ratioX * L.ratioX;
+    B /= L.ratioX * L.ratioY;
+    C /= L.ratioY * L.ratioY;
+    const float invDet = 1.0f / (-B * B + 4.0f * A * C), deltaU = 2.0f * sqrtf(C * invDet),
+                deltaV = 2.0f * sqrtf(A * invDet);
+    const int u0 = (int) ceilf(u - deltaU), u1 = (int) floorf(u + deltaU);
+    const int v0 = (int) ceilf(v - deltaV), v1 = (int) floorf(v + deltaV);
+    const float As = A * HPT_EWA_LUT, Bs = B * HPT_EWA_LUT, Cs = C * HPT_EWA_LUT;
+    V3 result = v3(0, 0, 0);
+    float denominator = 0.0f;
+    const float ddq = 2 * As, uu0 = (float) u0 - u;
+    for (int vt = v0; vt <= v1; ++vt) {
+        const float vv = (float) vt - v;
+        float q = As * uu0 * uu0 + (Bs * uu0 + Cs * vv) * vv;
+        float dq = As * (2 * uu0 + 1) + Bs * vv;
+        for (int ut = u0; ut <= u1; ++ut) {
+            if (q < (float) HPT_EWA_LUT) {
+                const uint32_t qi = (uint32_t) q;
+                if (qi < HPT_EWA_LUT) {
+                    const float weight = e.ewaLut[(int) q];
+                    result = result + mipTexel(e, level, ut, vt) * weight;
+                    denominator += weight;
+                }
+            }
+            q += dq;
+            dq += ddq;
+        }
+    }
+    if (denominator == 0) return mipBilinear(e, level, ux, uy);
+    return divs(result, denominator);
+}
+HD float log2Mts(float x) { return (float) log((double) x) * (1.0f / logf(2.0f)); } /* math.cpp:103-106 */
+HD float hypot2Mts(float a, float b) {                                                  /* math.cpp:74-86 */
+    if (fabsf(a) > fabsf(b)) {
+        const float r = b / a;
+        return fabsf(a) * sqrtf(1.0f + r * r);
+    }
+    if (b != 0.0f) {
+        const float r = a / b;
+        return fabsf(b) * sqrtf(1.0f + r * r);
+    }
+    return 0.0f;
+}
+/* MIPMap::eval(uv, d0, d1) with filterType EEWA (mipmap.h:629-720) */
+HD V3 mipEval(const HptEnvMap &e, float ux, float uy, float d0x, float d0y, float d1x, float d1y) {
+    const HptMipLevel L0 = e.levels[0];
+    const float du0 = d0x * L0.w, dv0 = d0y * L0.h, du1 = d1x * L0.w, dv1 = d1y * L0.h;
+    float A = dv0 * dv0 + dv1 * dv1, B = -2.0f * (du0 * dv0 + du1 * dv1), C = du0 * du0 + du1 * du1,
+          F = A * C - B * B * 0.25f;
+    const float root = hypot2Mts(A - C, B), Aprime = 0.5f * (A + C - root), Cprime = 0.5f * (A + C + root);
+    float majorRadius = Aprime != 0 ? sqrtf(F / Aprime) : 0, minorRadius = Cprime != 0 ? sqrtf(F / Cprime) : 0;
+    if (!(minorRadius > 0) || !(majorRadius > 0) || F < 0) {
+        const float level = log2Mts(fmaxr(majorRadius, kEpsilon));
+        const int ilevel = (int) floorf(level);
+        if (ilevel < 0) return mipBilinear(e, 0, ux, uy);
+        const float a = level - ilevel;
+        return mipBilinear(e, ilevel, ux, uy) * (1.0f - a) + mipBilinear(e, ilevel + 1, ux, uy) * a;
+    }
+    if (minorRadius * e.maxAnisotropy < majorRadius) {
+        /* artificially enlarge ellipses that are too skinny */
+        minorRadius = majorRadius / e.maxAnisotropy;
+        const float theta = 0.5f * atanf(B / (A - C));
+        float sinTheta, cosTheta;
+        sincosf(theta, &sinTheta, &cosTheta);
+        const float a2 = majorRadius * majorRadius, b2 = minorRadius * minorRadius, sinTheta2 = sinTheta * sinTheta,
+                    cosTheta2 = cosTheta * cosTheta, sin2Theta = 2 * sinTheta * cosTheta;
+        A = a2 * cosTheta2 + b2 * sinTheta2;
+        B = (a2 - b2) * sin2Theta;
+        C = a2 * sinTheta2 + b2 * cosTheta2;
+        F = a2 * b2;
+    }
+    const float scale = 1.0f / F;
+    A *= scale;
+    B *= scale;
+    C *= scale;
+    const float level = fmaxr(0.0f, log2Mts(minorRadius));
+    const int ilevel = (int) level;
+    const float a = level - ilevel;
+    if (majorRadius < 1 || !(A > 0 && C > 0)) return mipBilinear(e, ilevel, ux, uy);
+    return mipEWA(e, ilevel, ux, uy, A, B, C) * (1.0f - a) + mipEWA(e, ilevel + 1, ux, uy, A, B, C) * a;
+}
+/* evalEnvironment of a ray with differentials (envmap.cpp:380-410): camera rays */
+HD V3 envEvalFiltered(const HptEnvMap &e, V3 dir, V3 rxDir, V3 ryDir) {
+    const V3 v = envToLocal(e, dir);
+    const float ux = atan2f(v.x, -v.z) * kInvTwoPi, uy = acosf(fminr(1.0f, fmaxr(-1.0f, v.y))) * kInvPi;
+    const V3 dvdx = envToLocal(e, rxDir) - v, dvdy = envToLocal(e, ryDir) - v;
+    const float t1 = kInvTwoPi / (v.x * v.x + v.z * v.z),
+                t2 = -kInvPi / fmaxr(sqrtf(fmaxr(0.0f, 1.0f - v.y * v.y)), kEpsilon);
+    const V3 value = mipEval(e, ux, uy, t1 * (dvdx.z * v.x - dvdx.x * v.z), t2 * dvdx.y,
+                             t1 * (dvdy.z * v.x - dvdy.x * v.z), t2 * dvdy.y);
+    return value * e.scale;
+}
+
+/* camera ray differential directions of a film sample (perspective.cpp:283-296, scaled by
+   1/sqrt(sampleCount) like sensorRay.scaleDifferential, ray.h:163-168) */
+HD void cameraDifferentials(const HptCamera &c, float posx, float posy, V3 dW, V3 &rx, V3 &ry) {
+    const V3 nearP = xformPoint(c.s2c, v3(posx * c.invResX, posy * c.invResY, 0.0f));
+    rx = xformVector(c.toWorld, normalize(nearP + v3(c.dx[0], c.dx[1], c.dx[2])));
+    ry = xformVector(c.toWorld, normalize(nearP + v3(c.dy[0], c.dy[1], c.dy[2])));
+    rx = dW + (rx - dW) * c.diffScale;
+    ry = dW + (ry - dW) * c.diffScale;
+}
+
 /* internalPdfDirection (:603-633) */
 HD float envPdf(const HptEnvMap &e, V3 d) {
     float uvx = atan2f(d.x, -d.z) * kInvTwoPi, uvy = acosf(fminr(1.0f, fmaxr(-1.0f, d.y))) * kInvPi;
@@ -1884,8 +2018,13 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
         if (__float_as_int(h.x) >= 0) {
             alive = true;
         } else if (!sc.hideEmitters) {
-            float4 rd = P.rd[id];
-            V3 L = envEval(sc.env, v3(rd.x, rd.y, rd.z)); /* throughput == 1 */
+            /* a camera ray keeps its differentials: EWA-filtered lookup (envmap.cpp:394-406) */
+            const float4 rd = P.rd[id];
+            const float2 pos = P.pos[id];
+            const V3 d = v3(rd.x, rd.y, rd.z);
+            V3 rx, ry;
+            cameraDifferentials(sc.cam, pos.x, pos.y, d, rx, ry);
+            V3 L = envEvalFiltered(sc.env, d, rx, ry); /* throughput == 1 */
             V3 T = v3(1.0f, 1.0f, 1.0f);
             V3 c = mul(T, L);
             P.li[id] = make_float4(0.0f + c.x, 0.0f + c.y, 0.0f + c.z, 0.0f);
@@ -2332,6 +2471,17 @@ extern "C" __global__ void k_env_batch(HptScene sc, int n, const float *refp, co
     outEvalPdf[i] = envPdf(sc.env, envToLocal(sc.env, q));
 }
 
+extern "C" __global__ void k_env_filtered_batch(HptScene sc, int n, const float *d, const float *rx, const float *ry,
+                                                 float *out) {
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const V3 v = envEvalFiltered(sc.env, v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
+                                 v3(rx[3 * i], rx[3 * i + 1], rx[3 * i + 2]), v3(ry[3 * i], ry[3 * i + 1], ry[3 * i + 2]));
+    out[3 * i] = v.x;
+    out[3 * i + 1] = v.y;
+    out[3 * i + 2] = v.z;
+}
+
 /* tiny queue-rotation kernel: shade_in <- shade_out, reset the rest */
 extern "C" __global__ void k_rotate(uint32_t *counters, uint32_t *cursors) {
     for (uint32_t i = threadIdx.x; i < HPT_CURSORS; i += blockDim.x) cursors[i * HPT_CURSOR_STRIDE] = 0;
@@ -2458,6 +2608,12 @@ hipError_t hpt_launch_trace_batch(const HptScene &sc, int n, const float *o, con
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_trace_batch, dim3(persistentBlocks((const void *) k_trace_batch, (uint64_t) n)),
                        dim3(HPT_TRACE_BLOCK), 0, s, sc, n, o, d, mint, maxt, flags, ot, os, op, oh, cursor);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_env_filtered_batch(const HptScene &sc, int n, const float *d, const float *rx, const float *ry,
+                                        float *out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_env_filtered_batch, dim3(blocksFor(n, 256)), dim3(256), 0, s, sc, n, d, rx, ry, out);
     return hipGetLastError();
 }
 hipError_t hpt_launch_bsdf_batch(const HptScene &sc, int n, const float *wi, const float *wo, const float *u,

@@ -97,6 +97,8 @@ SIGNATURES = {
     "hpt_get_envmap": (C.c_int, [C.c_void_p, _f, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hpt_get_marschner_tables": (C.c_int, [C.c_void_p, _f, _f, _f, _f, _f, _f]),
     "hpt_sobol_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u32, _u32, _u32, _u32, _u64, _f]),
+    "hpt_env_eval_filtered": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f]),
+    "hpt_get_env_level": (C.c_int, [C.c_void_p, C.c_int, _f, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hpt_trace_batch": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f, C.c_int, _f, _i32, _f, _u8]),
     "hpt_bsdf_batch": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f, _f, _f, _f, _u32]),
     "hpt_env_batch": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f, _f, _f, _f, _f]),
@@ -335,6 +337,27 @@ class Renderer:
                                              (1 if shadow else 0) | (2 if tiny_stack else 0) | (4 if packet else 0),
                                              _p(ot, _f), _p(oiv, _i32), _p(op, _f), _p(oh, _u8)))
         return oh.astype(bool) if shadow else (ot, oiv, op)
+
+    def env_filtered(self, d, rx, ry):
+        """evalEnvironment of rays with differentials (EWA over the MIP pyramid)"""
+        d, rx, ry = (_f32(a).reshape(-1, 3) for a in (d, rx, ry))
+        out = np.zeros_like(d)
+        self._check(self.lib.hpt_env_eval_filtered(self.h, d.shape[0], _p(d, _f), _p(rx, _f), _p(ry, _f), _p(out, _f)))
+        return out
+
+    def env_levels(self):
+        """The environment's MIP pyramid as a list of (h, w, 3) float32 arrays."""
+        n = self.lib.hpt_get_env_level(self.h, -1, None, None, None)
+        if n < 0:
+            self._check(n)
+        out = []
+        for lv in range(n):
+            w, h = C.c_int(), C.c_int()
+            self.lib.hpt_get_env_level(self.h, lv, None, C.byref(w), C.byref(h))
+            a = np.zeros((h.value, w.value, 3), np.float32)
+            self.lib.hpt_get_env_level(self.h, lv, _p(a, _f), None, None)
+            out.append(a)
+        return out
 
     def bsdf(self, wi, wo, u):
         wi = _f32(wi).reshape(-1, 3)

@@ -209,6 +209,15 @@ int hpt_bsdf_batch(hpt_context *ctx, int n, const float *wi, const float *wo, co
    evalEnvironment / pdfDirect (:380-410, :545-556) for directions dq */
 int hpt_env_batch(hpt_context *ctx, int n, const float *ref_p, const float *u, const float *dq, float *out_d,
                   float *out_value, float *out_pdf, float *out_dist, float *out_eval, float *out_eval_pdf);
+/* evalEnvironment of rays WITH differentials -- camera rays: EWA-filtered MIP lookup
+   (envmap.cpp:380-410, mipmap.h:629-834); d, rx, ry are world directions of the ray and
+   of its x / y differential rays */
+int hpt_env_eval_filtered(hpt_context *ctx, int n, const float *d, const float *rx, const float *ry,
+                          float *out_rgb);
+/* MIP level `level` of the environment (mipmap.h:155-302: Lanczos-2 downsampled, stored as
+   half): width, height and w*h RGB texels (any pointer may be NULL).  Returns the number of
+   levels (a level out of range only returns it). */
+int hpt_get_env_level(hpt_context *ctx, int level, float *rgb, int *w, int *h);
 
 #ifdef __cplusplus
 }

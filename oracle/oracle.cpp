@@ -1498,6 +1498,204 @@ struct EnvMap {
     float m[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, minv[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
     V3 bsCenter;
     float bsRadius = 0;
+    /* MIP pyramid (mipmap.h:155-302): half-rounded RGB per level, m_sizeRatio, EWA LUT */
+    std::vector<std::vector<float>> lev;
+    std::vector<int> lw, lh;
+    std::vector<float> ratioX, ratioY;
+    float lut[64];
+    float maxAnisotropy = 10.0f; /* envmap.cpp:142 */
+
+    /* LanczosSincFilter::eval, lobes = 2 (lanczos.cpp:43-55; envmap.cpp:167-172) */
+    static float lanczos(float x) {
+        x = std::abs(x);
+        if (x < kEpsilon) return 1.0f;
+        else if (x > 2.0f) return 0.0f;
+        float x1 = (float) (M_PI * x);
+        float x2 = x1 / 2.0f;
+        return (std::sin(x1) * std::sin(x2)) / (x1 * x2);
+    }
+    /* Resampler<float> + resampleAndClamp(min 0, max inf) along one axis (rfilter.h:123-280, 437-458) */
+    static void resampleAxis(const float *src, size_t sStride, float *dst, size_t dStride, int sourceRes,
+                             int targetRes, bool repeat) {
+        float filterRadius = 2.0f, scale = 1.0f, invScale = 1.0f;
+        if (targetRes < sourceRes) {
+            scale = (float) sourceRes / (float) targetRes;
+            invScale = 1 / scale;
+            filterRadius *= scale;
+        }
+        const int taps = (int) std::ceil(filterRadius * 2);
+        std::vector<float> wts(taps);
+        for (int i = 0; i < targetRes; i++) {
+            float center = (i + 0.5f) / targetRes * sourceRes;
+            int start = (int) std::floor(center - filterRadius + 0.5f);
+            float sum = 0;
+            for (int j = 0; j < taps; j++) {
+                float w = lanczos((start + j + 0.5f - center) * invScale);
+                wts[j] = w;
+                sum += w;
+            }
+            float normalization = 1.0f / sum;
+            for (int j = 0; j < taps; j++) wts[j] = wts[j] * normalization;
+            for (int ch = 0; ch < 3; ++ch) {
+                float result = 0;
+                for (int j = 0; j < taps; ++j) {
+                    int pos = start + j;
+                    if (pos < 0 || pos >= sourceRes) pos = repeat ? modulo(pos, sourceRes) : clampv(pos, 0, sourceRes - 1);
+                    result += src[sStride * 3 * (size_t) pos + ch] * wts[j];
+                }
+                result = std::max(0.0f, result);
+                dst[dStride * 3 * (size_t) i + ch] = std::min(std::numeric_limits<float>::infinity(), result);
+            }
+        }
+    }
+    void buildPyramid(const float *rgb) {
+        std::vector<float> bmp((size_t) w * h * 3);
+        for (size_t i = 0; i < bmp.size(); ++i) bmp[i] = std::max(rgb[i], 0.0f);
+        auto keep = [&](const std::vector<float> &b, int W, int H) {
+            std::vector<float> q(b.size());
+            for (size_t i = 0; i < b.size(); ++i) q[i] = halfToFloat(floatToHalf(b[i]));
+            lev.push_back(q);
+            lw.push_back(W);
+            lh.push_back(H);
+            ratioX.push_back((float) W / (float) w);
+            ratioY.push_back((float) H / (float) h);
+        };
+        lev.clear(), lw.clear(), lh.clear(), ratioX.clear(), ratioY.clear();
+        keep(bmp, w, h);
+        int W = w, H = h;
+        while (W > 1 || H > 1) { /* Bitmap::resample (bitmap.cpp:2230-2329): x (repeat), then y (clamp) */
+            int nW = std::max(1, (W + 1) / 2), nH = std::max(1, (H + 1) / 2);
+            if (nW != W) {
+                std::vector<float> t((size_t) nW * H * 3);
+                for (int y = 0; y < H; ++y) resampleAxis(&bmp[(size_t) y * W * 3], 1, &t[(size_t) y * nW * 3], 1, W, nW, true);
+                bmp.swap(t);
+            }
+            if (nH != H) {
+                std::vector<float> t((size_t) nW * nH * 3);
+                for (int x = 0; x < nW; ++x) resampleAxis(&bmp[(size_t) x * 3], nW, &t[(size_t) x * 3], nW, H, nH, false);
+                bmp.swap(t);
+            }
+            W = nW, H = nH;
+            keep(bmp, W, H);
+        }
+        for (int i = 0; i < 64; ++i) {
+            float r2 = (float) i / (float) 63;
+            lut[i] = (float) ::exp((double) (-2.0f * r2)) - (float) ::exp((double) -2.0f); /* math::fastexp */
+        }
+    }
+    /* mipmap.h:503-563 at level l */
+    Spec texL(int l, int x, int y) const {
+        if (x < 0 || x >= lw[l]) x = modulo(x, lw[l]);
+        if (y < 0 || y >= lh[l]) y = clampv(y, 0, lh[l] - 1);
+        const float *p = &lev[l][3 * ((size_t) y * lw[l] + x)];
+        return Spec(p[0], p[1], p[2]);
+    }
+    Spec evalBox(int l, float ux, float uy) const { /* :566-569 */
+        return texL(l, floorToInt(ux * lw[l]), floorToInt(uy * lh[l]));
+    }
+    Spec evalBilinear(int l, float ux, float uy) const { /* :575-596 */
+        if (!std::isfinite(ux) || !std::isfinite(uy)) return Spec(0.0f);
+        if (l >= (int) lev.size()) return evalBox((int) lev.size() - 1, ux, uy);
+        float u = ux * lw[l] - 0.5f, v = uy * lh[l] - 0.5f;
+        int xPos = floorToInt(u), yPos = floorToInt(v);
+        float dx1 = u - xPos, dx2 = 1.0f - dx1, dy1 = v - yPos, dy2 = 1.0f - dy1;
+        return texL(l, xPos, yPos) * dx2 * dy2 + texL(l, xPos, yPos + 1) * dx2 * dy1 +
+               texL(l, xPos + 1, yPos) * dx1 * dy2 + texL(l, xPos + 1, yPos + 1) * dx1 * dy1;
+    }
+    Spec evalEWA(int l, float ux, float uy, float A, float B, float C) const { /* :764-834 */
+        if (!std::isfinite(A + B + C + ux + uy)) return Spec(0.0f);
+        if (l >= (int) lev.size()) return evalBox((int) lev.size() - 1, ux, uy);
+        float u = ux * lw[l] - 0.5f, v = uy * lh[l] - 0.5f;
+        A /= ratioX[l] * ratioX[l];
+        B /= ratioX[l] * ratioY[l];
+        C /= ratioY[l] * ratioY[l];
+        float invDet = 1.0f / (-B * B + 4.0f * A * C), deltaU = 2.0f * std::sqrt(C * invDet),
+              deltaV = 2.0f * std::sqrt(A * invDet);
+        int u0 = (int) std::ceil(u - deltaU), u1 = floorToInt(u + deltaU);
+        int v0 = (int) std::ceil(v - deltaV), v1 = floorToInt(v + deltaV);
+        float As = A * 64, Bs = B * 64, Cs = C * 64;
+        Spec result(0.0f);
+        float denominator = 0.0f;
+        float ddq = 2 * As, uu0 = (float) u0 - u;
+        for (int vt = v0; vt <= v1; ++vt) {
+            const float vv = (float) vt - v;
+            float q = As * uu0 * uu0 + (Bs * uu0 + Cs * vv) * vv;
+            float dq = As * (2 * uu0 + 1) + Bs * vv;
+            for (int ut = u0; ut <= u1; ++ut) {
+                if (q < (float) 64) {
+                    uint32_t qi = (uint32_t) q;
+                    if (qi < 64) {
+                        const float weight = lut[(int) q];
+                        result += texL(l, ut, vt) * weight;
+                        denominator += weight;
+                    }
+                }
+                q += dq;
+                dq += ddq;
+            }
+        }
+        if (denominator == 0) return evalBilinear(l, ux, uy);
+        return result / denominator;
+    }
+    static float log2f_(float x) { return (float) ::log((double) x) * (1.0f / std::log(2.0f)); } /* math.cpp:103 */
+    static float hypot2f_(float a, float b) {                                                       /* math.cpp:74 */
+        float r;
+        if (std::abs(a) > std::abs(b)) {
+            r = b / a;
+            r = std::abs(a) * std::sqrt(1.0f + r * r);
+        } else if (b != 0.0f) {
+            r = a / b;
+            r = std::abs(b) * std::sqrt(1.0f + r * r);
+        } else {
+            r = 0.0f;
+        }
+        return r;
+    }
+    /* MIPMap::eval, EEWA (mipmap.h:629-720) */
+    Spec mipEval(float ux, float uy, float d0x, float d0y, float d1x, float d1y) const {
+        float du0 = d0x * lw[0], dv0 = d0y * lh[0], du1 = d1x * lw[0], dv1 = d1y * lh[0];
+        float A = dv0 * dv0 + dv1 * dv1, B = -2.0f * (du0 * dv0 + du1 * dv1), C = du0 * du0 + du1 * du1,
+              F = A * C - B * B * 0.25f;
+        float root = hypot2f_(A - C, B), Aprime = 0.5f * (A + C - root), Cprime = 0.5f * (A + C + root),
+              majorRadius = Aprime != 0 ? std::sqrt(F / Aprime) : 0,
+              minorRadius = Cprime != 0 ? std::sqrt(F / Cprime) : 0;
+        if (!(minorRadius > 0) || !(majorRadius > 0) || F < 0) {
+            float level = log2f_(std::max(majorRadius, kEpsilon));
+            int ilevel = floorToInt(level);
+            if (ilevel < 0) return evalBilinear(0, ux, uy);
+            float a = level - ilevel;
+            return evalBilinear(ilevel, ux, uy) * (1.0f - a) + evalBilinear(ilevel + 1, ux, uy) * a;
+        }
+        if (minorRadius * maxAnisotropy < majorRadius) {
+            minorRadius = majorRadius / maxAnisotropy;
+            float theta = 0.5f * std::atan(B / (A - C)), sinTheta = std::sin(theta), cosTheta = std::cos(theta);
+            float a2 = majorRadius * majorRadius, b2 = minorRadius * minorRadius, sinTheta2 = sinTheta * sinTheta,
+                  cosTheta2 = cosTheta * cosTheta, sin2Theta = 2 * sinTheta * cosTheta;
+            A = a2 * cosTheta2 + b2 * sinTheta2;
+            B = (a2 - b2) * sin2Theta;
+            C = a2 * sinTheta2 + b2 * cosTheta2;
+            F = a2 * b2;
+        }
+        float scl = 1.0f / F;
+        A *= scl;
+        B *= scl;
+        C *= scl;
+        float level = std::max((float) 0.0f, log2f_(minorRadius));
+        int ilevel = (int) level;
+        float a = level - ilevel;
+        if (majorRadius < 1 || !(A > 0 && C > 0)) return evalBilinear(ilevel, ux, uy);
+        return evalEWA(ilevel, ux, uy, A, B, C) * (1.0f - a) + evalEWA(ilevel + 1, ux, uy, A, B, C) * a;
+    }
+    /* evalEnvironment of a RayDifferential with differentials (envmap.cpp:380-410) */
+    Spec evalEnvironmentFiltered(const V3 &dir, const V3 &rxDir, const V3 &ryDir) const {
+        V3 v = toLocal(dir);
+        float ux = std::atan2(v.x, -v.z) * kInvTwoPi, uy = safe_acos(v.y) * kInvPi;
+        V3 dvdx = toLocal(rxDir) - v, dvdy = toLocal(ryDir) - v;
+        float t1 = kInvTwoPi / (v.x * v.x + v.z * v.z), t2 = -kInvPi / std::max(safe_sqrt(1.0f - v.y * v.y), kEpsilon);
+        return mipEval(ux, uy, t1 * (dvdx.z * v.x - dvdx.x * v.z), t2 * dvdx.y, t1 * (dvdy.z * v.x - dvdy.x * v.z),
+                       t2 * dvdy.y) *
+               scale;
+    }
 
     Spec tex(int x, int y) const { /* mipmap.h:503-563, bcu=repeat, bcv=clamp */
         if (x < 0 || x >= w) x = modulo(x, w);
@@ -1506,6 +1704,7 @@ struct EnvMap {
         return Spec(p[0], p[1], p[2]);
     }
     void build(const float *rgb) { /* envmap.cpp:244-314 */
+        buildPyramid(rgb);
         texel.resize((size_t) w * h * 3);
         for (size_t i = 0; i < (size_t) w * h * 3; ++i)
             texel[i] = halfToFloat(floatToHalf(std::max(rgb[i], 0.0f)));
@@ -2051,9 +2250,14 @@ Spec Li(const orc_scene *s, const CamRay &cr, Sampler &sampler, Stats *st, int *
         if (!valid) {
             if (emitted && (!s->hideEmitters || scattered)) {
                 if (s->hasEnv) {
-                    if (primary && st && s->env.ewaMajorRadius(cr.ray.d, cr.rxDir, cr.ryDir) >= 1.0f)
-                        st->ewaViolations++;
-                    Li += throughput * s->env.evalEnvironment(ray.d);
+                    /* a camera ray keeps its differentials (EWA lookup); after a bounce
+                       ray = Ray(...) drops them (ray.h:196-208): bilinear at level 0 */
+                    if (primary) {
+                        if (st && s->env.ewaMajorRadius(cr.ray.d, cr.rxDir, cr.ryDir) >= 1.0f) st->ewaViolations++;
+                        Li += throughput * s->env.evalEnvironmentFiltered(cr.ray.d, cr.rxDir, cr.ryDir);
+                    } else {
+                        Li += throughput * s->env.evalEnvironment(ray.d);
+                    }
                 }
             }
             break;
@@ -2799,6 +3003,24 @@ void orc_env_eval(orc_scene *s, int n, const float *d, float *out_rgb, float *ou
         for (int k = 0; k < 3; ++k) out_rgb[3 * i + k] = v.s[k];
         out_pdf[i] = s->env.internalPdfDirection(s->env.toLocal(dd));
     }
+}
+
+void orc_env_eval_filtered(orc_scene *s, int n, const float *d, const float *rx, const float *ry, float *out_rgb) {
+    for (int i = 0; i < n; ++i) {
+        Spec v = s->env.evalEnvironmentFiltered(V3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
+                                                V3(rx[3 * i], rx[3 * i + 1], rx[3 * i + 2]),
+                                                V3(ry[3 * i], ry[3 * i + 1], ry[3 * i + 2]));
+        for (int k = 0; k < 3; ++k) out_rgb[3 * i + k] = v.s[k];
+    }
+}
+
+int orc_env_level(orc_scene *s, int level, float *rgb, int *w, int *h) {
+    const int n = (int) s->env.lev.size();
+    if (level < 0 || level >= n) return n;
+    if (w) *w = s->env.lw[level];
+    if (h) *h = s->env.lh[level];
+    if (rgb) std::memcpy(rgb, s->env.lev[level].data(), s->env.lev[level].size() * sizeof(float));
+    return n;
 }
 
 void orc_trace_paths(orc_scene *s, int n, const uint32_t *px, const uint32_t *py, const uint32_t *frame,

@@ -123,6 +123,11 @@ void orc_idist_warp(const float *weights, int size, int ndist, int n, const floa
 void orc_env_sample(orc_scene *s, int n, const float *ref_p, const float *u, float *out_d,
                     float *out_value, float *out_pdf, float *out_dist);
 void orc_env_eval(orc_scene *s, int n, const float *d, float *out_rgb, float *out_pdf);
+/* evalEnvironment of rays with differentials: EWA over the MIP pyramid (envmap.cpp:380-410,
+   mipmap.h:155-302, 629-834) */
+void orc_env_eval_filtered(orc_scene *s, int n, const float *d, const float *rx, const float *ry, float *out_rgb);
+/* MIP level of the environment (w*h RGB); returns the number of levels */
+int orc_env_level(orc_scene *s, int level, float *rgb, int *w, int *h);
 /* Full path radiance for one camera sample (debug / unit parity) */
 void orc_trace_paths(orc_scene *s, int n, const uint32_t *px, const uint32_t *py,
                      const uint32_t *frame, float *out_rgb, float *out_pos, int32_t *out_depth);

@@ -62,6 +62,8 @@ _SIG = {
     "orc_idist_warp": (None, [_f, C.c_int, C.c_int, C.c_int, _f, _f, _i32, _f, _f, _f]),
     "orc_env_sample": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f, _f]),
     "orc_env_eval": (None, [C.c_void_p, C.c_int, _f, _f, _f]),
+    "orc_env_eval_filtered": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f]),
+    "orc_env_level": (C.c_int, [C.c_void_p, C.c_int, _f, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "orc_trace_paths": (None, [C.c_void_p, C.c_int, _u32, _u32, _u32, _f, _f, _i32]),
 }
 
@@ -292,6 +294,23 @@ class Oracle:
         pdf = np.zeros(n, np.float32)
         self.lib.orc_env_eval(self.s, n, p(d, _f), p(rgb, _f), p(pdf, _f))
         return rgb, pdf
+
+    def env_eval_filtered(self, d, rx, ry):
+        d, rx, ry = (np.ascontiguousarray(a, np.float32).reshape(-1, 3) for a in (d, rx, ry))
+        out = np.zeros_like(d)
+        self.lib.orc_env_eval_filtered(self.s, d.shape[0], p(d, _f), p(rx, _f), p(ry, _f), p(out, _f))
+        return out
+
+    def env_levels(self):
+        n = self.lib.orc_env_level(self.s, -1, None, None, None)
+        out = []
+        for lv in range(n):
+            w, h = C.c_int(), C.c_int()
+            self.lib.orc_env_level(self.s, lv, None, C.byref(w), C.byref(h))
+            a = np.zeros((h.value, w.value, 3), np.float32)
+            self.lib.orc_env_level(self.s, lv, p(a, _f), None, None)
+            out.append(a)
+        return out
 
     def trace_paths(self, px, py, frame):
         px, py, frame = [np.ascontiguousarray(a, np.uint32) for a in (px, py, frame)]

@@ -319,3 +319,70 @@ def test_sunsky_rasterisation_geometry():
     assert np.all(lum[ang < radius - 1.5] > sky_hi)
     c = env[sun].mean(0)
     assert c[0] >= c[1] >= c[2] > 0  # attenuated solar spectrum: warm white
+
+
+def _lanczos2(x):
+    x = np.abs(x)
+    x1 = np.pi * x
+    with np.errstate(invalid="ignore", divide="ignore"):
+        v = np.sin(x1) * np.sin(x1 / 2) / (x1 * x1 / 2)
+    return np.where(x < 1e-4, 1.0, np.where(x > 2.0, 0.0, v))
+
+
+def _resample_axis(a, n_out, axis, repeat):
+    """Lanczos-2 resampling of one axis like rfilter.h's Resampler (float64, normalised taps)."""
+    a = np.moveaxis(a, axis, 0)
+    n_in = a.shape[0]
+    radius, inv = 2.0, 1.0
+    if n_out < n_in:
+        inv = n_out / n_in
+        radius = 2.0 * n_in / n_out
+    taps = int(np.ceil(radius * 2))
+    out = np.zeros((n_out,) + a.shape[1:])
+    for i in range(n_out):
+        c = (i + 0.5) / n_out * n_in
+        st = int(np.floor(c - radius + 0.5))
+        idx = np.arange(st, st + taps)
+        w = _lanczos2((idx + 0.5 - c) * inv)
+        w = w / w.sum()
+        idx = np.mod(idx, n_in) if repeat else np.clip(idx, 0, n_in - 1)
+        out[i] = np.maximum(np.tensordot(w, a[idx], axes=(0, 0)), 0.0)
+    return np.moveaxis(out, 0, axis)
+
+
+@pytest.mark.parametrize("resolution", [None, 75])
+def test_env_mip_pyramid(tmp_path, resolution):
+    """The environment's MIP pyramid (envmap.cpp:165-182 -> mipmap.h:155-302: Lanczos-2
+    downsampling, u repeat / v clamp, clamped to >= 0, stored as half) is bitwise the
+    oracle's restatement, halves (w+1)/2 x (h+1)/2 down to 1x1, and agrees with an
+    independent float64 numpy resampling of the same float chain."""
+    xml = scenes.make_scene("furball_marschner", str(tmp_path), n_strands=200)
+    if resolution:
+        src = open(xml).read().replace('<emitter type="sunsky">',
+                                       '<emitter type="sunsky"><integer name="resolution" value="%d"/>' % resolution)
+        xml = str(tmp_path / "res.xml")
+        open(xml, "w").write(src)
+    r = native.Renderer(device=native.HOST_ONLY)
+    r.load_scene_xml(xml, {"width": 16, "height": 16, "spp": 1, "maxDepth": 4})
+    r.prepare()
+    env = r.envmap()
+    levels = r.env_levels()
+    o = oracle_lib.Oracle()
+    e32 = np.ascontiguousarray(env, np.float32)
+    o.check(o.lib.orc_set_envmap(o.s, e32.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), env.shape[1], env.shape[0],
+                                 1.0, None))
+    ol = o.env_levels()
+    assert len(levels) == len(ol) >= 2
+    h, w = env.shape[:2]
+    for k, (a, b) in enumerate(zip(levels, ol)):
+        assert a.shape == (h, w, 3), (k, a.shape, (h, w))
+        np.testing.assert_array_equal(a, b)
+        h, w = max(1, (h + 1) // 2), max(1, (w + 1) // 2)
+    assert levels[-1].shape == (1, 1, 3)
+    # independent check of the first two downsampling steps (float64 numpy vs the float chain)
+    cur = np.maximum(env.astype(np.float64), 0.0)
+    for k in (1, 2):
+        hh, ww = levels[k].shape[:2]
+        cur = _resample_axis(cur, ww, 1, True) if cur.shape[1] != ww else cur
+        cur = _resample_axis(cur, hh, 0, False) if cur.shape[0] != hh else cur
+        np.testing.assert_allclose(levels[k], cur, rtol=2e-3, atol=1e-5 * float(env.max()))
