@@ -2225,9 +2225,12 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_post(HptScene sc, Hpt
 template <bool MULTI>
 __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
                                           uint32_t *__restrict__ counters, uint2 *stk) {
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = tid < counters[HPT_Q_SHADE_IN];
-    PathIO io{P, nullptr, nullptr, 0, 0, live ? shadeQ[tid] : 0u};
+    /* two lanes per path: the even lane shades, traces the shadow ray and runs
+       post; the odd lane traces the continuation ray at the same time */
+    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, lane = __lane_id(), partner = lane & ~1u;
+    const bool odd = (tid & 1u) != 0;
+    bool live = (tid >> 1) < counters[HPT_Q_SHADE_IN];
+    PathIO io{P, nullptr, nullptr, 0, 0, live ? shadeQ[tid >> 1] : 0u};
     uint32_t nb = 0;
     TraceCounters tc;
     auto trace = [&](bool shadowRay) {
@@ -2238,25 +2241,43 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
             }
         io.finish(sc, 0, r);
     };
-    while (live) {
+    while (__ballot(live) != 0) {
         bool cont = false, shadow = false;
-        ++nb;
-        shadePath<MULTI>(sc, P, io.id, counters, cont, shadow);
-        if (shadow) trace(true);
-        if (!cont) break;
-        trace(false);
-        if (!postPath(sc, P, io.id, counters)) break;
+        if (live && !odd) {
+            ++nb;
+            shadePath<MULTI>(sc, P, io.id, counters, cont, shadow);
+        }
+        __threadfence_block(); /* the continuation ray is in HBM for the odd lane */
+        const int f = __shfl((cont ? 1 : 0) | (shadow ? 2 : 0), (int) partner);
+        cont = (f & 1) != 0;
+        shadow = (f & 2) != 0;
+        if (live && !odd && shadow) trace(true);
+        if (live && odd && cont) trace(false);
+        __threadfence_block(); /* the hit record is in HBM for the even lane */
+        bool alive = false;
+        if (live && !odd && cont) alive = postPath(sc, P, io.id, counters);
+        live = live && __shfl(alive ? 1 : 0, (int) partner) != 0;
     }
     for (int off = 32; off > 0; off >>= 1) nb += __shfl_down(nb, off);
     if (__lane_id() == 0 && nb) atomicAdd(&counters[HPT_Q_TAIL_BOUNCES], nb);
 }
-extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_tail(HptScene sc, HptPaths P,
+#ifndef HPT_TAIL_WAVES
+#define HPT_TAIL_WAVES 4 /* register target: 4 waves/SIMD hold ~2.6e5 lanes = 1.3e5 paths resident */
+#endif
+/* small tails (every lane resident at 2 waves/SIMD): the spill-free register allocation */
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_tail_small(HptScene sc, HptPaths P,
+                                                                     const uint32_t *__restrict__ shadeQ,
+                                                                     uint32_t *__restrict__ counters) {
+    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    tailPaths<false>(sc, P, shadeQ, counters, stk + threadIdx.x);
+}
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void k_tail(HptScene sc, HptPaths P,
                                                                const uint32_t *__restrict__ shadeQ,
                                                                uint32_t *__restrict__ counters) {
     __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
     tailPaths<false>(sc, P, shadeQ, counters, stk + threadIdx.x);
 }
-extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_tail_multi(HptScene sc, HptPaths P,
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void k_tail_multi(HptScene sc, HptPaths P,
                                                                      const uint32_t *__restrict__ shadeQ,
                                                                      uint32_t *__restrict__ counters) {
     __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
@@ -2574,11 +2595,26 @@ hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t
 hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *counters,
                            uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
+    /* two lanes per path; tails that fit at 2 waves/SIMD (measured on MI355X: 2-wave
+       residency of 256 CUs = 1.3e5 lanes) run without register spills */
+    static int smallLanes = 0;
+    if (smallLanes == 0) {
+        int dev = 0;
+        hipDeviceProp_t prop;
+        smallLanes = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+                         ? prop.multiProcessorCount * 4 * 2 * 64
+                         : 131072;
+    }
+    if (sc.nShapes <= 1 && 2 * maxItems <= (uint64_t) smallLanes) {
+        hipLaunchKernelGGL(k_tail_small, dim3(blocksFor(2 * maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc,
+                           P, shadeQ, counters);
+        return hipGetLastError();
+    }
     if (sc.nShapes > 1)
-        hipLaunchKernelGGL(k_tail_multi, dim3(blocksFor(maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc, P,
-                           shadeQ, counters);
+        hipLaunchKernelGGL(k_tail_multi, dim3(blocksFor(2 * maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc,
+                           P, shadeQ, counters);
     else
-        hipLaunchKernelGGL(k_tail, dim3(blocksFor(maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc, P,
+        hipLaunchKernelGGL(k_tail, dim3(blocksFor(2 * maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc, P,
                            shadeQ, counters);
     return hipGetLastError();
 }
