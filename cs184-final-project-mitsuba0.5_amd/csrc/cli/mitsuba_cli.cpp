@@ -4,14 +4,18 @@
  * Mirrors src/mitsuba/mitsuba.cpp:52-400 for the hair path: parse options,
  * load each scene XML, render, develop the film and write it next to the
  * scene (or to -o).  Rendering runs on MI355X devices through libhairpt.so;
- * with --gpus N the 32x32 blocks are dealt block-cyclically over N devices
- * (one host thread + one hpt_context each) and the per-device films are
+ * with --gpus N the 32x32 blocks are dealt over N devices (Hilbert-cyclic,
+ * one host thread + one hpt_context each) and the per-device films are
  * summed -- the single-node analogue of the reference's -c remote workers.
+ * -r sec writes the partial image every `sec` seconds like the reference's
+ * flush timer (mitsuba.cpp:300-330): the samples are rendered in chunks and
+ * the film accumulated so far is developed between chunks.
  *
  *   mitsuba [options] <scene.xml> [<scene2.xml> ...]
  *     -D key=val   define $key for the XML        -o fname   output file
  *     -p count     (accepted; GPU render)          -q         quiet
- *     -x           skip scenes whose output exists -b/-r/-z/-v (accepted)
+ *     -x           skip scenes whose output exists -r sec  write partial images
+ *     -b/-z/-v (accepted)
  *     --spp N --width W --height H --max-depth D   overrides
  *     --device i   first device                    --gpus N   devices to use
  *     --stats      print timing / traversal statistics
@@ -41,6 +45,7 @@ void usage() {
         "   -p count    Override the detected number of processors (ignored: GPU render)\n"
         "   -q          Quiet mode - do not print any log messages to stdout\n"
         "   -x          Skip rendering of files where output already exists\n"
+        "   -r sec      Write (partial) output images every 'sec' seconds\n"
         "   --spp N --width W --height H --max-depth D   override scene parameters\n"
         "   --device I --gpus N   render on N devices starting at I\n"
         "   --stats     print per-kernel timing and traversal counters\n");
@@ -51,6 +56,7 @@ struct Opts {
     std::string out;
     bool quiet = false, skipExisting = false, stats = false;
     int spp = 0, width = 0, height = 0, maxDepth = -2, device = 0, gpus = 1;
+    double flushSec = 0; /* -r */
     std::vector<std::string> scenes;
 };
 
@@ -79,7 +85,8 @@ int main(int argc, char **argv) {
             if (eq == std::string::npos) { std::fprintf(stderr, "-D expects key=value\n"); return 1; }
             o.defines.push_back({kv.substr(0, eq), kv.substr(eq + 1)});
         } else if (a == "-o") o.out = next("-o");
-        else if (a == "-p" || a == "-b" || a == "-r" || a == "-L" || a == "-a") (void) next(a.c_str());
+        else if (a == "-r") o.flushSec = std::atof(next("-r").c_str());
+        else if (a == "-p" || a == "-b" || a == "-L" || a == "-a") (void) next(a.c_str());
         else if (a == "-q") o.quiet = true;
         else if (a == "-x") o.skipExisting = true;
         else if (a == "-v" || a == "-z" || a == "-t" || a == "-w") {}
@@ -161,34 +168,49 @@ int main(int argc, char **argv) {
         }
         std::vector<std::vector<float>> films(G, std::vector<float>((size_t) W * H * 4, 0.0f));
         std::vector<int> rcs(G, 0);
-        auto t0 = std::chrono::steady_clock::now();
-        std::vector<std::thread> th;
-        for (int g = 0; g < G; ++g)
-            th.emplace_back([&, g] {
-                hpt_render_params p;
-                std::memset(&p, 0, sizeof(p));
-                p.spp_begin = 0;
-                p.spp_end = spp;
-                p.shard = g;
-                p.n_shards = G;
-                p.collect_stats = o.stats ? 2 : 0;
-                rcs[g] = hpt_render(ctx[g], &p, films[g].data());
-            });
-        for (auto &t : th) t.join();
-        double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        for (int g = 0; g < G; ++g)
-            if (rcs[g]) { std::fprintf(stderr, "render failed on device %d: %s\n", o.device + g, hpt_last_error(ctx[g])); return 4; }
-        /* film combine (renderproc.cpp:142-145) + develop (Film::develop) */
-        std::vector<float> sum((size_t) W * H * 4, 0.0f);
-        for (int g = 0; g < G; ++g)
-            for (size_t i = 0; i < sum.size(); ++i) sum[i] += films[g][i];
         hpt_film_params fp;
         hpt_get_film_params(ctx[0], &fp);
         char written[4096];
-        if (hpt_write_film(ctx[0], out.c_str(), sum.data(), W, H, &fp, written, sizeof(written))) {
-            std::fprintf(stderr, "%s\n", hpt_last_error(ctx[0]));
-            return 5;
+        /* film combine (renderproc.cpp:142-145) + develop (Film::develop) */
+        auto develop = [&]() -> bool {
+            std::vector<float> sum((size_t) W * H * 4, 0.0f);
+            for (int g = 0; g < G; ++g)
+                for (size_t i = 0; i < sum.size(); ++i) sum[i] += films[g][i];
+            if (hpt_write_film(ctx[0], out.c_str(), sum.data(), W, H, &fp, written, sizeof(written))) {
+                std::fprintf(stderr, "%s\n", hpt_last_error(ctx[0]));
+                return false;
+            }
+            return true;
+        };
+        /* the samples in one call, or in chunks with a partial image every -r seconds */
+        const int chunk = o.flushSec > 0 ? std::max(1, spp / 16) : spp;
+        auto t0 = std::chrono::steady_clock::now(), lastFlush = t0;
+        for (int j0 = 0; j0 < spp; j0 += chunk) {
+            const int j1 = std::min(spp, j0 + chunk);
+            std::vector<std::thread> th;
+            for (int g = 0; g < G; ++g)
+                th.emplace_back([&, g] {
+                    hpt_render_params p;
+                    std::memset(&p, 0, sizeof(p));
+                    p.spp_begin = j0;
+                    p.spp_end = j1;
+                    p.shard = g;
+                    p.n_shards = G;
+                    p.collect_stats = o.stats ? 2 : 0;
+                    rcs[g] = hpt_render(ctx[g], &p, films[g].data());
+                });
+            for (auto &t : th) t.join();
+            for (int g = 0; g < G; ++g)
+                if (rcs[g]) { std::fprintf(stderr, "render failed on device %d: %s\n", o.device + g, hpt_last_error(ctx[g])); return 4; }
+            const auto now = std::chrono::steady_clock::now();
+            if (j1 < spp && o.flushSec > 0 && std::chrono::duration<double>(now - lastFlush).count() >= o.flushSec) {
+                if (!develop()) return 5;
+                lastFlush = now;
+                if (!o.quiet) std::printf("Wrote partial image (%d of %d spp) -> %s\n", j1, spp, written);
+            }
         }
+        double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (!develop()) return 5;
         out = written;
         if (!o.quiet) {
             double paths = (double) W * H * spp;
@@ -197,10 +219,12 @@ int main(int argc, char **argv) {
             if (o.stats) {
                 hpt_stats s;
                 hpt_get_stats(ctx[0], &s);
-                std::printf("device 0: trace %.2f ms (%llu launches) shade %.2f post %.2f camera %.2f gather %.2f; "
-                            "nodes %llu prims %llu bounces %llu max bounce %d\n",
-                            s.ms_trace, (unsigned long long) s.trace_launches, s.ms_shade, s.ms_post, s.ms_camera,
-                            s.ms_gather, (unsigned long long) s.nodes, (unsigned long long) s.prims,
+                std::printf("device 0 (last chunk): camera trace (packets) %.2f ms, trace %.2f ms (%llu launches), shade "
+                            "%.2f post %.2f tail %.2f (%llu paths) camera %.2f gather %.2f; nodes %llu prims %llu "
+                            "bounces %llu max bounce %d\n",
+                            s.ms_trace_packet, s.ms_trace, (unsigned long long) s.trace_launches, s.ms_shade,
+                            s.ms_post, s.ms_tail, (unsigned long long) s.tail_paths, s.ms_camera, s.ms_gather,
+                            (unsigned long long) s.nodes, (unsigned long long) s.prims,
                             (unsigned long long) s.bounces, s.max_bounces);
             }
         }

@@ -507,6 +507,21 @@ def test_cli_renders_and_develops(tmp_path):
     np.testing.assert_array_equal(ref.read_png(str(png)), ref.read_png(out))
     res = subprocess.run(cmd + ["-x"], capture_output=True, text=True, timeout=300)
     assert res.returncode == 0 and "Skipping" in res.stdout
+    # -r sec: partial images between sample chunks (spp/16 each); the final image is the
+    # chunk-accumulated film, as a library render of the same chunks develops it
+    cmd_r = [cli, "-D", "spp=32", "-D", "width=64", "-D", "height=48", "-r", "1e-9", "-o",
+             str(tmp_path / "part.png"), xml]
+    res = subprocess.run(cmd_r, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr
+    assert res.stdout.count("Wrote partial image") == 15, res.stdout
+    r2 = native.Renderer(device=0)
+    r2.load_scene_xml(xml, {"spp": 32, "width": 64, "height": 48})
+    r2.prepare()
+    f2 = None
+    for j0 in range(0, 32, 2):
+        f2 = r2.render(j0, j0 + 2, film=f2)
+    out2 = r2.write_film(tmp_path / "lib2.png", f2)
+    np.testing.assert_array_equal(ref.read_png(str(tmp_path / "part.png")), ref.read_png(out2))
 
 
 def test_sobol_scramble_render(tmp_path):
