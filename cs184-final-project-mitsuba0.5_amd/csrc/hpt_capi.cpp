@@ -884,7 +884,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     int maxB = 0;
     /* HPT_TRACE_REPORT=1 with counters on: per-launch traversal counters on stderr */
     const bool perLaunch = counted && std::getenv("HPT_TRACE_REPORT") != nullptr;
-    uint64_t prevSt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t prevSt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prevShadow[2] = {0, 0};
     auto reportLaunch = [&](const char *what) {
         if (!perLaunch) return;
         uint64_t hs[24];
@@ -901,6 +901,11 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         }
         uint64_t d[8];
         for (int i = 0; i < 8; ++i) d[i] = hs[i] - prevSt[i], prevSt[i] = hs[i];
+        const uint64_t dsN = hs[19] - prevShadow[0], dsP = hs[20] - prevShadow[1];
+        prevShadow[0] = hs[19], prevShadow[1] = hs[20];
+        std::fprintf(stderr, "[trace] %-8s shadow rays: nodes/ray %6.2f prims/ray %6.2f | closest rays: nodes/ray %6.2f "
+                     "prims/ray %6.2f\n", what, dsN / std::max(1.0, (double) d[3]), dsP / std::max(1.0, (double) d[3]),
+                     (d[0] - dsN) / std::max(1.0, (double) d[2]), (d[1] - dsP) / std::max(1.0, (double) d[2]));
         const double rays = (double) (d[2] + d[3]);
         std::fprintf(stderr, "[trace] %-8s closest %10llu shadow %10llu nodes/ray %6.2f prims/ray %6.2f exact/ray %5.2f "
                      "util nodes %.3f prims %.3f | max rounds %llu max restarts %llu restarted rays %llu restarts %llu\n", what, (unsigned long long) d[2], (unsigned long long) d[3],

@@ -302,6 +302,7 @@ HD bool beginRay(const HptScene &sc, TraceRay &r, V3 o, V3 d, float rmint, float
 
 struct TraceCounters {
     uint32_t nodes = 0, prims = 0, exact = 0, nodeSlots = 0, primSlots = 0;
+    uint32_t shadowNodes = 0, shadowPrims = 0; /* the part of nodes / prims spent on shadow rays */
 };
 
 HD bool waveLeader() { return __lane_id() == (uint32_t) (__ffsll((unsigned long long) __ballot(1)) - 1); }
@@ -336,6 +337,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     while (!(ref & 0x80000000u)) {
         if (STATS) {
             ++tc.nodes;
+            tc.shadowNodes += r.shadow ? 1u : 0u;
             if (waveLeader()) tc.nodeSlots += 64;
         }
         const uint4 na = nodes4[2 * ref], nb = nodes4[2 * ref + 1];
@@ -404,6 +406,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     }
     if (STATS) {
         ++tc.nodes;
+        tc.shadowNodes += r.shadow ? 1u : 0u;
         if (waveLeader()) tc.nodeSlots += 64;
     }
     uint32_t leafFirst = ref & 0x00ffffffu, leafLast = leafFirst + ((ref >> 24) & 0x7fu);
@@ -488,6 +491,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
             }
             if (STATS) {
                 ++tc.prims;
+                tc.shadowPrims += r.shadow ? 1u : 0u;
                 if (waveLeader()) tc.primSlots += 64;
             }
             if (segMayHit(fa, fb, o, d, sc.maxRadius)) mask |= 1u << (e - c0);
@@ -699,6 +703,8 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             nC += __shfl_down(nC, off);
             nS += __shfl_down(nS, off);
             nU += __shfl_down(nU, off);
+            tc.shadowNodes += __shfl_down(tc.shadowNodes, off);
+            tc.shadowPrims += __shfl_down(tc.shadowPrims, off);
             maxRounds = max(maxRounds, (uint32_t) __shfl_down(maxRounds, off));
             maxRestarts = max(maxRestarts, (uint32_t) __shfl_down(maxRestarts, off));
             restartRays += __shfl_down(restartRays, off);
@@ -720,6 +726,9 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             atomicMax(&st[9], (unsigned long long) maxRestarts);
             atomicAdd(&st[10], (unsigned long long) restartRays);
             atomicAdd(&st[11], (unsigned long long) restarts);
+            /* [19]/[20] node visits / primitive tests of shadow rays */
+            atomicAdd(&st[19], (unsigned long long) tc.shadowNodes);
+            atomicAdd(&st[20], (unsigned long long) tc.shadowPrims);
         }
     }
 }
