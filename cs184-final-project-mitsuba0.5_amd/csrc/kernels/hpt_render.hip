@@ -2273,13 +2273,6 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
 #ifndef HPT_TAIL_WAVES
 #define HPT_TAIL_WAVES 4 /* register target: 4 waves/SIMD hold ~2.6e5 lanes = 1.3e5 paths resident */
 #endif
-/* small tails (every lane resident at 2 waves/SIMD): the spill-free register allocation */
-extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_tail_small(HptScene sc, HptPaths P,
-                                                                     const uint32_t *__restrict__ shadeQ,
-                                                                     uint32_t *__restrict__ counters) {
-    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
-    tailPaths<false>(sc, P, shadeQ, counters, stk + threadIdx.x);
-}
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void k_tail(HptScene sc, HptPaths P,
                                                                const uint32_t *__restrict__ shadeQ,
                                                                uint32_t *__restrict__ counters) {
@@ -2604,21 +2597,7 @@ hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t
 hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *counters,
                            uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
-    /* two lanes per path; tails that fit at 2 waves/SIMD (measured on MI355X: 2-wave
-       residency of 256 CUs = 1.3e5 lanes) run without register spills */
-    static int smallLanes = 0;
-    if (smallLanes == 0) {
-        int dev = 0;
-        hipDeviceProp_t prop;
-        smallLanes = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-                         ? prop.multiProcessorCount * 4 * 2 * 64
-                         : 131072;
-    }
-    if (sc.nShapes <= 1 && 2 * maxItems <= (uint64_t) smallLanes) {
-        hipLaunchKernelGGL(k_tail_small, dim3(blocksFor(2 * maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc,
-                           P, shadeQ, counters);
-        return hipGetLastError();
-    }
+    /* two lanes per path (a spill-free 2-waves/SIMD build measured slower at every tail size) */
     if (sc.nShapes > 1)
         hipLaunchKernelGGL(k_tail_multi, dim3(blocksFor(2 * maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc,
                            P, shadeQ, counters);

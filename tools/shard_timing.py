@@ -56,6 +56,11 @@ def main():
         for k in ranks:
             t, s = timed(k, n)
             ts[k] = (round(t * 1e3, 3), round(s.ms_trace, 3), round(s.ms_tail, 3))
+            if k == 0:
+                kern = {n: round(getattr(s, "ms_" + n), 3) for n in
+                        ("camera", "trace_packet", "primary", "trace", "shade", "post", "tail", "gather")}
+                print("N=%d rank 0 kernels (ms): %s; sum %.2f of %.2f wall" % (n, kern, sum(kern.values()), t * 1e3),
+                      flush=True)
         worst = max(v[0] for v in ts.values())
         out["shards"][n] = {"per_rank_ms_trace_tail": ts, "max_ms": worst, "efficiency": round(t1 * 1e3 / (n * worst), 4)}
         print("N=%d ranks %s -> max %.2f ms, strong-scaling efficiency %.3f" % (n, ts, worst, t1 * 1e3 / (n * worst)),
