@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
+#include <unordered_map>
 
 #include "../hpt_device.h"
 #include "hpt_kernels.h"
@@ -2530,22 +2532,27 @@ hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPath
 /* persistent grid: as many one-wave blocks as can be resident at once
    (occupancy API x CUs), capped by the work */
 static unsigned persistentBlocks(const void *kernel, uint64_t items) {
-    static const void *keys[8] = {nullptr};
-    static int cached[8] = {0};
-    int slot = 0;
-    while (slot < 7 && keys[slot] && keys[slot] != kernel) ++slot;
-    keys[slot] = kernel;
-    if (cached[slot] == 0) {
-        int dev = 0, perCU = 0;
-        hipDeviceProp_t prop;
-        if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, HPT_TRACE_BLOCK, 0) != hipSuccess ||
-            perCU <= 0)
-            perCU = 8, prop.multiProcessorCount = 256;
-        cached[slot] = perCU * prop.multiProcessorCount;
+    /* resident blocks per kernel, measured once (render calls of several contexts
+       may run on several host threads: the cache is guarded) */
+    static std::mutex mu;
+    static std::unordered_map<const void *, int> cached;
+    int resident = 0;
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        auto it = cached.find(kernel);
+        if (it == cached.end()) {
+            int dev = 0, perCU = 0;
+            hipDeviceProp_t prop;
+            if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, HPT_TRACE_BLOCK, 0) != hipSuccess ||
+                perCU <= 0)
+                perCU = 8, prop.multiProcessorCount = 256;
+            it = cached.emplace(kernel, perCU * prop.multiProcessorCount).first;
+        }
+        resident = it->second;
     }
     const uint64_t need = (items + HPT_TRACE_BLOCK - 1) / HPT_TRACE_BLOCK;
-    return (unsigned) std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t) cached[slot]));
+    return (unsigned) std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t) resident));
 }
 
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
