@@ -360,6 +360,36 @@ def test_render_ewa_primary_misses():
     assert m["rel_rmse"] < 1e-3, m
 
 
+@pytest.mark.parametrize("strands", [[], [[(0.0, 12.0, 0.0)]], [[(0.0, 12.0, 0.0), (0.3, 12.6, 0.1)]]],
+                         ids=["empty", "one-vertex", "one-segment"])
+def test_render_degenerate_hair(tmp_path, strands):
+    """Empty and single-vertex hair files (no segment: the kd-tree is one empty
+    leaf, every ray misses -> the sky) and a single segment: GPU film == oracle."""
+    import re
+    from mitsuba_amd import synth_hair
+    xml = scene_util.scenes.make_scene("furball_marschner", str(tmp_path), n_strands=10)
+    hair = tmp_path / "h.mitshair"
+    synth_hair.write_binary_hair(str(hair), strands)
+    src = re.sub(r'value="furball_10\.mitshair"', 'value="h.mitshair"', open(xml).read())
+    x2 = tmp_path / "deg.xml"
+    x2.write_text(src)
+    r = native.Renderer(device=0)
+    r.load_scene_xml(str(x2), {"width": 32, "height": 24, "spp": 4})
+    r.prepare()
+    film = r.render(0, 4)
+    _, cam, bsdf = scene_util.config_params("furball_marschner")
+    o = oracle_lib.Oracle()
+    o.setup(cam, 35.0, 32, 24, str(hair), float(scene_util.scenes.CONFIGS["furball_marschner"]["radius"]), bsdf,
+            r.envmap(), 65, spp=4)
+    nodes, idx, _ = r.kdtree()
+    o.set_kdtree(nodes, idx)
+    o.prepare()
+    ofilm, _ = o.render(0, 4, width=32, height=24)
+    assert np.all(np.isfinite(film)) and film[..., 3].sum() > 0
+    m = scene_util.l2_metrics(native.develop(ofilm), native.develop(film))
+    assert m["rel_rmse"] < 1e-4, m
+
+
 def _reference_flags_floor(fixture, r, si):
     name, n = {"furball": ("furball_marschner", 3000), "straight": ("straight_kk", 1500),
                "furball_rp": ("furball_roughplastic", 3000), "straight_md": ("straight_dielectric", 1500),
