@@ -203,6 +203,7 @@ struct EnvHost {
     std::vector<float> ratioX, ratioY;
     float ewaLut[HPT_EWA_LUT] = {};
     std::vector<float> cdfRows, cdfCols, rowWeights;
+    std::vector<uint32_t> guideRows, guideCols; /* HptEnvMap::guideRows / guideCols */
     float normalization = 0, scale = 1, pixelSizeX = 0, pixelSizeY = 0;
     float toWorld[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
 };

@@ -574,6 +574,18 @@ void buildEnvMap(EnvHost &env) {
     env.normalization = 1.0f / (rowSum * (2 * kPi / w) * (kPi / h));
     env.pixelSizeX = 2 * kPi / w;
     env.pixelSizeY = kPi / h;
+    /* guide tables: the device's lower_bound starts between the entries bracketing
+       sample's bucket [k/G, (k+1)/G) -- the same first entry >= sample */
+    const int G = HPT_ENV_GUIDE;
+    auto guide = [&](const float *cdf, uint32_t n, uint32_t *out) {
+        for (int k = 0; k <= G; ++k)
+            out[k] = (uint32_t) (std::lower_bound(cdf, cdf + n, (float) k / (float) G) - cdf);
+    };
+    env.guideRows.assign(G + 1, 0);
+    guide(env.cdfRows.data(), (uint32_t) h + 1, env.guideRows.data());
+    env.guideCols.assign((size_t) h * (G + 1), 0);
+    for (int y = 0; y < h; ++y)
+        guide(env.cdfCols.data() + (size_t) y * (w + 1), (uint32_t) w + 1, env.guideCols.data() + (size_t) y * (G + 1));
 }
 
 /* ---------------- MIP pyramid (envmap.cpp:165-182, mipmap.h:155-302) ---------------- */

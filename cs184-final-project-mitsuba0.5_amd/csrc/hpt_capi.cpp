@@ -608,6 +608,8 @@ int hpt_prepare(hpt_context *c) {
     r |= upload(c, c->env.cdfRows.data(), c->env.cdfRows.size() * 4, (const void **) &E.cdfRows);
     r |= upload(c, c->env.cdfCols.data(), c->env.cdfCols.size() * 4, (const void **) &E.cdfCols);
     r |= upload(c, c->env.rowWeights.data(), c->env.rowWeights.size() * 4, (const void **) &E.rowWeights);
+    r |= upload(c, c->env.guideRows.data(), c->env.guideRows.size() * 4, (const void **) &E.guideRows);
+    r |= upload(c, c->env.guideCols.data(), c->env.guideCols.size() * 4, (const void **) &E.guideCols);
     {
         std::vector<HptMipLevel> lv(c->env.levelW.size());
         for (size_t l = 0; l < lv.size(); ++l)

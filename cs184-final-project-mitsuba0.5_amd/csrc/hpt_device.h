@@ -158,6 +158,7 @@ struct HptShape {
 /* EWA-filtered environment lookups for camera rays (envmap.cpp:391-406,
  * mipmap.h:629-834): the MIP pyramid's levels, and the 64-entry Gaussian LUT */
 #define HPT_EWA_LUT 64
+#define HPT_ENV_GUIDE 64
 struct HptMipLevel {
     int w, h, off;
     float ratioX, ratioY; /* level size / level-0 size (m_sizeRatio) */
@@ -173,6 +174,9 @@ struct HptEnvMap {
     const float *cdfRows;       /* h+1 */
     const float *cdfCols;       /* h*(w+1) */
     const float *rowWeights;    /* h */
+    /* guide tables of the CDF searches: guideRows[k] = lower_bound(cdfRows, k / HPT_ENV_GUIDE)
+       (k = 0..HPT_ENV_GUIDE), guideCols likewise per row (h x (HPT_ENV_GUIDE + 1)) */
+    const uint32_t *guideRows, *guideCols;
     int w, h;
     float normalization, scale, pixelSizeX, pixelSizeY;
     float bsCenter[3], bsRadius;

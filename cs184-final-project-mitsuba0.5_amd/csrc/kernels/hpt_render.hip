@@ -1758,8 +1758,11 @@ HD float envPdf(const HptEnvMap &e, V3 d) {
            e.normalization / fmaxr(fabsf(sinTheta), kEpsilon);
 }
 /* sampleReuse (:657-662): std::lower_bound + rescale */
-HD uint32_t sampleReuse(const float *cdf, uint32_t size, float &sample) {
-    uint32_t lo = 0, n = size + 1;
+HD uint32_t sampleReuse(const float *cdf, uint32_t size, float &sample, const uint32_t *guide) {
+    /* the first entry >= sample lies between the guide entries of sample's bucket
+       (host-built from the same cdf, so the search returns std::lower_bound's entry) */
+    const uint32_t k = min((uint32_t) (sample * (float) HPT_ENV_GUIDE), (uint32_t) HPT_ENV_GUIDE - 1u);
+    uint32_t lo = guide[k], n = guide[k + 1] - guide[k] + 1;
     while (n > 0) { /* first entry >= sample */
         uint32_t half = n >> 1;
         if (cdf[lo + half] < sample) {
@@ -1777,8 +1780,8 @@ HD uint32_t sampleReuse(const float *cdf, uint32_t size, float &sample) {
 }
 /* internalSampleDirection (:567-600) */
 HD void envSampleDir(const HptEnvMap &e, float sx, float sy, V3 &d, V3 &value, float &pdf) {
-    uint32_t row = sampleReuse(e.cdfRows, (uint32_t) e.h, sy);
-    uint32_t col = sampleReuse(e.cdfCols + row * (e.w + 1), (uint32_t) e.w, sx);
+    uint32_t row = sampleReuse(e.cdfRows, (uint32_t) e.h, sy, e.guideRows);
+    uint32_t col = sampleReuse(e.cdfCols + row * (e.w + 1), (uint32_t) e.w, sx, e.guideCols + row * (HPT_ENV_GUIDE + 1));
     float posx = (float) col + intervalToTent(sx), posy = (float) row + intervalToTent(sy);
     int xPos = (int) floorf(posx), yPos = (int) floorf(posy);
     float dx1 = posx - xPos, dx2 = 1.0f - dx1, dy1 = posy - yPos, dy2 = 1.0f - dy1;
