@@ -157,7 +157,8 @@ HD bool aabbIntersect(const HptScene &sc, V3 o, V3 d, V3 rcp, float &nearT, floa
    the scheduler from hoisting those loads (which would keep ~30 extra VGPRs
    live across the traversal loop).  The arithmetic is operation for
    operation the reference's (dot = x*x' + y*y' + z*z', no contraction). */
-HD bool insideMiters(const double *__restrict__ rec, D3 q) {
+template <class RecP>
+HD bool insideMiters(RecP rec, D3 q) {
     asm volatile("" ::: "memory");
     const D3 v1 = d3(rec[0], rec[1], rec[2]), n1 = d3(rec[6], rec[7], rec[8]);
     if (!(dot(q - v1, n1) >= 0)) return false;
@@ -166,15 +167,16 @@ HD bool insideMiters(const double *__restrict__ rec, D3 q) {
     return dot(q - v2, n2) <= 0;
 }
 
-HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, V3 of, V3 df, double r2, float mint,
-                     float maxt, float &t, V3 &p) {
+/* rec: the segment's 15 doubles (any address space: the packet tracer passes
+   a constant-space pointer so the wave-uniform record arrives by scalar loads) */
+template <class RecP>
+HD bool segIntersectRec(RecP rec, V3 of, V3 df, double r2, float mint, float maxt, float &t, V3 &p) {
     /* keep the fp64 ray out of the traversal loop's live registers: the
        conversions are re-done per exact test (rare: the fp32 pre-test passes
        ~2 segments per ray), which the opaque moves below enforce */
     float ox = of.x, oy = of.y, oz = of.z, dx = df.x, dy = df.y, dz = df.z;
     asm volatile("" : "+v"(ox), "+v"(oy), "+v"(oz), "+v"(dx), "+v"(dy), "+v"(dz));
     const D3 rayO = d3(ox, oy, oz), rayD = d3(dx, dy, dz);
-    const double *rec = reinterpret_cast<const double *>(segs + s);
     double nearT, farT;
     {
         const D3 axis = d3(rec[3], rec[4], rec[5]);
@@ -201,6 +203,11 @@ HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, V3 of, V3 
         return true;
     }
     return false;
+}
+
+HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, V3 of, V3 df, double r2, float mint,
+                     float maxt, float &t, V3 &p) {
+    return segIntersectRec(reinterpret_cast<const double *>(segs + s), of, df, r2, mint, maxt, t, p);
 }
 
 /* Conservative fp32 pre-test (see HptSegF): false only when the ray line
@@ -782,8 +789,23 @@ HD uint64_t uniform64(uint64_t v) {
 template <bool STATS>
 HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, TraceCounters &tc) {
     const uint32_t lane = __lane_id();
-    const HptNode *__restrict__ nodes = sc.nodes;
-    const float4 *__restrict__ leafF = reinterpret_cast<const float4 *>(sc.leafF);
+#ifdef __HIP_DEVICE_COMPILE__
+    /* the tree is read-only for the launch and every fetch address is wave-uniform:
+       constant-address-space reads let the compiler issue scalar loads */
+    typedef const __attribute__((address_space(4))) uint32_t *CU32;
+    typedef const __attribute__((address_space(4))) float *CF32;
+    const CU32 nodeW = (CU32) sc.nodes;
+    const CF32 leafW = (CF32) sc.leafF;
+    auto nodes = [&](uint32_t i) { return HptNode{nodeW[2 * i], nodeW[2 * i + 1]}; };
+    auto leaf = [&](uint32_t i) {
+        return make_float4(leafW[4 * i], leafW[4 * i + 1], leafW[4 * i + 2], leafW[4 * i + 3]);
+    };
+#else
+    const HptNode *__restrict__ nodeP = sc.nodes;
+    const float4 *__restrict__ leafP = reinterpret_cast<const float4 *>(sc.leafF);
+    auto nodes = [&](uint32_t i) { return nodeP[i]; };
+    auto leaf = [&](uint32_t i) { return leafP[i]; };
+#endif
     const V3 o = r.o, d = r.d, rcp = r.rcp;
     uint64_t done = ~__ballot(valid);
     uint64_t act = ~done;
@@ -796,7 +818,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
     uint32_t steps = 0;
     while (true) {
         /* ---- descend to a leaf ---- */
-        HptNode nd = nodes[node];
+        HptNode nd = nodes(node);
         while (!(nd.w0 & 0x80000000u)) {
             const bool me = (act >> lane) & 1u;
             if (STATS) {
@@ -828,7 +850,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
             if (mFirst == 0) { /* nobody needs the first child (so no lane is "both") */
                 node = second;
                 act = mFar;
-                nd = nodes[node];
+                nd = nodes(node);
                 continue;
             }
             if ((mBoth | mFar) != 0) {
@@ -840,7 +862,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
             }
             node = first;
             act = mFirst;
-            nd = nodes[node];
+            nd = nodes(node);
         }
         /* ---- leaf: the member lanes test its segments (pre-test, then exact) ---- */
         const bool me = (act >> lane) & 1u;
@@ -850,7 +872,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
         }
         const uint32_t lf = nd.w0 & 0x7fffffffu, ll = nd.w1;
         for (uint32_t e = lf; e < ll; ++e) {
-            const float4 fa = leafF[2 * e], fb = leafF[2 * e + 1];
+            const float4 fa = leaf(2 * e), fb = leaf(2 * e + 1);
             if (STATS) {
                 tc.prims += me ? 1u : 0u;
                 if (lane == 0) tc.primSlots += 64;
