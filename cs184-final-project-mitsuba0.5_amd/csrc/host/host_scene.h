@@ -226,6 +226,10 @@ void sunRadianceRGB(const SunSkyTables &t, float theta, float turbidity, float r
 bool loadEnvFile(const std::string &path, EnvHost &env, std::string &err); /* .hdr / .pfm */
 
 void setupCamera(const SceneDesc &d, HptCamera &cam);      /* perspective.cpp:125-165 */
+/* m_sampleToCamera of PerspectiveCameraImpl::configure (perspective.cpp:150-157), row-major,
+   built in float exactly as the reference (Transform products + Gauss-Jordan inverse) */
+bool cameraSampleToCamera(const SceneDesc &d, float s2c[16]);
+float cameraXFov(const SceneDesc &d);                       /* sensor.cpp:237-305 */
 void setupTent(float *lut, float &scale);                 /* rfilter.cpp:38-56 */
 
 /* float <-> IEEE half (round to nearest even) */

@@ -596,7 +596,7 @@ float lanczos2(float x) {
     x = std::abs(x);
     if (x < 1e-4f) return 1.0f; /* Epsilon */
     if (x > radius) return 0.0f;
-    const float x1 = (float) (M_PI * (double) x); /* M_PI is a double */
+    const float x1 = kPi * x; /* M_PI is M_PI_FLT under SINGLE_PRECISION (constants.h:80) */
     const float x2 = x1 / radius;
     return (std::sin(x1) * std::sin(x2)) / (x1 * x2);
 }
@@ -783,25 +783,126 @@ bool loadEnvFile(const std::string &path, EnvHost &env, std::string &err) {
 }
 
 /* ---------------- camera (perspective.cpp:125-165) ---------------- */
-void setupCamera(const SceneDesc &d, HptCamera &cam) {
-    float aspect = (float) d.width / (float) d.height;
-    float fovX = d.fov;
-    /* sensor.cpp:245-251 fovAxis handling */
+/* The reference builds sampleToCamera from single-precision Transforms:
+   m_cameraToSample = S(1/relSize) * T(-relOffset) * S(-0.5, -0.5 aspect, 1)
+   * T(-1, -1/aspect, 0) * perspective(xfov, near, far) (perspective.cpp:
+   150-155), each product of Transform (transform.cpp:28-31) multiplying the
+   matrices left to right and the inverses right to left (matrix.h:743-756:
+   sum = 0, sum += a_ik b_kj in k order), the inverse of perspective() coming
+   from Matrix4x4::invert, a float Gauss-Jordan elimination with full
+   pivoting (transform.h:50-55, matrix.inl:138-190); m_sampleToCamera is that
+   composed inverse (perspective.cpp:157).  Everything below is float. */
+namespace {
+typedef std::array<float, 16> M44;
+M44 mmul(const M44 &a, const M44 &b) {
+    M44 r;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            float sum = 0;
+            for (int k = 0; k < 4; ++k) sum += a[i * 4 + k] * b[k * 4 + j];
+            r[i * 4 + j] = sum;
+        }
+    return r;
+}
+/* Matrix<4,4,float>::invert (matrix.inl:138-190) */
+bool gaussJordanInvert(const M44 &src, M44 &t) {
+    int indxc[4], indxr[4], ipiv[4] = {0, 0, 0, 0};
+    t = src;
+    auto m = [&](int r, int c) -> float & { return t[r * 4 + c]; };
+    for (int i = 0; i < 4; i++) {
+        int irow = -1, icol = -1;
+        float big = 0;
+        for (int j = 0; j < 4; j++) {
+            if (ipiv[j] == 1) continue;
+            for (int k = 0; k < 4; k++) {
+                if (ipiv[k] == 0) {
+                    if (std::abs(m(j, k)) >= big) {
+                        big = std::abs(m(j, k));
+                        irow = j;
+                        icol = k;
+                    }
+                } else if (ipiv[k] > 1) {
+                    return false;
+                }
+            }
+        }
+        ++ipiv[icol];
+        if (irow != icol)
+            for (int k = 0; k < 4; ++k) std::swap(m(irow, k), m(icol, k));
+        indxr[i] = irow;
+        indxc[i] = icol;
+        if (m(icol, icol) == 0) return false;
+        const float pivinv = 1.f / m(icol, icol);
+        m(icol, icol) = 1.f;
+        for (int j = 0; j < 4; j++) m(icol, j) *= pivinv;
+        for (int j = 0; j < 4; j++) {
+            if (j == icol) continue;
+            const float save = m(j, icol);
+            m(j, icol) = 0;
+            for (int k = 0; k < 4; k++) m(j, k) -= m(icol, k) * save;
+        }
+    }
+    for (int j = 3; j >= 0; j--)
+        if (indxr[j] != indxc[j])
+            for (int k = 0; k < 4; k++) std::swap(m(k, indxr[j]), m(k, indxc[j]));
+    return true;
+}
+struct Xf {
+    M44 m, inv;
+};
+Xf xfMul(const Xf &a, const Xf &b) { return Xf{mmul(a.m, b.m), mmul(b.inv, a.inv)}; }
+Xf xfScale(float x, float y, float z) { /* transform.cpp:49-62 */
+    return Xf{M44{x, 0, 0, 0, 0, y, 0, 0, 0, 0, z, 0, 0, 0, 0, 1},
+              M44{1.0f / x, 0, 0, 0, 0, 1.0f / y, 0, 0, 0, 0, 1.0f / z, 0, 0, 0, 0, 1}};
+}
+Xf xfTranslate(float x, float y, float z) { /* transform.cpp:33-47 */
+    return Xf{M44{1, 0, 0, x, 0, 1, 0, y, 0, 0, 1, z, 0, 0, 0, 1}, M44{1, 0, 0, -x, 0, 1, 0, -y, 0, 0, 1, -z, 0, 0, 0, 1}};
+}
+/* util.h:294-297 (M_PI is M_PI_FLT under SINGLE_PRECISION, constants.h:80) */
+float degToRad(float v) { return v * (kPi / 180.0f); }
+float radToDeg(float v) { return v * (180.0f / kPi); }
+} // namespace
+
+/* the horizontal field of view after PerspectiveCamera::configure (sensor.cpp:237-305) */
+float cameraXFov(const SceneDesc &d) {
+    const float aspect = (float) d.width / (float) d.height; /* sensor.cpp:101-102 */
     std::string axis = d.fovAxis;
     if (axis == "smaller") axis = aspect > 1 ? "y" : "x";
     else if (axis == "larger") axis = aspect > 1 ? "x" : "y";
-    if (axis == "y") fovX = (float) (2.0 * std::atan(std::tan(d.fov * M_PI / 360.0) * aspect) * 180.0 / M_PI);
-    float cot = 1.0f / std::tan((fovX / 2.0f) * (kPi / 180.0f));
-    float recip = 1.0f / (d.farClip - d.nearClip);
-    float a = d.farClip * recip, b = -d.nearClip * d.farClip * recip;
-    double Pi[16] = {1.0 / cot, 0, 0, 0, 0, 1.0 / cot, 0, 0, 0, 0, 0, 1, 0, 0, 1.0 / b, -(double) a / b};
-    double A[16] = {-2, 0, 0, 1, 0, -2.0 / aspect, 0, 1.0 / aspect, 0, 0, 1, 0, 0, 0, 0, 1};
-    for (int r = 0; r < 4; ++r)
-        for (int c = 0; c < 4; ++c) {
-            double acc = 0;
-            for (int k = 0; k < 4; ++k) acc += Pi[r * 4 + k] * A[k * 4 + c];
-            cam.s2c[r * 4 + c] = (float) acc;
-        }
+    if (axis == "y") /* setYFov (:295-298) */
+        return radToDeg(2 * std::atan(std::tan(0.5f * degToRad(d.fov)) * aspect));
+    if (axis == "diagonal") { /* setDiagonalFov (:301-305) */
+        const float diagonal = 2 * std::tan(0.5f * degToRad(d.fov));
+        const float width = diagonal / std::sqrt(1.0f + 1.0f / (aspect * aspect));
+        return radToDeg(2 * std::atan(width * 0.5f));
+    }
+    return d.fov;
+}
+
+bool cameraSampleToCamera(const SceneDesc &d, float s2c[16]) {
+    const float aspect = (float) d.width / (float) d.height;
+    const float xfov = cameraXFov(d);
+    /* Transform::perspective (transform.cpp:99-119) and its Gauss-Jordan inverse */
+    const float recip = 1.0f / (d.farClip - d.nearClip);
+    const float cot = 1.0f / std::tan(degToRad(xfov / 2.0f));
+    Xf P;
+    P.m = M44{cot, 0, 0, 0, 0, cot, 0, 0, 0, 0, d.farClip * recip, -d.nearClip * d.farClip * recip, 0, 0, 1, 0};
+    if (!gaussJordanInvert(P.m, P.inv)) return false;
+    /* no crop window: relSize = 1, relOffset = 0 (perspective.cpp:133-138) */
+    const float relSizeX = (float) d.width / (float) d.width, relSizeY = (float) d.height / (float) d.height;
+    const float relOffX = 0.0f / (float) d.width, relOffY = 0.0f / (float) d.height;
+    const Xf c2s = xfMul(xfMul(xfMul(xfMul(xfScale(1.0f / relSizeX, 1.0f / relSizeY, 1.0f),
+                                           xfTranslate(-relOffX, -relOffY, 0.0f)),
+                                     xfScale(-0.5f, -0.5f * aspect, 1.0f)),
+                               xfTranslate(-1.0f, -1.0f / aspect, 0.0f)),
+                         P);
+    std::memcpy(s2c, c2s.inv.data(), 16 * sizeof(float));
+    return true;
+}
+
+void setupCamera(const SceneDesc &d, HptCamera &cam) {
+    if (!cameraSampleToCamera(d, cam.s2c))
+        throw std::runtime_error("Unable to invert singular matrix (perspective camera)");
     std::memcpy(cam.toWorld, d.toWorld, sizeof(cam.toWorld));
     cam.invResX = 1.0f / (float) d.width;
     cam.invResY = 1.0f / (float) d.height;

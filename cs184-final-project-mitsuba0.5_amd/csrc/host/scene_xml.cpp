@@ -459,8 +459,28 @@ void parseObject(Ctx &c, const XNode &nd, SceneDesc &d) {
         Props p;
         collectProps(c, nd, p);
         if (p.xform.count("toWorld")) parseTransform(c, *p.xform["toWorld"], d.toWorld);
-        d.fov = num1(p, "fov", 45.0f);
-        if (p.str.count("fovAxis")) d.fovAxis = p.str["fovAxis"];
+        if (p.num.count("fov")) {
+            d.fov = num1(p, "fov", 45.0f);
+            if (p.str.count("fovAxis")) { /* boost::to_lower_copy (sensor.cpp:247-248) */
+                d.fovAxis = p.str["fovAxis"];
+                for (char &ch : d.fovAxis) ch = (char) std::tolower((unsigned char) ch);
+            }
+        } else { /* no fov: a diagonal one from "focalLength" (sensor.cpp:264-276), 36x24 mm film */
+            std::string f = p.str.count("focalLength") ? p.str["focalLength"] : std::string("50mm");
+            if (f.size() >= 2 && f.compare(f.size() - 2, 2, "mm") == 0) f = f.substr(0, f.size() - 2);
+            char *end = nullptr;
+            const float value = (float) std::strtod(f.c_str(), &end);
+            if (!end || *end != '\0')
+                fail(c.file, nd.line, "Could not parse the focal length (must be of the form <x>mm, where <x> "
+                                      "is a positive integer)!");
+            const float kPiF = 3.14159265358979323846f; /* M_PI under SINGLE_PRECISION (constants.h:80) */
+            d.fov = 2 * 180 / kPiF * std::atan(std::sqrt((float) (36 * 36 + 24 * 24)) / (2 * value));
+            d.fovAxis = "diagonal";
+        }
+        if (d.fovAxis != "x" && d.fovAxis != "y" && d.fovAxis != "smaller" && d.fovAxis != "larger" &&
+            d.fovAxis != "diagonal")
+            fail(c.file, nd.line, "The 'fovAxis' parameter must be set to one of 'smaller', 'larger', 'diagonal', "
+                                  "'x', or 'y'!");
         d.nearClip = num1(p, "nearClip", 1e-2f);
         d.farClip = num1(p, "farClip", 1e4f);
         for (auto &kp : nd.kids) {

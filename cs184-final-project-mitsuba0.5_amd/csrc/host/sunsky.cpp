@@ -17,7 +17,8 @@
  *
  * Arithmetic follows the reference's SINGLE_PRECISION types expression by
  * expression (float where the reference has Float, double where it promotes
- * through M_PI or double literals).
+ * through double literals or variables; M_PI itself is the float M_PI_FLT
+ * under SINGLE_PRECISION, include/mitsuba/core/constants.h:79-80).
  */
 #include <algorithm>
 #include <cmath>
@@ -42,7 +43,10 @@ inline Vf cross(Vf a, Vf b) { return {a.y * b.z - a.z * b.y, a.z * b.x - a.x * b
 
 inline float safeAcos(float v) { return std::acos(std::min(1.0f, std::max(-1.0f, v))); }
 inline float safeSqrt(float v) { return std::sqrt(std::max(0.0f, v)); }
-inline float degToRad(float v) { return (float) (v * (M_PI / 180.0f)); } /* util.h:297 */
+/* M_PI is M_PI_FLT under SINGLE_PRECISION (constants.h:80): every M_PI below is this float; an
+   expression mixing it with a double literal or variable promotes only from there on */
+const float kPiF = 3.14159265358979323846f;
+inline float degToRad(float v) { return v * (kPiF / 180.0f); } /* util.h:297 */
 
 struct Sph { /* SphericalCoordinates (sunmodel.h:64-88) */
     float elevation, azimuth;
@@ -57,7 +61,7 @@ Vf toSphere(Sph c) { /* sunmodel.h:90-97 */
 Sph fromSphere(Vf d) { /* sunmodel.h:99-105 */
     float azimuth = std::atan2(d.x, -d.z);
     float elevation = safeAcos(d.y);
-    if (azimuth < 0) azimuth = (float) (azimuth + 2 * M_PI);
+    if (azimuth < 0) azimuth += 2 * kPiF;
     return {elevation, azimuth};
 }
 
@@ -93,7 +97,7 @@ Sph sunFromDateTime(int year, int month, int day, float hour, float minute, floa
     double dY = std::cos(eclipticObliquity) * sinEclipticLongitude;
     double dX = std::cos(eclipticLongitude);
     double rightAscension = std::atan2(dY, dX);
-    if (rightAscension < 0.0) rightAscension += 2 * M_PI;
+    if (rightAscension < 0.0) rightAscension += (double) (2 * kPiF);
     double declination = std::asin(std::sin(eclipticObliquity) * sinEclipticLongitude);
 
     double greenwichMeanSiderealTime = 6.6974243242 + 0.0657098283 * elapsedJulianDays + decHours;
@@ -108,7 +112,7 @@ Sph sunFromDateTime(int year, int month, int day, float hour, float minute, floa
     dY = -std::sin(hourAngle);
     dX = std::tan(declination) * cosLatitude - sinLatitude * cosHourAngle;
     double azimuth = std::atan2(dY, dX);
-    if (azimuth < 0.0) azimuth += 2 * M_PI;
+    if (azimuth < 0.0) azimuth += (double) (2 * kPiF);
     elevation += (6371.01 / 149597890) * std::sin(elevation); /* parallax */
     return {(float) elevation, (float) azimuth};
 }
@@ -135,7 +139,7 @@ void cookConfiguration(const double *dataset, HosekConfig config, double turbidi
                        double solarElevation) {
     int intTurbidity = (int) turbidity;
     double turbidityRem = turbidity - (double) intTurbidity;
-    solarElevation = std::pow(solarElevation / (M_PI / 2.0), (1.0 / 3.0));
+    solarElevation = std::pow(solarElevation / ((double) kPiF / 2.0), (1.0 / 3.0));
     auto blend = [&](const double *em, int i) {
         return std::pow(1.0 - solarElevation, 5.0) * em[i] +
                5.0 * std::pow(1.0 - solarElevation, 4.0) * solarElevation * em[i + 9] +
@@ -158,7 +162,7 @@ void cookConfiguration(const double *dataset, HosekConfig config, double turbidi
 double cookRadiance(const double *dataset, double turbidity, double albedo, double solarElevation) {
     int intTurbidity = (int) turbidity;
     double turbidityRem = turbidity - (double) intTurbidity;
-    solarElevation = std::pow(solarElevation / (M_PI / 2.0), (1.0 / 3.0));
+    solarElevation = std::pow(solarElevation / ((double) kPiF / 2.0), (1.0 / 3.0));
     auto blend = [&](const double *em) {
         return std::pow(1.0 - solarElevation, 5.0) * em[0] +
                5.0 * std::pow(1.0 - solarElevation, 4.0) * solarElevation * em[1] +
@@ -353,7 +357,7 @@ void sunRadiance(const SunSkyTables &t, float theta, float turbidity, float rgb[
     spec.wl.resize(91);
     spec.val.resize(91);
     float beta = 0.04608365822050f * turbidity - 0.04586025928522f;
-    float m = (float) (1.0f / (std::cos(theta) + 0.15f * std::pow(93.885f - theta / M_PI * 180.0f, (float) -1.253f)));
+    float m = (float) (1.0f / (std::cos(theta) + 0.15f * std::pow(93.885f - theta / kPiF * 180.0f, (float) -1.253f)));
     float lambda;
     int i;
     for (i = 0, lambda = 350; i < 91; i++, lambda += 5) {
@@ -393,7 +397,7 @@ inline float sobol2(uint32_t n) {
 Vf squareToUniformCone(float cosCutoff, float sx, float sy) {
     float cosTheta = (1 - sx) + sx * cosCutoff;
     float sinTheta = safeSqrt(1.0f - cosTheta * cosTheta);
-    float phi = (float) (2.0f * M_PI * sy);
+    float phi = 2.0f * kPiF * sy;
     float sinPhi = std::sin(phi), cosPhi = std::cos(phi);
     return {cosPhi * sinTheta, sinPhi * sinTheta, cosTheta};
 }
@@ -499,13 +503,13 @@ void rasterizeSunSky(const SceneDesc &d, const SunSkyTables &t, EnvHost &env) {
     sky.sun = sunCoordinates(d, worldToLum);
     sky.scale = d.skyScale;
     sky.stretch = d.skyStretch;
-    const float sunElevation = (float) (0.5f * M_PI - sky.sun.elevation);
+    const float sunElevation = 0.5f * kPiF - sky.sun.elevation;
     if (sunElevation < 0)
         throw std::runtime_error("The sun is below the horizon -- this is not supported by the sky model.");
     sky.init(t, d.turbidity, d.skyAlbedo, sunElevation);
 
     /* rasterise the sky (sunsky.cpp:131-145) */
-    const float fx = (float) ((2 * M_PI) / W), fy = (float) (M_PI / H);
+    const float fx = (2 * kPiF) / W, fy = kPiF / H;
     for (int y = 0; y < H; ++y) {
         const float theta = (y + .5f) * fy;
         for (int x = 0; x < W; ++x) {
@@ -533,12 +537,12 @@ void rasterizeSunSky(const SceneDesc &d, const SunSkyTables &t, EnvHost &env) {
     const float cosTheta = std::cos(theta * d.sunRadiusScale);
     const float coveredPortion = 0.5f * (1 - cosTheta);
     const size_t nSamples = (size_t) std::max((float) 100, (pixelCount * coveredPortion * 1000));
-    const float gx = (float) (W / (2 * M_PI)), gy = (float) (H / M_PI);
+    const float gx = W / (2 * kPiF), gy = H / kPiF;
     float value[3];
     {
-        const float k1 = (float) (2 * M_PI * (1 - std::cos(theta)));
+        const float k1 = 2 * kPiF * (1 - std::cos(theta));
         const float k2 = (float) (W * H);
-        const float k3 = (float) (2 * M_PI * M_PI * nSamples);
+        const float k3 = 2 * kPiF * kPiF * (float) nSamples;
         const float recip = 1.0f / k3;
         for (int c = 0; c < 3; ++c) value[c] = ((sunRgb[c] * k1) * k2) * recip;
     }

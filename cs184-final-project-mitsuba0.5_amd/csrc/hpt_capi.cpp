@@ -197,6 +197,23 @@ int ensureWave(hpt_context *c, uint64_t n) {
     return HPT_OK;
 }
 
+/* the traversal-bound fault word (HptScene::fault): cleared before a call's
+   launches, read after them; a set bit fails the call */
+int clearFault(hpt_context *c) {
+    HIPCHK(c, hipMemsetAsync(c->sc.fault, 0, 4, c->stream));
+    return HPT_OK;
+}
+int checkFault(hpt_context *c) {
+    uint32_t f = 0;
+    HIPCHK(c, hipMemcpyAsync(&f, c->sc.fault, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (f & HPT_FAULT_LEAVES)
+        return setErr(c, HPT_ETRAVERSAL, "kd-tree traversal exceeded 2^18 leaf rounds for a ray (malformed tree?)");
+    if (f & HPT_FAULT_RESTARTS)
+        return setErr(c, HPT_ETRAVERSAL, "kd-tree traversal exceeded its kd-restart bound for a ray");
+    return HPT_OK;
+}
+
 hipEvent_t takeEvent(hpt_context *c, size_t &used) {
     if (used >= c->evPool.size()) {
         hipEvent_t e;
@@ -329,7 +346,6 @@ int hpt_set_sampler_scramble(hpt_context *c, uint64_t scramble) {
 
 int hpt_set_integrator(hpt_context *c, int max_depth, int rr_depth, int strict_normals, int hide_emitters) {
     if (!c) return HPT_EINVAL;
-    if (max_depth > 250) return setErr(c, HPT_EINVAL, "maxDepth > 250 exceeds the Sobol dimension table");
     c->desc.maxDepth = max_depth;
     c->desc.rrDepth = rr_depth;
     c->desc.strictNormals = strict_normals != 0;
@@ -551,7 +567,11 @@ int hpt_prepare(hpt_context *c) {
     }
     HptScene &sc = c->sc;
     std::memset(&sc, 0, sizeof(sc));
-    setupCamera(d, sc.cam);
+    try {
+        setupCamera(d, sc.cam);
+    } catch (const std::exception &e) {
+        return setErr(c, HPT_EINVAL, e.what());
+    }
     int r = 0;
     r |= upload(c, c->tree.nodes.data(), c->tree.nodes.size() * sizeof(HptNode), (const void **) &sc.nodes);
     r |= upload(c, c->tree.nodes4.data(), c->tree.nodes4.size() * sizeof(HptNode4), (const void **) &sc.nodes4);
@@ -681,15 +701,16 @@ int hpt_prepare(hpt_context *c) {
     }
     r |= upload(c, c->vdc.data(), c->vdc.size() * 8, (const void **) &sc.vdc);
     r |= upload(c, c->vdcInv.data(), c->vdcInv.size() * 8, (const void **) &sc.vdcInv);
+    {
+        static const uint32_t zero[4] = {0, 0, 0, 0};
+        r |= upload(c, zero, sizeof(zero), (const void **) &sc.fault);
+    }
     if (r) return HPT_EDEVICE;
     setupTent(sc.tent, sc.tentScale);
     sc.maxDepth = d.maxDepth;
     sc.rrDepth = d.rrDepth;
     sc.strictNormals = d.strictNormals ? 1 : 0;
     sc.hideEmitters = d.hideEmitters ? 1 : 0;
-    /* Sobol dimensions consumed: 2 + 5 per bounce (sobol.cpp:225-228 errors past 1024) */
-    if (d.maxDepth > 250)
-        return setErr(c, HPT_EINVAL, "maxDepth > 250 is not supported (8-bit depth field)");
     if (sc.cam.logRes > (uint32_t) c->vdc.size() / HPT_SOBOL_BITS)
         return setErr(c, HPT_EINVAL, "image resolution exceeds the Sobol look-up tables");
     c->prepared = true;
@@ -880,6 +901,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         else evOther[cls].push_back({a, b});
         return e;
     };
+    if (int rf = clearFault(c)) return rf;
     uint32_t *hostCnt = nullptr;
     HIPCHK(c, hipHostMalloc((void **) &hostCnt, HPT_Q_COUNT * 4, hipHostMallocDefault));
     uint64_t bounces = 0;
@@ -997,6 +1019,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     (void) hipHostFree(hostCnt);
     if (e != hipSuccess || e2 != hipSuccess)
         return setErr(c, HPT_EDEVICE, std::string("render failed: ") + hipGetErrorString(e ? e : e2));
+    if (int rf = checkFault(c)) return rf;
     auto sumEv = [](std::vector<std::pair<hipEvent_t, hipEvent_t>> &v) {
         double tot = 0;
         for (auto &p : v) {
@@ -1104,6 +1127,21 @@ int hpt_get_envmap(hpt_context *c, float *rgb, int *w, int *h) {
     return HPT_OK;
 }
 
+int hpt_get_camera(hpt_context *c, float s2c[16], float dx[3], float dy[3]) {
+    if (!c || !s2c || !dx || !dy) return HPT_EINVAL;
+    if (!c->haveCamera) return setErr(c, HPT_ESTATE, "no camera");
+    HptCamera cam;
+    try {
+        setupCamera(c->desc, cam);
+    } catch (const std::exception &e) {
+        return setErr(c, HPT_EINVAL, e.what());
+    }
+    std::memcpy(s2c, cam.s2c, sizeof(cam.s2c));
+    std::memcpy(dx, cam.dx, sizeof(cam.dx));
+    std::memcpy(dy, cam.dy, sizeof(cam.dy));
+    return HPT_OK;
+}
+
 int hpt_get_marschner_tables(hpt_context *c, float *nR, float *nTT, float *nTRT, float *fdr, float *trans,
                              float *specw) {
     if (!c || !c->prepared || c->sc.bsdf.kind != HPT_BSDF_MARSCHNER)
@@ -1161,6 +1199,23 @@ int hpt_sobol_batch(hpt_context *c, int m, int n, const uint32_t *frame, const u
     return HPT_OK;
 }
 
+int hpt_camera_batch(hpt_context *c, int n, const float *pos, float *oo, float *od, float *omint, float *omaxt) {
+    if (!c || !c->prepared) return setErr(c, HPT_ESTATE, "prepare first");
+    if (c->device == HPT_HOST_ONLY) return setErr(c, HPT_EDEVICE, "host-only context has no device");
+    HIPCHK(c, hipSetDevice(c->device));
+    Scratch S;
+    const float *dp = S.in(pos, 2 * (size_t) n);
+    float *o = S.in<float>(nullptr, 3 * (size_t) n), *d = S.in<float>(nullptr, 3 * (size_t) n);
+    float *a = S.in<float>(nullptr, n), *b = S.in<float>(nullptr, n);
+    HIPCHK(c, hpt_launch_camera_batch(c->sc, n, dp, o, d, a, b, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    fetch(oo, o, 3 * (size_t) n);
+    fetch(od, d, 3 * (size_t) n);
+    fetch(omint, a, n);
+    fetch(omaxt, b, n);
+    return HPT_OK;
+}
+
 int hpt_trace_batch(hpt_context *c, int n, const float *o, const float *d, const float *mint, const float *maxt,
                     int flags, float *ot, int32_t *oiv, float *op, uint8_t *oh) {
     const int shadow = flags & HPT_TRACE_SHADOW;
@@ -1173,8 +1228,9 @@ int hpt_trace_batch(hpt_context *c, int n, const float *o, const float *d, const
     int32_t *ds = S.in<int32_t>(nullptr, n);
     uint8_t *dh = S.in<uint8_t>(nullptr, n);
     uint32_t *cur = S.in<uint32_t>(nullptr, HPT_CURSORS * HPT_CURSOR_STRIDE);
+    if (int rf = clearFault(c)) return rf;
     HIPCHK(c, hpt_launch_trace_batch(c->sc, n, a, b, mi, ma, flags, dt, ds, dp, dh, cur, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int rf = checkFault(c)) return rf;
     if (shadow) {
         fetch(oh, dh, n);
     } else {

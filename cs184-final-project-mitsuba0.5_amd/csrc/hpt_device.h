@@ -209,6 +209,7 @@ struct HptScene {
     float tent[HPT_FILTER_RES + 1];
     float tentScale;
     int maxDepth, rrDepth, strictNormals, hideEmitters;
+    uint32_t *fault;            /* device word: HPT_FAULT_* bits set by the traversal bounds */
 };
 
 #endif

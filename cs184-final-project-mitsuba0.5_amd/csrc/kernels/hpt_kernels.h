@@ -16,6 +16,11 @@
 #define HPT_Q_ERROR 4     /* set when a path runs out of Sobol dimensions */
 #define HPT_Q_TAIL_BOUNCES 5 /* path-bounces shaded inside k_tail */
 #define HPT_Q_COUNT 8
+/* HptScene::fault bits: a traversal bound fired (the ray would otherwise end
+   with whatever hit it had; the render / batch call fails instead) */
+#define HPT_FAULT_LEAVES 1u   /* more than 2^18 leaf rounds for one ray */
+#define HPT_FAULT_RESTARTS 2u /* more than HPT_MAX_RESTARTS kd-restarts for one ray */
+#define HPT_MAX_RESTARTS 1024
 /* k_trace work cursors (persistent waves claim rays from them), one per
    128-byte line, stored after the queue counters in the same buffer */
 #define HPT_CURSORS 64
@@ -35,13 +40,24 @@ struct HptWave {
     const int32_t *localOf;  /* image block index -> k, or -1 when another shard owns it */
 };
 
+/* HptPaths::state packing.  dim < 2048 (the Sobol table has 1024 dimensions
+   and a path stops before it runs out); depth < 8192, far beyond any path the
+   1024 dimensions allow (>= 2 per bounce), so maxDepth = -1 (unlimited) cannot
+   overflow it */
+#define HPT_ST_DIM_MASK 0x7ffu
+#define HPT_ST_DIM(st) ((st) & HPT_ST_DIM_MASK)
+#define HPT_ST_DEPTH(st) (((st) >> 11) & 0x1fffu)
+__host__ __device__ inline uint32_t hptState(uint32_t st, uint32_t depth, uint32_t dim) {
+    return (st & 0xff000000u) | (depth << 11) | dim;
+}
+
 /* path state, structure of arrays in HBM (16-byte rows where possible) */
 struct HptPaths {
     float4 *ro;        /* ray origin xyz, mint                       */
     float4 *rd;        /* ray direction xyz, maxt                    */
     float2 *pos;       /* film sample position (pixels)              */
     uint64_t *sobol;   /* Sobol index of the sample (look_up)        */
-    uint32_t *state;   /* dim[0:16) | depth[16:24) | sampledType[24:32) */
+    uint32_t *state;   /* dim[0:11) | depth[11:24) | sampledType[24:31) | scattered[31] */
     float4 *thr;       /* throughput rgb                             */
     float4 *li;        /* accumulated radiance rgb                   */
     float4 *hit;       /* segment id (int bits), t                   */
@@ -77,6 +93,8 @@ hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPath
                              hipStream_t s);
 hipError_t hpt_launch_sobol_batch(const HptScene &sc, int m, int n, const uint32_t *frame, const uint32_t *px,
                                   const uint32_t *py, const uint32_t *dim, uint64_t *oi, float *ov, hipStream_t s);
+hipError_t hpt_launch_camera_batch(const HptScene &sc, int n, const float *pos, float *o, float *d, float *mint,
+                                   float *maxt, hipStream_t s);
 hipError_t hpt_launch_trace_batch(const HptScene &sc, int n, const float *o, const float *d, const float *mint,
                                   const float *maxt, int flags, float *ot, int32_t *os, float *op, uint8_t *oh,
                                   uint32_t *cursor, hipStream_t s);

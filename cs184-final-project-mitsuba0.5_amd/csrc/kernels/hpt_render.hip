@@ -333,8 +333,11 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     /* the ray as plain values: selecting among struct members by axis would be
        folded into a dynamically addressed load and push the state to scratch */
     const V3 o = r.o, d = r.d, rcp = r.rcp;
-    /* hard bound so every wave drains even on a malformed tree */
-    if (++r.leaves > (1 << 18)) return true;
+    /* hard bound so every wave drains even on a malformed tree; the call fails loudly */
+    if (++r.leaves > (1 << 18)) {
+        atomicOr(sc.fault, HPT_FAULT_LEAVES);
+        return true;
+    }
 #if HPT_NODE4
     /* descent over two-level nodes (HptNode4): one 32-byte fetch decides the
        top split and the split of each child the ray interval reaches; the
@@ -569,7 +572,11 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
 #endif
     if (r.found && r.tHit <= r.tmax) return true;
     if (r.sp == 0) {
-        if (!r.lost || r.tmax >= r.maxt || ++r.restarts > 64) return true;
+        if (!r.lost || r.tmax >= r.maxt) return true;
+        if (++r.restarts > HPT_MAX_RESTARTS) {
+            atomicOr(sc.fault, HPT_FAULT_RESTARTS);
+            return true;
+        }
         /* kd-restart from the root for the remaining interval */
         r.lost = false;
         r.node = 0;
@@ -1286,12 +1293,12 @@ HD float mfEval(const HptRoughPlastic &m, V3 h) {
     const float a = m.alpha;
     const float beckmannExponent = ((h.x * h.x) / (a * a) + (h.y * h.y) / (a * a)) / cosTheta2;
     float result;
-    /* M_PI is a double: the denominators and the divisions run in double */
+    /* M_PI is M_PI_FLT under SINGLE_PRECISION (constants.h:80): float throughout */
     if (m.type == 0) {
-        result = (float) ((double) fastexpf(-beckmannExponent) / (M_PI * a * a * cosTheta2 * cosTheta2));
+        result = fastexpf(-beckmannExponent) / (kPi * a * a * cosTheta2 * cosTheta2);
     } else if (m.type == 1) {
         const float root = (1.0f + beckmannExponent) * cosTheta2;
-        result = (float) (1.0 / (M_PI * a * a * root * root));
+        result = 1.0f / (kPi * a * a * root * root);
     } else {
         result = sqrtf((m.exponent + 2) * (m.exponent + 2)) * kInvTwoPi * powf(h.z, m.exponent);
     }
@@ -1322,11 +1329,11 @@ HD float mfPdf(const HptRoughPlastic &m, V3 wi, V3 h) {
 }
 /* sampleVisible11 (microfacet.h:567-686), isotropic Beckmann / GGX */
 HD void mfSampleVisible11(const HptRoughPlastic &m, float thetaI, float sx, float sy, float &slopeX, float &slopeY) {
-    const float SQRT_PI_INV = (float) (1 / sqrt(M_PI));
+    const float SQRT_PI_INV = 1 / sqrtf(kPi);
     if (m.type == 0) {
         if (thetaI < 1e-4f) {
             const float r = sqrtf(-fastlogf(1.0f - sx));
-            const float ang = (float) (2 * M_PI * sy);
+            const float ang = 2 * kPi * sy;
             slopeX = r * cosf(ang);
             slopeY = r * sinf(ang);
             return;
@@ -1355,7 +1362,7 @@ HD void mfSampleVisible11(const HptRoughPlastic &m, float thetaI, float sx, floa
     /* GGX */
     if (thetaI < 1e-4f) {
         const float r = sqrtf(fmaxr(0.0f, sx / (1 - sx)));
-        const float ang = (float) (2 * M_PI * sy);
+        const float ang = 2 * kPi * sy;
         slopeX = r * cosf(ang);
         slopeY = r * sinf(ang);
         return;
@@ -1404,12 +1411,12 @@ HD V3 mfSample(const HptRoughPlastic &m, V3 wiIn, float sx, float sy) {
     /* sampleAll, isotropic */
     float cosThetaM, sinPhiM, cosPhiM;
     if (m.type == 2) {
-        const float phiM = (float) ((2.0 * M_PI) * sy);
+        const float phiM = (2.0f * kPi) * sy;
         sinPhiM = sinf(phiM);
         cosPhiM = cosf(phiM);
         cosThetaM = powf(sx, 1.0f / (m.exponent + 2.0f));
     } else {
-        const float ang = (float) ((2.0f * M_PI) * sy);
+        const float ang = (2.0f * kPi) * sy;
         sinPhiM = sinf(ang);
         cosPhiM = cosf(ang);
         const float alphaSqr = m.alpha * m.alpha;
@@ -1882,6 +1889,19 @@ HD void qpush(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
 /* Kernels                                                             */
 /* ================================================================== */
 
+/* PerspectiveCameraImpl::sampleRayDifferential, the ray itself (perspective.cpp:271-290) */
+HD void cameraRay(const HptCamera &c, float posx, float posy, V3 &o, V3 &dw, float &mint, float &maxt) {
+    const V3 nearP = xformPoint(c.s2c, v3(posx * c.invResX, posy * c.invResY, 0.0f));
+    const V3 d = normalize(nearP);
+    const float invZ = 1.0f / d.z;
+    const float *T = c.toWorld;
+    o = v3(T[0] * 0.0f + T[1] * 0.0f + T[2] * 0.0f + T[3], T[4] * 0.0f + T[5] * 0.0f + T[6] * 0.0f + T[7],
+           T[8] * 0.0f + T[9] * 0.0f + T[10] * 0.0f + T[11]);
+    dw = xformVector(T, d);
+    mint = c.nearClip * invZ;
+    maxt = c.farClip * invZ;
+}
+
 /* Decode a path id of the current wave: id = slot * nSpp + (j - sppBegin),
    slot = (k-th block owned by this shard) << 10 | pixel within the block. */
 HD bool decodePath(const HptWave &w, uint32_t id, int &px, int &py, uint32_t &j) {
@@ -1914,18 +1934,14 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
             oy = sobolSample(sc, sidx, 1);
         }
         float posx = px + ox, posy = py + oy;
-        V3 nearP = xformPoint(c.s2c, v3(posx * c.invResX, posy * c.invResY, 0.0f));
-        V3 d = normalize(nearP);
-        float invZ = 1.0f / d.z;
-        const float *T = c.toWorld;
-        V3 o = v3(T[0] * 0.0f + T[1] * 0.0f + T[2] * 0.0f + T[3], T[4] * 0.0f + T[5] * 0.0f + T[6] * 0.0f + T[7],
-                  T[8] * 0.0f + T[9] * 0.0f + T[10] * 0.0f + T[11]);
-        V3 dw = xformVector(T, d);
-        P.ro[id] = make_float4(o.x, o.y, o.z, c.nearClip * invZ);
-        P.rd[id] = make_float4(dw.x, dw.y, dw.z, c.farClip * invZ);
+        V3 o, dw;
+        float mint, maxt;
+        cameraRay(c, posx, posy, o, dw, mint, maxt);
+        P.ro[id] = make_float4(o.x, o.y, o.z, mint);
+        P.rd[id] = make_float4(dw.x, dw.y, dw.z, maxt);
         P.pos[id] = make_float2(posx, posy);
         P.sobol[id] = sidx;
-        P.state[id] = 2u | (1u << 16); /* dim = 2, depth = 1 */
+        P.state[id] = hptState(0u, 1u, 2u); /* dim = 2, depth = 1 */
         P.thr[id] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
         P.li[id] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     } else if (id < w.nPaths) {
@@ -2084,7 +2100,7 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__rest
                   bool &shadow) {
     {
         uint32_t st = P.state[id];
-        uint32_t dim = st & 0xffffu, depth = (st >> 16) & 0xffu;
+        uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st);
         float4 h = P.hit[id], hp = P.hitp[id], rd = P.rd[id];
         V3 rayD = v3(rd.x, rd.y, rd.z);
         V3 p, wi;
@@ -2154,7 +2170,7 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__rest
             if (MULTI) shadeWith(sc.bsdfs[sc.shapes[sc.segs[seg].shape].bsdf]);
             else shadeWith(sc.bsdf);
         }
-        P.state[id] = (st & 0xffff0000u) | dim;
+        P.state[id] = (st & ~HPT_ST_DIM_MASK) | dim;
     }
 }
 template <bool MULTI>
@@ -2192,7 +2208,7 @@ HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__restr
     bool alive = false;
     {
         uint32_t st = P.state[id];
-        uint32_t dim = st & 0xffffu, depth = (st >> 16) & 0xffu, type = (st >> 24) & 0x7fu;
+        uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st), type = (st >> 24) & 0x7fu;
         const bool scattered = (st >> 31) != 0;
         float4 h = P.hit[id], bw = P.bw[id], thr = P.thr[id], rd = P.rd[id];
         bool hit = __float_as_int(h.x) >= 0;
@@ -2235,7 +2251,7 @@ HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__restr
                 }
                 depth += 1;
                 P.thr[id] = make_float4(T.x, T.y, T.z, 0.0f);
-                P.state[id] = (st & 0xff000000u) | (depth << 16) | dim;
+                P.state[id] = hptState(st, depth, dim);
             }
         }
     }
@@ -2423,6 +2439,20 @@ extern "C" __global__ void k_sobol_batch(HptScene sc, int m, int n, const uint32
     uint64_t idx = (m > 1) ? sobolLookUp(sc, (uint32_t) m, frame[i], px[i], py[i]) : (uint64_t) frame[i];
     outIdx[i] = idx;
     outVal[i] = sobolSample(sc, idx, dim[i]);
+}
+
+/* camera rays at film positions (pixels): k_camera's own ray construction */
+extern "C" __global__ void k_camera_batch(HptScene sc, int n, const float *pos, float *o, float *d, float *mint,
+                                          float *maxt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    V3 ro, rd;
+    float a, b;
+    cameraRay(sc.cam, pos[2 * i], pos[2 * i + 1], ro, rd, a, b);
+    o[3 * i] = ro.x, o[3 * i + 1] = ro.y, o[3 * i + 2] = ro.z;
+    d[3 * i] = rd.x, d[3 * i + 1] = rd.y, d[3 * i + 2] = rd.z;
+    mint[i] = a;
+    maxt[i] = b;
 }
 
 /* Batch trace through the production traversal (tracePersistent).  flags:
@@ -2660,6 +2690,12 @@ hipError_t hpt_launch_sobol_batch(const HptScene &sc, int m, int n, const uint32
                                   const uint32_t *py, const uint32_t *dim, uint64_t *oi, float *ov, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_sobol_batch, dim3(blocksFor(n, 256)), dim3(256), 0, s, sc, m, n, frame, px, py, dim, oi, ov);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_camera_batch(const HptScene &sc, int n, const float *pos, float *o, float *d, float *mint,
+                                   float *maxt, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_camera_batch, dim3(blocksFor(n, 256)), dim3(256), 0, s, sc, n, pos, o, d, mint, maxt);
     return hipGetLastError();
 }
 hipError_t hpt_launch_trace_batch(const HptScene &sc, int n, const float *o, const float *d, const float *mint,

@@ -96,9 +96,11 @@ SIGNATURES = {
     "hpt_get_kdtree": (C.c_int, [C.c_void_p, _u32, _i64, _u32, _i64, _f]),
     "hpt_get_envmap": (C.c_int, [C.c_void_p, _f, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hpt_get_marschner_tables": (C.c_int, [C.c_void_p, _f, _f, _f, _f, _f, _f]),
+    "hpt_get_camera": (C.c_int, [C.c_void_p, _f, _f, _f]),
     "hpt_sobol_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u32, _u32, _u32, _u32, _u64, _f]),
     "hpt_env_eval_filtered": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f]),
     "hpt_get_env_level": (C.c_int, [C.c_void_p, C.c_int, _f, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "hpt_camera_batch": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f]),
     "hpt_trace_batch": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f, C.c_int, _f, _i32, _f, _u8]),
     "hpt_bsdf_batch": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f, _f, _f, _f, _u32]),
     "hpt_env_batch": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f, _f, _f, _f, _f]),
@@ -304,6 +306,14 @@ class Renderer:
         self._check(self.lib.hpt_get_envmap(self.h, _p(rgb, _f), C.byref(w), C.byref(h)))
         return rgb
 
+    def camera(self):
+        """(sampleToCamera 4x4, dx, dy) as the host built them (perspective.cpp:150-163)."""
+        m = np.zeros(16, np.float32)
+        dx = np.zeros(3, np.float32)
+        dy = np.zeros(3, np.float32)
+        self._check(self.lib.hpt_get_camera(self.h, _p(m, _f), _p(dx, _f), _p(dy, _f)))
+        return m.reshape(4, 4), dx, dy
+
     def marschner_tables(self):
         t = [np.zeros((64 * 64, 3), np.float32) for _ in range(3)]
         fdr = np.zeros(1, np.float32)
@@ -322,6 +332,18 @@ class Renderer:
         self._check(self.lib.hpt_sobol_batch(self.h, m, n, _p(frame, _u32), _p(px, _u32), _p(py, _u32), _p(dim, _u32),
                                              _p(oi, _u64), _p(ov, _f)))
         return oi, ov
+
+    def camera_rays(self, pos):
+        """The device camera rays at film positions (n, 2) -> (o, d, mint, maxt)."""
+        pos = _f32(pos).reshape(-1, 2)
+        n = pos.shape[0]
+        o = np.zeros((n, 3), np.float32)
+        d = np.zeros((n, 3), np.float32)
+        mint = np.zeros(n, np.float32)
+        maxt = np.zeros(n, np.float32)
+        self._check(self.lib.hpt_camera_batch(self.h, n, _p(pos, _f), _p(o, _f), _p(d, _f), _p(mint, _f),
+                                              _p(maxt, _f)))
+        return o, d, mint, maxt
 
     def trace(self, o, d, mint, maxt, shadow=False, tiny_stack=False, packet=False):
         o = _f32(o).reshape(-1, 3)

@@ -31,6 +31,8 @@ extern "C" {
 #define HPT_EIO -2      /* file could not be read or parsed                */
 #define HPT_EDEVICE -3  /* HIP runtime error or no gfx950 device            */
 #define HPT_ESTATE -4   /* call order violated (e.g. render before prepare) */
+#define HPT_ETRAVERSAL -5 /* a ray hit the kd traversal's leaf-round or kd-restart bound: the
+                             result would be unreliable, so the render / trace call fails */
 
 typedef struct hpt_context hpt_context;
 
@@ -188,6 +190,10 @@ int64_t hpt_get_hair(hpt_context *ctx, float *xyz, uint8_t *starts_fiber /* n+1 
 int hpt_get_kdtree(hpt_context *ctx, uint32_t *nodes, int64_t *n_nodes, uint32_t *indices, int64_t *n_indices,
                    float aabb[6]);
 int hpt_get_envmap(hpt_context *ctx, float *rgb, int *w, int *h);
+/* the perspective camera's m_sampleToCamera (row-major 4x4) and near-plane position
+   differentials m_dx / m_dy (src/sensors/perspective.cpp:150-163), built in float
+   exactly as the reference (Transform products, Matrix4x4::invert Gauss-Jordan) */
+int hpt_get_camera(hpt_context *ctx, float sample_to_camera[16], float dx[3], float dy[3]);
 int hpt_get_marschner_tables(hpt_context *ctx, float *n_r, float *n_tt, float *n_trt, float *fdr, float *trans100,
                              float *spec_weight);
 
@@ -195,6 +201,10 @@ int hpt_get_marschner_tables(hpt_context *ctx, float *n_r, float *n_tt, float *n
 /* sobol::look_up + sobol::sampleSingle (src/samplers/sobolseq.h:43-131) */
 int hpt_sobol_batch(hpt_context *ctx, int m, int n, const uint32_t *frame, const uint32_t *px, const uint32_t *py,
                     const uint32_t *dim, uint64_t *out_index, float *out_value);
+/* PerspectiveCameraImpl::sampleRayDifferential (src/sensors/perspective.cpp:271-290): the
+   device's camera ray at film positions pos (2n floats, pixels) -> origin, direction (3n), mint, maxt */
+int hpt_camera_batch(hpt_context *ctx, int n, const float *pos, float *out_o, float *out_d, float *out_mint,
+                     float *out_maxt);
 /* ShapeKDTree::rayIntersect closest (skdtree.cpp:112-141) or shadow (:207-226);
    out_iv is the reference's primitive id (first vertex index of the segment) */
 #define HPT_TRACE_SHADOW 1      /* any-hit query (out_hit) instead of closest hit */

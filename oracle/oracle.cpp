@@ -8,8 +8,6 @@
  * statement by statement, in single precision, without fused multiply-adds.
  *
  * Deliberate, documented deviations from the reference binary:
- *   - sampleToCamera is the analytic inverse of the perspective matrix in
- *     double, rounded to float (the reference inverts a float Matrix4x4).
  *   - Primary-ray environment lookups use the level-0 bilinear filter; the
  *     reference's EWA path (mipmap.h:631-715) reduces to exactly that when the
  *     ellipse's major radius is < 1 texel, which the oracle checks and counts
@@ -30,6 +28,7 @@
 #include <fstream>
 #include <memory>
 #include <sstream>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -841,10 +840,10 @@ struct Microfacet {
         float beckmannExponent = ((m.x * m.x) / (alpha * alpha) + (m.y * m.y) / (alpha * alpha)) / cosTheta2;
         float result;
         if (type == EBeckmann) {
-            result = mathx::fastexp(-beckmannExponent) / (M_PI * alpha * alpha * cosTheta2 * cosTheta2);
+            result = mathx::fastexp(-beckmannExponent) / (kPi * alpha * alpha * cosTheta2 * cosTheta2);
         } else if (type == EGGX) {
             float root = (1.0f + beckmannExponent) * cosTheta2;
-            result = 1.0f / (M_PI * alpha * alpha * root * root);
+            result = 1.0f / (kPi * alpha * alpha * root * root);
         } else {
             result = std::sqrt((exponent + 2) * (exponent + 2)) * kInvTwoPi * std::pow(m.z, exponent);
         }
@@ -873,11 +872,11 @@ struct Microfacet {
         return eval(m) * m.z;
     }
     void sampleVisible11(float thetaI, float sx, float sy, float &slx, float &sly) const { /* :567-686 */
-        const float SQRT_PI_INV = 1 / std::sqrt(M_PI);
+        const float SQRT_PI_INV = 1 / std::sqrt(kPi);
         if (type == EBeckmann) {
             if (thetaI < 1e-4f) {
                 float r = std::sqrt(-mathx::fastlog(1.0f - sx));
-                float ang = 2 * M_PI * sy;
+                float ang = 2 * kPi * sy;
                 slx = r * std::cos(ang);
                 sly = r * std::sin(ang);
                 return;
@@ -904,7 +903,7 @@ struct Microfacet {
         }
         if (thetaI < 1e-4f) {
             float r = safe_sqrt(sx / (1 - sx));
-            float ang = 2 * M_PI * sy;
+            float ang = 2 * kPi * sy;
             slx = r * std::cos(ang);
             sly = r * std::sin(ang);
             return;
@@ -951,12 +950,12 @@ struct Microfacet {
         /* sampleAll (:291-385), isotropic */
         float cosThetaM, sinPhiM, cosPhiM;
         if (type == EPhong) {
-            float phiM = (2.0f * M_PI) * sy;
+            float phiM = (2.0f * kPi) * sy;
             sinPhiM = std::sin(phiM);
             cosPhiM = std::cos(phiM);
             cosThetaM = std::pow(sx, 1.0f / (exponent + 2.0f));
         } else {
-            float ang = (2.0f * M_PI) * sy;
+            float ang = (2.0f * kPi) * sy;
             sinPhiM = std::sin(ang);
             cosPhiM = std::cos(ang);
             float alphaSqr = alpha * alpha;
@@ -1510,7 +1509,7 @@ struct EnvMap {
         x = std::abs(x);
         if (x < kEpsilon) return 1.0f;
         else if (x > 2.0f) return 0.0f;
-        float x1 = (float) (M_PI * x);
+        float x1 = kPi * x;
         float x2 = x1 / 2.0f;
         return (std::sin(x1) * std::sin(x2)) / (x1 * x2);
     }
@@ -1932,20 +1931,101 @@ inline V3 xformVector(const float *M, const V3 &v) { /* transform.h:175-183 */
     return V3(x, y, z);
 }
 
-void setupCamera(orc_scene *s) {
-    float aspect = (float) s->width / (float) s->height;
-    float cot = 1.0f / std::tan(degToRad(s->fov / 2.0f));
-    float recip = 1.0f / (s->farClip - s->nearClip);
-    float a = s->farClip * recip, b = -s->nearClip * s->farClip * recip;
-    /* sampleToCamera = P^-1 * T(1, 1/aspect, 0) * S(-2, -2/aspect, 1) (double, rounded) */
-    double Pi[16] = {1.0 / cot, 0, 0, 0, 0, 1.0 / cot, 0, 0, 0, 0, 0, 1, 0, 0, 1.0 / b, -(double) a / b};
-    double A[16] = {-2, 0, 0, 1, 0, -2.0 / aspect, 0, 1.0 / aspect, 0, 0, 1, 0, 0, 0, 0, 1};
-    for (int r = 0; r < 4; ++r)
-        for (int c = 0; c < 4; ++c) {
-            double acc = 0;
-            for (int k = 0; k < 4; ++k) acc += Pi[r * 4 + k] * A[k * 4 + c];
-            s->s2c[r * 4 + c] = (float) acc;
+/* Matrix4x4 (matrix.h) in float: product (matrix.h:743-756) and the
+   Gauss-Jordan inverse with full pivoting (matrix.inl:138-190) */
+struct Mat4 {
+    float m[4][4];
+};
+static Mat4 matMul(const Mat4 &a, const Mat4 &b) {
+    Mat4 r;
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) {
+            float sum = 0;
+            for (int k = 0; k < 4; ++k) sum += a.m[i][k] * b.m[k][j];
+            r.m[i][j] = sum;
         }
+    return r;
+}
+static bool matInvert(const Mat4 &src, Mat4 &target) {
+    const int N = 4;
+    int indxc[N], indxr[N], ipiv[N];
+    std::memset(ipiv, 0, sizeof(ipiv));
+    target = src;
+    for (int i = 0; i < N; i++) {
+        int irow = -1, icol = -1;
+        float big = 0;
+        for (int j = 0; j < N; j++) {
+            if (ipiv[j] != 1) {
+                for (int k = 0; k < N; k++) {
+                    if (ipiv[k] == 0) {
+                        if (std::abs(target.m[j][k]) >= big) {
+                            big = std::abs(target.m[j][k]);
+                            irow = j;
+                            icol = k;
+                        }
+                    } else if (ipiv[k] > 1) {
+                        return false;
+                    }
+                }
+            }
+        }
+        ++ipiv[icol];
+        if (irow != icol)
+            for (int k = 0; k < N; ++k) std::swap(target.m[irow][k], target.m[icol][k]);
+        indxr[i] = irow;
+        indxc[i] = icol;
+        if (target.m[icol][icol] == 0) return false;
+        float pivinv = 1.f / target.m[icol][icol];
+        target.m[icol][icol] = 1.f;
+        for (int j = 0; j < N; j++) target.m[icol][j] *= pivinv;
+        for (int j = 0; j < N; j++) {
+            if (j != icol) {
+                float save = target.m[j][icol];
+                target.m[j][icol] = 0;
+                for (int k = 0; k < N; k++) target.m[j][k] -= target.m[icol][k] * save;
+            }
+        }
+    }
+    for (int j = N - 1; j >= 0; j--)
+        if (indxr[j] != indxc[j])
+            for (int k = 0; k < N; k++) std::swap(target.m[k][indxr[j]], target.m[k][indxc[j]]);
+    return true;
+}
+/* Transform = (matrix, inverse); operator* (transform.cpp:28-31) */
+struct Xform {
+    Mat4 t, inv;
+    Xform operator*(const Xform &o) const { return Xform{matMul(t, o.t), matMul(o.inv, inv)}; }
+};
+static Xform xformScale(float x, float y, float z) { /* transform.cpp:49-62 */
+    return Xform{{{{x, 0, 0, 0}, {0, y, 0, 0}, {0, 0, z, 0}, {0, 0, 0, 1}}},
+                 {{{1.0f / x, 0, 0, 0}, {0, 1.0f / y, 0, 0}, {0, 0, 1.0f / z, 0}, {0, 0, 0, 1}}}};
+}
+static Xform xformTranslate(float x, float y, float z) { /* transform.cpp:33-47 */
+    return Xform{{{{1, 0, 0, x}, {0, 1, 0, y}, {0, 0, 1, z}, {0, 0, 0, 1}}},
+                 {{{1, 0, 0, -x}, {0, 1, 0, -y}, {0, 0, 1, -z}, {0, 0, 0, 1}}}};
+}
+
+/* PerspectiveCameraImpl::configure (perspective.cpp:125-165): m_cameraToSample =
+   S(1/relSize) T(-relOffset) S(-0.5, -0.5 aspect, 1) T(-1, -1/aspect, 0) perspective(...),
+   m_sampleToCamera = its inverse (the Transform's stored inverse matrix) */
+void setupCamera(orc_scene *s) {
+    float aspect = s->width / (float) s->height; /* sensor.cpp:101-102 */
+    Xform persp; /* Transform::perspective (transform.cpp:99-119) -> Transform(Matrix4x4) inverts */
+    {
+        float recip = 1.0f / (s->farClip - s->nearClip);
+        float cot = 1.0f / std::tan(degToRad(s->fov / 2.0f));
+        persp.t = Mat4{{{cot, 0, 0, 0}, {0, cot, 0, 0}, {0, 0, s->farClip * recip, -s->nearClip * s->farClip * recip},
+                        {0, 0, 1, 0}}};
+        if (!matInvert(persp.t, persp.inv)) throw std::runtime_error("Unable to invert singular matrix");
+    }
+    float relSizeX = (float) s->width / (float) s->width, relSizeY = (float) s->height / (float) s->height;
+    float relOffsetX = (float) 0 / (float) s->width, relOffsetY = (float) 0 / (float) s->height;
+    Xform cameraToSample = xformScale(1.0f / relSizeX, 1.0f / relSizeY, 1.0f) *
+                           xformTranslate(-relOffsetX, -relOffsetY, 0.0f) *
+                           xformScale(-0.5f, -0.5f * aspect, 1.0f) *
+                           xformTranslate(-1.0f, -1.0f / aspect, 0.0f) * persp;
+    for (int r = 0; r < 4; ++r)
+        for (int c = 0; c < 4; ++c) s->s2c[r * 4 + c] = cameraToSample.inv.m[r][c];
     s->invResX = 1.0f / (float) s->width;
     s->invResY = 1.0f / (float) s->height;
     V3 p0 = xformPoint(s->s2c, V3(0.0f, 0.0f, 0.0f));
@@ -2734,7 +2814,26 @@ int orc_prepare(orc_scene *s) {
     if (s->m32.empty()) { s->err = "sobol tables not set"; return -1; }
     if (s->width <= 0) { s->err = "camera not set"; return -1; }
     if (s->hair.shapeFirst.empty()) { s->err = "no hair shape"; return -1; }
-    prepareScene(s);
+    try {
+        prepareScene(s);
+    } catch (const std::exception &e) {
+        s->err = e.what();
+        return -1;
+    }
+    return 0;
+}
+
+int orc_get_camera(orc_scene *s, float sample_to_camera[16], float dx[3], float dy[3]) {
+    if (s->width <= 0) { s->err = "camera not set"; return -1; }
+    try {
+        setupCamera(s);
+    } catch (const std::exception &e) {
+        s->err = e.what();
+        return -1;
+    }
+    std::memcpy(sample_to_camera, s->s2c, sizeof(s->s2c));
+    std::memcpy(dx, s->dx, sizeof(s->dx));
+    std::memcpy(dy, s->dy, sizeof(s->dy));
     return 0;
 }
 

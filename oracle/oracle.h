@@ -41,6 +41,10 @@ int orc_set_sobol(orc_scene *s, const uint32_t *m32, const uint64_t *vdc, int vd
 int orc_set_sobol_scramble(orc_scene *s, uint64_t scramble);
 int orc_set_camera(orc_scene *s, const float to_world[16], float fov_x_deg, int width,
                    int height, float near_clip, float far_clip);
+/* m_sampleToCamera (row-major, perspective.cpp:150-157: float Transform products and the
+   Gauss-Jordan inverse of matrix.inl:138-190) and the near-plane differentials m_dx / m_dy
+   (:160-163) */
+int orc_get_camera(orc_scene *s, float sample_to_camera[16], float dx[3], float dy[3]);
 /* hair.cpp:609-785 loader restatement (BINARY_HAIR or ASCII); to_world may be NULL.
    Each call adds one HairShape (vertices appended after the previous shapes'),
    with the default 0.5 diffuse BSDF; the orc_set_<bsdf> calls below set the

@@ -53,6 +53,7 @@ _SIG = {
     "orc_sobol_lookup": (None, [C.c_void_p, C.c_int, C.c_int, _u32, _u32, _u32, _u64]),
     "orc_sobol_sample": (None, [C.c_void_p, C.c_int, _u64, _u32, _f]),
     "orc_camera_rays": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f]),
+    "orc_get_camera": (C.c_int, [C.c_void_p, _f, _f, _f]),
     "orc_trace_closest": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f, _i32, _f, C.c_int]),
     "orc_trace_shadow": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f, _u8, C.c_int]),
     "orc_bsdf_eval": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f]),
@@ -219,6 +220,14 @@ class Oracle:
         out = np.zeros(index.size, np.float32)
         self.lib.orc_sobol_sample(self.s, index.size, p(index, _u64), p(dim, _u32), p(out, _f))
         return out
+
+    def camera(self):
+        m = np.zeros(16, np.float32)
+        dx = np.zeros(3, np.float32)
+        dy = np.zeros(3, np.float32)
+        if self.lib.orc_get_camera(self.s, p(m, _f), p(dx, _f), p(dy, _f)) != 0:
+            raise RuntimeError(self.lib.orc_last_error(self.s).decode())
+        return m.reshape(4, 4), dx, dy
 
     def camera_rays(self, pos):
         pos = f32(pos).reshape(-1, 2)
