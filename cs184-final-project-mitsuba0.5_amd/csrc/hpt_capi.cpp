@@ -1051,6 +1051,9 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         c->stats.packet_node_slots = hs[16];
         c->stats.packet_prim_slots = hs[17];
         c->stats.packet_fallbacks = hs[18];
+        c->stats.max_leaf_rounds = hs[8];
+        c->stats.max_restarts = hs[9];
+        c->stats.restarted_rays = hs[10];
         c->stats.nodes = hs[0];
         c->stats.prims = hs[1];
         c->stats.closest_rays = hs[2];
@@ -1187,6 +1190,12 @@ int hpt_sobol_batch(hpt_context *c, int m, int n, const uint32_t *frame, const u
                     const uint32_t *dim, uint64_t *oi, float *ov) {
     if (!c || !c->prepared) return setErr(c, HPT_ESTATE, "prepare first");
     if (c->device == HPT_HOST_ONLY) return setErr(c, HPT_EDEVICE, "host-only context has no device");
+    /* the kernel indexes the tables by m and dim: reject what they do not hold */
+    const int rows = (int) std::min(c->vdc.size(), c->vdcInv.size()) / HPT_SOBOL_BITS;
+    if (n < 0 || m < 0 || m > rows) return setErr(c, HPT_EINVAL, "Sobol look-up resolution out of range");
+    for (int i = 0; i < n; ++i)
+        if (dim[i] >= HPT_SOBOL_DIMS)
+            return setErr(c, HPT_EINVAL, "Lookup dimension exceeds the direction number table size!");
     HIPCHK(c, hipSetDevice(c->device));
     Scratch S;
     const uint32_t *df = S.in(frame, n), *dx = S.in(px, n), *dy = S.in(py, n), *dd = S.in(dim, n);

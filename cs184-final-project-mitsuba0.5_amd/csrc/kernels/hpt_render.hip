@@ -26,8 +26,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <map>
 #include <mutex>
-#include <unordered_map>
+#include <utility>
 
 #include "../hpt_device.h"
 #include "hpt_kernels.h"
@@ -167,8 +168,10 @@ HD bool insideMiters(RecP rec, D3 q) {
     return dot(q - v2, n2) <= 0;
 }
 
-/* rec: the segment's 15 doubles (any address space: the packet tracer passes
-   a constant-space pointer so the wave-uniform record arrives by scalar loads) */
+/* rec: the segment's 15 doubles (templated on the pointer type so a
+   constant-address-space view could be passed; every caller today passes the
+   generic pointer, so the record is fetched with vector loads -- loading it
+   by scalar loads in the packet tracer measured neutral) */
 template <class RecP>
 HD bool segIntersectRec(RecP rec, V3 of, V3 df, double r2, float mint, float maxt, float &t, V3 &p) {
     /* keep the fp64 ray out of the traversal loop's live registers: the
@@ -298,6 +301,8 @@ HD bool beginRay(const HptScene &sc, TraceRay &r, V3 o, V3 d, float rmint, float
     r.found = false;
     r.tHit = finf();
     r.segHit = 0;
+    r.restarts = 0; /* read by the counted kernels' per-ray tails even when the ray misses */
+    r.leaves = 0;
     float mint, maxt;
     if (!aabbIntersect(sc, o, d, r.rcp, mint, maxt)) return false;
     const float rayMinT = adaptiveMint(o, rmint, shadow);
@@ -309,8 +314,6 @@ HD bool beginRay(const HptScene &sc, TraceRay &r, V3 o, V3 d, float rmint, float
     r.node = 0;
     r.top = 0;
     r.sp = 0;
-    r.restarts = 0;
-    r.leaves = 0;
     r.lost = false;
     return true;
 }
@@ -942,8 +945,13 @@ __device__ __forceinline__ void tracePackets(const HptScene &sc, IO &io, uint32_
         uint32_t start = 0, got = 0;
         bool exhausted = false;
         while (true) { /* wave-uniform */
-            const uint32_t lo = (uint32_t) ((uint64_t) total * shard / HPT_CURSORS);
-            const uint32_t size = (uint32_t) ((uint64_t) total * (shard + 1) / HPT_CURSORS) - lo;
+            /* shard bounds on multiples of 64, so a packet is 64 queue-consecutive rays
+               (with nSpp a multiple of 64: the samples of one pixel) */
+            auto bound = [&](uint32_t k) {
+                return k >= HPT_CURSORS ? total : (uint32_t) ((uint64_t) total * k / HPT_CURSORS) & ~63u;
+            };
+            const uint32_t lo = bound(shard);
+            const uint32_t size = bound(shard + 1) - lo;
             uint32_t base = 0;
             if (lane == 0) base = atomicAdd(&cursors[shard * HPT_CURSOR_STRIDE], 64u);
             base = __shfl(base, 0);
@@ -2596,19 +2604,20 @@ static unsigned persistentBlocks(const void *kernel, uint64_t items) {
     /* resident blocks per kernel, measured once (render calls of several contexts
        may run on several host threads: the cache is guarded) */
     static std::mutex mu;
-    static std::unordered_map<const void *, int> cached;
-    int resident = 0;
+    static std::map<std::pair<int, const void *>, int> cached; /* (device, kernel): devices may differ */
+    int resident = 0, dev = 0;
+    (void) hipGetDevice(&dev);
     {
         std::lock_guard<std::mutex> lock(mu);
-        auto it = cached.find(kernel);
+        auto it = cached.find({dev, kernel});
         if (it == cached.end()) {
-            int dev = 0, perCU = 0;
+            int perCU = 0;
             hipDeviceProp_t prop;
-            if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess ||
+            if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
                 hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, HPT_TRACE_BLOCK, 0) != hipSuccess ||
                 perCU <= 0)
                 perCU = 8, prop.multiProcessorCount = 256;
-            it = cached.emplace(kernel, perCU * prop.multiProcessorCount).first;
+            it = cached.emplace(std::make_pair(dev, kernel), perCU * prop.multiProcessorCount).first;
         }
         resident = it->second;
     }

@@ -61,7 +61,8 @@ class Stats(C.Structure):
                 ("tail_paths", C.c_uint64), ("ms_trace_packet", C.c_double), ("packet_launches", C.c_uint64),
                 ("packet_rays", C.c_uint64), ("packet_nodes", C.c_uint64), ("packet_prims", C.c_uint64),
                 ("packet_exact", C.c_uint64), ("packet_node_slots", C.c_uint64), ("packet_prim_slots", C.c_uint64),
-                ("packet_fallbacks", C.c_uint64)]
+                ("packet_fallbacks", C.c_uint64), ("max_leaf_rounds", C.c_uint64), ("max_restarts", C.c_uint64),
+                ("restarted_rays", C.c_uint64)]
 
 
 # every symbol declared in include/hairpt.h: (restype, argtypes)

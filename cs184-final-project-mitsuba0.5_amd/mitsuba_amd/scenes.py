@@ -68,6 +68,10 @@ THIN_DIELECTRIC = """  <bsdf type="thindielectric" id="hair">
     <rgb name="specularReflectance" value="%s"/>
   </bsdf>""" % (HAIR_DIFFUSE, HAIR_DIFFUSE)                        # models/straight-hair/scene_thindielectric.xml:31-37
 
+# thindielectric with unit weights: every bounce keeps throughput 1, so only Russian
+# roulette (q = 0.95) ends a path -- the long-path case of maxDepth = -1 (tests)
+THIN_DIELECTRIC_WHITE = THIN_DIELECTRIC.replace(HAIR_DIFFUSE, "1, 1, 1")
+
 HAIRCURL_CAM = ("-1 4.24672e-010 1.50958e-007 -0.055286 1.11022e-016 0.999996 -0.00281317 5.92976 "
                 "-1.50959e-007 -0.00281317 -0.999996 17.0651 0 0 0 1")      # models/hair-curl/scene.xml:12
 HAIRCURL_COLOURS = [("black_hair", "6.344e-006, 7.62186e-012, 6.53751e-030"),
@@ -111,6 +115,9 @@ CONFIGS = {
     "straight_thindielectric": dict(cam=STRAIGHT_CAM, bsdf=THIN_DIELECTRIC, radius="0.00566563",
                                     sun="0.19033 0.758426 -0.623349", width=1024, height=1024, spp=128, max_depth=65,
                                     geom="straight", n=10000),
+    "furball_thin_white": dict(cam=FURBALL_CAM, bsdf=THIN_DIELECTRIC_WHITE, radius="0.00216667",
+                               sun="-0.376047 0.758426 0.532333", width=128, height=128, spp=16, max_depth=-1,
+                               geom="furball", n=40000),
     "furball_1m": dict(cam=FURBALL_CAM, bsdf=MARSCHNER, radius="0.00216667", sun="-0.376047 0.758426 0.532333",
                        width=1024, height=1024, spp=1024, max_depth=64, geom="furball", n=125000),
 }

@@ -151,6 +151,10 @@ typedef struct hpt_stats {
     uint64_t packet_rays, packet_nodes /* binary-node visits per member lane */, packet_prims, packet_exact;
     uint64_t packet_node_slots, packet_prim_slots; /* 64 per packet step: visits / slots = lane use */
     uint64_t packet_fallbacks;     /* packets whose stack overflowed (their lanes traced alone) */
+    /* counted frames: the longest ray of the per-lane traversal (k_trace) in leaf rounds, its most
+       kd-restarts, and how many rays restarted at all (the bounds that fail a call with
+       HPT_ETRAVERSAL are 2^18 rounds / 1024 restarts) */
+    uint64_t max_leaf_rounds, max_restarts, restarted_rays;
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 

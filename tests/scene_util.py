@@ -102,7 +102,7 @@ def make(name, n_strands, width, height, spp, max_depth=None, device=native.HOST
     return xml, r, o
 
 
-def reference_flags_floor(name, n_strands, r, width, height, spp, radii=None):
+def reference_flags_floor(name, n_strands, r, width, height, spp, radii=None, max_depth=None, shard=0, n_shards=1):
     """L2 between the strict oracle and the oracle built with the reference's
     own compiler flags (liboracle_ref.so): the float-nondeterminism floor that
     any re-implementation of the path inherits (SURVEY.md 7 'Hard parts' i)."""
@@ -112,11 +112,13 @@ def reference_flags_floor(name, n_strands, r, width, height, spp, radii=None):
     nodes, idx, _ = r.kdtree()
     for variant in ("parity", "ref"):
         o = oracle_lib.Oracle(variant=variant)
-        o.setup(cam, 35.0, width, height, shapes, None, None, r.envmap(), cfg["max_depth"], spp=spp)
+        o.setup(cam, 35.0, width, height, shapes, None, None, r.envmap(),
+                cfg["max_depth"] if max_depth is None else max_depth, spp=spp)
         o.set_kdtree(nodes, idx)
         o.prepare()
-        films.append(native.develop(o.render(0, spp, threads=16, width=width, height=height)[0]))
-    a, b = films
+        films.append(o.render(0, spp, threads=16, shard=shard, n_shards=n_shards, width=width, height=height)[0])
+    mask = films[0][..., 3] > 0  # a shard's pixels (every pixel of a full frame)
+    a, b = [native.develop(f)[mask] for f in films]
     same = np.all(np.abs(a - b) <= 1e-5 * np.abs(a) + 1e-7, axis=-1)
     return l2_metrics(a, b), float(same.mean())
 

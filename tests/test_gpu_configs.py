@@ -1,0 +1,131 @@
+"""GPU parity on the BASELINE configs that run at 1024^2 (C4 curly, C5 furball-1M).
+
+BASELINE.json configs[3] (models/curly-hair, Marschner, 1024x1024 @ 256 spp,
+helical hair of ~2.7e6 segments, models/curly-hair/scene.xml:12,31-38) and
+configs[4] (furball scaled to ~1e6 segments, 1024x1024 @ 1024 spp, maxDepth
+64).  Both select the Sobol pixel resolution 1024 (m = 10, sobol.cpp:147-158)
+and build the deepest kd-trees of the configs.
+
+  - reduced size, same generator and radius: GPU film vs the oracle at the
+    reference-flags noise floor (scene_util.reference_flags_floor);
+  - full size: the frame is deterministic and invariant under shard and spp
+    splits; at full resolution (the m = 10 look-up) a quarter of the blocks at
+    64 spp matches the oracle at the floor;
+  - the traversal bounds (2^18 leaf rounds, 1024 kd-restarts per ray) fail a
+    render loudly (HPT_ETRAVERSAL): every render here passing proves they
+    never fired, and the counted frame reports how far below them the longest
+    ray stayed.
+"""
+import numpy as np
+import pytest
+
+import scene_util
+from mitsuba_amd import native
+
+pytestmark = pytest.mark.gpu
+
+
+def _parity(name, n, r, o, w, h, spp, max_depth=None, factor=2.0, shard=0, n_shards=1):
+    film = r.render(0, spp, shard=shard, n_shards=n_shards, collect_stats=2)
+    s = r.stats()
+    ofilm, ostats = o.render(0, spp, threads=16, shard=shard, n_shards=n_shards, width=w, height=h)
+    np.testing.assert_allclose(film[..., 3], ofilm[..., 3], rtol=1e-5)
+    mask = film[..., 3] > 0  # the shard's pixels
+    a, b = native.develop(film)[mask], native.develop(ofilm)[mask]
+    m = scene_util.l2_metrics(b, a)
+    same = np.all(np.abs(a - b) <= 1e-5 * np.abs(b) + 1e-7, axis=-1)
+    floor, floor_same = scene_util.reference_flags_floor(name, n, r, w, h, spp, max_depth=max_depth, shard=shard,
+                                                         n_shards=n_shards)
+    print(name, n, (w, h, spp), "gpu vs oracle", m, "identical %.4f" % same.mean(), "| floor", floor,
+          "identical %.4f" % floor_same, "| longest ray: %d leaf rounds, %d restarts, %d rays restarted"
+          % (s.max_leaf_rounds, s.max_restarts, s.restarted_rays))
+    assert m["rmse"] < 1e-3, m
+    assert m["rmse"] <= factor * floor["rmse"] + 1e-6, (m, floor)
+    assert same.mean() >= floor_same - 0.05
+    assert s.max_leaf_rounds < (1 << 18) and s.max_restarts < 1024
+    return s
+
+
+def test_sobol_m10_bit_exact():
+    """hpt_sobol_batch at the 1024^2 configs' look-up resolution (m = 10) and its
+    neighbours, over every frame bit a 1024-spp render uses, vs the oracle."""
+    _, r, o = scene_util.make("furball_marschner", 300, 1024, 1024, 4, device=0)
+    rng = np.random.default_rng(10)
+    n = 200000
+    for m in (9, 10, 11):
+        frame = rng.integers(0, 1024, n).astype(np.uint32)
+        px = rng.integers(0, 1 << m, n).astype(np.uint32)
+        py = rng.integers(0, 1 << m, n).astype(np.uint32)
+        dim = rng.integers(0, 1024, n).astype(np.uint32)
+        frame[:4], px[:4], py[:4], dim[:4] = [0, 1023, 512, 1], [0, (1 << m) - 1, 3, 0], [0, (1 << m) - 1, 7, 0], \
+            [0, 1023, 2, 1]
+        gi, gv = r.sobol(m, frame, px, py, dim)
+        oi = o.sobol_lookup(m, frame, px, py)
+        np.testing.assert_array_equal(gi, oi)
+        np.testing.assert_array_equal(gv, o.sobol_sample(oi, dim))
+
+
+def test_curly_reduced_matches_oracle():
+    """C4 geometry generator and radius at 2,000 strands (5.4e5 segments), 128x96 @ 8 spp."""
+    _, r, o = scene_util.make("curly_marschner", 2000, 128, 96, 8, device=0)
+    assert r.info().segments > 500000
+    _parity("curly_marschner", 2000, r, o, 128, 96, 8)
+
+
+def test_furball_1m_reduced_matches_oracle():
+    """C5 geometry (125,000 strands, ~1e6 segments) and maxDepth 64 at 128x96 @ 8 spp."""
+    _, r, o = scene_util.make("furball_1m", 125000, 128, 96, 8, max_depth=64, device=0)
+    si = r.info()
+    assert si.segments > 900000 and si.max_depth == 64
+    _parity("furball_1m", 125000, r, o, 128, 96, 8, max_depth=64)
+
+
+def _full_size(name, n, w, h, spp, max_depth, parity_spp=64):
+    _, r, o = scene_util.make(name, n, w, h, spp, max_depth=max_depth, device=0)
+    si = r.info()
+    print(name, "segments", si.segments, "kd nodes", si.kd_nodes, "depth", si.kd_depth,
+          "build %.2f s" % si.kd_build_seconds)
+    a = r.render(0, spp)
+    np.testing.assert_array_equal(a, r.render(0, spp))
+    s = r.render(0, spp, shard=0, n_shards=3)
+    s = r.render(0, spp, shard=1, n_shards=3, film=s)
+    s = r.render(0, spp, shard=2, n_shards=3, film=s)
+    np.testing.assert_allclose(s, a, rtol=1e-5, atol=1e-5)
+    c = r.render(0, spp // 3)
+    c = r.render(spp // 3, spp, film=c)
+    np.testing.assert_allclose(c, a, rtol=1e-5, atol=1e-5)
+    img = native.develop(a)
+    assert np.all(np.isfinite(img)) and img.mean() > 0
+    # full resolution (the m = 10 look-up) vs the oracle: one Hilbert-dealt quarter of the
+    # 32x32 blocks (the 4-GPU shard 0) at 64 spp, where a flipped discrete event (a path
+    # that reaches the sun on one side only) is averaged like the headline's samples
+    _parity(name, n, r, o, w, h, parity_spp, max_depth=max_depth, factor=3.0, shard=0, n_shards=4)
+    return si
+
+
+def test_curly_full_size():
+    """C4 at full size: 10,000 helical strands (~2.7e6 segments), 1024x1024 @ 256 spp."""
+    si = _full_size("curly_marschner", 10000, 1024, 1024, 256, 65)
+    assert si.segments > 2600000
+
+
+def test_furball_1m_full_size():
+    """C5 at full size: 125,000 strands, 1024x1024 @ 1024 spp, maxDepth 64."""
+    si = _full_size("furball_1m", 125000, 1024, 1024, 1024, 64)
+    assert si.segments > 900000
+
+
+def test_unlimited_depth_delta_only():
+    """maxDepth = -1 (the reference's default, 'unlimited') with a delta-only BSDF
+    of unit weights (thindielectric, reflectance = transmittance = 1: no NEE, 3
+    Sobol dimensions per bounce, throughput stays 1) through the dense furball:
+    paths cross fiber after fiber until Russian roulette (q = 0.95) ends them,
+    long past the old 8-bit depth field."""
+    _, r, o = scene_util.make("furball_thin_white", 40000, 48, 40, 64, max_depth=-1, device=0)
+    assert r.info().max_depth == -1
+    film = r.render(0, 64, collect_stats=True)
+    st = r.stats()
+    ofilm, _ = o.render(0, 64, threads=16, width=48, height=40)
+    m = scene_util.l2_metrics(native.develop(ofilm), native.develop(film))
+    print("unlimited depth: path-bounces", st.bounces, "max bounce launches", st.max_bounces, m)
+    assert m["rmse"] < 1e-3, m
