@@ -260,6 +260,9 @@ HD bool segIntersectF32(const HptSegment *__restrict__ segs, uint32_t s, V3 o, V
     return false;
 }
 #define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, p) segIntersectF32(segs, s, o, d, radius, mint, maxt, t, p)
+#elif defined(HPT_EXPERIMENT_NO_EXACT)
+/* register-pressure experiment only (never the product): no exact test */
+#define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, p) ((t = (mint)), (p = o), (s) == 0xffffffffu)
 #else
 #define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, p) segIntersect(segs, s, o, d, r2, mint, maxt, t, p)
 #endif
