@@ -72,6 +72,7 @@ def cpu_baseline(args, cfg, xml_defines, hair_src, env_rgb, nodes, idx):
     _, cam, _ = scene_util.config_params(args.config)
     o = oracle_lib.Oracle(variant="ref")
     W, H = xml_defines["width"], xml_defines["height"]
+    env_rgb = scene_util.oracle_envmap(args.config) if env_rgb is None else env_rgb
     o.setup(cam, 35.0, W, H, scene_util.oracle_shapes(args.config, hair_src[1], hair_src[0]), None, None, env_rgb,
             xml_defines["maxDepth"])
     o.set_kdtree(nodes, idx)
@@ -187,7 +188,7 @@ def main():
         cpu = None
         if args.cpu_baseline == "auto" and world == 1:
             nodes, idx, _ = r.kdtree()
-            cpu = cpu_baseline(args, cfg, defines, hair_src, r.envmap(), nodes, idx)
+            cpu = cpu_baseline(args, cfg, defines, hair_src, None, nodes, idx)
         img = native.develop(film.cpu().numpy())
         out = {
             "metric": "Mpaths/sec + achieved HBM GB/s, furball Marschner 512² @ 256spp",

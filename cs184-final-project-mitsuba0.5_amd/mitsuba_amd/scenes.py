@@ -154,14 +154,19 @@ XML = """<?xml version="1.0" encoding="utf-8"?>
 {bsdf}
 {shapes}
   <emitter type="sunsky">
-    <float name="turbidity" value="3"/>
+    <float name="turbidity" value="{turbidity}"/>
     <vector name="sunDirection" x="{sx}" y="{sy}" z="{sz}"/>
-    <float name="skyScale" value="5"/>
-    <float name="sunScale" value="19.0912"/>
-    <float name="sunRadiusScale" value="37.9165"/>
+    <float name="skyScale" value="{skyScale}"/>
+    <float name="sunScale" value="{sunScale}"/>
+    <float name="sunRadiusScale" value="{sunRadiusScale}"/>
   </emitter>
 </scene>
 """
+
+
+# the sunsky block of models/furball/scene.xml and models/*-hair/scene*.xml (turbidity 3,
+# skyScale 5, sunScale 19.0912, sunRadiusScale 37.9165; default resolution 512, albedo 0.2)
+SUNSKY = dict(turbidity="3", skyScale="5", sunScale="19.0912", sunRadiusScale="37.9165")
 
 
 def hair_strands(geom: str, n: int):
@@ -215,7 +220,7 @@ def make_scene(name: str, workdir: str, n_strands: int | None = None, **override
     sx, sy, sz = cfg["sun"].split()
     xml = XML.format(name=name, spp=cfg["spp"], width=cfg["width"], height=cfg["height"],
                      max_depth=cfg["max_depth"], hairdefaults=defaults, cam=cfg["cam"],
-                     bsdf=cfg["bsdf"], shapes=shapes, sx=sx, sy=sy, sz=sz)
+                     bsdf=cfg["bsdf"], shapes=shapes, sx=sx, sy=sy, sz=sz, **SUNSKY)
     path = os.path.join(workdir, "%s_%d.xml" % (name, n))
     _write_atomic(path, xml)
     return path

@@ -85,6 +85,13 @@ int orc_set_integrator(orc_scene *s, int max_depth, int rr_depth, int strict_nor
 int orc_set_sample_count(orc_scene *s, int spp);
 int orc_prepare(orc_scene *s);
 
+/* The sunsky emitter's lat-long bitmap (sunsky.cpp:100-240, sky.cpp, skymodel.cpp,
+   sunmodel.h), restated in oracle/sunsky_ref.cpp: resolution x resolution/2 RGB floats.
+   sunDirection given, emitter toWorld identity.  data_dir = the package's data/sunsky. */
+int orc_rasterize_sunsky(const char *data_dir, const float sun_dir[3], float turbidity, float albedo,
+                         float stretch, float sky_scale, float sun_scale, float sun_radius_scale, int resolution,
+                         float *rgb);
+
 /* Render samples [spp_begin, spp_end) of every pixel; film_rgbw = W*H*4 floats
    (sum of w*L and sum of w, like the reference's RGBAW image block minus A). */
 int orc_render(orc_scene *s, int spp_begin, int spp_end, int n_threads, float *film_rgbw,

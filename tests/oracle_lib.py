@@ -54,6 +54,8 @@ _SIG = {
     "orc_sobol_sample": (None, [C.c_void_p, C.c_int, _u64, _u32, _f]),
     "orc_camera_rays": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f]),
     "orc_get_camera": (C.c_int, [C.c_void_p, _f, _f, _f]),
+    "orc_rasterize_sunsky": (C.c_int, [C.c_char_p, _f, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
+                                       C.c_float, C.c_int, _f]),
     "orc_trace_closest": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f, _i32, _f, C.c_int]),
     "orc_trace_shadow": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f, _u8, C.c_int]),
     "orc_bsdf_eval": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f]),
@@ -352,3 +354,16 @@ def idist_warp(weights, size, ndist, dist, u):
     osum = np.zeros(n, np.float32)
     lib.orc_idist_warp(p(w, _f), size, ndist, n, p(dist, _f), p(u, _f), p(ox, _i32), p(ou, _f), p(op, _f), p(osum, _f))
     return ox, ou, op, osum
+
+
+def sunsky_bitmap(sun_dir, turbidity=3.0, albedo=0.2, stretch=1.0, sky_scale=1.0, sun_scale=1.0,
+                  sun_radius_scale=1.0, resolution=512, variant="parity"):
+    """The oracle's own sunsky rasterisation (oracle/sunsky_ref.cpp): (resolution/2, resolution, 3)."""
+    lib = Oracle(variant=variant).lib
+    rgb = np.zeros((resolution // 2, resolution, 3), np.float32)
+    d = f32(sun_dir)
+    rc = lib.orc_rasterize_sunsky(os.path.join(DATA, "sunsky").encode(), p(d, _f), turbidity, albedo, stretch,
+                                  sky_scale, sun_scale, sun_radius_scale, resolution, p(rgb, _f))
+    if rc != 0:
+        raise RuntimeError("orc_rasterize_sunsky failed (%d)" % rc)
+    return rgb

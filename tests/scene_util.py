@@ -1,8 +1,8 @@
 """Shared scene setup for parity tests: one config -> product context + oracle.
 
 The oracle receives the scene as raw inputs (camera matrix, hair file, BSDF
-parameters, environment bitmap) and re-derives everything else itself
-(hair loading + merging, AABB, BSDF tables, envmap CDFs).  Only the kd-tree
+parameters, sunsky parameters) and re-derives everything else itself (hair
+loading + merging, AABB, BSDF tables, its own sunsky bitmap, envmap CDFs).  Only the kd-tree
 node/index arrays are taken from the product's host builder; the oracle
 checks them against a brute-force intersection (tests/test_host.py).
 """
@@ -75,6 +75,17 @@ def config_params(name):
     return cfg, cam, blocks[cfg.get("shapes", ["hair"])[0]]
 
 
+def oracle_envmap(name, resolution=512):
+    """The oracle's OWN sunsky bitmap for a config (oracle/sunsky_ref.cpp, written from the
+    reference; tests/test_independent_pins.py checks it bitwise against the product's and
+    against a float64 restatement) -- the oracle is never lit by the product's bitmap."""
+    cfg = scenes.CONFIGS[name]
+    ss = scenes.SUNSKY
+    return oracle_lib.sunsky_bitmap([float(x) for x in cfg["sun"].split()], float(ss["turbidity"]), 0.2, 1.0,
+                                    float(ss["skyScale"]), float(ss["sunScale"]), float(ss["sunRadiusScale"]),
+                                    resolution)
+
+
 def oracle_shapes(name, n_strands, workdir=None, radii=None):
     """[(hair file, radius, oracle BSDF dict)] per hair shape of a config."""
     cfg = scenes.CONFIGS[name]
@@ -92,7 +103,7 @@ def make(name, n_strands, width, height, spp, max_depth=None, device=native.HOST
     r = native.Renderer(device=device)
     r.load_scene_xml(xml, {"width": width, "height": height, "spp": spp, "maxDepth": max_depth})
     r.prepare()
-    env = r.envmap()
+    env = oracle_envmap(name)
     nodes, idx, _ = r.kdtree()
     o = oracle_lib.Oracle()
     o.setup(cam, 35.0, width, height, oracle_shapes(name, n_strands, radii=radii), None, None, env, max_depth,
@@ -112,7 +123,7 @@ def reference_flags_floor(name, n_strands, r, width, height, spp, radii=None, ma
     nodes, idx, _ = r.kdtree()
     for variant in ("parity", "ref"):
         o = oracle_lib.Oracle(variant=variant)
-        o.setup(cam, 35.0, width, height, shapes, None, None, r.envmap(),
+        o.setup(cam, 35.0, width, height, shapes, None, None, oracle_envmap(name),
                 cfg["max_depth"] if max_depth is None else max_depth, spp=spp)
         o.set_kdtree(nodes, idx)
         o.prepare()

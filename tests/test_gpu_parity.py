@@ -380,7 +380,7 @@ def test_render_degenerate_hair(tmp_path, strands):
     _, cam, bsdf = scene_util.config_params("furball_marschner")
     o = oracle_lib.Oracle()
     o.setup(cam, 35.0, 32, 24, str(hair), float(scene_util.scenes.CONFIGS["furball_marschner"]["radius"]), bsdf,
-            r.envmap(), 65, spp=4)
+            scene_util.oracle_envmap("furball_marschner"), 65, spp=4)
     nodes, idx, _ = r.kdtree()
     o.set_kdtree(nodes, idx)
     o.prepare()
