@@ -182,7 +182,6 @@ int ensureWave(hpt_context *c, uint64_t n) {
     r |= alloc(n * 16, (void **) &c->P.thr);
     r |= alloc(n * 16, (void **) &c->P.li);
     r |= alloc(n * 16, (void **) &c->P.hit);
-    r |= alloc(n * 16, (void **) &c->P.hitp);
     r |= alloc(n * 16, (void **) &c->P.bw);
     r |= alloc(n * 16, (void **) &c->P.sdir);
     r |= alloc(n * 16, (void **) &c->P.scontrib);

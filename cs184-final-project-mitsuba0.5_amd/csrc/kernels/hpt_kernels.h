@@ -60,8 +60,7 @@ struct HptPaths {
     uint32_t *state;   /* dim[0:11) | depth[11:24) | sampledType[24:31) | scattered[31] */
     float4 *thr;       /* throughput rgb                             */
     float4 *li;        /* accumulated radiance rgb                   */
-    float4 *hit;       /* segment id (int bits), t                   */
-    float4 *hitp;      /* hit point xyz (fp64 -> fp32, hair.cpp:526) */
+    float4 *hit;       /* segment id (int bits, -1 = miss), t, far-root flag (uint bits) */
     float4 *bw;        /* bsdf weight rgb, bsdf pdf                  */
     float4 *sdir;      /* shadow ray direction xyz, maxt             */
     float4 *scontrib;  /* NEE contribution rgb (added if unoccluded) */

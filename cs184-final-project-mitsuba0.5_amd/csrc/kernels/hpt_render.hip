@@ -36,15 +36,6 @@
 
 using namespace hk;
 
-#ifndef HPT_NODE4
-#define HPT_NODE4 1 /* 1: descend over two-level nodes (HptNode4); 0: binary HptNode */
-#endif
-#ifndef HPT_LEAF_BATCH
-#define HPT_LEAF_BATCH 1 /* leaf records fetched per round trip in the pre-test pass */
-#endif
-#ifndef HPT_LEAF_MODE
-#define HPT_LEAF_MODE 2 /* 0 prefetch next record, 1 no prefetch, 2 mask then exact (fastest) */
-#endif
 /* block size of the queue-producing kernels (k_camera, k_primary, k_shade, k_post) */
 #ifndef HPT_SHADE_BLOCK
 #define HPT_SHADE_BLOCK 256 /* k_shade: 4 waves/SIMD of registers; 256-thread blocks overlap better than 1024 (shade 20.9 -> 18.1 ms) */
@@ -168,49 +159,71 @@ HD bool insideMiters(RecP rec, D3 q) {
     return dot(q - v2, n2) <= 0;
 }
 
-/* rec: the segment's 15 doubles (templated on the pointer type so a
-   constant-address-space view could be passed; every caller today passes the
-   generic pointer, so the record is fetched with vector loads -- loading it
-   by scalar loads in the packet tracer measured neutral) */
+/* The fp64 ray and the quadratic of hair.cpp:496-517 for the segment record
+   rec (15 doubles: v1, axis, n1, n2, v2).  The fp32 ray is passed through
+   opaque moves so the fp64 copies are not kept live across the traversal
+   loop: they are re-derived per exact test (rare: the fp32 pre-test passes
+   ~2 segments per ray). */
 template <class RecP>
-HD bool segIntersectRec(RecP rec, V3 of, V3 df, double r2, float mint, float maxt, float &t, V3 &p) {
-    /* keep the fp64 ray out of the traversal loop's live registers: the
-       conversions are re-done per exact test (rare: the fp32 pre-test passes
-       ~2 segments per ray), which the opaque moves below enforce */
+HD bool segQuadratic(RecP rec, V3 of, V3 df, double r2, D3 &rayO, D3 &rayD, double &nearT, double &farT) {
     float ox = of.x, oy = of.y, oz = of.z, dx = df.x, dy = df.y, dz = df.z;
     asm volatile("" : "+v"(ox), "+v"(oy), "+v"(oz), "+v"(dx), "+v"(dy), "+v"(dz));
-    const D3 rayO = d3(ox, oy, oz), rayD = d3(dx, dy, dz);
+    rayO = d3(ox, oy, oz);
+    rayD = d3(dx, dy, dz);
+    const D3 axis = d3(rec[3], rec[4], rec[5]);
+    const D3 relOrigin = rayO - d3(rec[0], rec[1], rec[2]);
+    const D3 projOrigin = relOrigin - axis * dot(axis, relOrigin);
+    const D3 projDirection = rayD - axis * dot(axis, rayD);
+    const double A = dot(projDirection, projDirection);
+    const double B = 2 * dot(projOrigin, projDirection);
+    const double C = dot(projOrigin, projOrigin) - r2;
+    return solveQuadraticDouble(A, B, C, nearT, farT);
+}
+
+/* HairKDTree::intersect (hair.cpp:485-548): t of the accepted root and which
+   root it was (farRoot: the near root was outside the miters or before mint).
+   The hit point is not formed here: segHitPoint re-derives it from the same
+   root with the same operations, in the kernel that shades the hit, so the
+   traversal kernels carry no fp64 point (fewer registers, no point record). */
+template <class RecP>
+HD bool segIntersectRec(RecP rec, V3 of, V3 df, double r2, float mint, float maxt, float &t, uint32_t &farRoot) {
+    D3 rayO, rayD;
     double nearT, farT;
-    {
-        const D3 axis = d3(rec[3], rec[4], rec[5]);
-        const D3 relOrigin = rayO - d3(rec[0], rec[1], rec[2]);
-        const D3 projOrigin = relOrigin - axis * dot(axis, relOrigin);
-        const D3 projDirection = rayD - axis * dot(axis, rayD);
-        const double A = dot(projDirection, projDirection);
-        const double B = 2 * dot(projOrigin, projDirection);
-        const double C = dot(projOrigin, projOrigin) - r2;
-        if (!solveQuadraticDouble(A, B, C, nearT, farT)) return false;
-    }
+    if (!segQuadratic(rec, of, df, r2, rayO, rayD, nearT, farT)) return false;
     if (!(nearT <= (double) maxt && farT >= (double) mint)) return false;
-    const D3 pointNear = rayO + rayD * nearT;
-    if (insideMiters(rec, pointNear) && nearT >= (double) mint) {
-        p = v3((float) pointNear.x, (float) pointNear.y, (float) pointNear.z);
+    if (nearT >= (double) mint && insideMiters(rec, rayO + rayD * nearT)) {
         t = (float) nearT;
+        farRoot = 0;
         return true;
     }
-    const D3 pointFar = rayO + rayD * farT;
-    if (insideMiters(rec, pointFar)) {
+    if (insideMiters(rec, rayO + rayD * farT)) {
         if (farT > (double) maxt) return false;
-        p = v3((float) pointFar.x, (float) pointFar.y, (float) pointFar.z);
         t = (float) farT;
+        farRoot = 1;
         return true;
     }
     return false;
 }
 
 HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, V3 of, V3 df, double r2, float mint,
-                     float maxt, float &t, V3 &p) {
-    return segIntersectRec(reinterpret_cast<const double *>(segs + s), of, df, r2, mint, maxt, t, p);
+                     float maxt, float &t, uint32_t &farRoot) {
+    return segIntersectRec(reinterpret_cast<const double *>(segs + s), of, df, r2, mint, maxt, t, farRoot);
+}
+
+/* radius of segment s's hair shape (uniform branch: one shape in every shipped scene but hair-curl) */
+HD float segRadius(const HptScene &sc, uint32_t s) {
+    return sc.nShapes > 1 ? sc.shapes[sc.segs[s].shape].radius : sc.radius;
+}
+
+/* the hit point of an accepted root (hair.cpp:519-541: rayO + rayD * root, rounded to float) */
+HD V3 segHitPoint(const HptScene &sc, uint32_t s, V3 of, V3 df, uint32_t farRoot) {
+    const float rad = segRadius(sc, s);
+    const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
+    D3 rayO, rayD;
+    double nearT = 0, farT = 0;
+    segQuadratic(reinterpret_cast<const double *>(sc.segs + s), of, df, r2, rayO, rayD, nearT, farT);
+    const D3 q = rayO + rayD * (farRoot ? farT : nearT);
+    return v3((float) q.x, (float) q.y, (float) q.z);
 }
 
 /* Conservative fp32 pre-test (see HptSegF): false only when the ray line
@@ -222,10 +235,6 @@ HD bool segIntersect(const HptSegment *__restrict__ segs, uint32_t s, V3 of, V3 
    most 11u |w|_1 and r|n| by at most 12u r; the test keeps a 4x margin on
    both (3e-6 (r + |w|_1)) and never divides by |n|, so it holds for rays
    of any direction, near-parallel ones included. */
-/* radius of segment s's hair shape (uniform branch: one shape in every shipped scene but hair-curl) */
-HD float segRadius(const HptScene &sc, uint32_t s) {
-    return sc.nShapes > 1 ? sc.shapes[sc.segs[s].shape].radius : sc.radius;
-}
 
 HD bool segMayHit(const float4 a, const float4 b, V3 o, V3 d, float r) {
     const float wx = o.x - a.x, wy = o.y - a.y, wz = o.z - a.z;
@@ -237,34 +246,11 @@ HD bool segMayHit(const float4 a, const float4 b, V3 o, V3 d, float r) {
     return wn <= r * __builtin_amdgcn_sqrtf(nn) * 1.000001f + 3e-6f * (r + fabsf(wx) + fabsf(wy) + fabsf(wz));
 }
 
-#ifdef HPT_EXPERIMENT_FP32
-/* timing experiment only (never the product): the cylinder test in fp32 */
-HD bool segIntersectF32(const HptSegment *__restrict__ segs, uint32_t s, V3 o, V3 d, float r, float mint,
-                        float maxt, float &t, V3 &p) {
-    const float4 *rec = reinterpret_cast<const float4 *>(segs + s);
-    const double *rd = reinterpret_cast<const double *>(segs + s);
-    V3 v1 = v3((float) rd[0], (float) rd[1], (float) rd[2]), axis = v3((float) rd[3], (float) rd[4], (float) rd[5]);
-    V3 rel = o - v1;
-    V3 po = rel - axis * dot(axis, rel), pd = d - axis * dot(axis, d);
-    float A = dot(pd, pd), B = 2 * dot(po, pd), C = dot(po, po) - r * r;
-    float nearT, farT;
-    if (!solveQuadratic(A, B, C, nearT, farT)) return false;
-    if (!(nearT <= maxt && farT >= mint)) return false;
-    V3 n1 = v3((float) rd[6], (float) rd[7], (float) rd[8]), n2 = v3((float) rd[9], (float) rd[10], (float) rd[11]);
-    V3 v2 = v3((float) rd[12], (float) rd[13], (float) rd[14]);
-    V3 pn = o + d * nearT;
-    if (dot(pn - v1, n1) >= 0 && dot(pn - v2, n2) <= 0 && nearT >= mint) { p = pn; t = nearT; return true; }
-    V3 pf = o + d * farT;
-    if (dot(pf - v1, n1) >= 0 && dot(pf - v2, n2) <= 0 && farT <= maxt) { p = pf; t = farT; return true; }
-    (void) rec;
-    return false;
-}
-#define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, p) segIntersectF32(segs, s, o, d, radius, mint, maxt, t, p)
-#elif defined(HPT_EXPERIMENT_NO_EXACT)
+#ifdef HPT_EXPERIMENT_NO_EXACT
 /* register-pressure experiment only (never the product): no exact test */
-#define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, p) ((t = (mint)), (p = o), (s) == 0xffffffffu)
+#define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, far) ((t = (mint)), (far = 0), (s) == 0xffffffffu)
 #else
-#define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, p) segIntersect(segs, s, o, d, r2, mint, maxt, t, p)
+#define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, far) segIntersect(segs, s, o, d, r2, mint, maxt, t, far)
 #endif
 
 /* adaptive ray epsilon: skdtree.cpp:126-129 (closest) / :213-216 (shadow) */
@@ -331,20 +317,32 @@ HD bool waveLeader() { return __lane_id() == (uint32_t) (__ffsll((unsigned long 
 /* One round: descend to the next leaf, test its segments, pop.  Returns
    true when the ray is finished (r.found / r.tHit / r.segHit hold
    the answer). */
+/* Per-lane LDS area of the traversal: the STACK ring-stack entries, then
+   HPT_RAY_ROWS rows holding the ray's cold values -- rcp (read once per
+   round) and maxt (read at a restart) -- so
+   that none of them occupies a register while the fp64 exact test runs (that
+   test is the register peak of the traversal kernels).  Row k of lane i is
+   stk[k * stride]. */
+#define HPT_RAY_ROWS 2
+template <int STACK>
+HD void stashRay(uint2 *stk, int stride, const TraceRay &r) {
+    stk[STACK * stride] = make_uint2(__float_as_uint(r.rcp.x), __float_as_uint(r.rcp.y));
+    stk[(STACK + 1) * stride] = make_uint2(__float_as_uint(r.rcp.z), __float_as_uint(r.maxt));
+}
+
 template <int STACK, bool STATS>
 HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, TraceCounters &tc) {
     static_assert((STACK & (STACK - 1)) == 0, "the ring stack index is masked");
-    const HptNode *__restrict__ nodes = sc.nodes;
     const float4 *__restrict__ leafF = reinterpret_cast<const float4 *>(sc.leafF);
     /* the ray as plain values: selecting among struct members by axis would be
        folded into a dynamically addressed load and push the state to scratch */
-    const V3 o = r.o, d = r.d, rcp = r.rcp;
+    const uint2 cr0 = stk[STACK * stride], cr1 = stk[(STACK + 1) * stride];
+    const V3 o = r.o, d = r.d, rcp = v3(__uint_as_float(cr0.x), __uint_as_float(cr0.y), __uint_as_float(cr1.x));
     /* hard bound so every wave drains even on a malformed tree; the call fails loudly */
     if (++r.leaves > (1 << 18)) {
         atomicOr(sc.fault, HPT_FAULT_LEAVES);
         return true;
     }
-#if HPT_NODE4
     /* descent over two-level nodes (HptNode4): one 32-byte fetch decides the
        top split and the split of each child the ray interval reaches; the
        binary traversal's front-to-back order and intervals are kept exactly
@@ -438,74 +436,15 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
         leafLast = sc.leafTable[2 * leafFirst + 1];
         leafFirst = sc.leafTable[2 * leafFirst];
     }
-#else
-    HptNode nd = nodes[r.node];
-    while (!(nd.w0 & 0x80000000u)) {
-        if (STATS) {
-            ++tc.nodes;
-            if (waveLeader()) tc.nodeSlots += 64;
-        }
-        const uint32_t axis = nd.w0 & 3u;
-        const uint32_t left = nd.w0 >> 2;
-        const float split = __uint_as_float(nd.w1);
-        /* per-axis selects (v_cndmask), not a dynamically indexed vector */
-        const float oa = axis == 0 ? o.x : (axis == 1 ? o.y : o.z);
-        const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
-        const float ra = axis == 0 ? rcp.x : (axis == 1 ? rcp.y : rcp.z);
-        const float tsplit = (split - oa) * ra;
-        /* branch-free front-to-back order (bitwise, so the wave keeps one path) */
-        const bool belowFirst = (oa < split) | ((oa == split) & (da <= 0.0f));
-        const uint32_t first = left + (belowFirst ? 0u : 1u), second = left + (belowFirst ? 1u : 0u);
-        const bool nearOnly = !(tsplit <= r.tmax) | (tsplit <= 0.0f);
-        const bool farOnly = !nearOnly & (tsplit < r.tmin);
-        const bool both = !(nearOnly | farOnly);
-        if (both) stk[(r.top & (STACK - 1)) * stride] = make_uint2(second, __float_as_uint(r.tmax));
-        r.lost = r.lost | (both & (r.sp == STACK));
-        r.top += both ? 1u : 0u;
-        r.sp += (both & (r.sp < STACK)) ? 1 : 0;
-        r.node = farOnly ? second : first;
-        r.tmax = both ? tsplit : r.tmax;
-        nd = nodes[r.node];
-    }
-    if (STATS) {
-        ++tc.nodes;
-        if (waveLeader()) tc.nodeSlots += 64;
-    }
-    const uint32_t leafFirst = nd.w0 & 0x7fffffffu, leafLast = nd.w1;
-#endif
-#if HPT_LEAF_MODE == 2
     /* leaf, two passes: the fp32 pre-test marks candidates in a bit mask
-       (32 records per chunk), then the exact fp64 test runs on the marked
-       ones -- the prefetched records are dead by then, so the fp64 test's
-       registers do not stack on top of them */
+       (32 records per chunk; the next record is fetched while the current one
+       is tested), then the exact fp64 test runs on the marked ones -- the
+       prefetched records are dead by then, so the fp64 test's registers do
+       not stack on top of them */
     const uint32_t first = leafFirst, last = leafLast;
     for (uint32_t c0 = first; c0 < last; c0 += 32) {
         const uint32_t c1 = min(last, c0 + 32);
         uint32_t mask = 0;
-#if HPT_LEAF_BATCH > 1
-        /* HPT_LEAF_BATCH records per round trip: their loads are issued
-           together (indices clamped into the leaf; extra lanes' results are
-           ignored), so a typical leaf costs one memory latency */
-        for (uint32_t e0 = c0; e0 < c1; e0 += HPT_LEAF_BATCH) {
-            float4 fa[HPT_LEAF_BATCH], fb[HPT_LEAF_BATCH];
-#pragma unroll
-            for (int k = 0; k < HPT_LEAF_BATCH; ++k) {
-                const uint32_t e = min(e0 + (uint32_t) k, c1 - 1u);
-                fa[k] = leafF[2 * e];
-                fb[k] = leafF[2 * e + 1];
-            }
-#pragma unroll
-            for (int k = 0; k < HPT_LEAF_BATCH; ++k) {
-                if (e0 + (uint32_t) k < c1) {
-                    if (STATS) {
-                        ++tc.prims;
-                        if (waveLeader()) tc.primSlots += 64;
-                    }
-                    if (segMayHit(fa[k], fb[k], o, d, sc.maxRadius)) mask |= 1u << (e0 + (uint32_t) k - c0);
-                }
-            }
-        }
-#else
         float4 na = leafF[2 * c0], nb = leafF[2 * c0 + 1];
         for (uint32_t e = c0; e < c1; ++e) {
             const float4 fa = na, fb = nb;
@@ -520,7 +459,6 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
             }
             if (segMayHit(fa, fb, o, d, sc.maxRadius)) mask |= 1u << (e - c0);
         }
-#endif
         while (mask) {
             const uint32_t e = c0 + (uint32_t) (__ffs(mask) - 1);
             mask &= mask - 1;
@@ -529,56 +467,19 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
             const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
             if (STATS) ++tc.exact;
             float t;
-            V3 p;
-            if (HPT_SEG_TEST(sc.segs, s, o, d, r2, r.mint, r.tHit, t, p)) {
+            uint32_t far;
+            if (HPT_SEG_TEST(sc.segs, s, o, d, r2, r.mint, r.tHit, t, far)) {
                 r.found = true;
                 if (r.shadow) return true;
                 r.tHit = t;
-                r.segHit = s;
+                r.segHit = s | (far << 31);
             }
         }
     }
-#else
-    /* leaf: records are contiguous; the next one is fetched before the
-       current one is tested, so the loads of a leaf overlap */
-    const uint32_t first = leafFirst, last = leafLast;
-    float4 na = make_float4(0, 0, 0, 0), nb = na;
-    if (first < last) {
-        na = leafF[2 * first];
-        nb = leafF[2 * first + 1];
-    }
-    for (uint32_t e = first; e < last; ++e) {
-#if HPT_LEAF_MODE == 1
-        const float4 fa = leafF[2 * e], fb = leafF[2 * e + 1];
-#else
-        const float4 fa = na, fb = nb;
-        if (e + 1 < last) {
-            na = leafF[2 * e + 2];
-            nb = leafF[2 * e + 3];
-        }
-#endif
-        if (STATS) {
-            ++tc.prims;
-            if (waveLeader()) tc.primSlots += 64;
-        }
-        if (!segMayHit(fa, fb, o, d, sc.maxRadius)) continue;
-        const uint32_t s = __float_as_uint(fb.z);
-        const float rad = segRadius(sc, s);
-        const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
-        if (STATS) ++tc.exact;
-        float t;
-        V3 p;
-        if (HPT_SEG_TEST(sc.segs, s, o, d, r2, r.mint, r.tHit, t, p)) {
-            r.found = true;
-            if (r.shadow) return true;
-            r.tHit = t;
-            r.segHit = s;
-        }
-    }
-#endif
     if (r.found && r.tHit <= r.tmax) return true;
     if (r.sp == 0) {
-        if (!r.lost || r.tmax >= r.maxt) return true;
+        const float maxt = __uint_as_float(stk[(STACK + 1) * stride].y);
+        if (!r.lost || r.tmax >= maxt) return true;
         if (++r.restarts > HPT_MAX_RESTARTS) {
             atomicOr(sc.fault, HPT_FAULT_RESTARTS);
             return true;
@@ -587,7 +488,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
         r.lost = false;
         r.node = 0;
         r.tmin = r.tmax;
-        r.tmax = r.maxt;
+        r.tmax = maxt;
         return false;
     }
     r.top--;
@@ -599,20 +500,9 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     return r.tmin > r.tHit;
 }
 
-/* The hit point of a finished closest-hit ray: the exact test of the
-   winning segment re-run with an open far end takes the same branch (near /
-   far root, hair.cpp:519-541) as when it was accepted, so p is the value the
-   traversal saw -- recomputing it here keeps three registers out of the
-   traversal loop. */
-HD V3 hitPoint(const HptScene &sc, const TraceRay &r) {
-    if (!r.found) return v3(0.0f, 0.0f, 0.0f);
-    float t;
-    V3 p = v3(0.0f, 0.0f, 0.0f);
-    const float radius = segRadius(sc, r.segHit);
-    const double r2 = (double) (radius * radius);
-    segIntersect(sc.segs, r.segHit, r.o, r.d, r2, r.mint, finf(), t, p);
-    return p;
-}
+/* segment id / far-root flag of a finished closest-hit ray (TraceRay::segHit = id | far << 31) */
+HD uint32_t hitSegment(const TraceRay &r) { return r.segHit & 0x7fffffffu; }
+HD uint32_t hitFarRoot(const TraceRay &r) { return r.segHit >> 31; }
 
 #ifndef HPT_XCD_SHARDS
 #define HPT_XCD_SHARDS 0 /* 1: waves claim their own XCD's shards first */
@@ -697,6 +587,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
                 if (rank < got) {
                     item = k;
                     active = io.begin(sc, k, r);
+                    if (active) stashRay<STACK>(stk, (int) blockDim.x, r);
                     if (STATS) {
                         nC += r.shadow ? 0u : 1u;
                         nS += r.shadow ? 1u : 0u;
@@ -788,7 +679,7 @@ struct PacketLds {
     PacketEntry ent[HPT_PACKET_STACK];
     float saved[HPT_PACKET_STACK][64];
 };
-static_assert(sizeof(float) * HPT_PACKET_STACK * 64 >= sizeof(uint2) * 8 * 64,
+static_assert(sizeof(float) * HPT_PACKET_STACK * 64 >= sizeof(uint2) * (8 + HPT_RAY_ROWS) * 64,
               "the fallback ring stack reuses the packet stack's LDS");
 
 /* a wave-uniform 64-bit value into scalar registers (readfirstlane returns a
@@ -896,11 +787,11 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
                 const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
                 if (STATS) ++tc.exact;
                 float t;
-                V3 p;
-                if (HPT_SEG_TEST(sc.segs, sg, o, d, r2, r.mint, r.tHit, t, p)) {
+                uint32_t far;
+                if (HPT_SEG_TEST(sc.segs, sg, o, d, r2, r.mint, r.tHit, t, far)) {
                     r.found = true;
                     r.tHit = t;
-                    r.segHit = sg;
+                    r.segHit = sg | (far << 31);
                 }
             }
         }
@@ -981,7 +872,7 @@ __device__ __forceinline__ void tracePackets(const HptScene &sc, IO &io, uint32_
             /* packet stack overflow: every lane re-traces its ray alone (same result) */
             if (STATS) fallbacks += lane == 0 ? 1u : 0u;
             uint2 *stk = reinterpret_cast<uint2 *>(&L.saved[0][0]) + lane;
-            if (lane < got && io.begin(sc, k, r))
+            if (lane < got && io.begin(sc, k, r) && (stashRay<8>(stk, 64, r), true))
                 while (!traceRound<8, STATS>(sc, r, stk, 64, tc)) {
                 }
         }
@@ -1983,10 +1874,9 @@ struct PathIO {
     /* returns 1 for an unoccluded shadow ray */
     HD uint32_t finish(const HptScene &sc, uint32_t k, const TraceRay &r) {
         if (!r.shadow) {
-            P.hit[id] = make_float4(__int_as_float(r.found ? (int32_t) r.segHit : -1), r.found ? r.tHit : finf(),
-                                    0.0f, 0.0f);
-            const V3 p = hitPoint(sc, r);
-            P.hitp[id] = make_float4(p.x, p.y, p.z, 0.0f);
+            /* hit record: segment (-1: miss), t, accepted root (the shading kernel re-derives the point) */
+            P.hit[id] = make_float4(__int_as_float(r.found ? (int32_t) hitSegment(r) : -1), r.found ? r.tHit : finf(),
+                                    __uint_as_float(hitFarRoot(r)), 0.0f);
             return 0;
         }
         if (r.found) return 0;
@@ -2019,7 +1909,7 @@ struct PathIO {
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
     uint32_t *__restrict__ counters, uint32_t *__restrict__ cursors) {
-    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     PathIO io{P, traceQ, shadowQ, counters[HPT_Q_TRACE], counters[HPT_Q_SHADOW], 0};
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
@@ -2029,7 +1919,7 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
                                                                               uint32_t *__restrict__ counters,
                                                                               uint32_t *__restrict__ cursors,
                                                                               uint32_t *stats) {
-    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     PathIO io{P, traceQ, shadowQ, counters[HPT_Q_TRACE], counters[HPT_Q_SHADOW], 0};
     tracePersistent<HPT_STACK, true>(sc, io, cursors, stk + threadIdx.x, stats);
 }
@@ -2112,12 +2002,14 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__rest
     {
         uint32_t st = P.state[id];
         uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st);
-        float4 h = P.hit[id], hp = P.hitp[id], rd = P.rd[id];
+        float4 h = P.hit[id], ro = P.ro[id], rd = P.rd[id];
         V3 rayD = v3(rd.x, rd.y, rd.z);
         V3 p, wi;
         Frame geo, sh;
         const uint32_t seg = (uint32_t) __float_as_int(h.x);
-        fillIts(sc, seg, v3(hp.x, hp.y, hp.z), rayD, p, geo, sh, wi);
+        /* the traced ray is still in ro / rd: the hit point from the accepted root (hair.cpp:519-541) */
+        const V3 hp = segHitPoint(sc, seg, v3(ro.x, ro.y, ro.z), rayD, __float_as_uint(h.z));
+        fillIts(sc, seg, hp, rayD, p, geo, sh, wi);
         bool stop = ((int) depth >= sc.maxDepth && sc.maxDepth > 0) ||
                     (sc.strictNormals && dot(rayD, geo.n) * wi.z >= 0);
         if (!stop && dim + 3 >= HPT_SOBOL_DIMS) {
@@ -2305,7 +2197,8 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
     auto trace = [&](bool shadowRay) {
         TraceRay r;
         const float4 ro = P.ro[io.id], rd = shadowRay ? P.sdir[io.id] : P.rd[io.id];
-        if (beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(rd.x, rd.y, rd.z), shadowRay ? kEpsilon : ro.w, rd.w, shadowRay))
+        if (beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(rd.x, rd.y, rd.z), shadowRay ? kEpsilon : ro.w, rd.w, shadowRay) &&
+            (stashRay<HPT_STACK>(stk, (int) blockDim.x, r), true))
             while (!traceRound<HPT_STACK, false>(sc, r, stk, (int) blockDim.x, tc)) {
             }
         io.finish(sc, 0, r);
@@ -2336,13 +2229,13 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void k_tail(HptScene sc, HptPaths P,
                                                                const uint32_t *__restrict__ shadeQ,
                                                                uint32_t *__restrict__ counters) {
-    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     tailPaths<false>(sc, P, shadeQ, counters, stk + threadIdx.x);
 }
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void k_tail_multi(HptScene sc, HptPaths P,
                                                                      const uint32_t *__restrict__ shadeQ,
                                                                      uint32_t *__restrict__ counters) {
-    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     tailPaths<true>(sc, P, shadeQ, counters, stk + threadIdx.x);
 }
 
@@ -2488,8 +2381,8 @@ struct BatchIO {
             return 0;
         }
         outT[i] = r.found ? r.tHit : finf();
-        outSeg[i] = r.found ? (int32_t) r.segHit : -1;
-        const V3 p = hitPoint(sc, r);
+        outSeg[i] = r.found ? (int32_t) hitSegment(r) : -1;
+        const V3 p = r.found ? segHitPoint(sc, hitSegment(r), r.o, r.d, hitFarRoot(r)) : v3(0.0f, 0.0f, 0.0f);
         outP[3 * i] = p.x;
         outP[3 * i + 1] = p.y;
         outP[3 * i + 2] = p.z;
@@ -2503,7 +2396,7 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptS
                                                                             float *outT, int32_t *outSeg,
                                                                             float *outP, uint8_t *outHit,
                                                                             uint32_t *cursor) {
-    __shared__ uint2 stk[HPT_STACK * HPT_TRACE_BLOCK];
+    __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     __shared__ PacketLds lds[HPT_TRACE_BLOCK / 64];
     BatchIO io{o, d, mint, maxt, outT, outP, outSeg, outHit, (uint32_t) n, (flags & 1) != 0};
     if ((flags & 4) && !(flags & 1))
