@@ -275,7 +275,7 @@ struct TraceRay {
     float tmin, tmax;   /* interval of the current subtree */
     float tHit;
     uint32_t node, top, segHit;
-    int sp, restarts, leaves;
+    int sp;             /* the leaf / kd-restart counters and mint, maxt, rcp are read from LDS by traceRound (stashRay) */
     bool lost, found, shadow;
 };
 
@@ -290,8 +290,6 @@ HD bool beginRay(const HptScene &sc, TraceRay &r, V3 o, V3 d, float rmint, float
     r.found = false;
     r.tHit = finf();
     r.segHit = 0;
-    r.restarts = 0; /* read by the counted kernels' per-ray tails even when the ray misses */
-    r.leaves = 0;
     float mint, maxt;
     if (!aabbIntersect(sc, o, d, r.rcp, mint, maxt)) return false;
     const float rayMinT = adaptiveMint(o, rmint, shadow);
@@ -318,16 +316,33 @@ HD bool waveLeader() { return __lane_id() == (uint32_t) (__ffsll((unsigned long 
    true when the ray is finished (r.found / r.tHit / r.segHit hold
    the answer). */
 /* Per-lane LDS area of the traversal: the STACK ring-stack entries, then
-   HPT_RAY_ROWS rows holding the ray's cold values -- rcp (read once per
-   round) and maxt (read at a restart) -- so
-   that none of them occupies a register while the fp64 exact test runs (that
-   test is the register peak of the traversal kernels).  Row k of lane i is
-   stk[k * stride]. */
-#define HPT_RAY_ROWS 2
+   HPT_RAY_ROWS rows holding the ray's cold values, so that none of them
+   occupies a register while the fp64 exact test runs (that test is the
+   register peak of the traversal kernels; registers decide how many waves a
+   SIMD holds, and the latency-bound traversal runs faster with more):
+     row STACK+0  rcp.x, rcp.y       read once per round
+     row STACK+1  rcp.z, key         key: what the IO's finish() needs (path id / ray index)
+     row STACK+2  mint, maxt         mint read by the exact tests, maxt at a kd-restart
+     row STACK+3  counters           leaves visited | kd-restarts << 20
+   Row k of lane i is stk[k * stride]. */
+#define HPT_RAY_ROWS 4
+#define HPT_CNT_RESTART (1u << 20)
 template <int STACK>
-HD void stashRay(uint2 *stk, int stride, const TraceRay &r) {
+HD void stashRay(uint2 *stk, int stride, const TraceRay &r, uint32_t key) {
     stk[STACK * stride] = make_uint2(__float_as_uint(r.rcp.x), __float_as_uint(r.rcp.y));
-    stk[(STACK + 1) * stride] = make_uint2(__float_as_uint(r.rcp.z), __float_as_uint(r.maxt));
+    stk[(STACK + 1) * stride] = make_uint2(__float_as_uint(r.rcp.z), key);
+    stk[(STACK + 2) * stride] = make_uint2(__float_as_uint(r.mint), __float_as_uint(r.maxt));
+    stk[(STACK + 3) * stride] = make_uint2(0u, 0u);
+    /* the rows must be re-read, not forwarded from these stores (forwarding keeps the values in registers) */
+    asm volatile("" ::: "memory");
+}
+template <int STACK> HD uint32_t rayKey(const uint2 *stk, int stride) { return stk[(STACK + 1) * stride].y; }
+/* leaves visited / kd-restarts of the lane's current ray */
+template <int STACK> HD uint32_t rayLeaves(const uint2 *stk, int stride) {
+    return stk[(STACK + 3) * stride].x & (HPT_CNT_RESTART - 1u);
+}
+template <int STACK> HD uint32_t rayRestarts(const uint2 *stk, int stride) {
+    return stk[(STACK + 3) * stride].x / HPT_CNT_RESTART;
 }
 
 template <int STACK, bool STATS>
@@ -339,9 +354,13 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     const uint2 cr0 = stk[STACK * stride], cr1 = stk[(STACK + 1) * stride];
     const V3 o = r.o, d = r.d, rcp = v3(__uint_as_float(cr0.x), __uint_as_float(cr0.y), __uint_as_float(cr1.x));
     /* hard bound so every wave drains even on a malformed tree; the call fails loudly */
-    if (++r.leaves > (1 << 18)) {
-        atomicOr(sc.fault, HPT_FAULT_LEAVES);
-        return true;
+    {
+        const uint32_t cnt = stk[(STACK + 3) * stride].x + 1u;
+        stk[(STACK + 3) * stride].x = cnt;
+        if ((cnt & (HPT_CNT_RESTART - 1u)) > (1u << 18)) {
+            atomicOr(sc.fault, HPT_FAULT_LEAVES);
+            return true;
+        }
     }
     /* descent over two-level nodes (HptNode4): one 32-byte fetch decides the
        top split and the split of each child the ray interval reaches; the
@@ -468,7 +487,8 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
             if (STATS) ++tc.exact;
             float t;
             uint32_t far;
-            if (HPT_SEG_TEST(sc.segs, s, o, d, r2, r.mint, r.tHit, t, far)) {
+            const float mint = __uint_as_float(stk[(STACK + 2) * stride].x);
+            if (HPT_SEG_TEST(sc.segs, s, o, d, r2, mint, r.tHit, t, far)) {
                 r.found = true;
                 if (r.shadow) return true;
                 r.tHit = t;
@@ -478,9 +498,11 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     }
     if (r.found && r.tHit <= r.tmax) return true;
     if (r.sp == 0) {
-        const float maxt = __uint_as_float(stk[(STACK + 1) * stride].y);
+        const float maxt = __uint_as_float(stk[(STACK + 2) * stride].y);
         if (!r.lost || r.tmax >= maxt) return true;
-        if (++r.restarts > HPT_MAX_RESTARTS) {
+        const uint32_t cnt = stk[(STACK + 3) * stride].x + HPT_CNT_RESTART;
+        stk[(STACK + 3) * stride].x = cnt;
+        if (cnt / HPT_CNT_RESTART > HPT_MAX_RESTARTS) {
             atomicOr(sc.fault, HPT_FAULT_RESTARTS);
             return true;
         }
@@ -518,8 +540,9 @@ HD uint32_t hitFarRoot(const TraceRay &r) { return r.segHit >> 31; }
    to the next one when its shard runs dry, so claims spread over 64
    addresses instead of serialising on one (device-scope atomics to a single
    word cost ~10 ns each) and neighbouring rays stay together.
-   IO supplies count(), begin(k, r) (load ray k; false = nothing to trace)
-   and finish(k, r).  Every wave exits once all shards are exhausted and its
+   IO supplies count(), begin(k, r) (load ray k; false = nothing to trace),
+   key() (after begin: what finish needs, kept in LDS while the ray is
+   traced) and finish(key, r).  Every wave exits once all shards are exhausted and its
    lanes have drained, so the grid always completes. */
 template <int STACK, bool STATS, class IO>
 __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint32_t *cursors, uint2 *stk,
@@ -528,14 +551,14 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
     const uint32_t lane = __lane_id();
     TraceRay r;
     TraceCounters tc;
-    uint32_t item = 0, nC = 0, nS = 0, nU = 0;
+    uint32_t nC = 0, nS = 0, nU = 0;
     uint32_t maxRounds = 0, maxRestarts = 0, restartRays = 0, restarts = 0; /* STATS: per-ray tails */
-    auto rayDone = [&](const TraceRay &q) {
+    auto rayDone = [&](uint32_t leaves, uint32_t rs) {
         if (STATS) {
-            maxRounds = max(maxRounds, (uint32_t) q.leaves);
-            maxRestarts = max(maxRestarts, (uint32_t) q.restarts);
-            restartRays += q.restarts > 0 ? 1u : 0u;
-            restarts += (uint32_t) q.restarts;
+            maxRounds = max(maxRounds, leaves);
+            maxRestarts = max(maxRestarts, rs);
+            restartRays += rs > 0 ? 1u : 0u;
+            restarts += rs;
         }
     };
     bool active = false, exhausted = false;
@@ -582,17 +605,18 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
 #endif
             }
             if (!active) {
-                const uint32_t rank = (uint32_t) __popcll(idle & ((1ull << lane) - 1ull));
+                /* idle lanes below this one (v_mbcnt: no 64-bit lane mask kept live across the loop) */
+                const uint32_t rank =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t) (idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) idle, 0u));
                 const uint32_t k = start + rank;
                 if (rank < got) {
-                    item = k;
                     active = io.begin(sc, k, r);
-                    if (active) stashRay<STACK>(stk, (int) blockDim.x, r);
+                    if (active) stashRay<STACK>(stk, (int) blockDim.x, r, io.key());
                     if (STATS) {
                         nC += r.shadow ? 0u : 1u;
                         nS += r.shadow ? 1u : 0u;
                     }
-                    if (!active) nU += io.finish(sc, k, r), rayDone(r);
+                    if (!active) nU += io.finish(sc, io.key(), r), rayDone(0u, 0u);
                 }
             }
         }
@@ -601,8 +625,8 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             continue;
         }
         if (active && traceRound<STACK, STATS>(sc, r, stk, (int) blockDim.x, tc)) {
-            nU += io.finish(sc, item, r);
-            rayDone(r);
+            nU += io.finish(sc, rayKey<STACK>(stk, (int) blockDim.x), r);
+            if (STATS) rayDone(rayLeaves<STACK>(stk, (int) blockDim.x), rayRestarts<STACK>(stk, (int) blockDim.x));
             active = false;
         }
     }
@@ -872,11 +896,11 @@ __device__ __forceinline__ void tracePackets(const HptScene &sc, IO &io, uint32_
             /* packet stack overflow: every lane re-traces its ray alone (same result) */
             if (STATS) fallbacks += lane == 0 ? 1u : 0u;
             uint2 *stk = reinterpret_cast<uint2 *>(&L.saved[0][0]) + lane;
-            if (lane < got && io.begin(sc, k, r) && (stashRay<8>(stk, 64, r), true))
+            if (lane < got && io.begin(sc, k, r) && (stashRay<8>(stk, 64, r, io.key()), true))
                 while (!traceRound<8, STATS>(sc, r, stk, 64, tc)) {
                 }
         }
-        if (lane < got) io.finish(sc, k, r);
+        if (lane < got) io.finish(sc, io.key(), r);
     }
     if (STATS) {
         for (int off = 32; off > 0; off >>= 1) {
@@ -1871,12 +1895,17 @@ struct PathIO {
         const float4 ro = P.ro[id], sd = P.sdir[id];
         return beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(sd.x, sd.y, sd.z), kEpsilon, sd.w, true);
     }
-    /* returns 1 for an unoccluded shadow ray */
-    HD uint32_t finish(const HptScene &sc, uint32_t k, const TraceRay &r) {
+    HD uint32_t key() const { return id; }
+    /* id: the path; returns 1 for an unoccluded shadow ray */
+    HD uint32_t finish(const HptScene &sc, uint32_t id, const TraceRay &r) {
         if (!r.shadow) {
             /* hit record: segment (-1: miss), t, accepted root (the shading kernel re-derives the point) */
-            P.hit[id] = make_float4(__int_as_float(r.found ? (int32_t) hitSegment(r) : -1), r.found ? r.tHit : finf(),
-                                    __uint_as_float(hitFarRoot(r)), 0.0f);
+            /* the miss constants are materialised here, not hoisted out of the trace loop (no
+               literal operands on VOP3 here: a hoisted +inf would hold a register for the loop) */
+            uint32_t missT;
+            asm volatile("v_mov_b32 %0, 0x7f800000" : "=v"(missT));
+            P.hit[id] = make_float4(__int_as_float(r.found ? (int32_t) hitSegment(r) : -1),
+                                    r.found ? r.tHit : __uint_as_float(missT), __uint_as_float(hitFarRoot(r)), 0.0f);
             return 0;
         }
         if (r.found) return 0;
@@ -1898,7 +1927,7 @@ struct PathIO {
 #define HPT_STACK 8
 #endif
 #ifndef HPT_TRACE_WAVES
-#define HPT_TRACE_WAVES 5
+#define HPT_TRACE_WAVES 6
 #endif
 #if HPT_TRACE_WAVES > 0 /* occupancy target (waves per SIMD) for k_trace's register allocation */
 #define HPT_TRACE_OCCUPANCY __attribute__((amdgpu_waves_per_eu(HPT_TRACE_WAVES)))
@@ -2198,10 +2227,10 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
         TraceRay r;
         const float4 ro = P.ro[io.id], rd = shadowRay ? P.sdir[io.id] : P.rd[io.id];
         if (beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(rd.x, rd.y, rd.z), shadowRay ? kEpsilon : ro.w, rd.w, shadowRay) &&
-            (stashRay<HPT_STACK>(stk, (int) blockDim.x, r), true))
+            (stashRay<HPT_STACK>(stk, (int) blockDim.x, r, io.id), true))
             while (!traceRound<HPT_STACK, false>(sc, r, stk, (int) blockDim.x, tc)) {
             }
-        io.finish(sc, 0, r);
+        io.finish(sc, io.id, r);
     };
     while (__ballot(live) != 0) {
         bool cont = false, shadow = false;
@@ -2370,8 +2399,11 @@ struct BatchIO {
     uint8_t *outHit;
     uint32_t n;
     bool shadow;
+    uint32_t cur;
     HD uint32_t count() const { return n; }
+    HD uint32_t key() const { return cur; }
     HD bool begin(const HptScene &sc, uint32_t i, TraceRay &r) {
+        cur = i;
         return beginRay(sc, r, v3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), v3(d[3 * i], d[3 * i + 1], d[3 * i + 2]),
                         mint[i], maxt[i], shadow);
     }
@@ -2398,7 +2430,7 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptS
                                                                             uint32_t *cursor) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     __shared__ PacketLds lds[HPT_TRACE_BLOCK / 64];
-    BatchIO io{o, d, mint, maxt, outT, outP, outSeg, outHit, (uint32_t) n, (flags & 1) != 0};
+    BatchIO io{o, d, mint, maxt, outT, outP, outSeg, outHit, (uint32_t) n, (flags & 1) != 0, 0u};
     if ((flags & 4) && !(flags & 1))
         tracePackets<false>(sc, io, cursor, lds[threadIdx.x >> 6], nullptr);
     else if (flags & 2)
