@@ -33,16 +33,18 @@ from mitsuba_amd import distributed, native, scenes  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
-# algorithmic bytes of k_trace (DESIGN.md "Byte model"):
-#   closest ray: queue id 4 + ray 32 + hit record 32 = 68 B
+# Algorithmic bytes of the traversal kernels.
+# roofline.achieved uses SURVEY.md 8(d)'s per-unit model: 8 B per binary kd-node visit, 4 B leaf
+# index + 52 B primitive per primitive test, plus the ray's own I/O:
+#   closest ray: queue id 4 + ray 32 + hit record 16 (segment, t, root) = 52 B
 #   shadow ray:  queue id 4 + origin 16 + direction/maxt 16 = 36 B, +48 B (contribution + radiance RMW)
 #                when unoccluded
-#   node visit 32 B (two-level HptNode4); primitive test 32 B leaf-ordered fp32 pre-test record;
-#   exact fp64 test (pre-test survivors) + 128 B segment record
-BYTES_CLOSEST, BYTES_SHADOW, BYTES_UNOCC, BYTES_NODE, BYTES_PRIM, BYTES_EXACT = 68, 36, 48, 32, 32, 128
-# k_trace_packet (the camera pass, 64-ray packets over the binary kd-tree): per member lane, an 8-byte
-# HptNode per binary node visit; rays, records and exact tests as above
-BYTES_NODE2 = 8
+BYTES_CLOSEST, BYTES_SHADOW, BYTES_UNOCC = 52, 36, 48
+B8D_NODE, B8D_REF, B8D_PRIM = 8, 4, 52
+# the layout-specific figure (what this build's records actually are): 32 B per two-level HptNode4
+# fetch, 32 B leaf-ordered fp32 pre-test record per primitive test, 128 B segment record per exact
+# fp64 test; the packet pass reads 8-byte binary HptNodes
+BYTES_NODE4, BYTES_PRIM, BYTES_EXACT, BYTES_NODE2 = 32, 32, 128, 8
 
 
 def parse():
@@ -59,7 +61,8 @@ def parse():
     ap.add_argument("--kd", default="", help="kd-tree build overrides k=v,... (hair shape kd* properties)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-spp", type=int, default=96, help="spp of the bounded CPU-baseline sample")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="0 = this process's CPUs, at most 16 (the GPU box's CPU share per GPU)")
     ap.add_argument("--workdir", default=os.path.join(tempfile.gettempdir(), "hpt_bench"))
     return ap.parse_args()
 
@@ -77,12 +80,22 @@ def cpu_baseline(args, cfg, xml_defines, hair_src, env_rgb, nodes, idx):
             xml_defines["maxDepth"])
     o.set_kdtree(nodes, idx)
     o.prepare()
-    threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    threads = args.cpu_threads if args.cpu_threads > 0 else min(16, avail)
     t0 = time.perf_counter()
     o.render(0, args.cpu_spp, threads=threads, width=W, height=H)
     dt = time.perf_counter() - t0
     paths = W * H * args.cpu_spp
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model)
+    except OSError:
+        pass
     return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
+            "cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": avail,
+            "threads_note": "one worker thread per core like mitsuba.cpp:135,281; capped at the GPU box's "
+                            "16-CPU share per GPU",
             "sample": "%dx%d @ %d spp of the same scene (%d paths), %.2f s, liboracle_ref.so "
                       "(-O3 -march=nocona -msse2 -funsafe-math-optimizations, config-ubuntu-20.04.py:8)"
                       % (W, H, args.cpu_spp, paths, dt)}
@@ -131,7 +144,7 @@ def main():
     # render is deterministic, so every frame has exactly these counts)
     step(2)
     c = r.stats()
-    frame = dict(nodes=c.nodes, prims=c.prims, exact=c.prim_exact, closest=c.closest_rays, shadow=c.shadow_rays,
+    frame = dict(nodes=c.nodes, bnodes=c.binary_nodes, prims=c.prims, exact=c.prim_exact, closest=c.closest_rays, shadow=c.shadow_rays,
                  unocc=c.shadow_unoccluded, bounces=c.bounces, launches=c.trace_launches,
                  node_slots=c.node_slots, prim_slots=c.prim_slots,
                  p_rays=c.packet_rays, p_nodes=c.packet_nodes, p_prims=c.packet_prims, p_exact=c.packet_exact,
@@ -166,13 +179,16 @@ def main():
         args.config, W, H, spp, max_depth, n, info.segments)
     paths_total = W * H * spp * args.steps
     value = paths_total / dt / 1e6
-    bytes_alg = (BYTES_CLOSEST * tot["closest"] + BYTES_SHADOW * tot["shadow"] + BYTES_UNOCC * tot["unocc"]
-                 + BYTES_NODE * tot["nodes"] + BYTES_PRIM * tot["prims"] + BYTES_EXACT * tot["exact"])
-    achieved = bytes_alg / (ms_trace * 1e-3) / 1e9 if ms_trace > 0 else 0.0
-    bytes_pk = (BYTES_CLOSEST * tot["p_rays"] + BYTES_NODE2 * tot["p_nodes"] + BYTES_PRIM * tot["p_prims"]
-                + BYTES_EXACT * tot["p_exact"])
-    achieved_pk = bytes_pk / (ms_packet * 1e-3) / 1e9 if ms_packet > 0 else 0.0
-    traffic, traffic_src, traffic_pk = None, None, None
+    io = BYTES_CLOSEST * tot["closest"] + BYTES_SHADOW * tot["shadow"] + BYTES_UNOCC * tot["unocc"]
+    bytes_alg = io + B8D_NODE * tot["bnodes"] + (B8D_REF + B8D_PRIM) * tot["prims"]
+    bytes_lay = io + BYTES_NODE4 * tot["nodes"] + BYTES_PRIM * tot["prims"] + BYTES_EXACT * tot["exact"]
+    gbs = lambda b, ms: b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0  # noqa: E731
+    achieved, achieved_lay = gbs(bytes_alg, ms_trace), gbs(bytes_lay, ms_trace)
+    io_pk = BYTES_CLOSEST * tot["p_rays"]
+    bytes_pk = io_pk + B8D_NODE * tot["p_nodes"] + (B8D_REF + B8D_PRIM) * tot["p_prims"]
+    bytes_pk_lay = io_pk + BYTES_NODE2 * tot["p_nodes"] + BYTES_PRIM * tot["p_prims"] + BYTES_EXACT * tot["p_exact"]
+    achieved_pk, achieved_pk_lay = gbs(bytes_pk, ms_packet), gbs(bytes_pk_lay, ms_packet)
+    traffic, traffic_src, traffic_pk, limiter = None, None, None, None
     tj = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
     if os.path.exists(tj):
         # HBM-side bytes per k_trace launch from the committed rocprofv3 PMC passes
@@ -183,6 +199,7 @@ def main():
             traffic_src = "profiles/" + os.path.basename(tj)
             if "k_trace_packet" in t["kernels"]:
                 traffic_pk = round(t["kernels"]["k_trace_packet"]["bytes_per_launch"])
+            limiter = t.get("limiter")
     out = None
     if rank == 0:
         cpu = None
@@ -207,10 +224,19 @@ def main():
                        "paths_per_step": W * H * spp, "parallelism": "tiles%d" % world,
                        "kd_nodes": int(info.kd_nodes), "kd_depth": int(info.kd_depth),
                        "prepare_s": round(t_prep, 3)},
-            "roofline": {"bound": "hbm", "kernel": "k_trace", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "traffic_source": traffic_src,
+            # bound: the roofline the kernel is priced against (HBM: no dense contraction here);
+            # limiter: what the PMC counters say actually holds it below that roofline
+            "roofline": {"bound": "hbm", "limiter": limiter, "kernel": "k_trace", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "achieved_hbm": round(traffic / (ms_trace / max(1, launches)) * 1e-6, 1) if traffic else None,
+                         "frac_hbm": round(traffic / (ms_trace / max(1, launches)) * 1e-6 / HBM_PEAK_GBS, 4)
+                         if traffic else None,
+                         "algorithmic_model": "SURVEY.md 8(d): 8 B per binary kd-node visit, 4+52 B per primitive "
+                                              "test, ray I/O 52 (closest) / 36 (+48 unoccluded) B",
                          "algorithmic_bytes_per_launch": int(bytes_alg // max(1, launches)),
+                         "achieved_layout": round(achieved_lay, 1),
+                         "layout_bytes_per_launch": int(bytes_lay // max(1, launches)),
                          "avg_launch_ms": round(ms_trace / max(1, launches), 4), "launches": int(launches),
                          "bytes_per_step": int(bytes_alg // args.steps),
                          "rank0_trace_ms_per_step": round(ms_trace / args.steps, 3)},
@@ -218,13 +244,17 @@ def main():
             "roofline_packet": {"bound": "hbm", "kernel": "k_trace_packet", "achieved": round(achieved_pk, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_pk / HBM_PEAK_GBS, 4),
                                 "traffic": traffic_pk,
+                                "achieved_hbm": round(traffic_pk / (ms_packet / max(1, p_launches)) * 1e-6, 1)
+                                if traffic_pk else None,
                                 "algorithmic_bytes_per_launch": int(bytes_pk // max(1, p_launches)),
+                                "achieved_layout": round(achieved_pk_lay, 1),
                                 "avg_launch_ms": round(ms_packet / max(1, p_launches), 4),
                                 "launches": int(p_launches)},
             "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in ms_kernels.items()},
             "cpu_baseline": cpu,
             "stats": {"bounces_per_path": round(tot["bounces"] / max(1, paths_total / world), 4),
                       "nodes_per_ray": round(tot["nodes"] / max(1, tot["closest"] + tot["shadow"]), 2),
+                      "binary_nodes_per_ray": round(tot["bnodes"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "prims_per_ray": round(tot["prims"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "exact_tests_per_ray": round(tot["exact"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "simd_util_nodes": round(tot["nodes"] / max(1, tot["node_slots"]), 3),

@@ -1061,6 +1061,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         c->stats.prim_exact = hs[5];
         c->stats.node_slots = hs[6];
         c->stats.prim_slots = hs[7];
+        c->stats.binary_nodes = hs[21];
     }
     c->stats.bounces = bounces;
     c->stats.max_bounces = maxB;

@@ -185,18 +185,29 @@ HD bool segQuadratic(RecP rec, V3 of, V3 df, double r2, D3 &rayO, D3 &rayD, doub
    The hit point is not formed here: segHitPoint re-derives it from the same
    root with the same operations, in the kernel that shades the hit, so the
    traversal kernels carry no fp64 point (fewer registers, no point record). */
+/* rayO + rayD * t with the fp64 ray re-derived from the fp32 one (opaque
+   moves: the conversions are redone here instead of keeping 12 registers of
+   fp64 ray live across the quadratic's solve) */
+HD D3 rayPointD(V3 of, V3 df, double t) {
+    float ox = of.x, oy = of.y, oz = of.z, dx = df.x, dy = df.y, dz = df.z;
+    asm volatile("" : "+v"(ox), "+v"(oy), "+v"(oz), "+v"(dx), "+v"(dy), "+v"(dz));
+    return d3(ox, oy, oz) + d3(dx, dy, dz) * t;
+}
+
 template <class RecP>
 HD bool segIntersectRec(RecP rec, V3 of, V3 df, double r2, float mint, float maxt, float &t, uint32_t &farRoot) {
-    D3 rayO, rayD;
     double nearT, farT;
-    if (!segQuadratic(rec, of, df, r2, rayO, rayD, nearT, farT)) return false;
+    {
+        D3 rayO, rayD;
+        if (!segQuadratic(rec, of, df, r2, rayO, rayD, nearT, farT)) return false;
+    }
     if (!(nearT <= (double) maxt && farT >= (double) mint)) return false;
-    if (nearT >= (double) mint && insideMiters(rec, rayO + rayD * nearT)) {
+    if (nearT >= (double) mint && insideMiters(rec, rayPointD(of, df, nearT))) {
         t = (float) nearT;
         farRoot = 0;
         return true;
     }
-    if (insideMiters(rec, rayO + rayD * farT)) {
+    if (insideMiters(rec, rayPointD(of, df, farT))) {
         if (farT > (double) maxt) return false;
         t = (float) farT;
         farRoot = 1;
@@ -290,6 +301,7 @@ HD bool beginRay(const HptScene &sc, TraceRay &r, V3 o, V3 d, float rmint, float
     r.found = false;
     r.tHit = finf();
     r.segHit = 0;
+    r.mint = r.maxt = 0.0f; /* defined for stashRay even when the ray misses */
     float mint, maxt;
     if (!aabbIntersect(sc, o, d, r.rcp, mint, maxt)) return false;
     const float rayMinT = adaptiveMint(o, rmint, shadow);
@@ -308,6 +320,7 @@ HD bool beginRay(const HptScene &sc, TraceRay &r, V3 o, V3 d, float rmint, float
 struct TraceCounters {
     uint32_t nodes = 0, prims = 0, exact = 0, nodeSlots = 0, primSlots = 0;
     uint32_t shadowNodes = 0, shadowPrims = 0; /* the part of nodes / prims spent on shadow rays */
+    uint32_t binNodes = 0; /* binary kd-node visits (Havran's count: inner nodes entered + leaves) */
 };
 
 HD bool waveLeader() { return __lane_id() == (uint32_t) (__ffsll((unsigned long long) __ballot(1)) - 1); }
@@ -332,7 +345,7 @@ HD void stashRay(uint2 *stk, int stride, const TraceRay &r, uint32_t key) {
     stk[STACK * stride] = make_uint2(__float_as_uint(r.rcp.x), __float_as_uint(r.rcp.y));
     stk[(STACK + 1) * stride] = make_uint2(__float_as_uint(r.rcp.z), key);
     stk[(STACK + 2) * stride] = make_uint2(__float_as_uint(r.mint), __float_as_uint(r.maxt));
-    stk[(STACK + 3) * stride] = make_uint2(0u, 0u);
+    reinterpret_cast<uint32_t *>(stk + (STACK + 3) * stride)[0] = 0u; /* counters (.y unused) */
     /* the rows must be re-read, not forwarded from these stores (forwarding keeps the values in registers) */
     asm volatile("" ::: "memory");
 }
@@ -424,6 +437,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
         }
         /* side A, over [tmin, tA] */
         const bool innerA = (flags >> (6 + sideA)) & 1u;
+        if (STATS) tc.binNodes += 1u + (innerA ? 1u : 0u) + ((both0 && ((flags >> (6 + sideB)) & 1u)) ? 1u : 0u);
         const uint32_t rA0 = sideA ? nb.z : nb.x, rA1 = sideA ? nb.w : nb.y;
         if (innerA) {
             const uint32_t ax = (flags >> (2 + 2 * sideA)) & 3u;
@@ -447,6 +461,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     }
     if (STATS) {
         ++tc.nodes;
+        ++tc.binNodes;
         tc.shadowNodes += r.shadow ? 1u : 0u;
         if (waveLeader()) tc.nodeSlots += 64;
     }
@@ -611,12 +626,18 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
                 const uint32_t k = start + rank;
                 if (rank < got) {
                     active = io.begin(sc, k, r);
-                    if (active) stashRay<STACK>(stk, (int) blockDim.x, r, io.key());
                     if (STATS) {
                         nC += r.shadow ? 0u : 1u;
                         nS += r.shadow ? 1u : 0u;
                     }
-                    if (!active) nU += io.finish(sc, io.key(), r), rayDone(0u, 0u);
+                    /* the LDS rows are written unconditionally, right where they were
+                       computed (under a branch, mint / maxt stayed live across the miss
+                       path and were spilled); a miss never reads them */
+                    stashRay<STACK>(stk, (int) blockDim.x, r, io.key());
+                    if (!active) {
+                        nU += io.finish(sc, io.key(), r);
+                        rayDone(0u, 0u);
+                    }
                 }
             }
         }
@@ -648,6 +669,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             nU += __shfl_down(nU, off);
             tc.shadowNodes += __shfl_down(tc.shadowNodes, off);
             tc.shadowPrims += __shfl_down(tc.shadowPrims, off);
+            tc.binNodes += __shfl_down(tc.binNodes, off);
             maxRounds = max(maxRounds, (uint32_t) __shfl_down(maxRounds, off));
             maxRestarts = max(maxRestarts, (uint32_t) __shfl_down(maxRestarts, off));
             restartRays += __shfl_down(restartRays, off);
@@ -672,6 +694,8 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             /* [19]/[20] node visits / primitive tests of shadow rays */
             atomicAdd(&st[19], (unsigned long long) tc.shadowNodes);
             atomicAdd(&st[20], (unsigned long long) tc.shadowPrims);
+            /* [21] binary kd-node visits (the byte model of SURVEY.md 8(d): 8 B per binary node) */
+            atomicAdd(&st[21], (unsigned long long) tc.binNodes);
         }
     }
 }

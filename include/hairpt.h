@@ -155,6 +155,9 @@ typedef struct hpt_stats {
        kd-restarts, and how many rays restarted at all (the bounds that fail a call with
        HPT_ETRAVERSAL are 2^18 rounds / 1024 restarts) */
     uint64_t max_leaf_rounds, max_restarts, restarted_rays;
+    /* counted frames: binary kd-node visits of k_trace (inner nodes entered + leaves, the count of
+       rayIntersectHavran, sahkdtree3.h:178-308; `nodes` counts the two-level HptNode4 fetches) */
+    uint64_t binary_nodes;
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 
