@@ -727,7 +727,7 @@ struct PacketLds {
     PacketEntry ent[HPT_PACKET_STACK];
     float saved[HPT_PACKET_STACK][64];
 };
-static_assert(sizeof(float) * HPT_PACKET_STACK * 64 >= sizeof(uint2) * (8 + HPT_RAY_ROWS) * 64,
+static_assert(sizeof(PacketLds) >= sizeof(uint2) * (8 + HPT_RAY_ROWS) * 64,
               "the fallback ring stack reuses the packet stack's LDS");
 
 /* a wave-uniform 64-bit value into scalar registers (readfirstlane returns a
@@ -736,6 +736,10 @@ HD uint64_t uniform64(uint64_t v) {
     return (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) v) |
            ((uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) (v >> 32)) << 32);
 }
+
+/* this lane's bit of a wave-uniform lane mask: v_cndmask on the mask itself
+   (no lane index or 64-bit shift kept in vector registers) */
+HD bool laneIn(uint64_t mask) { return __builtin_amdgcn_inverse_ballot_w64(mask); }
 
 /* returns false when the packet stack overflowed (the caller then traces each lane alone) */
 template <bool STATS>
@@ -772,7 +776,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
         /* ---- descend to a leaf ---- */
         HptNode nd = nodes(node);
         while (!(nd.w0 & 0x80000000u)) {
-            const bool me = (act >> lane) & 1u;
+            const bool me = laneIn(act);
             if (STATS) {
                 tc.nodes += me ? 1u : 0u;
                 if (lane == 0) tc.nodeSlots += 64;
@@ -795,7 +799,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
                 ++sp;
                 act = mBelow;
             }
-            const bool in = (act >> lane) & 1u;
+            const bool in = laneIn(act);
             const uint32_t belowG = (act & mBelow) != 0 ? 1u : 0u;
             const uint32_t first = left + (belowG ? 0u : 1u), second = left + (belowG ? 1u : 0u);
             const uint64_t mFirst = __ballot(in & !farOnly), mBoth = __ballot(in & both), mFar = __ballot(in & farOnly);
@@ -817,7 +821,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
             nd = nodes(node);
         }
         /* ---- leaf: the member lanes test its segments (pre-test, then exact) ---- */
-        const bool me = (act >> lane) & 1u;
+        const bool me = laneIn(act);
         if (STATS) {
             tc.nodes += me ? 1u : 0u;
             if (lane == 0) tc.nodeSlots += 64;
@@ -855,7 +859,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
             if (__builtin_amdgcn_readfirstlane(en.revisit)) {
                 act = enBoth & ~done;
             } else {
-                const bool inB = ((enBoth & ~done) >> lane) & 1u;
+                const bool inB = laneIn(enBoth & ~done);
                 if (inB) {
                     r.tmin = r.tmax;
                     r.tmax = L.saved[sp][lane];
@@ -919,7 +923,7 @@ __device__ __forceinline__ void tracePackets(const HptScene &sc, IO &io, uint32_
         if (!tracePacket<STATS>(sc, r, valid, L, tc)) {
             /* packet stack overflow: every lane re-traces its ray alone (same result) */
             if (STATS) fallbacks += lane == 0 ? 1u : 0u;
-            uint2 *stk = reinterpret_cast<uint2 *>(&L.saved[0][0]) + lane;
+            uint2 *stk = reinterpret_cast<uint2 *>(&L) + lane;
             if (lane < got && io.begin(sc, k, r) && (stashRay<8>(stk, 64, r, io.key()), true))
                 while (!traceRound<8, STATS>(sc, r, stk, 64, tc)) {
                 }
