@@ -286,7 +286,8 @@ struct TraceRay {
     float tmin, tmax;   /* interval of the current subtree */
     float tHit;
     uint32_t node, top, segHit;
-    int sp;             /* the leaf / kd-restart counters and mint, maxt, rcp are read from LDS by traceRound (stashRay) */
+    int sp;             /* mint, maxt, rcp are read from LDS by traceRound (stashRay) */
+    uint32_t cnt;       /* leaves visited | kd-restarts << 20 (traceRound's bounds) */
     bool lost, found, shadow;
 };
 
@@ -336,27 +337,22 @@ HD bool waveLeader() { return __lane_id() == (uint32_t) (__ffsll((unsigned long 
      row STACK+0  rcp.x, rcp.y       read once per round
      row STACK+1  rcp.z, key         key: what the IO's finish() needs (path id / ray index)
      row STACK+2  mint, maxt         mint read by the exact tests, maxt at a kd-restart
-     row STACK+3  counters           leaves visited | kd-restarts << 20
    Row k of lane i is stk[k * stride]. */
-#define HPT_RAY_ROWS 4
+#define HPT_RAY_ROWS 3
 #define HPT_CNT_RESTART (1u << 20)
 template <int STACK>
-HD void stashRay(uint2 *stk, int stride, const TraceRay &r, uint32_t key) {
+HD void stashRay(uint2 *stk, int stride, TraceRay &r, uint32_t key) {
     stk[STACK * stride] = make_uint2(__float_as_uint(r.rcp.x), __float_as_uint(r.rcp.y));
     stk[(STACK + 1) * stride] = make_uint2(__float_as_uint(r.rcp.z), key);
     stk[(STACK + 2) * stride] = make_uint2(__float_as_uint(r.mint), __float_as_uint(r.maxt));
-    reinterpret_cast<uint32_t *>(stk + (STACK + 3) * stride)[0] = 0u; /* counters (.y unused) */
+    r.cnt = 0u;
     /* the rows must be re-read, not forwarded from these stores (forwarding keeps the values in registers) */
     asm volatile("" ::: "memory");
 }
 template <int STACK> HD uint32_t rayKey(const uint2 *stk, int stride) { return stk[(STACK + 1) * stride].y; }
 /* leaves visited / kd-restarts of the lane's current ray */
-template <int STACK> HD uint32_t rayLeaves(const uint2 *stk, int stride) {
-    return stk[(STACK + 3) * stride].x & (HPT_CNT_RESTART - 1u);
-}
-template <int STACK> HD uint32_t rayRestarts(const uint2 *stk, int stride) {
-    return stk[(STACK + 3) * stride].x / HPT_CNT_RESTART;
-}
+HD uint32_t rayLeaves(const TraceRay &r) { return r.cnt & (HPT_CNT_RESTART - 1u); }
+HD uint32_t rayRestarts(const TraceRay &r) { return r.cnt / HPT_CNT_RESTART; }
 
 template <int STACK, bool STATS>
 HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, TraceCounters &tc) {
@@ -368,8 +364,8 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     const V3 o = r.o, d = r.d, rcp = v3(__uint_as_float(cr0.x), __uint_as_float(cr0.y), __uint_as_float(cr1.x));
     /* hard bound so every wave drains even on a malformed tree; the call fails loudly */
     {
-        const uint32_t cnt = stk[(STACK + 3) * stride].x + 1u;
-        stk[(STACK + 3) * stride].x = cnt;
+        const uint32_t cnt = r.cnt + 1u;
+        r.cnt = cnt;
         if ((cnt & (HPT_CNT_RESTART - 1u)) > (1u << 18)) {
             atomicOr(sc.fault, HPT_FAULT_LEAVES);
             return true;
@@ -515,8 +511,8 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     if (r.sp == 0) {
         const float maxt = __uint_as_float(stk[(STACK + 2) * stride].y);
         if (!r.lost || r.tmax >= maxt) return true;
-        const uint32_t cnt = stk[(STACK + 3) * stride].x + HPT_CNT_RESTART;
-        stk[(STACK + 3) * stride].x = cnt;
+        const uint32_t cnt = r.cnt + HPT_CNT_RESTART;
+        r.cnt = cnt;
         if (cnt / HPT_CNT_RESTART > HPT_MAX_RESTARTS) {
             atomicOr(sc.fault, HPT_FAULT_RESTARTS);
             return true;
@@ -647,7 +643,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
         }
         if (active && traceRound<STACK, STATS>(sc, r, stk, (int) blockDim.x, tc)) {
             nU += io.finish(sc, rayKey<STACK>(stk, (int) blockDim.x), r);
-            if (STATS) rayDone(rayLeaves<STACK>(stk, (int) blockDim.x), rayRestarts<STACK>(stk, (int) blockDim.x));
+            if (STATS) rayDone(rayLeaves(r), rayRestarts(r));
             active = false;
         }
     }
@@ -1946,8 +1942,12 @@ struct PathIO {
 /* k_trace launch shape (measured on MI355X, furball 512^2 @ 256 spp):
    persistent 256-thread blocks (64 and 128 are within 1.5%); an 8-entry ring
    stack (64 B/lane, kd-restart on overflow) beats 16 (-5%) and 4 (-11%, +12%
-   node visits) entries; a 5-waves/SIMD register target beats the natural
-   allocation at 4 waves/SIMD.  Overridable for experiments (make variant). */
+   node visits) entries.  The traversal is latency-bound, so waves per SIMD
+   decide its speed (k_trace per frame: 4 waves 141 ms, 5: 117, 6: 106, 7: 99):
+   7 waves need <= 72 VGPRs and <= 91 B of LDS per lane (64 B stack + 24 B of
+   ray rows), which the LDS ray rows, the fp64 ray re-derivation in the exact
+   test and the hit point moved to k_shade make possible without spills.
+   Overridable for experiments (make variant). */
 #ifndef HPT_TRACE_BLOCK
 #define HPT_TRACE_BLOCK 256
 #endif
@@ -1955,7 +1955,7 @@ struct PathIO {
 #define HPT_STACK 8
 #endif
 #ifndef HPT_TRACE_WAVES
-#define HPT_TRACE_WAVES 6
+#define HPT_TRACE_WAVES 7
 #endif
 #if HPT_TRACE_WAVES > 0 /* occupancy target (waves per SIMD) for k_trace's register allocation */
 #define HPT_TRACE_OCCUPANCY __attribute__((amdgpu_waves_per_eu(HPT_TRACE_WAVES)))
