@@ -713,7 +713,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
    the same intervals as its own traversal, and its result is bit-identical.
    A packet whose stack would overflow finishes lane by lane (traceRound). */
 #ifndef HPT_PACKET_STACK
-#define HPT_PACKET_STACK 24
+#define HPT_PACKET_STACK 23 /* 6.4 KB of LDS per wave: 6 waves/SIMD fit the 160 KB (24 entries did not) */
 #endif
 struct PacketEntry {
     uint32_t node, revisit;
@@ -1983,7 +1983,7 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
 
 /* k_trace_packet: the camera pass's closest-hit rays as 64-ray packets */
 #ifndef HPT_PACKET_WAVES
-#define HPT_PACKET_WAVES 5
+#define HPT_PACKET_WAVES 6 /* 34.6 -> 32.9 ms per frame vs 5 (spills only in the per-packet prologue) */
 #endif
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_PACKET_WAVES))) void
 k_trace_packet(HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, uint32_t *__restrict__ counters,
