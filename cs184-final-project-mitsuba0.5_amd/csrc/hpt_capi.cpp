@@ -71,6 +71,7 @@ struct hpt_context {
     std::vector<uint32_t> sobol32;
     std::vector<uint64_t> vdc, vdcInv;
     HptScene sc;
+    HptScene *scDev = nullptr;     /* device copy of sc (kernels that read the scene through a pointer) */
     std::vector<DevBuf> sceneBufs;
     /* wave buffers */
     uint64_t capacity = 0;
@@ -273,6 +274,7 @@ void hpt_context_destroy(hpt_context *c) {
     if (c->partial) (void) hipFree(c->partial);
     if (c->dBlockOf) (void) hipFree(c->dBlockOf);
     if (c->dLocalOf) (void) hipFree(c->dLocalOf);
+    if (c->scDev) (void) hipFree(c->scDev);
     for (auto e : c->evPool) (void) hipEventDestroy(e);
     (void) hipStreamDestroy(c->stream);
     delete c;
@@ -885,6 +887,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         c->partialSlots = slots;
     }
     hipStream_t s = c->stream;
+    if (!c->scDev) HIPCHK(c, hipMalloc((void **) &c->scDev, sizeof(HptScene)));
+    HIPCHK(c, hipMemcpy(c->scDev, &c->sc, sizeof(HptScene), hipMemcpyHostToDevice));
     const bool st = prm->collect_stats != 0;      /* HIP event timing per kernel class */
     const bool counted = prm->collect_stats >= 2; /* + traversal counters (k_trace_counted) */
     if (counted) HIPCHK(c, hipMemsetAsync(c->dstats, 0, 24 * 8, s));
@@ -990,7 +994,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                 c->stats.tail_paths += n;
                 break;
             }
-            e = timed(2, [&] { return hpt_launch_shade(sc, c->P, shadeIn, c->qTrace, c->qShadow, c->counters, n, s); });
+            e = timed(2, [&] { return hpt_launch_shade(sc, c->scDev, c->P, shadeIn, c->qTrace, c->qShadow, c->counters, n, s); });
             if (e) break;
             e = timed(-1, [&] {
                 return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, c->counters,

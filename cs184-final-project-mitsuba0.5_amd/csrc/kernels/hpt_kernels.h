@@ -79,7 +79,7 @@ hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const 
                                    uint32_t *stats, uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
                               uint32_t *counters, uint64_t maxItems, hipStream_t s);
-hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *traceQ,
+hipError_t hpt_launch_shade(const HptScene &sc, const HptScene *scDev, const HptPaths &P, const uint32_t *shadeQ, uint32_t *traceQ,
                             uint32_t *shadowQ, uint32_t *counters, uint64_t maxItems, hipStream_t s);
 /* the rest of every live path (shade queue) to termination in one launch */
 hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *counters,

@@ -1079,17 +1079,38 @@ HD float sampleM(float v, float sinThetaI, float cosThetaI, float xi1, float xi2
     return -cosTheta * sinThetaI + sinTheta * cosPhi * cosThetaI;
 }
 
+/* Where MarschnerDiffuse::sample reads the per-lobe InterpolatedDistribution1D
+   cdfs and sums: GlobalTabs = the scene's HBM arrays (through L2), LdsTabs =
+   a copy staged in LDS by k_shade_mlds (the binary search of azSample is a
+   chain of dependent reads: LDS latency instead of L2 latency). */
+struct GlobalTabs {
+    const HptMarschner &m;
+    HD const float *cdf(int l) const { return l == 0 ? m.cdf[0] : (l == 1 ? m.cdf[1] : m.cdf[2]); }
+    HD const float *sums(int l) const { return l == 0 ? m.sums[0] : (l == 1 ? m.sums[1] : m.sums[2]); }
+};
+#define HPT_CDF_WORDS (HPT_AZ_RES * (HPT_AZ_RES + 1))
+struct MarschnerLds {
+    float cdf[3][HPT_CDF_WORDS];
+    float sums[3][HPT_AZ_RES];
+};
+struct LdsTabs {
+    const MarschnerLds &t;
+    HD const float *cdf(int l) const { return t.cdf[l]; }
+    HD const float *sums(int l) const { return t.sums[l]; }
+};
+
 /* MarschnerDiffuse::sample (:594-744); pdf() == 1 (:517-520) */
-HD V3 marschnerSample(const HptMarschner &m, V3 wi, float sx, float sy, V3 &wo, uint32_t &type) {
+template <class Tabs>
+HD V3 marschnerSample(const HptMarschner &m, const Tabs &tabs, V3 wi, float sx, float sy, V3 &wo, uint32_t &type) {
     float sinThetaI = wi.y;
     float cosThetaI = trigInverse(sinThetaI);
     float thetaI = asinf(clampf(sinThetaI, -1.0f, 1.0f));
     float thetaIR = thetaI - 2.0f * m.scaleAngleRad;
     float thetaITT = thetaI + m.scaleAngleRad;
     float thetaITRT = thetaI + 4.0f * m.scaleAngleRad;
-    float weightR = azWeight(m.sums[0], cosThetaI);
-    float weightTT = azWeight(m.sums[1], cosThetaI);
-    float weightTRT = azWeight(m.sums[2], cosThetaI);
+    float weightR = azWeight(tabs.sums(0), cosThetaI);
+    float weightTT = azWeight(tabs.sums(1), cosThetaI);
+    float weightTRT = azWeight(tabs.sums(2), cosThetaI);
     int lobe;
     float v, theta;
     float target = sx * (weightR + weightTT + weightTRT);
@@ -1105,7 +1126,7 @@ HD V3 marschnerSample(const HptMarschner &m, V3 wi, float sx, float sy, V3 &wo, 
     float thetaO = asinf(clampf(sinThetaO, -1.0f, 1.0f));
     float thetaD = (thetaO - thetaI) * 0.5f;
     float cosThetaD = cosf(thetaD);
-    float phi = azSample(m.cdf[lobe], cosThetaD, sy);
+    float phi = azSample(tabs.cdf(lobe), cosThetaD, sy);
     float sinPhi = sinf(phi), cosPhi = cosf(phi);
     float probSpecular = 1 - roughTrans(m, wi.z);
     float w = m.specularSamplingWeight;
@@ -1539,15 +1560,19 @@ HD float bsdfPdf(const HptBsdf &b, V3 wi, V3 wo) {
     default: return 0.0f;
     }
 }
-HD V3 bsdfSample(const HptBsdf &b, V3 wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
+template <class Tabs>
+HD V3 bsdfSampleT(const HptBsdf &b, const Tabs &tabs, V3 wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
     switch (b.kind) {
-    case HPT_BSDF_MARSCHNER: pdf = 1.0f; return marschnerSample(b.mar, wi, sx, sy, wo, type);
+    case HPT_BSDF_MARSCHNER: pdf = 1.0f; return marschnerSample(b.mar, tabs, wi, sx, sy, wo, type);
     case HPT_BSDF_KAJIYAKAY: return kkSample(b.kk, wi, sx, sy, wo, pdf, type);
     case HPT_BSDF_ROUGHPLASTIC: return rpSample(b.rp, wi, sx, sy, wo, pdf, type);
     case HPT_BSDF_MARSCHNERDIELECTRIC: return mdSample(b.md, wi, sx, sy, wo, pdf, type);
     case HPT_BSDF_THINDIELECTRIC: return tdSample(b.md, wi, sx, wo, pdf, type);
     default: return dfSample(b.df, wi, sx, sy, wo, pdf, type);
     }
+}
+HD V3 bsdfSample(const HptBsdf &b, V3 wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) {
+    return bsdfSampleT(b, GlobalTabs{b.mar}, wi, sx, sy, wo, pdf, type);
 }
 
 /* ------------------------------------------------------------------ */
@@ -2053,9 +2078,9 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
    MULTI: several hair shapes, the hit shape's BSDF comes from sc.bsdfs (a
    separate kernel, so the single-shape one never mixes a kernel-argument
    pointer with a global one -- that would copy the scene to scratch) */
-template <bool MULTI>
+template <bool MULTI, bool LDS = false>
 HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__restrict__ counters, bool &cont,
-                  bool &shadow) {
+                  bool &shadow, const MarschnerLds *ldsTabs = nullptr) {
     {
         uint32_t st = P.state[id];
         uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st);
@@ -2111,7 +2136,9 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__rest
             V3 woL;
             float bpdf = 0.0f;
             uint32_t type = 0;
-            V3 w = bsdfSample(B, wi, bx, by, woL, bpdf, type);
+            V3 w;
+            if constexpr (LDS) w = bsdfSampleT(B, LdsTabs{*ldsTabs}, wi, bx, by, woL, bpdf, type);
+            else w = bsdfSample(B, wi, bx, by, woL, bpdf, type);
             if (!isZero(w)) {
                 V3 wo = sh.toWorld(woL);
                 float woDotGeoN = dot(geo.n, wo);
@@ -2155,6 +2182,50 @@ extern "C" __global__ __launch_bounds__(HPT_SHADE_BLOCK) void k_shade(HptScene s
                                                            uint32_t *__restrict__ counters) {
     shadeBounce<false>(sc, P, shadeQ, traceQ, shadowQ, counters);
 }
+/* k_shade for a single Marschner hair shape with the lobe cdfs / sums staged
+   in LDS (51 KB): persistent blocks (two per CU, 10 waves each = 5 waves per
+   SIMD) stage the tables once and walk the shade queue in block-sized steps,
+   so the staging cost is paid per block, not per path */
+#ifndef HPT_SHADE_LDS_BLOCK
+#define HPT_SHADE_LDS_BLOCK 640
+#endif
+#ifndef HPT_SHADE_LDS_WAVES
+#define HPT_SHADE_LDS_WAVES 5
+#endif
+extern "C" __global__ __launch_bounds__(HPT_SHADE_LDS_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_SHADE_LDS_WAVES))) void k_shade_mlds(const HptScene *scg, HptPaths P,
+                                                                            const uint32_t *__restrict__ shadeQ,
+                                                                            uint32_t *__restrict__ traceQ,
+                                                                            uint32_t *__restrict__ shadowQ,
+                                                                            uint32_t *__restrict__ counters) {
+    /* the scene through a global pointer, not the kernel argument: the loop below would
+       hoist every argument field it touches into scalar registers (they spill) */
+    const HptScene &sc = *scg;
+    __shared__ MarschnerLds T;
+    /* lobe by lobe with uniform pointers (a per-lane index into the kernel argument's
+       pointer arrays would copy the argument to scratch) */
+#pragma unroll
+    for (int l = 0; l < 3; ++l) {
+        const float *cdf = l == 0 ? sc.bsdf.mar.cdf[0] : (l == 1 ? sc.bsdf.mar.cdf[1] : sc.bsdf.mar.cdf[2]);
+        const float *sums = l == 0 ? sc.bsdf.mar.sums[0] : (l == 1 ? sc.bsdf.mar.sums[1] : sc.bsdf.mar.sums[2]);
+        for (uint32_t i = threadIdx.x; i < HPT_CDF_WORDS; i += blockDim.x) T.cdf[l][i] = cdf[i];
+        for (uint32_t i = threadIdx.x; i < HPT_AZ_RES; i += blockDim.x) T.sums[l][i] = sums[i];
+    }
+    __syncthreads();
+    const uint32_t n = counters[HPT_Q_SHADE_IN];
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) { /* block-uniform */
+        asm volatile("" ::: "memory"); /* scene fields are re-read per step, not hoisted (scalar loads, cached) */
+        const uint32_t tid = base + threadIdx.x;
+        bool cont = false, shadow = false;
+        uint32_t id = 0;
+        if (tid < n) {
+            id = shadeQ[tid];
+            shadePath<false, true>(sc, P, id, counters, cont, shadow, &T);
+        }
+        qpushBlock<HPT_SHADE_LDS_BLOCK>(cont, id, traceQ, &counters[HPT_Q_TRACE]);
+        qpushBlock<HPT_SHADE_LDS_BLOCK>(shadow, id, shadowQ, &counters[HPT_Q_SHADOW]);
+    }
+}
+
 extern "C" __global__ __launch_bounds__(HPT_SHADE_BLOCK) void k_shade_multi(HptScene sc, HptPaths P,
                                                                  const uint32_t *__restrict__ shadeQ,
                                                                  uint32_t *__restrict__ traceQ,
@@ -2556,7 +2627,7 @@ hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPath
 }
 /* persistent grid: as many one-wave blocks as can be resident at once
    (occupancy API x CUs), capped by the work */
-static unsigned persistentBlocks(const void *kernel, uint64_t items) {
+static unsigned persistentBlocks(const void *kernel, uint64_t items, int block = HPT_TRACE_BLOCK) {
     /* resident blocks per kernel, measured once (render calls of several contexts
        may run on several host threads: the cache is guarded) */
     static std::mutex mu;
@@ -2570,14 +2641,14 @@ static unsigned persistentBlocks(const void *kernel, uint64_t items) {
             int perCU = 0;
             hipDeviceProp_t prop;
             if (hipGetDeviceProperties(&prop, dev) != hipSuccess ||
-                hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, HPT_TRACE_BLOCK, 0) != hipSuccess ||
+                hipOccupancyMaxActiveBlocksPerMultiprocessor(&perCU, kernel, block, 0) != hipSuccess ||
                 perCU <= 0)
                 perCU = 8, prop.multiProcessorCount = 256;
             it = cached.emplace(std::make_pair(dev, kernel), perCU * prop.multiProcessorCount).first;
         }
         resident = it->second;
     }
-    const uint64_t need = (items + HPT_TRACE_BLOCK - 1) / HPT_TRACE_BLOCK;
+    const uint64_t need = (items + block - 1) / block;
     return (unsigned) std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t) resident));
 }
 
@@ -2610,12 +2681,29 @@ hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint3
     hipLaunchKernelGGL(k_primary, dim3(blocksFor(maxItems, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, P, traceQ, shadeQ, counters);
     return hipGetLastError();
 }
-hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *traceQ,
+/* HAIRPT_SHADE_LDS=1 selects k_shade_mlds (Marschner cdfs / sums staged in LDS).  Measured on
+   MI355X at the headline (furball 512^2 @ 256, shade per frame): L2 tables 18.2 ms; LDS staging
+   19.4 ms (512-thread persistent blocks, 4 waves/SIMD) and 27.8 ms (640 threads, 5 waves): the
+   persistent loop needs 168 VGPRs and spills, which costs more than the L2-latency binary search
+   it saves.  Off by default; kept for the A/B. */
+static bool hptShadeLds() {
+    static const bool on = [] {
+        const char *e = getenv("HAIRPT_SHADE_LDS");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+hipError_t hpt_launch_shade(const HptScene &sc, const HptScene *scDev, const HptPaths &P, const uint32_t *shadeQ, uint32_t *traceQ,
                             uint32_t *shadowQ, uint32_t *counters, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
     if (sc.nShapes > 1)
         hipLaunchKernelGGL(k_shade_multi, dim3(blocksFor(maxItems, HPT_SHADE_BLOCK)), dim3(HPT_SHADE_BLOCK), 0, s, sc, P, shadeQ,
                            traceQ, shadowQ, counters);
+    else if (sc.bsdf.kind == HPT_BSDF_MARSCHNER && hptShadeLds())
+        hipLaunchKernelGGL(k_shade_mlds,
+                           dim3(persistentBlocks((const void *) k_shade_mlds, maxItems, HPT_SHADE_LDS_BLOCK)),
+                           dim3(HPT_SHADE_LDS_BLOCK), 0, s, scDev, P, shadeQ, traceQ, shadowQ, counters);
     else
         hipLaunchKernelGGL(k_shade, dim3(blocksFor(maxItems, HPT_SHADE_BLOCK)), dim3(HPT_SHADE_BLOCK), 0, s, sc, P, shadeQ,
                            traceQ, shadowQ, counters);
