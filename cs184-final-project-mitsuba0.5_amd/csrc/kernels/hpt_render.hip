@@ -366,6 +366,10 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     {
         const uint32_t cnt = r.cnt + 1u;
         r.cnt = cnt;
+#ifdef HPT_EXPERIMENT_MAX_ROUNDS
+        /* timing experiment only (never the product): rays end after this many leaf rounds */
+        if ((cnt & (HPT_CNT_RESTART - 1u)) > HPT_EXPERIMENT_MAX_ROUNDS) return true;
+#endif
         if ((cnt & (HPT_CNT_RESTART - 1u)) > (1u << 18)) {
             atomicOr(sc.fault, HPT_FAULT_LEAVES);
             return true;

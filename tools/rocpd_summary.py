@@ -19,6 +19,46 @@ def one_db(d):
     return sqlite3.connect(f[0])
 
 
+def fmt(x, digits=2):
+    if x is None:
+        return "-"
+    return ("%%.%df" % digits) % x
+
+
+def pmc_summary(d):
+    """per kernel: counter sums over every launch, from every group database under d"""
+    sums = {}
+    for g in sorted(glob.glob(os.path.join(d, "g*"))):
+        if not os.path.isdir(g):
+            continue
+        try:
+            db = one_db(g)
+        except SystemExit:
+            continue
+        for kn, ctr, val in db.execute("select kernel_name, counter_name, sum(value) from counters_collection "
+                                       "group by kernel_name, counter_name"):
+            sums.setdefault(kn, {})[ctr] = val
+    out = {}
+    for kn, c in sums.items():
+        cyc = c.get("SQ_WAVE_CYCLES")
+        waves = c.get("SQ_WAVES")
+        r = {}
+        if cyc:
+            r["wait"] = c.get("SQ_WAIT_ANY", 0) / cyc
+            r["inst_wait"] = c.get("SQ_WAIT_INST_ANY", 0) / cyc
+            r["valu"] = c.get("SQ_ACTIVE_INST_VALU", 0) / cyc
+        if c.get("TCC_HIT_sum") is not None and c.get("TCC_MISS_sum") is not None:
+            r["l2_hit"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+        if c.get("TCP_TOTAL_CACHE_ACCESSES_sum"):
+            r["l1_miss"] = c.get("TCP_TCC_READ_REQ_sum", 0) / c["TCP_TOTAL_CACHE_ACCESSES_sum"]
+        if waves:
+            r["vmem_per_wave"] = c.get("SQ_INSTS_VMEM_RD", 0) / waves
+            r["lds_per_wave"] = c.get("SQ_INSTS_LDS", 0) / waves
+        r["counters"] = c
+        out[kn] = r
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("prof_dir", help="gpurun_out/prof_<tag> (trace/, fetch/, write/)")
@@ -26,6 +66,7 @@ def main():
     ap.add_argument("--title", default="")
     ap.add_argument("--json", default=None, help="also write per-launch traffic as JSON (read by bench.py)")
     ap.add_argument("--workload", default="", help="workload string the traffic belongs to (bench config)")
+    ap.add_argument("--pmc", default=None, help="gpurun_out/pmc_<tag> (g1..gN from scripts/gpu_pmc.sh)")
     a = ap.parse_args()
     lines = []
     if a.title:
@@ -61,6 +102,23 @@ def main():
                 continue
             kn = kn if len(kn) < 60 else kn[:57] + "..."
             lines.append("| %s | %d | %.1f | %.1f | %.1f |" % (kn, f[0], fm, wm, fm + wm))
+    pmc = pmc_summary(a.pmc) if a.pmc else {}
+    if pmc:
+        lines += ["", "## Occupancy / stall / cache counters (scripts/gpu_pmc.sh, one rocprofv3 --pmc pass per group)",
+                  "", "Ratios of counters summed over all launches of the kernel: wait = SQ_WAIT_ANY / "
+                  "SQ_WAVE_CYCLES (wave-cycles parked on a dependency, mostly memory), valu = "
+                  "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES, inst-wait = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES, "
+                  "L2 hit = TCC_HIT / (TCC_HIT + TCC_MISS), L1 miss to L2 = TCP_TCC_READ_REQ / "
+                  "TCP_TOTAL_CACHE_ACCESSES.", "",
+                  "| kernel | wait | inst-wait | valu | L2 hit | L1->L2 reads | VMEM rd / wave | LDS inst / wave |",
+                  "|---|---:|---:|---:|---:|---:|---:|---:|"]
+        for kn in ("k_trace", "k_trace_packet", "k_shade", "k_post", "k_tail", "k_camera", "k_primary"):
+            v = pmc.get(kn)
+            if not v:
+                continue
+            lines.append("| %s | %s | %s | %s | %s | %s | %s | %s |" % (
+                kn, fmt(v.get("wait")), fmt(v.get("inst_wait")), fmt(v.get("valu")), fmt(v.get("l2_hit")),
+                fmt(v.get("l1_miss")), fmt(v.get("vmem_per_wave"), 0), fmt(v.get("lds_per_wave"), 0)))
     open(a.out, "w").write("\n".join(lines) + "\n")
     if a.json:
         import json
@@ -68,6 +126,12 @@ def main():
         out = {"workload": a.workload, "source": os.path.basename(a.out),
                "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and --pmc WRITE_SIZE in separate passes; "
                          "bytes per launch averaged over all launches of the kernel", "kernels": {}}
+        if "k_trace" in pmc:
+            v = pmc["k_trace"]
+            out["limiter"] = ("memory latency: waves wait on dependencies %.0f%% of their cycles (SQ_WAIT_ANY / "
+                              "SQ_WAVE_CYCLES), VALU busy %.0f%%, L2 hit %.0f%%; HBM-side traffic well below peak"
+                              % (100 * v.get("wait", 0), 100 * v.get("valu", 0), 100 * v.get("l2_hit", 0)))
+            out["pmc"] = {k: pmc[k] for k in pmc if k in ("k_trace", "k_trace_packet", "k_shade")}
         for kn, v in traffic.items():
             f = v.get("FETCH_SIZE", (1, 0.0, 0))
             w = v.get("WRITE_SIZE", (1, 0.0, 0))
