@@ -101,6 +101,28 @@ def cpu_baseline(args, cfg, xml_defines, hair_src, env_rgb, nodes, idx):
                       % (W, H, args.cpu_spp, paths, dt)}
 
 
+def timed_steps(step, steps, world, dist_mod, sync, device, after_step=None):
+    """Time exactly `steps` calls of step(), bracketed by a barrier + device sync on both
+    sides; returns the MAX over ranks of the elapsed seconds (the driver's contract).
+    Covered on the CPU by tests/test_distributed.py (gloo, world size 2)."""
+    if world > 1:
+        dist_mod.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+        if after_step is not None:
+            after_step()
+    sync()
+    if world > 1:
+        dist_mod.barrier()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=device)
+    if world > 1:
+        dist_mod.all_reduce(t, op=dist_mod.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
@@ -149,30 +171,20 @@ def main():
                  node_slots=c.node_slots, prim_slots=c.prim_slots,
                  p_rays=c.packet_rays, p_nodes=c.packet_nodes, p_prims=c.packet_prims, p_exact=c.packet_exact,
                  p_node_slots=c.packet_node_slots, p_prim_slots=c.packet_prim_slots, p_fallbacks=c.packet_fallbacks)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ms_trace = ms_packet = 0.0
-    launches = p_launches = 0
-    ms_kernels = {}
-    for _ in range(args.steps):
-        step(1)  # HIP events around every kernel (on the library's stream), no counters
-        s = r.stats()
-        ms_trace += s.ms_trace
-        launches += s.trace_launches
-        ms_packet += s.ms_trace_packet
-        p_launches += s.packet_launches
+    acc = {"ms_trace": 0.0, "ms_packet": 0.0, "launches": 0, "p_launches": 0, "kernels": {}}
+
+    def collect():
+        s = r.stats()  # HIP events around every kernel (on the library's stream), no counters
+        acc["ms_trace"] += s.ms_trace
+        acc["launches"] += s.trace_launches
+        acc["ms_packet"] += s.ms_trace_packet
+        acc["p_launches"] += s.packet_launches
         for k in ("camera", "trace_packet", "trace", "primary", "shade", "post", "tail", "gather"):
-            ms_kernels[k] = ms_kernels.get(k, 0.0) + getattr(s, "ms_" + k)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device="cuda:%d" % local)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
+            acc["kernels"][k] = acc["kernels"].get(k, 0.0) + getattr(s, "ms_" + k)
+
+    dt = timed_steps(lambda: step(1), args.steps, world, dist, torch.cuda.synchronize, "cuda:%d" % local, collect)
+    ms_trace, ms_packet, launches, p_launches = acc["ms_trace"], acc["ms_packet"], acc["launches"], acc["p_launches"]
+    ms_kernels = acc["kernels"]
     tot = {k: v * args.steps for k, v in frame.items()}
 
     workload = "%s %dx%d @ %d spp, maxDepth %d, %d strands / %d segments" % (

@@ -87,3 +87,31 @@ def test_block_order_is_a_balanced_permutation(nbx, nby):
         owner = np.array(distributed.block_owner(nbx, nby, 8)).reshape(nby, nbx)
         for r in range(8):
             assert len(np.unique(np.nonzero(owner == r)[1])) >= 8  # spans at least 8 columns
+
+
+def _bench_worker(rank, world, port, out_dir):
+    """bench.py's own timing helper over gloo: both ranks must report the slower rank's time."""
+    import sys
+    import time
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = []
+        dt = bench.timed_steps(lambda: time.sleep(0.02 * (rank + 1)), 3, world, dist, lambda: None, "cpu",
+                               after_step=lambda: calls.append(1))
+        np.save(os.path.join(out_dir, "dt%d.npy" % rank), np.array([dt, len(calls)]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_timed_steps_takes_max_over_ranks(tmp_path):
+    world = 2
+    mp.spawn(_bench_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    d0, d1 = np.load(tmp_path / "dt0.npy"), np.load(tmp_path / "dt1.npy")
+    assert d0[1] == d1[1] == 3  # exactly K timed steps, each followed by the stats callback
+    assert d0[0] == d1[0]       # every rank holds the MAX over ranks
+    assert d0[0] >= 3 * 0.04    # ... which is the slower rank's (rank 1 sleeps 40 ms per step)
