@@ -8,9 +8,11 @@
  *   - consecutive vertices whose tangent changes by less than angleThreshold
  *     degrees are merged into one segment (:615-616, :698-705);
  *   - coincident vertices are dropped as degenerate (:706-708);
- *   - 'reduction' stochastically drops strands and enlarges the radius
- *     (:618-629) -- supported only for reduction == 0 here (the reference's
- *     culling draws from an unseeded Random, so it is not reproducible);
+ *   - 'reduction' drops each strand with probability `reduction` and scales the
+ *     radius by 1 / (1 - reduction) (:618-629, :671-673, :768-770).  The draws
+ *     come from `new Random()`, which on Linux seeds SFMT19937 with the default
+ *     5489 (random.cpp:473-489, random.h:113) -- deterministic, so the same
+ *     strands are dropped as in the reference: Sfmt19937 below restates it;
  *   - toWorld is applied to vertices and scales the radius (:632-633).
  */
 #include <cmath>
@@ -83,6 +85,91 @@ struct Builder {
     }
 };
 
+/* SFMT19937 as Random (src/libcore/random.cpp): init_gen_rand (:397-406, the
+   64-bit LCG fill + period certification), gen_rand_all over 128-bit words
+   (:330-360; the SSE recursion of :170-186 computes the same words as the
+   portable one), gen_rand64 (:296-304) and the single-precision nextFloat
+   (:630-640: the low 32 bits of a 64-bit output, >> 9 into [1, 2), minus 1). */
+class Sfmt19937 {
+    static const int kN = 19937 / 128 + 1, kN32 = kN * 4, kN64 = kN * 2, kPos1 = 122;
+    static const int kSL1 = 18, kSL2 = 1, kSR1 = 11, kSR2 = 1;
+    uint32_t st[kN32];
+    int idx;
+
+    /* 128-bit word k of the state (little-endian: st[4k] is the low 32 bits) */
+    static void shl8(const uint32_t *in, uint32_t *out, int bytes) {
+        uint64_t lo = (uint64_t) in[0] | ((uint64_t) in[1] << 32), hi = (uint64_t) in[2] | ((uint64_t) in[3] << 32);
+        uint64_t oh = (hi << (bytes * 8)) | (lo >> (64 - bytes * 8)), ol = lo << (bytes * 8);
+        out[0] = (uint32_t) ol, out[1] = (uint32_t) (ol >> 32), out[2] = (uint32_t) oh, out[3] = (uint32_t) (oh >> 32);
+    }
+    static void shr8(const uint32_t *in, uint32_t *out, int bytes) {
+        uint64_t lo = (uint64_t) in[0] | ((uint64_t) in[1] << 32), hi = (uint64_t) in[2] | ((uint64_t) in[3] << 32);
+        uint64_t ol = (lo >> (bytes * 8)) | (hi << (64 - bytes * 8)), oh = hi >> (bytes * 8);
+        out[0] = (uint32_t) ol, out[1] = (uint32_t) (ol >> 32), out[2] = (uint32_t) oh, out[3] = (uint32_t) (oh >> 32);
+    }
+    void recursion(int r, int a, int b, int c, int d) {
+        static const uint32_t msk[4] = {0xdfffffefu, 0xddfecb7fu, 0xbffaffffu, 0xbffffff6u};
+        uint32_t x[4], y[4], out[4];
+        shl8(&st[4 * a], x, kSL2);
+        shr8(&st[4 * c], y, kSR2);
+        for (int i = 0; i < 4; ++i)
+            out[i] = st[4 * a + i] ^ x[i] ^ ((st[4 * b + i] >> kSR1) & msk[i]) ^ y[i] ^ (st[4 * d + i] << kSL1);
+        std::memcpy(&st[4 * r], out, sizeof(out));
+    }
+    void genAll() {
+        int r1 = kN - 2, r2 = kN - 1, i = 0;
+        for (; i < kN - kPos1; ++i) {
+            recursion(i, i, i + kPos1, r1, r2);
+            r1 = r2;
+            r2 = i;
+        }
+        for (; i < kN; ++i) {
+            recursion(i, i, i + kPos1 - kN, r1, r2);
+            r1 = r2;
+            r2 = i;
+        }
+    }
+
+public:
+    explicit Sfmt19937(uint64_t seed = 5489ull) {
+        uint64_t v = seed;
+        for (int i = 0; i < kN64; ++i) {
+            if (i) v = 6364136223846793005ull * (v ^ (v >> 62)) + (uint64_t) i;
+            st[2 * i] = (uint32_t) v;
+            st[2 * i + 1] = (uint32_t) (v >> 32);
+        }
+        idx = kN32;
+        /* period certification (parity 0x1, 0, 0, 0x13c9e684) */
+        static const uint32_t parity[4] = {0x00000001u, 0u, 0u, 0x13c9e684u};
+        uint32_t inner = 0;
+        for (int i = 0; i < 4; ++i) inner ^= st[i] & parity[i];
+        for (int i = 16; i > 0; i >>= 1) inner ^= inner >> i;
+        if (!(inner & 1u)) {
+            for (int i = 0; i < 4; ++i)
+                for (int j = 0; j < 32; ++j)
+                    if (((1u << j) & parity[i]) != 0) {
+                        st[i] ^= 1u << j;
+                        return;
+                    }
+        }
+    }
+    uint64_t nextULong() {
+        if (idx >= kN32) {
+            genAll();
+            idx = 0;
+        }
+        const uint64_t r = (uint64_t) st[idx] | ((uint64_t) st[idx + 1] << 32);
+        idx += 2;
+        return r;
+    }
+    float nextFloat() {
+        uint32_t u = ((uint32_t) (nextULong() & 0xFFFFFFFFull) >> 9) | 0x3f800000u;
+        float f;
+        std::memcpy(&f, &u, 4);
+        return f - 1.0f;
+    }
+};
+
 inline P3 xform(const float *M, const P3 &p) {
     /* transform.h:108-125 (projective point transform) */
     float x = M[0] * p.x + M[1] * p.y + M[2] * p.z + M[3];
@@ -100,8 +187,9 @@ HairData loadHair(const std::string &path, float radius, float angleThresholdDeg
                   const float *toWorld) {
     if (reduction < 0 || reduction >= 1)
         throw std::runtime_error("The 'reduction' parameter must have a value in [0, 1)!");
-    if (reduction > 0)
-        throw std::runtime_error("hair 'reduction' > 0 is not supported (unseeded culling in the reference)");
+    if (reduction > 0) radius *= 1.0f / (1 - reduction); /* hair.cpp:622-626 */
+    Sfmt19937 random;                                     /* hair.cpp:628: new Random() */
+    bool ignore = false;
     bool identity = true;
     if (toWorld)
         for (int i = 0; i < 16; ++i) identity &= toWorld[i] == ((i % 5 == 0) ? 1.0f : 0.0f);
@@ -142,13 +230,19 @@ HairData loadHair(const std::string &path, float radius, float angleThresholdDeg
                 p.y = rd();
                 p.z = rd();
                 newFiber = true;
+                if (reduction > 0) ignore = random.nextFloat() < reduction; /* hair.cpp:671-673 */
             } else {
                 p.x = value;
                 p.y = rd();
                 p.z = rd();
             }
             if (!identity) p = xform(toWorld, p);
-            b.add(p, newFiber);
+            if (ignore) { /* hair.cpp:683-685 */
+                ++b.nSkipped;
+                newFiber = false;
+            } else {
+                b.add(p, newFiber);
+            }
         }
     } else {
         std::string text(buf.begin(), buf.end());
@@ -166,9 +260,15 @@ HairData loadHair(const std::string &path, float radius, float angleThresholdDeg
             iss >> p.x >> p.y >> p.z;
             if (!iss.fail()) {
                 if (!identity) p = xform(toWorld, p);
-                b.add(p, newFiber);
+                if (ignore) { /* hair.cpp:734-736 */
+                    ++b.nSkipped;
+                    newFiber = false;
+                } else {
+                    b.add(p, newFiber);
+                }
             } else {
                 newFiber = true;
+                if (reduction > 0) ignore = random.nextFloat() < reduction; /* hair.cpp:768-770 */
             }
         }
     }

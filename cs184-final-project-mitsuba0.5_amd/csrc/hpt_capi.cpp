@@ -370,6 +370,17 @@ int hpt_set_hair_file(hpt_context *c, const char *path, float radius, float angl
     return HPT_OK;
 }
 
+int hpt_set_hair_reduction(hpt_context *c, float reduction) {
+    if (!c) return HPT_EINVAL;
+    if (!c->hairFromFile || c->desc.shapes.empty())
+        return setErr(c, HPT_ESTATE, "hpt_set_hair_reduction: no hair file shape (hpt_set_hair_file first)");
+    if (!(reduction >= 0 && reduction < 1))
+        return setErr(c, HPT_EINVAL, "The 'reduction' parameter must have a value in [0, 1)!");
+    c->desc.shapes.back().reduction = reduction;
+    c->prepared = false;
+    return HPT_OK;
+}
+
 int hpt_set_hair_vertices(hpt_context *c, const float *xyz, const uint8_t *starts, uint64_t n, float radius) {
     if (!c || (!xyz && n)) return HPT_EINVAL;
     c->hairFromFile = false;

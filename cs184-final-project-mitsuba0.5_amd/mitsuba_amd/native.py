@@ -77,6 +77,7 @@ SIGNATURES = {
     "hpt_set_sampler_scramble": (C.c_int, [C.c_void_p, C.c_uint64]),
     "hpt_set_integrator": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
     "hpt_set_hair_file": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_float, _f]),
+    "hpt_set_hair_reduction": (C.c_int, [C.c_void_p, C.c_float]),
     "hpt_set_hair_vertices": (C.c_int, [C.c_void_p, _f, _u8, C.c_uint64, C.c_float]),
     "hpt_set_bsdf_marschner": (C.c_int, [C.c_void_p, C.c_float, C.c_float, C.c_int, C.c_float, _f, _f]),
     "hpt_set_bsdf_kajiyakay": (C.c_int, [C.c_void_p, _f, _f, C.c_float]),
@@ -189,8 +190,10 @@ class Renderer:
     def set_integrator(self, max_depth, rr_depth=5, strict_normals=True, hide_emitters=False):
         self._check(self.lib.hpt_set_integrator(self.h, max_depth, rr_depth, int(strict_normals), int(hide_emitters)))
 
-    def set_hair_file(self, path, radius, angle_threshold=1.0):
+    def set_hair_file(self, path, radius, angle_threshold=1.0, reduction=0.0):
         self._check(self.lib.hpt_set_hair_file(self.h, path.encode(), radius, angle_threshold, None))
+        if reduction:
+            self._check(self.lib.hpt_set_hair_reduction(self.h, reduction))
 
     def set_hair_vertices(self, xyz, starts, radius):
         xyz = _f32(xyz).reshape(-1, 3)

@@ -68,6 +68,11 @@ int hpt_set_integrator(hpt_context *ctx, int max_depth, int rr_depth, int strict
 /* HairShape(Properties) (src/shapes/hair.cpp:609-785); to_world may be NULL */
 int hpt_set_hair_file(hpt_context *ctx, const char *path, float radius, float angle_threshold_deg,
                       const float *to_world);
+/* HairShape "reduction" property (hair.cpp:618-629, 671-673, 768-770) of the hair file set by
+   hpt_set_hair_file: each strand is dropped with this probability, drawn from SFMT19937 seeded
+   with 5489 like the reference's `new Random()` on Linux, and the radius grows by
+   1 / (1 - reduction).  Must be in [0, 1). */
+int hpt_set_hair_reduction(hpt_context *ctx, float reduction);
 /* HairShape(Stream) equivalent (hair.cpp:787-801): vertices already merged;
    starts_fiber has n_vertices entries (a trailing terminator is implied). */
 int hpt_set_hair_vertices(hpt_context *ctx, const float *xyz, const uint8_t *starts_fiber, uint64_t n_vertices,

@@ -2553,9 +2553,97 @@ int orc_set_camera(orc_scene *s, const float to_world[16], float fov_x_deg, int 
     return 0;
 }
 
+/* SFMT19937 (src/libcore/random.cpp) as the hair loader's `new Random()` uses it:
+   Random() -> seed() -> init_gen_rand(5489) (:473-489, random.h:113), the state
+   viewed as 64-bit words (psfmt64), gen_rand_all with the portable do_recursion
+   (:170-186, :330-360), gen_rand64 (:296-304), single-precision nextFloat (:630-640). */
+struct OracleSfmt {
+    enum { N = 19937 / 128 + 1, N32 = N * 4, N64 = N * 2, POS1 = 122, SL1 = 18, SL2 = 1, SR1 = 11, SR2 = 1 };
+    union {
+        uint64_t u64[N][2];
+        uint32_t u32[N][4];
+        uint64_t psfmt64[N64];
+        uint32_t psfmt32[N32];
+    };
+    int idx;
+    static void rshift128(uint64_t out[2], const uint64_t in[2], int shift) {
+        out[0] = (in[0] >> (shift * 8)) | (in[1] << (64 - shift * 8));
+        out[1] = in[1] >> (shift * 8);
+    }
+    static void lshift128(uint64_t out[2], const uint64_t in[2], int shift) {
+        out[1] = (in[1] << (shift * 8)) | (in[0] >> (64 - shift * 8));
+        out[0] = in[0] << (shift * 8);
+    }
+    void doRecursion(int r, int a, int b, int c, int d) {
+        static const uint32_t MSK[4] = {0xdfffffefU, 0xddfecb7fU, 0xbffaffffU, 0xbffffff6U};
+        uint64_t x[2], y[2];
+        lshift128(x, u64[a], SL2);
+        rshift128(y, u64[c], SR2);
+        uint32_t xs[4] = {(uint32_t) x[0], (uint32_t) (x[0] >> 32), (uint32_t) x[1], (uint32_t) (x[1] >> 32)};
+        uint32_t ys[4] = {(uint32_t) y[0], (uint32_t) (y[0] >> 32), (uint32_t) y[1], (uint32_t) (y[1] >> 32)};
+        uint32_t out[4];
+        for (int k = 0; k < 4; ++k)
+            out[k] = u32[a][k] ^ xs[k] ^ ((u32[b][k] >> SR1) & MSK[k]) ^ ys[k] ^ (u32[d][k] << SL1);
+        for (int k = 0; k < 4; ++k) u32[r][k] = out[k];
+    }
+    explicit OracleSfmt(uint64_t seed) {
+        psfmt64[0] = seed;
+        for (int i = 1; i < N64; ++i)
+            psfmt64[i] = 6364136223846793005ULL * (psfmt64[i - 1] ^ (psfmt64[i - 1] >> 62)) + (uint64_t) i;
+        idx = N32;
+        const uint32_t parity[4] = {0x00000001U, 0x00000000U, 0x00000000U, 0x13c9e684U};
+        int inner = 0;
+        for (int i = 0; i < 4; ++i) inner ^= psfmt32[i] & parity[i];
+        for (int i = 16; i > 0; i >>= 1) inner ^= inner >> i;
+        if ((inner & 1) == 1) return;
+        for (int i = 0; i < 4; ++i) {
+            uint32_t work = 1;
+            for (int j = 0; j < 32; ++j) {
+                if ((work & parity[i]) != 0) {
+                    psfmt32[i] ^= work;
+                    return;
+                }
+                work = work << 1;
+            }
+        }
+    }
+    uint64_t nextULong() {
+        if (idx >= N32) {
+            int i, r1 = N - 2, r2 = N - 1;
+            for (i = 0; i < N - POS1; ++i) {
+                doRecursion(i, i, i + POS1, r1, r2);
+                r1 = r2;
+                r2 = i;
+            }
+            for (; i < N; ++i) {
+                doRecursion(i, i, i + POS1 - N, r1, r2);
+                r1 = r2;
+                r2 = i;
+            }
+            idx = 0;
+        }
+        uint64_t r = psfmt64[idx / 2];
+        idx += 2;
+        return r;
+    }
+    float nextFloat() {
+        union {
+            uint32_t u;
+            float f;
+        } x;
+        x.u = ((nextULong() & 0xFFFFFFFF) >> 9) | 0x3f800000UL;
+        return x.f - 1.0f;
+    }
+};
+
 /* hair.cpp:609-785 */
 int orc_load_hair(orc_scene *s, const char *path, float radius, float angle_threshold_deg,
                   const float *to_world) {
+    return orc_load_hair_reduced(s, path, radius, angle_threshold_deg, 0.0f, to_world);
+}
+
+int orc_load_hair_reduced(orc_scene *s, const char *path, float radius, float angle_threshold_deg,
+                          float reduction, const float *to_world) {
     float angleThreshold = degToRad(angle_threshold_deg);
     float dpThresh = std::cos(angleThreshold);
     float M[16];
@@ -2564,6 +2652,15 @@ int orc_load_hair(orc_scene *s, const char *path, float radius, float angle_thre
         std::memcpy(M, to_world, sizeof(M));
         for (int i = 0; i < 16; ++i) ident &= M[i] == ((i % 5 == 0) ? 1.0f : 0.0f);
     }
+    if (reduction < 0 || reduction >= 1) {
+        s->err = "The 'reduction' parameter must have a value in [0, 1)!";
+        return -1;
+    } else if (reduction > 0) {
+        float correction = 1.0f / (1 - reduction); /* hair.cpp:622-626 */
+        radius *= correction;
+    }
+    OracleSfmt random(5489ULL);
+    bool ignore = false;
     if (!ident) radius *= xformVector(M, V3(0, 0, 1)).length();
     std::ifstream f(path, std::ios::binary);
     if (!f) { s->err = std::string("cannot open ") + path; return -1; }
@@ -2620,11 +2717,15 @@ int orc_load_hair(orc_scene *s, const char *path, float radius, float angle_thre
             if (std::isinf(value)) {
                 if (!rd(p.x) || !rd(p.y) || !rd(p.z)) { s->err = "truncated hair file"; return -1; }
                 newFiber = true;
+                if (reduction > 0) ignore = random.nextFloat() < reduction;
             } else {
                 p.x = value;
                 if (!rd(p.y) || !rd(p.z)) { s->err = "truncated hair file"; return -1; }
             }
-            addPoint(p, newFiber);
+            if (ignore)
+                newFiber = false; /* ++nSkipped */
+            else
+                addPoint(p, newFiber);
         }
     } else {
         std::string text(buf.begin(), buf.end());
@@ -2639,10 +2740,15 @@ int orc_load_hair(orc_scene *s, const char *path, float radius, float angle_thre
             }
             std::istringstream iss(line);
             iss >> p.x >> p.y >> p.z;
-            if (!iss.fail())
-                addPoint(p, newFiber);
-            else
+            if (!iss.fail()) {
+                if (ignore)
+                    newFiber = false; /* ++nSkipped */
+                else
+                    addPoint(p, newFiber);
+            } else {
                 newFiber = true;
+                if (reduction > 0) ignore = random.nextFloat() < reduction;
+            }
         }
     }
     starts.push_back(1);

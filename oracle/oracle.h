@@ -51,6 +51,10 @@ int orc_get_camera(orc_scene *s, float sample_to_camera[16], float dx[3], float 
    BSDF of the most recently added shape. */
 int orc_load_hair(orc_scene *s, const char *path, float radius, float angle_threshold_deg,
                   const float *to_world);
+/* same with HairShape's "reduction" (hair.cpp:618-629, 671-673, 768-770): strands dropped by
+   SFMT19937 draws seeded with 5489 (Random() on Linux, random.cpp:473-489) */
+int orc_load_hair_reduced(orc_scene *s, const char *path, float radius, float angle_threshold_deg,
+                          float reduction, const float *to_world);
 int64_t orc_hair_vertex_count(orc_scene *s);
 int orc_hair_get(orc_scene *s, float *xyz, uint8_t *starts_fiber /* n+1 */);
 /* kd-tree produced by the product's host builder (8-byte nodes: see DESIGN.md),

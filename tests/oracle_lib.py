@@ -32,6 +32,7 @@ _SIG = {
     "orc_set_sobol": (C.c_int, [C.c_void_p, _u32, _u64, C.c_int, _u64, C.c_int]),
     "orc_set_camera": (C.c_int, [C.c_void_p, _f, C.c_float, C.c_int, C.c_int, C.c_float, C.c_float]),
     "orc_load_hair": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_float, _f]),
+    "orc_load_hair_reduced": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_float, C.c_float, _f]),
     "orc_hair_vertex_count": (C.c_int64, [C.c_void_p]),
     "orc_hair_get": (C.c_int, [C.c_void_p, _f, _u8]),
     "orc_set_kdtree": (C.c_int, [C.c_void_p, _u32, C.c_int64, _u32, C.c_int64]),

@@ -386,3 +386,34 @@ def test_env_mip_pyramid(tmp_path, resolution):
         cur = _resample_axis(cur, ww, 1, True) if cur.shape[1] != ww else cur
         cur = _resample_axis(cur, hh, 0, False) if cur.shape[0] != hh else cur
         np.testing.assert_allclose(levels[k], cur, rtol=2e-3, atol=1e-5 * float(env.max()))
+
+
+@pytest.mark.parametrize("binary", [True, False])
+def test_hair_reduction_matches_oracle(tmp_path, binary):
+    """HairShape 'reduction' (hair.cpp:618-629, 671-673, 768-770): strands dropped by the draws of
+    `new Random()` (SFMT19937 seeded with 5489 on Linux, random.cpp:473-489), radius scaled by
+    1 / (1 - reduction).  Product loader == oracle loader bitwise, hair AABB included."""
+    strands = synth_hair.furball(400)
+    path = str(tmp_path / ("h.bin" if binary else "h.txt"))
+    (synth_hair.write_binary_hair if binary else synth_hair.write_ascii_hair)(path, strands)
+    red = 0.37
+    r = native.Renderer(device=native.HOST_ONLY)
+    r.set_hair_file(path, 0.01, 1.0, reduction=red)
+    r.set_camera(np.eye(4, dtype=np.float32), 40, 8, 8)
+    r.set_kajiyakay((0.2, 0.2, 0.2))
+    r.set_sunsky((0, 1, 0))
+    r.prepare()
+    o = oracle_lib.Oracle()
+    o.check(o.lib.orc_load_hair_reduced(o.s, path.encode(), 0.01, 1.0, red, None))
+    pxyz, pst = r.hair()
+    oxyz, ost = o.hair()
+    np.testing.assert_array_equal(pxyz, oxyz)
+    np.testing.assert_array_equal(pst, ost)
+    kept = int(pst[:-1].sum())
+    assert 0.5 * len(strands) < kept < 0.75 * len(strands)  # ~63 % of the strands survive
+    info = r.info()
+    mn, mx = o.aabb()
+    np.testing.assert_array_equal(np.array(info.aabb_min), mn)
+    np.testing.assert_array_equal(np.array(info.aabb_max), mx)
+    with pytest.raises(native.HairPTError, match="reduction"):
+        r.set_hair_file(path, 0.01, 1.0, reduction=1.0)

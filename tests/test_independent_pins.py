@@ -19,7 +19,7 @@ import numpy as np
 import pytest
 
 import scene_util
-from mitsuba_amd import native
+from mitsuba_amd import native, synth_hair
 
 RES = 64           # Azimuthal::AzimuthalResolution (marschner_diffuse.cpp:66)
 NGAUSS = 2048      # NumGaussianSamples (:775)
@@ -306,3 +306,80 @@ def test_sunsky_bitmap_matches_float64_restatement(case):
     got = (p - sky)[sun_px].sum(0)
     print("  sun energy product", got, "float64", energy, "rel", got / energy - 1)
     np.testing.assert_allclose(got, energy, rtol=5e-5)
+
+
+# ---------------------------------------------------------------------------
+# SFMT19937 (src/libcore/random.cpp), written here over Python 128-bit integers
+# (one int per state word) -- independent of the product's and the oracle's
+# 32/64-bit formulations -- to pin which strands HairShape's 'reduction' drops.
+# ---------------------------------------------------------------------------
+_M128 = (1 << 128) - 1
+
+
+def _sfmt_floats(count, seed=5489):
+    n = 19937 // 128 + 1
+    n64 = 2 * n
+    lo = [0] * n64
+    lo[0] = seed
+    for i in range(1, n64):  # init_gen_rand (random.cpp:397-406)
+        lo[i] = (6364136223846793005 * (lo[i - 1] ^ (lo[i - 1] >> 62)) + i) & ((1 << 64) - 1)
+    w = [lo[2 * k] | (lo[2 * k + 1] << 64) for k in range(n)]
+    parity = 0x13c9e684 << 96 | 0x00000001
+    if bin(w[0] & parity).count("1") % 2 == 0:  # period certification: flip the lowest parity bit
+        w[0] ^= 1
+    msk = 0xbffffff6 << 96 | 0xbffaffff << 64 | 0xddfecb7f << 32 | 0xdfffffef
+
+    def lanes_shr(x, s):  # per-32-bit-lane shift right
+        return sum((((x >> (32 * k)) & 0xffffffff) >> s) << (32 * k) for k in range(4))
+
+    def lanes_shl(x, s):
+        return sum(((((x >> (32 * k)) & 0xffffffff) << s) & 0xffffffff) << (32 * k) for k in range(4))
+
+    out = []
+    while len(out) < count:
+        r1, r2 = n - 2, n - 1
+        for i in range(n):  # gen_rand_all
+            b = w[(i + 122) % n]
+            w[i] = (w[i] ^ ((w[i] << 8) & _M128) ^ (lanes_shr(b, 11) & msk) ^ (w[r1] >> 8) ^ lanes_shl(w[r2], 18))
+            r1, r2 = r2, i
+        for k in range(n64):  # gen_rand64, then the single-precision nextFloat
+            u64 = (w[k // 2] >> (64 * (k % 2))) & ((1 << 64) - 1)
+            bits = ((u64 & 0xffffffff) >> 9) | 0x3f800000
+            out.append(np.float32(np.array([bits], np.uint32).view(np.float32)[0] - np.float32(1.0)))
+    return np.array(out[:count], np.float32)
+
+
+def test_sfmt_independent_pin_of_hair_reduction(tmp_path):
+    """The strands the product keeps are exactly those whose SFMT draw is >= reduction (one draw
+    per BINARY_HAIR strand marker, hair.cpp:671-673), the radius scaled by 1 / (1 - reduction)."""
+    rng = np.random.default_rng(5)
+    k = 1500
+    # three non-collinear distinct vertices per strand: nothing merges or degenerates
+    base = rng.uniform(-5, 5, (k, 1, 3)).astype(np.float32)
+    strands = [b + np.array([[0, 0, 0], [0.3, 0.1, 0], [0.35, 0.5, 0.2]], np.float32) for b in base]
+    path = str(tmp_path / "r.bin")
+    synth_hair.write_binary_hair(path, strands)
+    red = 0.25
+    r = native.Renderer(device=native.HOST_ONLY)
+    r.set_hair_file(path, 0.01, 1.0, reduction=red)
+    r.set_camera(np.eye(4, dtype=np.float32), 40, 8, 8)
+    r.set_kajiyakay((0.2, 0.2, 0.2))
+    r.set_sunsky((0, 1, 0))
+    r.prepare()
+    pxyz, pst = r.hair()
+    u = _sfmt_floats(k)
+    keep = u >= np.float32(red)
+    want = np.concatenate([s for s, kp in zip(strands, keep) if kp])
+    np.testing.assert_array_equal(pxyz, want)
+    assert int(pst[:-1].sum()) == int(keep.sum())
+    # the radius: the same strands loaded without reduction at radius / (1 - reduction) give the same AABB
+    kept_path = str(tmp_path / "k.bin")
+    synth_hair.write_binary_hair(kept_path, [s for s, kp in zip(strands, keep) if kp])
+    r2 = native.Renderer(device=native.HOST_ONLY)
+    r2.set_hair_file(kept_path, np.float32(0.01) * (np.float32(1) / (np.float32(1) - np.float32(red))), 1.0)
+    r2.set_camera(np.eye(4, dtype=np.float32), 40, 8, 8)
+    r2.set_kajiyakay((0.2, 0.2, 0.2))
+    r2.set_sunsky((0, 1, 0))
+    r2.prepare()
+    assert list(r.info().aabb_min) == list(r2.info().aabb_min)
+    assert list(r.info().aabb_max) == list(r2.info().aabb_max)
