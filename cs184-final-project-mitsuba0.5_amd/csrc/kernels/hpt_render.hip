@@ -26,6 +26,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -2652,6 +2653,13 @@ static unsigned persistentBlocks(const void *kernel, uint64_t items, int block =
         }
         resident = it->second;
     }
+    /* HPT_PERSIST_FRAC=k: persistent grids take 1/k of the resident slots (experiments with
+       several render calls sharing the device) */
+    static const int frac = [] {
+        const char *v = std::getenv("HPT_PERSIST_FRAC");
+        return v ? std::max(1, std::atoi(v)) : 1;
+    }();
+    resident = std::max(1, resident / frac);
     const uint64_t need = (items + block - 1) / block;
     return (unsigned) std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t) resident));
 }
