@@ -26,9 +26,11 @@ struct Vec3f {
 
 /* SAH kd-tree build parameters.  Defaults are HairKDTree's (hair.cpp:130-136,
  * gkdtree.h:731-746) except stopPrims: the reference splits down to single
- * segments; on gfx950 a leaf of up to 4 segments is cheaper to test (fp32
+ * segments; on gfx950 a leaf of up to 6 segments is cheaper to test (fp32
  * pre-test over contiguous records) than the extra dependent node fetches
- * (measured: +19% Mpaths/s on the furball).  The scene-level names of scene.cpp:44-78 (kdIntersectionCost,
+ * (measured on the furball headline: stopPrims 1 -> 4 +19 % Mpaths/s in round 1;
+ * with k_trace at 7 waves/SIMD, 2: 368, 3: 398, 4: 417, 5: 424, 6: 428-432,
+ * 8: 426, 10: 414, 12: 400, 16: 369 Mpaths/s).  The scene-level names of scene.cpp:44-78 (kdIntersectionCost,
  * kdTraversalCost, kdEmptySpaceBonus, kdStopPrims, kdMaxDepth, kdClip,
  * kdMaxBadRefines) may be set on the hair shape.  The tree never changes a
  * result (traversal finds the exact closest hit), only the speed. */
@@ -36,7 +38,7 @@ struct KDBuildParams {
     float traversalCost = 10.0f;
     float queryCost = 15.0f;
     float emptySpaceBonus = 0.9f;
-    int stopPrims = 4;             /* reference HairKDTree: 1 */
+    int stopPrims = 6;             /* reference HairKDTree: 1 */
     int maxBadRefines = 3;
     int maxDepth = 0;              /* 0 = automatic: min(8 + 1.3 log2 N, 48) */
     int bins = 128;                /* min-max bins */

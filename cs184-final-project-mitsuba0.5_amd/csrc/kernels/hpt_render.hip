@@ -338,19 +338,37 @@ HD bool waveLeader() { return __lane_id() == (uint32_t) (__ffsll((unsigned long 
      row STACK+0  rcp.x, rcp.y       read once per round
      row STACK+1  rcp.z, key         key: what the IO's finish() needs (path id / ray index)
      row STACK+2  mint, maxt         mint read by the exact tests, maxt at a kd-restart
+   With HPT_RCP_LDS=0 the reciprocal direction is recomputed at the start of
+   every round instead (1.0f / d, the same IEEE division beginRay does) and the
+   rows shrink to (key, -), (mint, maxt): 80 B of LDS per lane with the stack.
    Row k of lane i is stk[k * stride]. */
+#ifndef HPT_RCP_LDS
+#define HPT_RCP_LDS 1
+#endif
+#if HPT_RCP_LDS
 #define HPT_RAY_ROWS 3
+#define HPT_ROW_KEY 1 /* .y */
+#define HPT_ROW_MM 2
+#else
+#define HPT_RAY_ROWS 2
+#define HPT_ROW_KEY 0 /* .y */
+#define HPT_ROW_MM 1
+#endif
 #define HPT_CNT_RESTART (1u << 20)
 template <int STACK>
 HD void stashRay(uint2 *stk, int stride, TraceRay &r, uint32_t key) {
+#if HPT_RCP_LDS
     stk[STACK * stride] = make_uint2(__float_as_uint(r.rcp.x), __float_as_uint(r.rcp.y));
     stk[(STACK + 1) * stride] = make_uint2(__float_as_uint(r.rcp.z), key);
-    stk[(STACK + 2) * stride] = make_uint2(__float_as_uint(r.mint), __float_as_uint(r.maxt));
+#else
+    stk[STACK * stride] = make_uint2(0u, key);
+#endif
+    stk[(STACK + HPT_ROW_MM) * stride] = make_uint2(__float_as_uint(r.mint), __float_as_uint(r.maxt));
     r.cnt = 0u;
     /* the rows must be re-read, not forwarded from these stores (forwarding keeps the values in registers) */
     asm volatile("" ::: "memory");
 }
-template <int STACK> HD uint32_t rayKey(const uint2 *stk, int stride) { return stk[(STACK + 1) * stride].y; }
+template <int STACK> HD uint32_t rayKey(const uint2 *stk, int stride) { return stk[(STACK + HPT_ROW_KEY) * stride].y; }
 /* leaves visited / kd-restarts of the lane's current ray */
 HD uint32_t rayLeaves(const TraceRay &r) { return r.cnt & (HPT_CNT_RESTART - 1u); }
 HD uint32_t rayRestarts(const TraceRay &r) { return r.cnt / HPT_CNT_RESTART; }
@@ -361,8 +379,12 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     const float4 *__restrict__ leafF = reinterpret_cast<const float4 *>(sc.leafF);
     /* the ray as plain values: selecting among struct members by axis would be
        folded into a dynamically addressed load and push the state to scratch */
+#if HPT_RCP_LDS
     const uint2 cr0 = stk[STACK * stride], cr1 = stk[(STACK + 1) * stride];
     const V3 o = r.o, d = r.d, rcp = v3(__uint_as_float(cr0.x), __uint_as_float(cr0.y), __uint_as_float(cr1.x));
+#else
+    const V3 o = r.o, d = r.d, rcp = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+#endif
     /* hard bound so every wave drains even on a malformed tree; the call fails loudly */
     {
         const uint32_t cnt = r.cnt + 1u;
@@ -503,7 +525,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
             if (STATS) ++tc.exact;
             float t;
             uint32_t far;
-            const float mint = __uint_as_float(stk[(STACK + 2) * stride].x);
+            const float mint = __uint_as_float(stk[(STACK + HPT_ROW_MM) * stride].x);
             if (HPT_SEG_TEST(sc.segs, s, o, d, r2, mint, r.tHit, t, far)) {
                 r.found = true;
                 if (r.shadow) return true;
@@ -514,7 +536,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     }
     if (r.found && r.tHit <= r.tmax) return true;
     if (r.sp == 0) {
-        const float maxt = __uint_as_float(stk[(STACK + 2) * stride].y);
+        const float maxt = __uint_as_float(stk[(STACK + HPT_ROW_MM) * stride].y);
         if (!r.lost || r.tmax >= maxt) return true;
         const uint32_t cnt = r.cnt + HPT_CNT_RESTART;
         r.cnt = cnt;
