@@ -2202,7 +2202,15 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
     qpushBlock<HPT_SHADE_BLOCK>(cont, id, traceQ, &counters[HPT_Q_TRACE]);
     qpushBlock<HPT_SHADE_BLOCK>(shadow, id, shadowQ, &counters[HPT_Q_SHADOW]);
 }
-extern "C" __global__ __launch_bounds__(HPT_SHADE_BLOCK) void k_shade(HptScene sc, HptPaths P,
+#ifndef HPT_SHADE_WAVES
+#define HPT_SHADE_WAVES 0 /* 0: natural allocation (100 VGPRs = 5 waves/SIMD) */
+#endif
+#if HPT_SHADE_WAVES > 0
+#define HPT_SHADE_OCCUPANCY __attribute__((amdgpu_waves_per_eu(HPT_SHADE_WAVES)))
+#else
+#define HPT_SHADE_OCCUPANCY
+#endif
+extern "C" __global__ __launch_bounds__(HPT_SHADE_BLOCK) HPT_SHADE_OCCUPANCY void k_shade(HptScene sc, HptPaths P,
                                                            const uint32_t *__restrict__ shadeQ,
                                                            uint32_t *__restrict__ traceQ,
                                                            uint32_t *__restrict__ shadowQ,

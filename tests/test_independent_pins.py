@@ -383,3 +383,264 @@ def test_sfmt_independent_pin_of_hair_reduction(tmp_path):
     r2.prepare()
     assert list(r.info().aabb_min) == list(r2.info().aabb_min)
     assert list(r.info().aabb_max) == list(r2.info().aabb_max)
+
+
+# ---------------------------------------------------------------------------
+# Hair intersection (a5/a6), restated in float64 numpy straight from the
+# reference: HairKDTree::intersect (hair.cpp:485-548), the tangent / miter
+# helpers (:551-596), solveQuadraticDouble (util.cpp:487-525), Mitsuba's
+# normalize = v * (1 / |v|) (vector.h:546-553, 641-643) and the ray's entry
+# clip (aabb.h:308-338, skdtree.cpp:124-132, hair.cpp:200-210), as a brute
+# force over every segment.  Pins the oracle's (and through the GPU parity
+# tests, the GPU's) closest hits, points and any-hit answers.
+# ---------------------------------------------------------------------------
+def _dot(a, b):
+    return (a[..., 0] * b[..., 0] + a[..., 1] * b[..., 1]) + a[..., 2] * b[..., 2]
+
+
+def _normalize(v):
+    with np.errstate(divide="ignore", invalid="ignore"):  # zero vectors only where np.where discards them
+        return v * (1.0 / np.sqrt(_dot(v, v)))[..., None]
+
+
+def _segments(xyz, starts):
+    n = len(xyz)
+    iv = np.nonzero(starts[1:n] == 0)[0]           # segment iv -> iv + 1 exists
+    v = xyz.astype(np.float64)                       # Point3d(m_vertices[i])
+    v1, v2 = v[iv], v[iv + 1]
+    axis = _normalize(v2 - v1)                       # tangentDouble
+    has_prev = starts[iv] == 0                       # prevSegmentExists
+    has_next = starts[iv + 2] == 0                   # nextSegmentExists (starts has n + 1 entries)
+    prev_t = _normalize(v1 - v[np.maximum(iv - 1, 0)])
+    next_t = _normalize(v[np.minimum(iv + 2, n - 1)] - v2)
+    n1 = np.where(has_prev[:, None], _normalize(prev_t + axis), axis)
+    n2 = np.where(has_next[:, None], _normalize(axis + next_t), axis)
+    return iv, v1, v2, axis, n1, n2
+
+
+def _entry_clip(o, d, mint, maxt, lo, hi):
+    """float32 AABB slab clip + adaptive epsilon (Epsilon = 1e-4 in single precision)"""
+    f = np.float32
+    rcp = (f(1) / d).astype(f)
+    near = np.full(len(o), -np.inf, f)
+    far = np.full(len(o), np.inf, f)
+    ok = np.ones(len(o), bool)
+    for i in range(3):
+        par = d[:, i] == 0
+        ok &= ~(par & ((o[:, i] < lo[i]) | (o[:, i] > hi[i])))
+        t1 = ((f(lo[i]) - o[:, i]) * rcp[:, i]).astype(f)
+        t2 = ((f(hi[i]) - o[:, i]) * rcp[:, i]).astype(f)
+        a, b = np.where(t1 > t2, t2, t1), np.where(t1 > t2, t1, t2)
+        near = np.where(par, near, np.where(near < a, a, near))   # std::max(t1, nearT)
+        far = np.where(par, far, np.where(b < far, b, far))       # std::min(t2, farT)
+        ok &= par | (near <= far)
+    eps = f(1e-4)
+    m = np.maximum(np.maximum(np.maximum(np.abs(o[:, 0]), np.abs(o[:, 1])), np.abs(o[:, 2])), eps)
+    rmint = np.where(mint == eps, (mint * m).astype(f), mint)
+    lo_t = np.where(rmint > near, rmint, near)
+    hi_t = np.where(maxt < far, maxt, far)
+    return ok & (hi_t > lo_t), lo_t.astype(f), hi_t.astype(f)
+
+
+def _brute_force(o, d, mint, maxt, radius, segs):
+    """per ray: (hit, float t, iv, float point, set of iv tied at that float t)"""
+    iv, v1, v2, axis, n1, n2 = segs
+    r2 = np.float64(np.float32(radius) * np.float32(radius))       # Float product, then promoted
+    out_t = np.full(len(o), np.inf, np.float32)
+    out_iv = np.full(len(o), -1, np.int64)
+    out_p = np.zeros((len(o), 3), np.float32)
+    ties = [None] * len(o)
+    for k in range(len(o)):
+        ro = o[k].astype(np.float64)
+        rd = d[k].astype(np.float64)
+        rel = ro - v1
+        po = rel - _dot(axis, rel)[:, None] * axis
+        pd = rd - _dot(axis, rd[None, :])[:, None] * axis
+        A = _dot(pd, pd)
+        B = 2 * _dot(po, pd)
+        C = _dot(po, po) - r2
+        disc = B * B - 4.0 * A * C
+        with np.errstate(invalid="ignore", divide="ignore"):
+            sq = np.sqrt(disc)
+            temp = np.where(B < 0, -0.5 * (B - sq), -0.5 * (B + sq))
+            x0, x1 = temp / A, C / temp
+        near, far = np.minimum(x0, x1), np.maximum(x0, x1)
+        real = (disc >= 0) & (A != 0)
+        lo, hi = np.float64(mint[k]), np.float64(maxt[k])
+        cand = real & (near <= hi) & (far >= lo)
+        pn = ro + rd * near[:, None]
+        pf = ro + rd * far[:, None]
+        in_n = (_dot(pn - v1, n1) >= 0) & (_dot(pn - v2, n2) <= 0)
+        in_f = (_dot(pf - v1, n1) >= 0) & (_dot(pf - v2, n2) <= 0)
+        use_near = cand & in_n & (near >= lo)
+        use_far = cand & ~use_near & in_f & (far <= hi)
+        root = np.where(use_near, near, np.where(use_far, far, np.inf))
+        j = int(np.argmin(root))
+        if not np.isfinite(root[j]):
+            continue
+        tf = np.float32(root[j])
+        out_t[k], out_iv[k] = tf, iv[j]
+        out_p[k] = (ro + rd * root[j]).astype(np.float32)
+        ties[k] = set(iv[root <= np.float64(tf)].tolist())  # roots that round to the same float t
+    return out_t, out_iv, out_p, ties
+
+
+def _intersection_pin(r, o):
+    xyz, starts = r.hair()
+    segs = _segments(xyz, starts)
+    info = r.info()
+    lo, hi = np.array(info.aabb_min, np.float32), np.array(info.aabb_max, np.float32)
+    rng = np.random.default_rng(17)
+    n = 600
+    # origins around and inside the ball, a quarter aimed at segments (so most rays hit)
+    orig = rng.uniform(lo - 1.0, hi + 1.0, (n, 3)).astype(np.float32)
+    sv = segs[0][rng.integers(0, len(segs[0]), n)]
+    aim = (xyz[sv] + rng.uniform(0, 1, (n, 1)) * (xyz[sv + 1] - xyz[sv])).astype(np.float64) \
+        + rng.normal(0, 0.0015, (n, 3))
+    d = np.where(np.arange(n)[:, None] % 4 == 0, rng.normal(size=(n, 3)), aim - orig)
+    d = (d / np.linalg.norm(d, axis=1, keepdims=True)).astype(np.float32)
+    mint = np.where(np.arange(n) % 2 == 0, np.float32(1e-4), np.float32(0.0)).astype(np.float32)
+    maxt = np.where(np.arange(n) % 3 == 0, np.float32(np.inf), rng.uniform(1, 30, n).astype(np.float32))
+    ok, lo_t, hi_t = _entry_clip(orig, d, mint, maxt, lo, hi)
+    want_t, want_iv, want_p, ties = _brute_force(orig, d, lo_t, hi_t, float(scene_util.scenes.CONFIGS[
+        "furball_marschner"]["radius"]), segs)
+    want_t[~ok], want_iv[~ok] = np.inf, -1
+    tracer = o if o is not None else r  # the oracle (CPU test) or the GPU (gpu test)
+    got_t, got_iv, got_p = tracer.trace(orig, d, mint, maxt)
+    assert (want_iv >= 0).sum() > 250
+    np.testing.assert_array_equal(got_t, want_t)
+    hit = want_iv >= 0
+    same = got_iv == want_iv
+    # a different segment is only allowed inside a one-ulp tie (test order decides, hair.cpp:519-541)
+    assert all(got_iv[k] in ties[k] for k in np.nonzero(hit & ~same)[0])
+    assert same.mean() > 0.99
+    np.testing.assert_array_equal(got_p[hit & same], want_p[hit & same])
+    # any-hit (shadow) answers: occluded iff some segment is hit inside [mint, maxt]
+    got_sh = tracer.trace(orig, d, mint, maxt, shadow=True)
+    np.testing.assert_array_equal(got_sh, hit)
+
+
+def test_hair_intersection_independent_pin():
+    _, r, o = scene_util.make("furball_marschner", 600, 32, 32, 4)
+    _intersection_pin(r, o)
+
+
+@pytest.mark.gpu
+def test_hair_intersection_independent_pin_gpu():
+    """the same brute-force numpy restatement against the GPU's k_trace_batch (no oracle involved)"""
+    _, r, _ = scene_util.make("furball_marschner", 600, 32, 32, 4, device=0)
+    _intersection_pin(r, None)
+
+
+# ---------------------------------------------------------------------------
+# MarschnerDiffuse::eval (marschner_diffuse.cpp:377-482) restated in float32
+# numpy from the reference: longitudinal M with the small-roughness branch and
+# logI0 (:279-299, :364-374), the shifted lobes (beta_R = 0.1, v = beta^2,
+# scale angle -0.1 rad; :143-150), the bilinear Azimuthal::eval (:80-94) over
+# the tables (pinned above against the float64 restatement), the rough
+# transmittance slice through evalCubicInterp1D (rtrans.h:183-199,
+# spline.cpp:23-61) and the diffuse term (:469-479, m_invEta2 at :218).
+# numpy's float32 transcendentals differ from glibc / ocml by ulps: rtol 2e-4.
+# ---------------------------------------------------------------------------
+def _marschner_eval_np(wi, wo, tables, trans, fdr, diffuse, eta):
+    f = np.float32
+    pi = f(np.pi)
+    sa = f(-0.1)
+    vR, vTT, vTRT = f(0.1) * f(0.1), (f(0.1) * f(0.5)) ** 2, (f(0.1) * f(2.0)) ** 2
+
+    def trig_inverse(x):
+        return np.minimum(np.sqrt(np.maximum(f(1) - x * x, f(0))), f(1))
+
+    def i0(x):
+        res, xsq = np.ones_like(x), x * x
+        xi, denom = xsq.copy(), f(4)
+        for i in range(1, 11):
+            res = res + xi / denom
+            xi = xi * xsq
+            denom = denom * (f(4) * f((i + 1) * (i + 1)))
+        return res
+
+    def log_i0(x):
+        with np.errstate(divide="ignore", over="ignore", invalid="ignore"):
+            big = x + f(0.5) * (np.log(f(1) / (pi * f(2) * x)) + f(1) / (f(8) * x))
+            return np.where(x > f(12), big, np.log(i0(np.where(x > f(12), f(0), x))))
+
+    def longitudinal(v, sin_i, sin_o, cos_i, cos_o):
+        a = cos_i * cos_o / v
+        b = sin_i * sin_o / v
+        return np.exp(-b + log_i0(a) - f(1) / v + f(0.6931) + np.log(f(1) / (f(2) * v)))  # v < 0.1 branch
+
+    def azimuthal(tab, phi, cos_d):
+        u = f(63) * phi * (f(1) / (f(2) * pi))
+        v = f(63) * cos_d
+        x0 = np.clip(u.astype(np.int32), 0, 62)
+        y0 = np.clip(v.astype(np.int32), 0, 62)
+        u = np.clip(u - x0.astype(f), f(0), f(1))[:, None]
+        v = np.clip(v - y0.astype(f), f(0), f(1))[:, None]
+        t = tab.reshape(64 * 64, 3)
+        r0 = t[x0 + y0 * 64] * (f(1) - u) + t[x0 + 1 + y0 * 64] * u
+        r1 = t[x0 + (y0 + 1) * 64] * (f(1) - u) + t[x0 + 1 + (y0 + 1) * 64] * u
+        return r0 * (f(1) - v) + r1 * v
+
+    def rough_trans(cos_t):
+        w = np.power(np.abs(cos_t), f(0.25))
+        size = len(trans)
+        t = ((w - f(0)) * f(size - 1)) / (f(1) - f(0))
+        k = np.minimum(t.astype(np.int64), size - 2)
+        f0, f1 = trans[k], trans[k + 1]
+        d0 = np.where(k > 0, f(0.5) * (trans[np.minimum(k + 1, size - 1)] - trans[np.maximum(k - 1, 0)]), f1 - f0)
+        d1 = np.where(k + 2 < size, f(0.5) * (trans[np.minimum(k + 2, size - 1)] - f0), f1 - f0)
+        t = t - k.astype(f)
+        t2 = t * t
+        t3 = t2 * t
+        res = (f(2) * t3 - f(3) * t2 + f(1)) * f0 + (f(-2) * t3 + f(3) * t2) * f1 + (t3 - f(2) * t2 + t) * d0 + \
+            (t3 - t2) * d1
+        res = np.where((w >= 0) & (w <= 1), res, f(0))
+        return np.where(cos_t >= 0, np.minimum(f(1), np.maximum(f(0), res)), f(0))
+
+    sin_i, sin_o = wi[:, 1], wo[:, 1]
+    cos_o = trig_inverse(sin_o)
+    th_i = np.arcsin(np.clip(sin_i, f(-1), f(1)))
+    th_o = np.arcsin(np.clip(sin_o, f(-1), f(1)))
+    cos_d = np.cos((th_o - th_i) * f(0.5))
+    phi = np.arctan2(wo[:, 0], wo[:, 2])
+    phi = np.where(phi < 0, phi + pi * f(2), phi)
+    th_r, th_tt, th_trt = th_i - f(2) * sa, th_i + sa, th_i + f(4) * sa
+    mr = longitudinal(vR, np.sin(th_r), sin_o, np.cos(th_r), cos_o)
+    mtt = longitudinal(vTT, np.sin(th_tt), sin_o, np.cos(th_tt), cos_o)
+    mtrt = longitudinal(vTRT, np.sin(th_trt), sin_o, np.cos(th_trt), cos_o)
+    res = (f(0.15) * mr)[:, None] * azimuthal(tables[0], phi, cos_d) + mtt[:, None] * azimuthal(tables[1], phi, cos_d) \
+        + mtrt[:, None] * azimuthal(tables[2], phi, cos_d)
+    inv_eta2 = f(1) / (f(eta) * f(eta))
+    diff = np.asarray(diffuse, f) / (f(1) - f(fdr))
+    scale = f(1 / np.pi) * wo[:, 2] * rough_trans(wi[:, 2]) * rough_trans(wo[:, 2]) * inv_eta2
+    return (res + diff[None, :] * scale[:, None]).astype(f)
+
+
+def _marschner_pin(r, o):
+    tables, fdr, trans, _ = r.marschner_tables()
+    rng = np.random.default_rng(23)
+    n = 20000
+    wi = rng.normal(size=(n, 3))
+    wo = rng.normal(size=(n, 3))
+    wi = (wi / np.linalg.norm(wi, axis=1, keepdims=True)).astype(np.float32)
+    wo = (wo / np.linalg.norm(wo, axis=1, keepdims=True)).astype(np.float32)
+    diffuse = np.array([0.143016, 0.0156076, 1.80928e-05], np.float32)   # scenes.HAIR_DIFFUSE
+    want = _marschner_eval_np(wi, wo, tables, trans.astype(np.float32), fdr, diffuse, np.float32(1.55) / np.float32(1))
+    got = o.bsdf_eval(wi, wo)[0] if o is not None else r.bsdf(wi, wo, np.zeros((n, 2), np.float32))[0]
+    scale = np.maximum(np.abs(want).max(axis=1, keepdims=True), 1e-6)
+    err = np.abs(got - want) / scale
+    assert np.quantile(err, 0.99) < 2e-5, np.quantile(err, 0.99)
+    assert err.max() < (2e-4 if o is not None else 5e-4), err.max()  # GPU: ocml ulps as in test_bsdf_matches_oracle
+
+
+def test_marschner_eval_independent_pin():
+    _, r, o = scene_util.make("furball_marschner", 300, 16, 16, 1)
+    _marschner_pin(r, o)
+
+
+@pytest.mark.gpu
+def test_marschner_eval_independent_pin_gpu():
+    """the numpy restatement against the GPU's marschnerEval (hpt_bsdf_batch), no oracle involved"""
+    _, r, _ = scene_util.make("furball_marschner", 300, 16, 16, 1, device=0)
+    _marschner_pin(r, None)
