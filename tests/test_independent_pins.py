@@ -644,3 +644,47 @@ def test_marschner_eval_independent_pin_gpu():
     """the numpy restatement against the GPU's marschnerEval (hpt_bsdf_batch), no oracle involved"""
     _, r, _ = scene_util.make("furball_marschner", 300, 16, 16, 1, device=0)
     _marschner_pin(r, None)
+
+
+# ---------------------------------------------------------------------------
+# KajiyaKay::eval (kajiyakay.cpp:105-179) in float32 numpy from the reference
+# (specular 0.2 default :64-65, no energy-conservation scaling at these
+# colours, INV_FOURPI / INV_PI single precision); the scene of
+# models/straight-hair/scene_kkay.xml (exponent 10).
+# ---------------------------------------------------------------------------
+def _kk_eval_np(wi, wo, kd, ks, exponent):
+    f = np.float32
+    tl, te = np.abs(wi[:, 0]), np.abs(wo[:, 0])
+    alpha = tl * te + np.sqrt(f(1) - tl * tl) * np.sqrt(f(1) - te * te)
+    spec_on = (alpha > 0) & (wi[:, 0] * wo[:, 0] < 0)
+    with np.errstate(invalid="ignore"):
+        s = ((f(exponent) + f(2)) * f(1 / (4 * np.pi))) * np.power(alpha, f(exponent))
+    res = np.where(spec_on[:, None], (f(0.15) * np.asarray(ks, f))[None, :] * s[:, None], f(0))
+    res = res + (np.asarray(kd, f) * f(1 / np.pi))[None, :]
+    res = res * wo[:, 2][:, None]
+    return np.where(((wi[:, 2] > 0) & (wo[:, 2] > 0))[:, None], res, f(0)).astype(f)
+
+
+def _kk_pin(r, o):
+    rng = np.random.default_rng(29)
+    n = 20000
+    wi = rng.normal(size=(n, 3))
+    wo = rng.normal(size=(n, 3))
+    wi = (wi / np.linalg.norm(wi, axis=1, keepdims=True)).astype(np.float32)
+    wo = (wo / np.linalg.norm(wo, axis=1, keepdims=True)).astype(np.float32)
+    kd = np.array([0.143016, 0.0156076, 1.80928e-05], np.float32)
+    want = _kk_eval_np(wi, wo, kd, [0.2, 0.2, 0.2], 10.0)
+    got = o.bsdf_eval(wi, wo)[0] if o is not None else r.bsdf(wi, wo, np.zeros((n, 2), np.float32))[0]
+    assert (want[:, 0] > 0).mean() > 0.2
+    np.testing.assert_allclose(got, want, rtol=2e-5 if o is not None else 5e-4, atol=1e-7)
+
+
+def test_kajiyakay_eval_independent_pin():
+    _, r, o = scene_util.make("straight_kk", 300, 16, 16, 1)
+    _kk_pin(r, o)
+
+
+@pytest.mark.gpu
+def test_kajiyakay_eval_independent_pin_gpu():
+    _, r, _ = scene_util.make("straight_kk", 300, 16, 16, 1, device=0)
+    _kk_pin(r, None)
