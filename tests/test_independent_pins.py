@@ -688,3 +688,149 @@ def test_kajiyakay_eval_independent_pin():
 def test_kajiyakay_eval_independent_pin_gpu():
     _, r, _ = scene_util.make("straight_kk", 300, 16, 16, 1, device=0)
     _kk_pin(r, None)
+
+
+# ---------------------------------------------------------------------------
+# EnvironmentMap in float32 numpy from the reference: the sampling CDFs of
+# configure() (envmap.cpp:260-323, sequential float sums, sin row weights in
+# double), evalEnvironment without differentials = MIPMap::evalBilinear at
+# level 0 (envmap.cpp:380-393, mipmap.h:575-596; u repeats, v clamps),
+# internalPdfDirection (:603-633) and internalSampleDirection (:567-600 with
+# the local sampleReuse :657-662 and warp::squareToTent warp.cpp:143-162).
+# The scenes' envmaps have no toWorld, so local == world directions.
+# ---------------------------------------------------------------------------
+class _EnvNp:
+    def __init__(self, tex, scale=1.0):
+        f = np.float32
+        self.f = f
+        self.tex = np.asarray(tex, f)
+        self.h, self.w = self.tex.shape[:2]
+        self.scale = f(scale)
+        lum = self._lum(self.tex)                                    # (h, w)
+        col = np.cumsum(lum, axis=1, dtype=f)                        # sequential float sums
+        col_sum = col[:, -1]
+        self.cdf_cols = np.zeros((self.h, self.w + 1), f)
+        with np.errstate(divide="ignore", invalid="ignore"):  # black rows: NaN CDFs never sampled (row pdf 0)
+            self.cdf_cols[:, 1:self.w] = col[:, :self.w - 1] * (f(1) / col_sum)[:, None]
+        self.cdf_cols[:, self.w] = 1
+        ys = np.arange(self.h, dtype=f) + f(0.5)
+        self.row_w = np.sin(ys.astype(np.float64) * np.pi / self.h).astype(f)
+        row = np.cumsum(col_sum * self.row_w, dtype=f)
+        row_sum = row[-1]
+        self.cdf_rows = np.zeros(self.h + 1, f)
+        self.cdf_rows[1:self.h] = row[:self.h - 1] * (f(1) / row_sum)
+        self.cdf_rows[self.h] = 1
+        self.norm = f(1.0 / (np.float64(row_sum) * (2 * np.pi / self.w) * (np.pi / self.h)))
+        self.pix = (f(2 * np.pi / self.w), f(np.pi / self.h))
+
+    def _lum(self, s):
+        f = self.f
+        return s[..., 0] * f(0.212671) + s[..., 1] * f(0.715160) + s[..., 2] * f(0.072169)
+
+    def _texel(self, x, y):
+        return self.tex[np.clip(y, 0, self.h - 1), np.mod(x, self.w)]
+
+    def _uv(self, d):
+        f = self.f
+        u = np.arctan2(d[:, 0], -d[:, 2]) * f(1 / (2 * np.pi))
+        v = np.arccos(np.clip(d[:, 1], f(-1), f(1))) * f(1 / np.pi)
+        return u * f(self.w) - f(0.5), v * f(self.h) - f(0.5)
+
+    def _split(self, u, v):
+        f = self.f
+        x, y = np.floor(u).astype(np.int64), np.floor(v).astype(np.int64)
+        dx1, dy1 = u - x.astype(f), v - y.astype(f)
+        return x, y, dx1, f(1) - dx1, dy1, f(1) - dy1
+
+    def eval(self, d):
+        x, y, dx1, dx2, dy1, dy2 = self._split(*self._uv(d))
+        t = self._texel
+        c = lambda a: a[:, None]  # noqa: E731
+        v = t(x, y) * c(dx2) * c(dy2) + t(x, y + 1) * c(dx2) * c(dy1) \
+            + t(x + 1, y) * c(dx1) * c(dy2) + t(x + 1, y + 1) * c(dx1) * c(dy1)
+        return v * self.scale
+
+    def _pdf_xy(self, x, y, dx1, dx2, dy1, dy2):
+        t = self._texel
+        c = lambda a: a[:, None]  # noqa: E731
+        v1 = t(x, y) * c(dx2) * c(dy2) + t(x + 1, y) * c(dx1) * c(dy2)
+        v2 = t(x, y + 1) * c(dx2) * c(dy1) + t(x + 1, y + 1) * c(dx1) * c(dy1)
+        pdf = (self._lum(v1) * self.row_w[np.clip(y, 0, self.h - 1)]
+               + self._lum(v2) * self.row_w[np.clip(y + 1, 0, self.h - 1)]) * self.norm
+        return v1 + v2, pdf
+
+    def pdf(self, d):
+        f = self.f
+        _, pdf = self._pdf_xy(*self._split(*self._uv(d)))
+        sin_t = np.sqrt(np.maximum(f(1) - d[:, 1] * d[:, 1], f(0)))
+        return pdf / np.maximum(np.abs(sin_t), f(1e-4))
+
+    @staticmethod
+    def _reuse(cdf, size, s):
+        idx = np.searchsorted(cdf, s, side="left") if cdf.ndim == 1 else \
+            np.array([np.searchsorted(c, v, side="left") for c, v in zip(cdf, s)])
+        idx = np.minimum(np.maximum(idx - 1, 0), size - 1)
+        lo = np.take_along_axis(cdf, idx[:, None], 1)[:, 0] if cdf.ndim == 2 else cdf[idx]
+        hi = np.take_along_axis(cdf, idx[:, None] + 1, 1)[:, 0] if cdf.ndim == 2 else cdf[idx + 1]
+        return idx, (s - lo) / (hi - lo)
+
+    @staticmethod
+    def _tent(s):
+        f = np.float32
+        neg = s >= f(0.5)
+        s2 = np.where(neg, f(2) * (s - f(0.5)), s * f(2))
+        return np.where(neg, f(-1), f(1)) * (f(1) - np.sqrt(s2))
+
+    def sample(self, u):
+        f = self.f
+        row, sy = self._reuse(self.cdf_rows, self.h, u[:, 1].copy())
+        col, sx = self._reuse(self.cdf_cols[row], self.w, u[:, 0].copy())
+        px = col.astype(f) + self._tent(sx.astype(f))
+        py = row.astype(f) + self._tent(sy.astype(f))
+        value, pdf = self._pdf_xy(*self._split(px, py))
+        value = value * self.scale
+        phi, theta = self.pix[0] * (px + f(0.5)), self.pix[1] * (py + f(0.5))
+        sp, cp, st, ct = np.sin(phi), np.cos(phi), np.sin(theta), np.cos(theta)
+        d = np.stack([sp * st, ct, -cp * st], axis=1).astype(f)
+        pdf = pdf / np.maximum(np.abs(st), f(1e-4))
+        return d, value, pdf
+
+
+def _env_pin(r, o):
+    tex = (o.env_levels() if o is not None else r.env_levels())[0]
+    env = _EnvNp(tex)
+    rng = np.random.default_rng(31)
+    n = 30000
+    dq = rng.normal(size=(n, 3))
+    dq = (dq / np.linalg.norm(dq, axis=1, keepdims=True)).astype(np.float32)
+    u = rng.random((n, 2)).astype(np.float32)
+    ref = (np.array([0.0, 12.3, 0.0]) + rng.normal(0, 1.0, (n, 3))).astype(np.float32)
+    want_e, want_p = env.eval(dq), env.pdf(dq)
+    want_d, want_v, want_sp = env.sample(u)
+    if o is not None:
+        got_e, got_p = o.env_eval(dq)
+        got_d, got_w, got_sp, _ = o.env_sample(ref, u)
+    else:
+        got_d, got_w, got_sp, _, got_e, got_p = r.env(ref, u, dq)
+    # atan2/acos/sin ulps move bilinear weights by ~1e-7 x 512 texels; at the sun-disk edge
+    # a texel jump of ~60 turns that into ~1e-3, so: a tight bulk bound plus a loose max
+    for got, want in ((got_e, want_e), (got_p, want_p)):
+        want = want.reshape(got.shape)
+        close = np.abs(got - want) <= 2e-5 * np.abs(want) + 1e-7
+        assert close.mean() > 0.995, close.mean()
+        np.testing.assert_allclose(got, want, rtol=5e-3, atol=2e-3)
+    np.testing.assert_allclose(got_d, want_d, rtol=1e-5, atol=2e-6)
+    assert (want_e[:, 0] > 0).mean() > 0.3
+    np.testing.assert_allclose(got_sp, want_sp, rtol=5e-5 if o is not None else 2e-4, atol=1e-7)
+    np.testing.assert_allclose(got_w, want_v / want_sp[:, None], rtol=2e-4, atol=1e-6)
+
+
+def test_envmap_independent_pin():
+    _, r, o = scene_util.make("furball_marschner", 300, 16, 16, 1)
+    _env_pin(r, o)
+
+
+@pytest.mark.gpu
+def test_envmap_independent_pin_gpu():
+    _, r, _ = scene_util.make("furball_marschner", 300, 16, 16, 1, device=0)
+    _env_pin(r, None)
