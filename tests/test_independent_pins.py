@@ -834,3 +834,189 @@ def test_envmap_independent_pin():
 def test_envmap_independent_pin_gpu():
     _, r, _ = scene_util.make("furball_marschner", 300, 16, 16, 1, device=0)
     _env_pin(r, None)
+
+
+# ---------------------------------------------------------------------------
+# MarschnerDiffuse::sample (marschner_diffuse.cpp:594-744) in float32 numpy:
+# lobe choice by Azimuthal::weight (:101-105) over the dilated-max
+# InterpolatedDistribution1D (:39-64, InterpolatedDistribution1D.hpp:38-110),
+# sampleM (:579-592), Azimuthal::sample's interpolated-CDF bisection
+# (:68-77, .hpp:68-92), the specular/diffuse split by the rough transmittance
+# and m_specularSamplingWeight (:216, specularReflectance 0.5 default :127-128)
+# and squareToCosineHemisphere (warp.cpp:43-52, 81-102).  pdf() is 1 whenever
+# the diffuse component is enabled (:517-519), so the weight is eval(wo).
+# ---------------------------------------------------------------------------
+class _AzimuthalSamplerNp:
+    def __init__(self, tab):
+        f = np.float32
+        size = 64
+        w = np.asarray(tab, f).reshape(size, size, 3).max(axis=2)   # [y (cos_d), x (phi)]
+        for y in range(size):                                         # dilation in the order of :50-61
+            for x in range(size - 1):
+                w[y, x] = max(w[y, x], w[y, x + 1])
+            for x in range(size - 1, 0, -1):
+                w[y, x] = max(w[y, x], w[y, x - 1])
+        for x in range(size):
+            for y in range(size - 1):
+                w[y, x] = max(w[y, x], w[y + 1, x])
+            for y in range(size - 1, 0, -1):
+                w[y, x] = max(w[y, x], w[y - 1, x])
+        cdf = np.zeros((size, size + 1), f)
+        cdf[:, 1:] = np.cumsum(w, axis=1, dtype=f)
+        self.sums = cdf[:, size].copy()
+        with np.errstate(divide="ignore", invalid="ignore"):  # degenerate rows are replaced below
+            scale = (f(1) / self.sums)[:, None]
+            pdf = w * scale
+            cdf[:, :size] = cdf[:, :size] * scale
+        degen = self.sums < f(1e-4)
+        pdf[degen] = f(1) / size
+        cdf[degen, :size] = np.arange(size, dtype=f) * (f(1) / size)
+        cdf[:, size] = 1
+        self.pdf, self.cdf, self.size = pdf, cdf, size
+
+    def _interp(self, dist):
+        f = np.float32
+        d0 = np.clip(dist.astype(np.int32), 0, self.size - 1)
+        d1 = np.minimum(d0 + 1, self.size - 1)
+        return d0, d1, np.clip(dist - d0.astype(f), f(0), f(1))
+
+    def weight(self, cos_t):
+        f = np.float32
+        d0, d1, v = self._interp(f(63) * cos_t)
+        return (self.sums[d0] * (f(1) - v) + self.sums[d1] * v) * f(2 * np.float32(np.pi) / 64)
+
+    def sample(self, cos_d, xi):
+        f = np.float32
+        d0, d1, v = self._interp(f(63) * cos_d)
+        n = cos_d.shape[0]
+        lo, hi = np.zeros(n, np.int64), np.full(n, self.size, np.int64)
+        lo_u, hi_u = np.zeros(n, f), np.ones(n, f)
+        while np.any(hi - lo != 1):
+            act = hi - lo != 1
+            mid = (hi + lo) // 2
+            mid_u = self.cdf[d0, mid] * (f(1) - v) + self.cdf[d1, mid] * v
+            go = act & (mid_u < xi)
+            stay = act & ~go
+            lo, lo_u = np.where(go, mid, lo), np.where(go, mid_u, lo_u)
+            hi, hi_u = np.where(stay, mid, hi), np.where(stay, mid_u, hi_u)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            xi = np.clip((xi - lo_u) / (hi_u - lo_u), f(0), f(1))
+        two_pi = f(2) * f(np.pi)
+        return two_pi * (lo.astype(f) + xi) * f(1 / 64)
+
+
+def _marschner_sample_np(wi, u, tables, trans, spec_weight):
+    f = np.float32
+    sa = f(-0.1)
+    vs = (f(0.1) * f(0.1), (f(0.1) * f(0.5)) ** 2, (f(0.1) * f(2.0)) ** 2)
+    lobes = [_AzimuthalSamplerNp(t) for t in tables]
+
+    def trig_inverse(x):
+        return np.minimum(np.sqrt(np.maximum(f(1) - x * x, f(0))), f(1))
+
+    sin_i = wi[:, 1]
+    cos_i = trig_inverse(sin_i)
+    th_i = np.arcsin(np.clip(sin_i, f(-1), f(1)))
+    thetas = (th_i - f(2) * sa, th_i + sa, th_i + f(4) * sa)
+    w = [lb.weight(cos_i) for lb in lobes]
+    target = u[:, 0] * (w[0] + w[1] + w[2])
+    lobe = np.where(target < w[0], 0, np.where(target < w[0] + w[1], 1, 2))
+    v = np.choose(lobe, vs).astype(f)
+    theta = np.choose(lobe, thetas).astype(f)
+    # sampleM with xi = (u.x, u.y)
+    with np.errstate(divide="ignore", over="ignore"):
+        cos_t = f(1) + v * np.log(u[:, 0] + (f(1) - u[:, 0]) * np.exp(f(-2) / v))
+    sin_t = trig_inverse(cos_t)
+    cos_phi = np.cos(f(2) * f(np.pi) * u[:, 1])
+    sin_o = -cos_t * np.sin(theta) + sin_t * cos_phi * np.cos(theta)
+    cos_o = trig_inverse(sin_o)
+    th_o = np.arcsin(np.clip(sin_o, f(-1), f(1)))
+    cos_d = np.cos((th_o - th_i) * f(0.5))
+    phi = np.zeros_like(cos_d)
+    for k in range(3):
+        m = lobe == k
+        phi[m] = lobes[k].sample(cos_d[m], u[m, 1].copy())
+    wo_spec = np.stack([np.sin(phi) * cos_o, sin_o, np.cos(phi) * cos_o], axis=1)
+    # the specular / diffuse split
+    p_spec = f(1) - _rough_trans_np(wi[:, 2], trans)
+    p_spec = (p_spec * f(spec_weight)) / (p_spec * f(spec_weight) + (f(1) - p_spec) * (f(1) - f(spec_weight)))
+    r1, r2 = f(2) * u[:, 0] - f(1), f(2) * u[:, 1] - f(1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        phi_a = (np.pi / 4.0 * (r2 / r1).astype(np.float64)).astype(f)
+        phi_b = (np.pi / 2.0 - (r1 / r2).astype(np.float64) * (np.pi / 4.0)).astype(f)
+    first = r1 * r1 > r2 * r2
+    r = np.where(first, r1, r2)
+    ph = np.where(first, phi_a, phi_b)
+    zero = (r1 == 0) & (r2 == 0)
+    r, ph = np.where(zero, f(0), r), np.where(zero, f(0), ph)
+    px, py = r * np.cos(ph), r * np.sin(ph)
+    z = np.sqrt(np.maximum(f(1) - px * px - py * py, f(0)))
+    z = np.where(z == 0, f(1e-10), z)
+    wo_diff = np.stack([px, py, z], axis=1)
+    spec = u[:, 1] < p_spec
+    return np.where(spec[:, None], wo_spec, wo_diff).astype(f), spec
+
+
+def _rough_trans_np(cos_t, trans):
+    """the rough-transmittance slice of _marschner_eval_np (rtrans.h:183-199, spline.cpp:23-61)"""
+    f = np.float32
+    w = np.power(np.abs(cos_t), f(0.25))
+    size = len(trans)
+    t = ((w - f(0)) * f(size - 1)) / (f(1) - f(0))
+    k = np.minimum(t.astype(np.int64), size - 2)
+    f0, f1 = trans[k], trans[k + 1]
+    d0 = np.where(k > 0, f(0.5) * (trans[np.minimum(k + 1, size - 1)] - trans[np.maximum(k - 1, 0)]), f1 - f0)
+    d1 = np.where(k + 2 < size, f(0.5) * (trans[np.minimum(k + 2, size - 1)] - f0), f1 - f0)
+    t = t - k.astype(f)
+    t2 = t * t
+    t3 = t2 * t
+    res = (f(2) * t3 - f(3) * t2 + f(1)) * f0 + (f(-2) * t3 + f(3) * t2) * f1 + (t3 - f(2) * t2 + t) * d0 + \
+        (t3 - t2) * d1
+    res = np.where((w >= 0) & (w <= 1), res, f(0))
+    return np.where(cos_t >= 0, np.minimum(f(1), np.maximum(f(0), res)), f(0))
+
+
+def _marschner_sample_pin(r, o):
+    f = np.float32
+    tables, fdr, trans, sw = (o if o is not None else r).marschner_tables()
+    diffuse = np.array([0.143016, 0.0156076, 1.80928e-05], f)
+    lum = lambda s: s[0] * f(0.212671) + s[1] * f(0.715160) + s[2] * f(0.072169)  # noqa: E731
+    s_avg, d_avg = lum(np.full(3, f(0.5))), lum(diffuse)
+    spec_weight = s_avg / (d_avg + s_avg)
+    assert abs(sw - spec_weight) <= 1e-7, (sw, spec_weight)
+    rng = np.random.default_rng(37)
+    n = 20000
+    wi = rng.normal(size=(n, 3))
+    wi = (wi / np.linalg.norm(wi, axis=1, keepdims=True)).astype(f)
+    wi[:, 2] = np.abs(wi[:, 2])
+    u = rng.random((n, 2)).astype(f)
+    want, spec = _marschner_sample_np(wi, u, tables, trans.astype(f), spec_weight)
+    if o is not None:
+        got, weight, pdf, _ = o.bsdf_sample(wi, u)
+    else:
+        _, _, got, weight, pdf, _ = r.bsdf(wi, np.zeros_like(wi), u)
+    assert 0.05 < spec.mean() < 0.95, spec.mean()
+    # arcsin/log/exp/cos ulps move sin_o by a few 1e-7; a lobe's CDF-bisection step can
+    # flip on it for a handful of samples (a whole azimuthal bin: compare bulk + count)
+    err = np.abs(got - want).max(axis=1)
+    if o is not None:
+        assert err.max() <= 1e-5, err.max()          # measured: 53% bitwise, max 2.7e-6
+    assert np.mean(err <= 2e-5) > 0.998, np.mean(err <= 2e-5)
+    assert np.mean(err <= 1e-5) > 0.98, np.mean(err <= 1e-5)
+    np.testing.assert_array_equal(pdf, np.ones(n, f))
+    ok = err <= 2e-5
+    w_np = _marschner_eval_np(wi[ok], got[ok], [t.astype(f) for t in tables], trans.astype(f), fdr, diffuse,
+                              f(1.55) / f(1))
+    scale = np.maximum(np.abs(w_np).max(axis=1, keepdims=True), 1e-6)
+    assert np.quantile(np.abs(weight[ok] - w_np) / scale, 0.99) < 2e-5
+
+
+def test_marschner_sample_independent_pin():
+    _, r, o = scene_util.make("furball_marschner", 300, 16, 16, 1)
+    _marschner_sample_pin(r, o)
+
+
+@pytest.mark.gpu
+def test_marschner_sample_independent_pin_gpu():
+    _, r, _ = scene_util.make("furball_marschner", 300, 16, 16, 1, device=0)
+    _marschner_sample_pin(r, None)
