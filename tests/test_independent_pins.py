@@ -1023,3 +1023,296 @@ def test_marschner_sample_independent_pin():
 def test_marschner_sample_independent_pin_gpu():
     _, r, _ = scene_util.make("furball_marschner", 300, 16, 16, 1, device=0)
     _marschner_sample_pin(r, None)
+
+
+# ---------------------------------------------------------------------------
+# MIPathTracer::Li (path.cpp:119-300) restated in numpy over the pins above:
+# the per-sample driver of SamplingIntegrator::renderBlock
+# (integrator.cpp:163-183: samplePos = pixel + next2D, Sobol dims 0/1 scaled
+# to the pixel, sobol.cpp:230-250), hair fillIntersectionRecord (hair.cpp:
+# 825-853: frame s = float tangent, n from the relative hit point, t = n x s,
+# the radius shift of the hit point), strictNormals (the scenes' integrator
+# block), NEE through Scene::sampleEmitterDirect (scene.cpp:828-852) with the
+# power heuristic, Marschner sampling with pdf 1, env hits weighted against
+# pdfDirect unless the sampled lobe is delta, Russian roulette from rrDepth 5
+# with the reciprocal division of Spectrum::operator/= (spectrum.h:447-455).
+# Inputs taken from pinned pieces: Sobol values (known answers + the
+# reference's own tables, test_oracle_golden) and camera rays (bitwise equal
+# to the numpy camera of test_camera.py).  Two documented simplifications:
+# shadow rays run to infinity instead of dist*(1-ShadowEpsilon) (the hair
+# lies well inside the scene's bounding sphere) and camera-ray misses, whose
+# radiance is the EWA lookup of the MIP pyramid, are left out (the pyramid is
+# pinned by test_env_mip_pyramid; the EWA by the GPU-vs-oracle tests).
+# ---------------------------------------------------------------------------
+def _closest_batch(o, d, mint, maxt, radius, segs, lo, hi, chunk=96):
+    """float t, segment iv, float hit point for each ray (t = inf, iv = -1 on a miss)"""
+    ok, lo_t, hi_t = _entry_clip(o, d, mint, maxt, lo, hi)
+    iv, v1, v2, axis, n1, n2 = segs
+    r2 = np.float64(np.float32(radius) * np.float32(radius))
+    n = len(o)
+    out_t = np.full(n, np.inf, np.float32)
+    out_iv = np.full(n, -1, np.int64)
+    out_p = np.zeros((n, 3), np.float32)
+    for b in range(0, n, chunk):
+        sl = slice(b, min(n, b + chunk))
+        ro = o[sl].astype(np.float64)[:, None, :]
+        rd = d[sl].astype(np.float64)[:, None, :]
+        rel = ro - v1[None]
+        po = rel - _dot(axis[None], rel)[..., None] * axis[None]
+        pd = rd - _dot(axis[None], rd)[..., None] * axis[None]
+        A = _dot(pd, pd)
+        B = 2 * _dot(po, pd)
+        C = _dot(po, po) - r2
+        disc = B * B - 4.0 * A * C
+        with np.errstate(invalid="ignore", divide="ignore"):
+            sq = np.sqrt(disc)
+            temp = np.where(B < 0, -0.5 * (B - sq), -0.5 * (B + sq))
+            x0, x1 = temp / A, C / temp
+        near, far = np.minimum(x0, x1), np.maximum(x0, x1)
+        lo_k = lo_t[sl].astype(np.float64)[:, None]
+        hi_k = hi_t[sl].astype(np.float64)[:, None]
+        cand = (disc >= 0) & (A != 0) & (near <= hi_k) & (far >= lo_k)
+        pn = ro + rd * near[..., None]
+        pf = ro + rd * far[..., None]
+        in_n = (_dot(pn - v1[None], n1[None]) >= 0) & (_dot(pn - v2[None], n2[None]) <= 0)
+        in_f = (_dot(pf - v1[None], n1[None]) >= 0) & (_dot(pf - v2[None], n2[None]) <= 0)
+        use_near = cand & in_n & (near >= lo_k)
+        use_far = cand & ~use_near & in_f & (far <= hi_k)
+        root = np.where(use_near, near, np.where(use_far, far, np.inf))
+        j = np.argmin(root, axis=1)
+        best = root[np.arange(root.shape[0]), j]
+        hit = np.isfinite(best) & ok[sl]
+        out_t[sl] = np.where(hit, best.astype(np.float32), np.float32(np.inf))
+        out_iv[sl] = np.where(hit, iv[j], -1)
+        p = (ro[:, 0, :] + rd[:, 0, :] * np.where(hit, best, 0)[:, None]).astype(np.float32)
+        out_p[sl] = np.where(hit[:, None], p, 0)
+    return out_t, out_iv, out_p
+
+
+def _cross32(a, b):
+    return np.stack([a[:, 1] * b[:, 2] - a[:, 2] * b[:, 1], a[:, 2] * b[:, 0] - a[:, 0] * b[:, 2],
+                     a[:, 0] * b[:, 1] - a[:, 1] * b[:, 0]], axis=1)
+
+
+def _normalize32(v):
+    f = np.float32
+    return v * (f(1) / np.sqrt(_dot(v, v)))[:, None]
+
+
+def _li_np(o, r, width, frames, max_depth=65, rr_depth=5):
+    f = np.float32
+    name = "furball_marschner"
+    radius = f(float(scene_util.scenes.CONFIGS[name]["radius"]))
+    xyz, starts = r.hair()
+    xyz = np.asarray(xyz, f)
+    segs = _segments(xyz, starts)
+    info = r.info()
+    lo, hi = np.array(info.aabb_min, f), np.array(info.aabb_max, f)
+    tables, fdr, trans, sw = o.marschner_tables()
+    tables = [t.astype(f) for t in tables]
+    trans = trans.astype(f)
+    diffuse = np.array([0.143016, 0.0156076, 1.80928e-05], f)
+    eta = f(1.55) / f(1)
+    env = _EnvNp(o.env_levels()[0])
+
+    # renderBlock: pixel, Sobol index, samplePos from dims 0 / 1
+    m = int(np.log2(width))
+    res = f(1 << m)
+    px = np.tile(np.repeat(np.arange(width, dtype=np.uint32), width), len(frames))
+    py = np.tile(np.tile(np.arange(width, dtype=np.uint32), width), len(frames))
+    fr = np.repeat(np.asarray(frames, np.uint32), width * width)
+    idx = o.sobol_lookup(m, fr, px, py)
+    s0 = o.sobol_sample(idx, np.zeros_like(px))
+    s1 = o.sobol_sample(idx, np.ones_like(px))
+    pos = np.stack([px.astype(f) + (s0 * res - px.astype(f)), py.astype(f) + (s1 * res - py.astype(f))], axis=1)
+    pos_all = pos
+    co, cd, cmint, cmaxt = o.camera_rays(pos)
+    # which camera rays to follow: those the kd-tree says hit (selection only -- the hits
+    # themselves are recomputed by brute force below, and must agree)
+    sel = o.trace(co, cd, cmint, cmaxt)[1] >= 0
+    t0, iv0, p0 = _closest_batch(co[sel], cd[sel], cmint[sel], cmaxt[sel], radius, segs, lo, hi)
+    assert (iv0 >= 0).all()
+    px, py, fr, idx, pos = px[sel], py[sel], fr[sel], idx[sel], pos[sel]
+    n = len(px)
+    d, its_iv, its_p = cd[sel], iv0, p0
+    L = np.zeros((n, 3), f)
+    thr = np.ones((n, 3), f)
+    depth = np.ones(n, np.int64)
+    dim = np.full(n, 2, np.uint32)
+    alive = np.ones(n, bool)
+
+    def next1d(a):
+        v = o.sobol_sample(idx[a], dim[a])
+        dim[a] += 1
+        return v
+
+    def next2d(a):
+        u = np.stack([o.sobol_sample(idx[a], dim[a]), o.sobol_sample(idx[a], dim[a] + 1)], axis=1)
+        dim[a] += 2
+        return u
+
+    def mis(a, b):
+        a, b = a * a, b * b
+        return a / (a + b)
+
+    while alive.any():
+        a = np.nonzero(alive)[0]
+        v1 = xyz[its_iv[a]]
+        s = _normalize32(xyz[its_iv[a] + 1] - v1)                  # tangent(iv), float
+        rel = its_p[a] - v1
+        nrm = _normalize32(rel - _dot(s, rel)[:, None] * s)
+        tt = _cross32(nrm, s)
+        ly, lz = _dot(rel, tt), _dot(rel, nrm)
+        p = its_p[a] + nrm * (radius - np.sqrt(ly * ly + lz * lz))[:, None]
+        to_local = lambda v: np.stack([_dot(v, s), _dot(v, tt), _dot(v, nrm)], axis=1)  # noqa: E731
+        wi = to_local(-d[a])
+        stop = (depth[a] >= max_depth) | (_dot(d[a], nrm) * wi[:, 2] >= 0)
+        alive[a[stop]] = False
+        a, s, nrm, tt, p, wi = a[~stop], s[~stop], nrm[~stop], tt[~stop], p[~stop], wi[~stop]
+        if len(a) == 0:
+            break
+        to_local = lambda v: np.stack([_dot(v, s), _dot(v, tt), _dot(v, nrm)], axis=1)  # noqa: E731
+        # direct illumination (the envmap is the only emitter: emPdf 1, sample unchanged)
+        u = next2d(a)
+        dn, val, epdf = env.sample(u)
+        ok = (epdf != 0) & np.any(val != 0, axis=1)
+        with np.errstate(divide="ignore"):
+            value = val * (f(1) / epdf)[:, None]
+        sh_t, _, _ = _closest_batch(p, dn, np.full(len(a), f(1e-4)), np.full(len(a), f(np.inf)), radius, segs, lo, hi)
+        ok &= ~np.isfinite(sh_t)
+        wo = to_local(dn)
+        bval = _marschner_eval_np(wi, wo, tables, trans, fdr, diffuse, eta)
+        ok &= np.any(bval != 0, axis=1) & (_dot(nrm, dn) * wo[:, 2] > 0)
+        w = mis(epdf, f(1))
+        contrib = thr[a] * value * bval * w[:, None]
+        L[a] = np.where(ok[:, None], L[a] + contrib, L[a])
+        # BSDF sampling
+        u = next2d(a)
+        wo_l, spec = _marschner_sample_np(wi, u, tables, trans, sw)
+        bw = _marschner_eval_np(wi, wo_l, tables, trans, fdr, diffuse, eta)   # eval / pdf, pdf = 1
+        stop = ~np.any(bw != 0, axis=1)
+        wo_w = s * wo_l[:, 0:1] + tt * wo_l[:, 1:2] + nrm * wo_l[:, 2:3]
+        stop |= _dot(nrm, wo_w) * wo_l[:, 2] <= 0
+        alive[a[stop]] = False
+        keep2 = ~stop
+        a, p, wo_w, bw, spec = a[keep2], p[keep2], wo_w[keep2], bw[keep2], spec[keep2]
+        if len(a) == 0:
+            break
+        nt, niv, np_ = _closest_batch(p, wo_w, np.full(len(a), f(1e-4)), np.full(len(a), f(np.inf)), radius, segs,
+                                      lo, hi)
+        thr[a] = thr[a] * bw
+        miss = niv < 0
+        if miss.any():
+            am = a[miss]
+            value = env.eval(wo_w[miss])
+            lum_pdf = np.where(spec[miss], f(0), env.pdf(wo_w[miss]))
+            L[am] = L[am] + thr[am] * value * mis(f(1), lum_pdf)[:, None]
+            alive[am] = False
+        a, niv, np_, wo_w = a[~miss], niv[~miss], np_[~miss], wo_w[~miss]
+        if len(a) == 0:
+            break
+        rr = depth[a] >= rr_depth
+        depth[a] += 1
+        if rr.any():
+            ar = a[rr]
+            q = np.minimum(thr[ar].max(axis=1) * f(1) * f(1), f(0.95))
+            die = next1d(ar) >= q
+            thr[ar] = np.where(die[:, None], thr[ar], thr[ar] * (f(1) / q)[:, None])
+            alive[ar[die]] = False
+            live = ~np.isin(a, ar[die])
+            a, niv, np_, wo_w = a[live], niv[live], np_[live], wo_w[live]
+        its_iv[a], its_p[a], d[a] = niv, np_, wo_w
+    L_all = np.zeros((len(pos_all), 3), f)
+    L_all[sel] = L
+    return px, py, fr, pos, L, pos_all, L_all
+
+
+def _tent_weights():
+    """ReconstructionFilter::configure (rfilter.cpp:37-55) for the tent (tent.cpp:34-44, radius 1)"""
+    f = np.float32
+    res = 31                                              # MTS_FILTER_RESOLUTION
+    vals = np.zeros(res + 1, f)
+    total = f(0)
+    for i in range(res):
+        x = (f(1) * f(i)) / f(res)
+        vals[i] = max(f(0), f(1) - abs(x / f(1)))
+        total = f(total + vals[i])
+    total = f(total * (f(2) * f(1) / f(res)))
+    vals[:res] = vals[:res] * (f(1) / total)
+    return vals, f(res) / f(1)
+
+
+def _splat_np(pos, L, width, height):
+    """ImageBlock::put (imageblock.h:144-189) of every sample into one RGBW film (the blocks'
+    integer offsets cancel exactly in float, so the global splat equals the per-block one up to
+    the order of the sums)"""
+    f = np.float32
+    vals, scale = _tent_weights()
+    film = np.zeros((height, width, 4), np.float64)
+    x = pos[:, 0] - f(0.5)
+    y = pos[:, 1] - f(0.5)
+    x0 = np.maximum(np.ceil(x - f(1)).astype(np.int64), 0)
+    y0 = np.maximum(np.ceil(y - f(1)).astype(np.int64), 0)
+    x1 = np.minimum(np.floor(x + f(1)).astype(np.int64), width - 1)
+    y1 = np.minimum(np.floor(y + f(1)).astype(np.int64), height - 1)
+    val = np.concatenate([L, np.ones((len(L), 1), f)], axis=1)
+    for dy in range(3):
+        for dx in range(3):
+            xx, yy = x0 + dx, y0 + dy
+            ok = (xx <= x1) & (yy <= y1)
+            wx = vals[np.minimum(np.abs((xx.astype(f) - x) * scale).astype(np.int64), 31)]
+            wy = vals[np.minimum(np.abs((yy.astype(f) - y) * scale).astype(np.int64), 31)]
+            w = (wx * wy).astype(f)
+            np.add.at(film, (yy[ok], xx[ok]), (w[:, None] * val)[ok].astype(f))
+    return film.astype(f)
+
+
+def _film_pin(got_film, want_film):
+    np.testing.assert_allclose(got_film[..., 3], want_film[..., 3], rtol=1e-5)
+    a, b = got_film[..., :3], want_film[..., :3]
+    scale = np.maximum(np.abs(b).max(axis=-1), 1e-3 * want_film[..., 3])
+    err = np.abs(a - b).max(axis=-1) / scale
+    lit = b.max(axis=-1) > 0
+    print("film pixels lit", lit.sum(), "within 1e-4", np.mean(err[lit] <= 1e-4), "max", err.max())
+    assert lit.sum() > 300
+    assert np.mean(err[lit] <= 1e-4) > 0.85, np.mean(err[lit] <= 1e-4)
+    rel_l2 = np.sqrt(((a - b) ** 2).sum() / (b ** 2).sum())
+    assert rel_l2 < 0.02, rel_l2
+
+
+def _hidden_emitter_scene(device):
+    _, r, o = scene_util.make("furball_marschner", 1000, 64, 64, 6, device=device)
+    si = r.info()
+    r.set_integrator(si.max_depth, si.rr_depth, True, True)     # strictNormals, hideEmitters
+    r.prepare()
+    o.lib.orc_set_integrator(o.s, si.max_depth, si.rr_depth, 1, 1)
+    return r, o
+
+
+def test_path_li_and_film_independent_pin():
+    """numpy Li per path against the oracle's Li, then numpy tent splat against the oracle's
+    film; hideEmitters makes camera-ray misses black so the film needs no EWA lookup
+    (path.cpp:138-141) and leaves every other path's radiance unchanged (Marschner never
+    samples ENull, so the path has 'scattered' before any environment hit)"""
+    r, o = _hidden_emitter_scene(native.HOST_ONLY)
+    px, py, fr, pos, li, pos_all, l_all = _li_np(o, r, 64, range(6))
+    got_li, got_pos, _ = o.trace_paths(px, py, fr)
+    np.testing.assert_array_equal(got_pos, pos)
+    assert len(px) > 300 and (li.max(axis=1) > 0).mean() > 0.5
+    err = np.abs(got_li - li).max(axis=1) / np.maximum(np.abs(li).max(axis=1), 1e-4)
+    print("paths", len(px), "bitwise", np.mean(err == 0), "<=1e-5", np.mean(err <= 1e-5), "max", err.max())
+    assert np.mean(err <= 1e-5) > 0.9, np.mean(err <= 1e-5)   # measured 0.934; max 1.4e-2
+    assert np.mean(err <= 1e-4) > 0.97, np.mean(err <= 1e-4)
+    want = _splat_np(pos_all, l_all, 64, 64)
+    got, _ = o.render(0, 6, width=64, height=64)
+    _film_pin(got, want)
+
+
+@pytest.mark.gpu
+def test_path_film_independent_pin_gpu():
+    """the same numpy film against the GPU's hpt_render (the oracle only supplies Sobol
+    values, camera rays and which camera rays hit)"""
+    r, o = _hidden_emitter_scene(0)
+    *_, pos_all, l_all = _li_np(o, r, 64, range(6))
+    want = _splat_np(pos_all, l_all, 64, 64)
+    _film_pin(r.render(0, 6), want)
