@@ -2037,17 +2037,20 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
 #ifndef HPT_PACKET_WAVES
 #define HPT_PACKET_WAVES 6 /* 34.6 -> 32.9 ms per frame vs 5 (spills only in the per-packet prologue) */
 #endif
-extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_PACKET_WAVES))) void
+#ifndef HPT_PACKET_BLOCK
+#define HPT_PACKET_BLOCK HPT_TRACE_BLOCK
+#endif
+extern "C" __global__ __launch_bounds__(HPT_PACKET_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_PACKET_WAVES))) void
 k_trace_packet(HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, uint32_t *__restrict__ counters,
                uint32_t *__restrict__ cursors) {
-    __shared__ PacketLds lds[HPT_TRACE_BLOCK / 64];
+    __shared__ PacketLds lds[HPT_PACKET_BLOCK / 64];
     PathIO io{P, traceQ, nullptr, counters[HPT_Q_TRACE], 0, 0};
     tracePackets<false>(sc, io, cursors, lds[threadIdx.x >> 6], nullptr);
 }
-extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_packet_counted(
+extern "C" __global__ __launch_bounds__(HPT_PACKET_BLOCK) void k_trace_packet_counted(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, uint32_t *__restrict__ counters,
     uint32_t *__restrict__ cursors, uint32_t *stats) {
-    __shared__ PacketLds lds[HPT_TRACE_BLOCK / 64];
+    __shared__ PacketLds lds[HPT_PACKET_BLOCK / 64];
     PathIO io{P, traceQ, nullptr, counters[HPT_Q_TRACE], 0, 0};
     tracePackets<true>(sc, io, cursors, lds[threadIdx.x >> 6], stats);
 }
@@ -2710,11 +2713,12 @@ hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const 
                                    uint32_t *stats, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
     if (stats)
-        hipLaunchKernelGGL(k_trace_packet_counted, dim3(persistentBlocks((const void *) k_trace_packet_counted, maxItems)),
-                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, counters, counters + HPT_CURSOR_OFFSET, stats);
+        hipLaunchKernelGGL(k_trace_packet_counted,
+                           dim3(persistentBlocks((const void *) k_trace_packet_counted, maxItems, HPT_PACKET_BLOCK)),
+                           dim3(HPT_PACKET_BLOCK), 0, s, sc, P, traceQ, counters, counters + HPT_CURSOR_OFFSET, stats);
     else
-        hipLaunchKernelGGL(k_trace_packet, dim3(persistentBlocks((const void *) k_trace_packet, maxItems)),
-                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, counters, counters + HPT_CURSOR_OFFSET);
+        hipLaunchKernelGGL(k_trace_packet, dim3(persistentBlocks((const void *) k_trace_packet, maxItems, HPT_PACKET_BLOCK)),
+                           dim3(HPT_PACKET_BLOCK), 0, s, sc, P, traceQ, counters, counters + HPT_CURSOR_OFFSET);
     return hipGetLastError();
 }
 hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
