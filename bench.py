@@ -126,7 +126,9 @@ def timed_steps(step, steps, world, dist_mod, sync, device, after_step=None):
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # ranks beyond the visible devices share them (a rehearsal of the N > 1 path on a
+    # one-GPU box); on a full node LOCAL_RANK < device count and this is the identity
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         dist.init_process_group("nccl")  # RCCL over xGMI on ROCm
