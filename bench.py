@@ -130,8 +130,11 @@ def main():
     # one-GPU box); on a full node LOCAL_RANK < device count and this is the identity
     local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    # HPT_BENCH_BACKEND=gloo only rehearses N > 1 on a one-GPU box (RCCL refuses two
+    # ranks on one device): the film is reduced from a host copy.  Never the bench.
+    backend = os.environ.get("HPT_BENCH_BACKEND", "nccl")
     if world > 1:
-        dist.init_process_group("nccl")  # RCCL over xGMI on ROCm
+        dist.init_process_group(backend)  # "nccl" = RCCL over xGMI on ROCm
     torch.cuda.set_device(local)
     cfg = scenes.CONFIGS[args.config]
     n = args.strands or cfg["n"]
@@ -153,14 +156,22 @@ def main():
     t_prep = time.perf_counter() - t0
     info = r.info()
     film = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:%d" % local)
+    host_film = torch.zeros((H, W, 4), dtype=torch.float32) if backend == "gloo" else None
 
     def step(level):
         film.zero_()
         torch.cuda.synchronize()
-        distributed.render_frame(
-            lambda shard, n_shards, f: r.render_device(f.data_ptr(), 0, spp, shard=shard, n_shards=n_shards,
-                                                        collect_stats=level),
-            film, rank, world, dist)
+        if host_film is None:
+            distributed.render_frame(
+                lambda shard, n_shards, f: r.render_device(f.data_ptr(), 0, spp, shard=shard, n_shards=n_shards,
+                                                            collect_stats=level),
+                film, rank, world, dist)
+        else:
+            def shard_to_host(shard, n_shards, f):
+                r.render_device(film.data_ptr(), 0, spp, shard=shard, n_shards=n_shards, collect_stats=level)
+                f.copy_(film)
+            distributed.render_frame(shard_to_host, host_film, rank, world, dist)
+            film.copy_(host_film)
 
     for _ in range(args.warmup):
         step(1)
@@ -236,6 +247,8 @@ def main():
             "data": "synthetic hair (seeded, BINARY_HAIR; reference hair blobs absent) lit by the scene's sunsky (Hosek-Wilkie sky + Preetham sun rasterised like sunsky.cpp)",
             "config": {"workload": workload,
                        "paths_per_step": W * H * spp, "parallelism": "tiles%d" % world,
+                       **({"rehearsal": "HPT_BENCH_BACKEND=gloo: ranks share GPUs, host-copy reduce"}
+                          if host_film is not None and world > 1 else {}),
                        "kd_nodes": int(info.kd_nodes), "kd_depth": int(info.kd_depth),
                        "prepare_s": round(t_prep, 3)},
             # bound: the roofline the kernel is priced against (HBM: no dense contraction here);
