@@ -3,7 +3,7 @@
  * path (ja5087/cs184-final-project-mitsuba0.5).
  *
  * TEST INFRASTRUCTURE ONLY: loaded by tests/, __graft_entry__.smoke() and the
- * cpu_baseline leg of bench.py, never by the product.  Partially pinned (see
+ * cpu_baseline leg of bench.py, never by the product.  Pinned by independent restatements (see
  * oracle.h); where it is not pinned it follows the cited reference lines
  * statement by statement, in single precision, without fused multiply-adds.
  *

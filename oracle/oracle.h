@@ -6,17 +6,21 @@
  * cpu_baseline leg of bench.py may load liboracle*.so.  The product
  * (cs184-final-project-mitsuba0.5_amd/) never links, loads or calls this code.
  *
- * Pinning status: partially pinned.
+ * Pinning status:
  *   - GaussLegendre<140> nodes/weights and InterpolatedDistribution1D warps are
  *     pinned against golden vectors produced by compiling the reference's own
  *     headers (src/bsdfs/gausssexylingerie.hpp, InterpolatedDistribution1D.hpp)
  *     with oracle/_ref/Makefile.
- *   - The Sobol sampler is pinned structurally ((0,2)-stratification of
- *     look_up, van der Corput dim 0) over the reference's own tables.
- *   - Everything else (Marschner / Kajiya-Kay, hair intersection, envmap,
- *     MIPathTracer::Li, splat) is a line-by-line restatement whose parity with
- *     the reference binary is UNPINNED: the reference needs Boost/Xerces/...
- *     and cannot be built in this image.
+ *   - The Sobol sampler is pinned by known answers and (0,2)-stratification
+ *     over the reference's own tables.
+ *   - Everything else on the path (hair loader incl. SFMT reduction, hair
+ *     intersection, Marschner eval / sample, Kajiya-Kay eval, envmap sampling /
+ *     eval / pdf / EWA, sunsky, MIP pyramid, camera, MIPathTracer::Li and the
+ *     tent splat) is pinned by independent numpy restatements written from the
+ *     reference sources (tests/test_independent_pins.py, test_camera.py), not
+ *     by the reference binary: it needs Boost/Xerces/... and cannot be built in
+ *     this image.  roughplastic is pinned only
+ *     statistically (chi-square, tests/test_oracle_bsdf.py).
  */
 #ifndef HAIRPT_ORACLE_H
 #define HAIRPT_ORACLE_H
