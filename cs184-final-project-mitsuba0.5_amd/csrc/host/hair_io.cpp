@@ -205,9 +205,12 @@ HairData loadHair(const std::string &path, float radius, float angleThresholdDeg
     if (!f) throw std::runtime_error("cannot open hair file \"" + path + "\"");
     std::vector<char> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
 
+    /* the reference reads an 11-byte header before deciding the format (hair.cpp:641-646);
+       FileStream::read throws on a shorter file (fstream.cpp:317-327), ASCII or not */
+    if (buf.size() < 11) throw std::runtime_error("truncated hair file \"" + path + "\" (shorter than the 11-byte header)");
     HairData out;
     Builder b{out.xyz, out.starts, dpThresh};
-    if (buf.size() >= 11 && std::memcmp(buf.data(), "BINARY_HAIR", 11) == 0) {
+    if (std::memcmp(buf.data(), "BINARY_HAIR", 11) == 0) {
         if (buf.size() < 15) throw std::runtime_error("truncated hair file \"" + path + "\"");
         uint32_t vertexCount;
         std::memcpy(&vertexCount, buf.data() + 11, 4);

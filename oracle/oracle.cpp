@@ -2699,7 +2699,9 @@ int orc_load_hair_reduced(orc_scene *s, const char *path, float radius, float an
         }
         newFiber = false;
     };
-    if (buf.size() >= 11 && std::memcmp(buf.data(), "BINARY_HAIR", 11) == 0) {
+    /* hair.cpp:641-646 reads 11 header bytes first; FileStream::read throws on EOF (fstream.cpp:317) */
+    if (buf.size() < 11) { s->err = "truncated hair file (shorter than the 11-byte header)"; return -1; }
+    if (std::memcmp(buf.data(), "BINARY_HAIR", 11) == 0) {
         if (buf.size() < 15) { s->err = "truncated hair file"; return -1; }
         uint32_t vertexCount;
         std::memcpy(&vertexCount, buf.data() + 11, 4);

@@ -129,3 +129,23 @@ def test_unlimited_depth_delta_only():
     m = scene_util.l2_metrics(native.develop(ofilm), native.develop(film))
     print("unlimited depth: path-bounces", st.bounces, "max bounce launches", st.max_bounces, m)
     assert m["rmse"] < 1e-3, m
+
+
+def test_zero_segment_hair_renders_environment(tmp_path):
+    """A hair file of single-vertex strands loads with zero segments (hair.cpp:663-716):
+    the kd-tree is one empty leaf with an inverted AABB, every ray misses, nothing
+    faults, and the film is the environment alone."""
+    path = str(tmp_path / "singles.txt")
+    open(path, "wb").write(b"1 2 3\n\n4 5 6\n\n7 8 9\n")
+    r = native.Renderer(device=0)
+    r.set_hair_file(path, 0.01, 1.0)
+    r.set_camera(np.eye(4, dtype=np.float32), 40, 16, 16)
+    r.set_kajiyakay((0.2, 0.2, 0.2))
+    r.set_sunsky((0, 1, 0))
+    r.prepare()
+    assert r.info().segments == 0
+    film = r.render(0, 4)
+    assert np.all(np.isfinite(film)) and np.all(film[..., 3] > 0)
+    assert film[..., :3].max() > 0
+    st = r.stats()
+    assert st.prims == 0

@@ -417,3 +417,33 @@ def test_hair_reduction_matches_oracle(tmp_path, binary):
     np.testing.assert_array_equal(np.array(info.aabb_max), mx)
     with pytest.raises(native.HairPTError, match="reduction"):
         r.set_hair_file(path, 0.01, 1.0, reduction=1.0)
+
+
+def test_hair_file_edge_cases(tmp_path):
+    """hair.cpp:641-646 reads an 11-byte header before choosing the format, and
+    FileStream::read throws on a shorter file (fstream.cpp:317-327): an empty or
+    5-byte hair file is refused by both the product and the oracle.  A file of
+    single-vertex strands loads with zero segments (the reference then builds an
+    empty kd-tree and every ray misses)."""
+    cases = {"empty.txt": b"", "short.txt": b"1 2 3", "singles.txt": b"1 2 3\n\n4 5 6\n\n7 8 9\n"}
+    for name, content in cases.items():
+        path = str(tmp_path / name)
+        open(path, "wb").write(content)
+        o = oracle_lib.Oracle()
+        rc = o.lib.orc_load_hair(o.s, path.encode(), 0.01, 1.0, None)
+        r = native.Renderer(device=native.HOST_ONLY)
+        r.set_hair_file(path, 0.01, 1.0)
+        # the product loads at prepare(): a minimal scene around the hair
+        r.set_camera(np.eye(4, dtype=np.float32), 40, 8, 8)
+        r.set_kajiyakay((0.2, 0.2, 0.2))
+        r.set_sunsky((0, 1, 0))
+        if len(content) < 11:
+            assert rc != 0
+            with pytest.raises(native.HairPTError, match="truncated"):
+                r.prepare()
+        else:
+            assert rc == 0 and o.lib.orc_hair_vertex_count(o.s) == 3
+            r.prepare()
+            xyz, starts = r.hair()
+            assert len(xyz) == 3 and list(starts[:3]) == [1, 1, 1]
+            assert r.info().segments == 0
