@@ -447,3 +447,44 @@ def test_hair_file_edge_cases(tmp_path):
             xyz, starts = r.hair()
             assert len(xyz) == 3 and list(starts[:3]) == [1, 1, 1]
             assert r.info().segments == 0
+
+
+@pytest.mark.parametrize("reduction", [0.0, 0.4])
+def test_ascii_hair_ragged_lines(tmp_path, reduction):
+    """The ASCII branch of HairShape (hair.cpp:717-772) on ragged input: '#' lines start
+    a strand without a reduction draw, a line that fails `iss >> x >> y >> z` (blank,
+    whitespace, two values, 'nan' / 'inf' tokens, an out-of-range exponent) starts one
+    with a draw, extra values are ignored, CRLF endings and leading '+' parse.  Product
+    == oracle bitwise (both use std::istringstream, the reference's own parser)."""
+    rng = np.random.default_rng(5)
+    lines = []
+    for s in range(60):
+        base = rng.normal(size=3) * 2
+        for k in range(int(rng.integers(2, 9))):
+            p = base + k * 0.05 * rng.normal(size=3)
+            v = " ".join("%.7g" % x for x in p)
+            pick = rng.integers(0, 12)
+            if pick == 0:
+                v += " 4.5"                  # extra value: ignored
+            elif pick == 1:
+                v = "+" + v                   # leading sign
+            elif pick == 2:
+                v += "\r"                     # CRLF line ending
+            lines.append(v)
+        sep = rng.integers(0, 8)
+        lines.append(["", "   ", "# comment", "1.0 2.0", "nan 1 2", "inf 0 0", "1e99999 0 0", "#"][sep])
+    path = str(tmp_path / "ragged.txt")
+    open(path, "w").write("\n".join(lines) + "\n")
+    r = native.Renderer(device=native.HOST_ONLY)
+    r.set_hair_file(path, 0.01, 1.0, reduction=reduction)
+    r.set_camera(np.eye(4, dtype=np.float32), 40, 8, 8)
+    r.set_kajiyakay((0.2, 0.2, 0.2))
+    r.set_sunsky((0, 1, 0))
+    r.prepare()
+    o = oracle_lib.Oracle()
+    o.check(o.lib.orc_load_hair_reduced(o.s, path.encode(), 0.01, 1.0, reduction, None))
+    pxyz, pst = r.hair()
+    oxyz, ost = o.hair()
+    assert len(pxyz) > 50
+    np.testing.assert_array_equal(pxyz, oxyz)
+    np.testing.assert_array_equal(pst, ost)
