@@ -1179,6 +1179,22 @@ int hpt_get_marschner_tables(hpt_context *c, float *nR, float *nTT, float *nTRT,
     return HPT_OK;
 }
 
+int hpt_get_roughplastic_params(hpt_context *c, float *params, float *trans, int *trans_size) {
+    if (!c || !c->prepared || c->sc.bsdf.kind != HPT_BSDF_ROUGHPLASTIC || c->rp.empty())
+        return setErr(c, HPT_ESTATE, "no roughplastic bsdf prepared");
+    const RoughPlasticHost &h = c->rp[c->desc.shapes.empty() ? 0 : c->desc.shapes[0].bsdf];
+    const HptRoughPlastic &p = h.p;
+    if (params) {
+        const float v[16] = {(float) p.type, (float) p.sampleVisible, (float) p.nonlinear, p.alpha, p.exponent, p.eta,
+                             p.invEta2, p.specularSamplingWeight, p.diffuse[0], p.diffuse[1], p.diffuse[2],
+                             p.specular[0], p.specular[1], p.specular[2], p.fdr, (float) h.trans.size()};
+        std::memcpy(params, v, sizeof(v));
+    }
+    if (trans_size) *trans_size = (int) h.trans.size();
+    if (trans) std::memcpy(trans, h.trans.data(), h.trans.size() * 4);
+    return HPT_OK;
+}
+
 /* ---- batch helpers ---- */
 } /* extern "C" */
 namespace {

@@ -98,6 +98,7 @@ SIGNATURES = {
     "hpt_get_kdtree": (C.c_int, [C.c_void_p, _u32, _i64, _u32, _i64, _f]),
     "hpt_get_envmap": (C.c_int, [C.c_void_p, _f, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hpt_get_marschner_tables": (C.c_int, [C.c_void_p, _f, _f, _f, _f, _f, _f]),
+    "hpt_get_roughplastic_params": (C.c_int, [C.c_void_p, _f, _f, C.POINTER(C.c_int)]),
     "hpt_get_camera": (C.c_int, [C.c_void_p, _f, _f, _f]),
     "hpt_sobol_batch": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u32, _u32, _u32, _u32, _u64, _f]),
     "hpt_env_eval_filtered": (C.c_int, [C.c_void_p, C.c_int, _f, _f, _f, _f]),
@@ -326,6 +327,18 @@ class Renderer:
         self._check(self.lib.hpt_get_marschner_tables(self.h, _p(t[0], _f), _p(t[1], _f), _p(t[2], _f), _p(fdr, _f),
                                                       _p(tr, _f), _p(sw, _f)))
         return t, float(fdr[0]), tr, float(sw[0])
+
+    def roughplastic_params(self):
+        """(params dict, external rough-transmittance slice) of the prepared roughplastic BSDF"""
+        v = np.zeros(16, np.float32)
+        n = C.c_int()
+        self._check(self.lib.hpt_get_roughplastic_params(self.h, _p(v, _f), None, C.byref(n)))
+        tr = np.zeros(n.value, np.float32)
+        self._check(self.lib.hpt_get_roughplastic_params(self.h, None, _p(tr, _f), C.byref(n)))
+        keys = ("type", "sample_visible", "nonlinear", "alpha", "exponent", "eta", "inv_eta2", "spec_weight")
+        d = {k: float(x) for k, x in zip(keys, v[:8])}
+        d.update(diffuse=v[8:11].copy(), specular=v[11:14].copy(), fdr=float(v[14]))
+        return d, tr
 
     # ---- batch kernels ----
     def sobol(self, m, frame, px, py, dim):

@@ -208,6 +208,11 @@ int hpt_get_envmap(hpt_context *ctx, float *rgb, int *w, int *h);
 int hpt_get_camera(hpt_context *ctx, float sample_to_camera[16], float dx[3], float dy[3]);
 int hpt_get_marschner_tables(hpt_context *ctx, float *n_r, float *n_tt, float *n_trt, float *fdr, float *trans100,
                              float *spec_weight);
+/* RoughPlastic's configured state (roughplastic.cpp:197-296, rtrans.h): params[16] =
+   {type (0 beckmann, 1 ggx, 2 phong), sampleVisible, nonlinear, alpha, phong exponent, eta,
+   1/eta^2, specularSamplingWeight, diffuse rgb, specular rgb, Fdr = 1 - internal diffuse
+   transmittance, trans size}; trans = the external rough-transmittance slice at (eta, alpha) */
+int hpt_get_roughplastic_params(hpt_context *ctx, float *params, float *trans, int *trans_size);
 
 /* ---- per-function batch kernels (host arrays in/out, run on the device) ---- */
 /* sobol::look_up + sobol::sampleSingle (src/samplers/sobolseq.h:43-131) */

@@ -1500,3 +1500,116 @@ def test_env_filtered_independent_pin():
 def test_env_filtered_independent_pin_gpu():
     _, r, _ = scene_util.make("furball_marschner", 300, 16, 16, 1, device=0)
     _env_filtered_pin(r, None)
+
+
+# ---------------------------------------------------------------------------
+# RoughPlastic::eval (roughplastic.cpp:324-375) in float32 numpy: the GGX
+# MicrofacetDistribution::eval with its M_PI-in-double denominator and 1e-20
+# cut (microfacet.h:191-236), smithG1 with hypot2 (:477-522, math.cpp:74-86),
+# fresnelDielectricExt (util.cpp:651-680), the rough-transmittance slice of the
+# Marschner pin, Fdr and the (non)linear diffuse term.  The slice and Fdr come
+# from the engine's configured state (rtrans.h tables, shared with Marschner).
+# ---------------------------------------------------------------------------
+def _hypot2_vec(a, b):
+    f = np.float32
+    a, b = np.asarray(a, f), np.asarray(b, f)
+    big = np.abs(a) > np.abs(b)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ra, rb = b / a, a / b
+        ha = np.abs(a) * np.sqrt(f(1) + ra * ra)
+        hb = np.abs(b) * np.sqrt(f(1) + rb * rb)
+    return np.where(big, ha, np.where(b != 0, hb, f(0))).astype(f)
+
+
+def _fresnel_ext_f32(cos_i, eta):
+    f = np.float32
+    eta = f(eta)
+    scale = np.where(cos_i > 0, f(1) / eta, eta)
+    ct2 = f(1) - (f(1) - cos_i * cos_i) * (scale * scale)
+    ci = np.abs(cos_i)
+    with np.errstate(invalid="ignore"):
+        ct = np.sqrt(ct2)
+    rs = (ci - eta * ct) / (ci + eta * ct)
+    rp = (eta * ci - ct) / (eta * ci + ct)
+    return np.where(ct2 <= 0, f(1), f(0.5) * (rs * rs + rp * rp)).astype(f)
+
+
+def _ggx_smith_g1(v, m, alpha):
+    f = np.float32
+    temp = f(1) - v[:, 2] * v[:, 2]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tan = np.abs(np.where(temp <= 0, f(0), np.sqrt(np.maximum(temp, f(0))) / v[:, 2]))
+    g = f(2) / (f(1) + _hypot2_vec(np.ones_like(tan), f(alpha) * tan))
+    g = np.where(tan == 0, f(1), g)
+    return np.where(_dot(v, m) * v[:, 2] <= 0, f(0), g).astype(f)
+
+
+def _roughplastic_eval_np(wi, wo, p, trans):
+    f = np.float32
+    a = f(p["alpha"])
+    h = wo + wi
+    h = h * (f(1) / np.sqrt(_dot(h, h)))[:, None]
+    ct2 = h[:, 2] * h[:, 2]
+    with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
+        bexp = ((h[:, 0] * h[:, 0]) / (a * a) + (h[:, 1] * h[:, 1]) / (a * a)) / ct2
+        root = (f(1) + bexp) * ct2
+        D = (1.0 / (np.pi * np.float64(a) * np.float64(a) * root.astype(np.float64) * root.astype(np.float64))).astype(f)
+    D = np.where(h[:, 2] <= 0, f(0), D)
+    D = np.where(D * h[:, 2] < f(1e-20), f(0), D)
+    F = _fresnel_ext_f32(_dot(wi, h), p["eta"])
+    G = _ggx_smith_g1(wi, h, a) * _ggx_smith_g1(wo, h, a)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        value = F * D * G / (f(4) * wi[:, 2])
+    res = np.asarray(p["specular"], f)[None, :] * value[:, None]
+    diff = np.asarray(p["diffuse"], f)[None, :]
+    t12, t21 = _rough_trans_np(wi[:, 2], trans), _rough_trans_np(wo[:, 2], trans)
+    fdr = f(p["fdr"])
+    if p["nonlinear"]:
+        diff = diff / (f(1) - diff * fdr)
+    else:
+        diff = diff * (f(1) / (f(1) - fdr))
+    res = res + diff * (f(1 / np.pi) * wo[:, 2] * t12 * t21 * f(p["inv_eta2"]))[:, None]
+    ok = (wi[:, 2] > 0) & (wo[:, 2] > 0)
+    return np.where(ok[:, None], res, f(0)).astype(f)
+
+
+def _roughplastic_pin(r, o, nonlinear):
+    if nonlinear:
+        dif, spec = (0.143016, 0.0156076, 1.80928e-05), (1.0, 1.0, 1.0)
+        r.set_roughplastic(1.55, 1.0, 1, 0.2, True, True, dif, spec)
+        r.prepare()
+        if o is not None:
+            o.set_roughplastic({"eta": np.float32(1.55) / np.float32(1.0), "distribution": "ggx", "alpha": 0.2,
+                                "sample_visible": True, "nonlinear": True, "diffuse": dif, "specular": spec})
+    p, trans = r.roughplastic_params()
+    assert int(p["type"]) == 1 and bool(p["nonlinear"]) == nonlinear       # GGX (models/furball/scene.xml:31-38)
+    rng = np.random.default_rng(43)
+    n = 20000
+    wi = rng.normal(size=(n, 3))
+    wo = rng.normal(size=(n, 3))
+    wi = (wi / np.linalg.norm(wi, axis=1, keepdims=True)).astype(np.float32)
+    wo = (wo / np.linalg.norm(wo, axis=1, keepdims=True)).astype(np.float32)
+    wi[:, 2], wo[:, 2] = np.abs(wi[:, 2]), np.where(np.arange(n) % 5 == 0, wo[:, 2], np.abs(wo[:, 2]))
+    want = _roughplastic_eval_np(wi, wo, p, trans.astype(np.float32))
+    got = o.bsdf_eval(wi, wo)[0] if o is not None else r.bsdf(wi, wo, np.zeros((n, 2), np.float32))[0]
+    assert (want.max(axis=1) > 0).mean() > 0.5
+    scale = np.maximum(np.abs(want).max(axis=1, keepdims=True), 1e-6)
+    err = np.abs(got - want) / scale
+    print("roughplastic pin: q99", np.quantile(err, 0.99), "max", err.max(), "bitwise", np.mean(err == 0))
+    if o is not None:
+        assert err.max() < 2e-6                  # measured: 80 % bitwise, max 3.8e-7
+    assert np.quantile(err, 0.99) < 2e-5
+    assert err.max() < 5e-4                      # GPU: ocml ulps as in test_bsdf_matches_oracle
+
+
+@pytest.mark.parametrize("nonlinear", [False, True])
+def test_roughplastic_eval_independent_pin(nonlinear):
+    _, r, o = scene_util.make("furball_roughplastic", 300, 16, 16, 1)
+    _roughplastic_pin(r, o, nonlinear)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nonlinear", [False, True])
+def test_roughplastic_eval_independent_pin_gpu(nonlinear):
+    _, r, _ = scene_util.make("furball_roughplastic", 300, 16, 16, 1, device=0)
+    _roughplastic_pin(r, None, nonlinear)
