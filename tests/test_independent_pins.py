@@ -1613,3 +1613,54 @@ def test_roughplastic_eval_independent_pin(nonlinear):
 def test_roughplastic_eval_independent_pin_gpu(nonlinear):
     _, r, _ = scene_util.make("furball_roughplastic", 300, 16, 16, 1, device=0)
     _roughplastic_pin(r, None, nonlinear)
+
+
+# ---------------------------------------------------------------------------
+# ThinDielectric::sample with pdf (thindielectric.cpp:203-252): R from
+# fresnelDielectricExt(|cos|), the internal-reflection series R + T^2 R / (1 - R^2),
+# reflect (-x, -y, z) / transmit (-wi) (:144-151), weights and pdfs, in float32
+# numpy; models/straight-hair/scene_thindielectric.xml (eta 1.55, both colours
+# the hair diffuse).
+# ---------------------------------------------------------------------------
+def _thin_sample_np(wi, u, eta, spec_r, spec_t):
+    f = np.float32
+    R = _fresnel_ext_f32(np.abs(wi[:, 2]), eta)
+    T = f(1) - R
+    R = np.where(R < 1, R + T * T * R / (f(1) - R * R), R).astype(f)
+    refl = u[:, 0] <= R
+    wo = np.where(refl[:, None], wi * np.array([-1, -1, 1], f), -wi).astype(f)
+    w = np.where(refl[:, None], np.asarray(spec_r, f)[None, :], np.asarray(spec_t, f)[None, :])
+    pdf = np.where(refl, R, f(1) - R).astype(f)
+    return wo, w.astype(f), pdf
+
+
+def _thin_pin(r, o):
+    rng = np.random.default_rng(47)
+    n = 20000
+    wi = rng.normal(size=(n, 3))
+    wi = (wi / np.linalg.norm(wi, axis=1, keepdims=True)).astype(np.float32)
+    u = rng.random((n, 2)).astype(np.float32)
+    col = (0.143016, 0.0156076, 1.80928e-05)
+    want_wo, want_w, want_pdf = _thin_sample_np(wi, u, np.float32(1.55) / np.float32(1), col, col)
+    if o is not None:
+        got_wo, got_w, got_pdf, _ = o.bsdf_sample(wi, u)
+    else:
+        _, _, got_wo, got_w, got_pdf, _ = r.bsdf(wi, np.zeros_like(wi), u)
+    refl = (want_wo[:, 2] == wi[:, 2])
+    assert 0.02 < refl.mean() < 0.5
+    # the reflect / transmit choice compares u.x with R: an ulp of the GPU's sqrt can flip it
+    agree = np.all(got_wo == want_wo, axis=1)
+    assert agree.mean() >= (1.0 if o is not None else 0.999), agree.mean()
+    np.testing.assert_array_equal(got_w[agree], want_w[agree])
+    np.testing.assert_allclose(got_pdf[agree], want_pdf[agree], rtol=1e-6 if o is not None else 2e-6, atol=1e-7)
+
+
+def test_thindielectric_sample_independent_pin():
+    _, r, o = scene_util.make("straight_thindielectric", 200, 16, 16, 1)
+    _thin_pin(r, o)
+
+
+@pytest.mark.gpu
+def test_thindielectric_sample_independent_pin_gpu():
+    _, r, _ = scene_util.make("straight_thindielectric", 200, 16, 16, 1, device=0)
+    _thin_pin(r, None)
