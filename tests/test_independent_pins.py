@@ -1664,3 +1664,61 @@ def test_thindielectric_sample_independent_pin():
 def test_thindielectric_sample_independent_pin_gpu():
     _, r, _ = scene_util.make("straight_thindielectric", 200, 16, 16, 1, device=0)
     _thin_pin(r, None)
+
+
+# ---------------------------------------------------------------------------
+# MarschnerDielectric::sample with pdf (marschnerdielectric.cpp:424-506): the
+# specular / diffuse split by m_specularSamplingWeight = (s + t) / (d + s + t)
+# luminances (:207-210) with the sample rescaled, the thin-dielectric choice on
+# the specular side, squareToCosineHemisphere on the diffuse side whose weight
+# is eval / pdf = 0 (eval under ESolidAngle is zero: its reflection and
+# transmission flags need EDiscrete, :245-300).
+# ---------------------------------------------------------------------------
+def _md_pin(r, o):
+    f = np.float32
+    rng = np.random.default_rng(53)
+    n = 20000
+    wi = rng.normal(size=(n, 3))
+    wi = (wi / np.linalg.norm(wi, axis=1, keepdims=True)).astype(f)
+    wi[:, 2] = np.abs(wi[:, 2])
+    u = rng.random((n, 2)).astype(f)
+    col = np.array([0.143016, 0.0156076, 1.80928e-05], f)
+    lum = col[0] * f(0.212671) + col[1] * f(0.715160) + col[2] * f(0.072169)
+    ws = (lum + lum) / (lum + lum + lum)
+    spec = u[:, 0] <= ws
+    us = np.where(spec, u[:, 0] / ws, (u[:, 0] - ws) / (f(1) - ws)).astype(f)
+    u2 = np.stack([us, u[:, 1]], axis=1)
+    t_wo, t_w, t_pdf = _thin_sample_np(wi, u2, f(1.55) / f(1), col, col)
+    # diffuse side: squareToCosineHemisphere (warp.cpp:43-52, 81-102)
+    r1, r2 = f(2) * us - f(1), f(2) * u[:, 1] - f(1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        phi_a = (np.pi / 4.0 * (r2 / r1).astype(np.float64)).astype(f)
+        phi_b = (np.pi / 2.0 - (r1 / r2).astype(np.float64) * (np.pi / 4.0)).astype(f)
+    first = r1 * r1 > r2 * r2
+    rr, ph = np.where(first, r1, r2), np.where(first, phi_a, phi_b)
+    px, py = rr * np.cos(ph), rr * np.sin(ph)
+    z = np.sqrt(np.maximum(f(1) - px * px - py * py, f(0)))
+    d_wo = np.stack([px, py, np.where(z == 0, f(1e-10), z)], axis=1).astype(f)
+    want_wo = np.where(spec[:, None], t_wo, d_wo)
+    want_w = np.where(spec[:, None], t_w, f(0))
+    if o is not None:
+        got_wo, got_w, got_pdf, _ = o.bsdf_sample(wi, u)
+    else:
+        _, _, got_wo, got_w, got_pdf, _ = r.bsdf(wi, np.zeros_like(wi), u)
+    assert 0.5 < spec.mean() < 0.8
+    dirs = np.all(np.abs(got_wo - want_wo) <= 2e-6, axis=1)
+    assert dirs.mean() >= (0.9999 if o is not None else 0.999), dirs.mean()
+    np.testing.assert_array_equal(got_w[dirs], want_w[dirs])
+    sp = spec & dirs
+    np.testing.assert_allclose(got_pdf[sp], t_pdf[sp], rtol=2e-6, atol=1e-7)
+
+
+def test_marschnerdielectric_sample_independent_pin():
+    _, r, o = scene_util.make("straight_dielectric", 200, 16, 16, 1)
+    _md_pin(r, o)
+
+
+@pytest.mark.gpu
+def test_marschnerdielectric_sample_independent_pin_gpu():
+    _, r, _ = scene_util.make("straight_dielectric", 200, 16, 16, 1, device=0)
+    _md_pin(r, None)
