@@ -15,6 +15,8 @@ within float32 rounding:
     from the reference's GaussLegendre<140> (pinned separately by golden
     vectors in test_oracle_golden.py).
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -1722,3 +1724,79 @@ def test_marschnerdielectric_sample_independent_pin():
 def test_marschnerdielectric_sample_independent_pin_gpu():
     _, r, _ = scene_util.make("straight_dielectric", 200, 16, 16, 1, device=0)
     _md_pin(r, None)
+
+
+# ---------------------------------------------------------------------------
+# SmoothDiffuse (diffuse.cpp:110-150): eval = R / pi * cos(wo), pdf = cos(wo) / pi
+# (squareToCosineHemispherePdf), sample = squareToCosineHemisphere with weight R.
+# ---------------------------------------------------------------------------
+_DIFFUSE_R = (0.5, 0.3, 0.2)
+
+
+def _cosine_hemisphere_np(u):
+    f = np.float32
+    r1, r2 = f(2) * u[:, 0] - f(1), f(2) * u[:, 1] - f(1)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        phi_a = (np.pi / 4.0 * (r2 / r1).astype(np.float64)).astype(f)
+        phi_b = (np.pi / 2.0 - (r1 / r2).astype(np.float64) * (np.pi / 4.0)).astype(f)
+    first = r1 * r1 > r2 * r2
+    rr, ph = np.where(first, r1, r2), np.where(first, phi_a, phi_b)
+    zero = (r1 == 0) & (r2 == 0)
+    rr, ph = np.where(zero, f(0), rr), np.where(zero, f(0), ph)
+    px, py = rr * np.cos(ph), rr * np.sin(ph)
+    z = np.sqrt(np.maximum(f(1) - px * px - py * py, f(0)))
+    return np.stack([px, py, np.where(z == 0, f(1e-10), z)], axis=1).astype(f)
+
+
+def _diffuse_pin(eval_fn, sample_fn):
+    f = np.float32
+    rng = np.random.default_rng(59)
+    n = 20000
+    wi = rng.normal(size=(n, 3))
+    wo = rng.normal(size=(n, 3))
+    wi = (wi / np.linalg.norm(wi, axis=1, keepdims=True)).astype(f)
+    wo = (wo / np.linalg.norm(wo, axis=1, keepdims=True)).astype(f)
+    u = rng.random((n, 2)).astype(f)
+    R = np.asarray(_DIFFUSE_R, f)
+    ok = (wi[:, 2] > 0) & (wo[:, 2] > 0)
+    want_e = np.where(ok[:, None], R[None, :] * (f(1 / np.pi) * wo[:, 2])[:, None], f(0))
+    want_p = np.where(ok, f(1 / np.pi) * wo[:, 2], f(0))
+    got_e, got_p = eval_fn(wi, wo)
+    np.testing.assert_allclose(got_e, want_e, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(got_p, want_p, rtol=1e-6, atol=1e-9)
+    up = wi[:, 2] > 0
+    want_wo = _cosine_hemisphere_np(u)
+    got_wo, got_w, got_sp = sample_fn(wi, u)
+    np.testing.assert_allclose(got_wo[up], want_wo[up], rtol=1e-5, atol=5e-6)  # sinf / cosf ulps
+    np.testing.assert_array_equal(got_w[up], np.broadcast_to(R, got_w[up].shape))
+    # pdf of the direction actually returned (its z carries the sinf / cosf ulps above)
+    np.testing.assert_allclose(got_sp[up], f(1 / np.pi) * got_wo[up, 2], rtol=2e-6, atol=1e-9)
+
+
+def test_diffuse_independent_pin():
+    _, _, o = scene_util.make("furball_marschner", 200, 16, 16, 1)
+    refl = np.asarray(_DIFFUSE_R, np.float32)
+    o.check(o.lib.orc_set_diffuse(o.s, refl.ctypes.data_as(ctypes.POINTER(ctypes.c_float))))
+    _diffuse_pin(lambda wi, wo: o.bsdf_eval(wi, wo), lambda wi, u: o.bsdf_sample(wi, u)[:3])
+
+
+@pytest.mark.gpu
+def test_diffuse_independent_pin_gpu(tmp_path):
+    xml = scene_util.scenes.make_scene("furball_marschner", str(tmp_path), n_strands=200)
+    src = open(xml).read()
+    i, j = src.index("<bsdf"), src.index("</bsdf>") + len("</bsdf>")
+    src = src[:i] + '<bsdf type="diffuse" id="hair"><rgb name="reflectance" value="0.5, 0.3, 0.2"/></bsdf>' + src[j:]
+    path = str(tmp_path / "diffuse.xml")
+    open(path, "w").write(src)
+    r = native.Renderer(device=0)
+    r.load_scene_xml(path, {"width": 16, "height": 16, "spp": 1})
+    r.prepare()
+
+    def ev(wi, wo):
+        e, p, *_ = r.bsdf(wi, wo, np.zeros((len(wi), 2), np.float32))
+        return e, p
+
+    def sm(wi, u):
+        _, _, wo, w, sp, _ = r.bsdf(wi, np.zeros_like(wi), u)
+        return wo, w, sp
+    _diffuse_pin(ev, sm)
