@@ -19,9 +19,9 @@
  *     tent splat) is pinned by independent numpy restatements written from the
  *     reference sources (tests/test_independent_pins.py, test_camera.py), not
  *     by the reference binary: it needs Boost/Xerces/... and cannot be built in
- *     this image.  roughplastic eval, thindielectric and
- *     marschnerdielectric sampling are pinned the same way; roughplastic sampling
- *     by a chi-square test (tests/test_oracle_bsdf.py).
+ *     this image.  roughplastic eval, thindielectric /
+ *     marschnerdielectric sampling and the diffuse BSDF are pinned the same way;
+ *     roughplastic sampling by a chi-square test (tests/test_oracle_bsdf.py).
  */
 #ifndef HAIRPT_ORACLE_H
 #define HAIRPT_ORACLE_H
