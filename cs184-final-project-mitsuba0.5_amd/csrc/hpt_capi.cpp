@@ -54,6 +54,8 @@ struct hpt_context {
     uint32_t tailPaths = defaultTailPaths();
     bool packets = defaultPackets();
     hipStream_t stream = nullptr;
+    uint32_t *hostCnt = nullptr; /* pinned copy of the counter block */
+    std::vector<uint8_t> scShadow; /* the HptScene last copied to scDev */
     std::string err;
     std::string dataDir;
     SceneDesc desc;
@@ -77,7 +79,8 @@ struct hpt_context {
     uint64_t capacity = 0;
     std::vector<DevBuf> waveBufs;
     HptPaths P;
-    uint32_t *qTrace = nullptr, *qShadow = nullptr, *qShadeA = nullptr, *qShadeB = nullptr;
+    /* rays of the bounce; paths to shade by bounce parity (shadeQ[p] is post's output for p ^ 1) */
+    uint32_t *qTrace = nullptr, *qShadow = nullptr, *qShade[2] = {nullptr, nullptr};
     uint32_t *counters = nullptr;
     uint64_t *dstats = nullptr;
     float4 *partial = nullptr;     /* film splat partials: slots x 9 (k_splat -> k_gather) */
@@ -188,8 +191,8 @@ int ensureWave(hpt_context *c, uint64_t n) {
     r |= alloc(n * 16, (void **) &c->P.scontrib);
     r |= alloc(n * 4, (void **) &c->qTrace);
     r |= alloc(n * 4, (void **) &c->qShadow);
-    r |= alloc(n * 4, (void **) &c->qShadeA);
-    r |= alloc(n * 4, (void **) &c->qShadeB);
+    r |= alloc(n * 4, (void **) &c->qShade[0]);
+    r |= alloc(n * 4, (void **) &c->qShade[1]);
     r |= alloc(HPT_COUNTER_WORDS * 4, (void **) &c->counters);
     r |= alloc(24 * 8, (void **) &c->dstats);
     if (r) return HPT_EDEVICE;
@@ -250,7 +253,8 @@ int hpt_context_create(int device, hpt_context **out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return HPT_EDEVICE;
     hpt_context *c = new hpt_context();
     c->device = device;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void **) &c->hostCnt, HPT_Q_COUNT * 4, hipHostMallocDefault) != hipSuccess) {
         delete c;
         return HPT_EDEVICE;
     }
@@ -276,6 +280,7 @@ void hpt_context_destroy(hpt_context *c) {
     if (c->dLocalOf) (void) hipFree(c->dLocalOf);
     if (c->scDev) (void) hipFree(c->scDev);
     for (auto e : c->evPool) (void) hipEventDestroy(e);
+    (void) hipHostFree(c->hostCnt);
     (void) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -899,7 +904,10 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     }
     hipStream_t s = c->stream;
     if (!c->scDev) HIPCHK(c, hipMalloc((void **) &c->scDev, sizeof(HptScene)));
-    HIPCHK(c, hipMemcpy(c->scDev, &c->sc, sizeof(HptScene), hipMemcpyHostToDevice));
+    if (c->scShadow.size() != sizeof(HptScene) || std::memcmp(c->scShadow.data(), &c->sc, sizeof(HptScene)) != 0) {
+        HIPCHK(c, hipMemcpy(c->scDev, &c->sc, sizeof(HptScene), hipMemcpyHostToDevice));
+        c->scShadow.assign((const uint8_t *) &c->sc, (const uint8_t *) &c->sc + sizeof(HptScene));
+    }
     const bool st = prm->collect_stats != 0;      /* HIP event timing per kernel class */
     const bool counted = prm->collect_stats >= 2; /* + traversal counters (k_trace_counted) */
     if (counted) HIPCHK(c, hipMemsetAsync(c->dstats, 0, 24 * 8, s));
@@ -916,12 +924,13 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         return e;
     };
     if (int rf = clearFault(c)) return rf;
-    uint32_t *hostCnt = nullptr;
-    HIPCHK(c, hipHostMalloc((void **) &hostCnt, HPT_Q_COUNT * 4, hipHostMallocDefault));
+    uint32_t *hostCnt = c->hostCnt;
     uint64_t bounces = 0;
     int maxB = 0;
     /* HPT_TRACE_REPORT=1 with counters on: per-launch traversal counters on stderr */
     const bool perLaunch = counted && std::getenv("HPT_TRACE_REPORT") != nullptr;
+    /* HPT_BOUNCE_REPORT=1 with timing on: per-bounce queue sizes and trace time on stderr */
+    const bool bounceReport = std::getenv("HPT_BOUNCE_REPORT") != nullptr;
     uint64_t prevSt[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prevShadow[2] = {0, 0};
     auto reportLaunch = [&](const char *what) {
         if (!perLaunch) return;
@@ -967,62 +976,75 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         w.localOf = c->dLocalOf;
         c->stats.waves++;
         HIPCHK(c, hipMemsetAsync(c->counters, 0, HPT_COUNTER_WORDS * 4, s));
-        e = timed(0, [&] { return hpt_launch_camera(sc, w, c->P, c->qTrace, c->counters, s); });
+        uint32_t *C = c->counters, *dst = counted ? (uint32_t *) c->dstats : nullptr, *cur = C + HPT_CURSOR_OFFSET;
+        /* the camera pass is bounce 0 (parity 0) */
+        e = timed(0, [&] { return hpt_launch_camera(sc, w, c->P, c->qTrace, C + HPT_C_TRACE(0), s); });
         if (e) break;
         e = c->packets ? timed(6, [&] {
-            return hpt_launch_trace_packet(sc, c->P, c->qTrace, c->counters, counted ? (uint32_t *) c->dstats : nullptr,
-                                           w.nPaths, s);
+            return hpt_launch_trace_packet(sc, c->P, c->qTrace, C + HPT_C_TRACE(0), cur, dst, w.nPaths, s);
         })
                        : timed(-1, [&] {
-                             return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, c->counters,
-                                                     counted ? (uint32_t *) c->dstats : nullptr, w.nPaths, s);
+                             return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(0),
+                                                     C + HPT_C_SHADOW(0), cur, dst, w.nPaths, s);
                          });
         if (e) break;
         reportLaunch("camera");
-        e = timed(1, [&] { return hpt_launch_primary(sc, c->P, c->qTrace, c->qShadeA, c->counters, w.nPaths, s); });
+        e = hpt_launch_clear(C, 0, s);
         if (e) break;
-        e = hpt_launch_rotate(c->counters, s);
-        uint32_t *shadeIn = c->qShadeA, *shadeOut = c->qShadeB;
+        e = timed(1, [&] {
+            return hpt_launch_primary(sc, c->P, c->qTrace, C + HPT_C_TRACE(0), c->qShade[1], C + HPT_C_SHADE(1), w.nPaths, s);
+        });
+        if (e) break;
+        /* bounce b (parity p): shade -> trace -> clear -> post, one host sync per bounce for
+           the queue length (grid sizes, the switch to k_tail) */
         int bounce = 0;
-        while (e == hipSuccess) {
-            e = hipMemcpyAsync(hostCnt, c->counters, HPT_Q_COUNT * 4, hipMemcpyDeviceToHost, s);
+        for (int b = 1; e == hipSuccess; ++b) {
+            const uint32_t p = (uint32_t) b & 1u, q = p ^ 1u;
+            e = hipMemcpyAsync(hostCnt, C, HPT_Q_COUNT * 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e) break;
-            e = hipStreamSynchronize(s);
-            if (e) break;
-            const uint32_t n = hostCnt[HPT_Q_SHADE_IN];
+            const uint32_t n = hostCnt[HPT_C_SHADE(p)];
             if (n == 0) break;
-            bounces += n;
             ++bounce;
             if (n < c->tailPaths) {
                 /* few live paths: finish them all in one launch (k_tail) */
-                e = timed(5, [&] { return hpt_launch_tail(sc, c->P, shadeIn, c->counters, n, s); });
+                e = timed(5, [&] { return hpt_launch_tail(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), C, n, s); });
                 if (e) break;
-                e = hipMemcpyAsync(hostCnt, c->counters, HPT_Q_COUNT * 4, hipMemcpyDeviceToHost, s);
+                e = hipMemcpyAsync(hostCnt, C, HPT_Q_COUNT * 4, hipMemcpyDeviceToHost, s);
+                if (e == hipSuccess) e = hipStreamSynchronize(s);
                 if (e) break;
-                e = hipStreamSynchronize(s);
-                if (e) break;
-                bounces += hostCnt[HPT_Q_TAIL_BOUNCES] - n; /* k_tail counts its first bounce too */
+                bounces += hostCnt[HPT_C_TAIL_BOUNCES]; /* k_tail counts its first bounce too */
                 c->stats.tail_paths += n;
                 break;
             }
-            e = timed(2, [&] { return hpt_launch_shade(sc, c->scDev, c->P, shadeIn, c->qTrace, c->qShadow, c->counters, n, s); });
+            bounces += n;
+            e = timed(2, [&] {
+                return hpt_launch_shade(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), c->qTrace, C + HPT_C_TRACE(p), c->qShadow,
+                                        C + HPT_C_SHADOW(p), C, n, s);
+            });
             if (e) break;
             e = timed(-1, [&] {
-                return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, c->counters,
-                                        counted ? (uint32_t *) c->dstats : nullptr, 2ull * n, s);
+                return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(p), C + HPT_C_SHADOW(p), cur, dst,
+                                        2ull * n, s);
             });
             if (e) break;
             reportLaunch("bounce");
-            e = timed(3, [&] { return hpt_launch_post(sc, c->P, c->qTrace, shadeOut, c->counters, n, s); });
+            if (bounceReport && st && !evTrace.empty()) {
+                float ms = 0;
+                (void) hipStreamSynchronize(s);
+                (void) hipEventElapsedTime(&ms, evTrace.back().first, evTrace.back().second);
+                std::fprintf(stderr, "[bounce %d] shade %u -> trace %.3f ms\n", b, n, ms);
+            }
+            e = hpt_launch_clear(C, p, s);
             if (e) break;
-            e = hpt_launch_rotate(c->counters, s);
-            std::swap(shadeIn, shadeOut);
+            e = timed(3, [&] {
+                return hpt_launch_post(sc, c->P, c->qTrace, C + HPT_C_TRACE(p), c->qShade[q], C + HPT_C_SHADE(q), C, n, s);
+            });
         }
         maxB = std::max(maxB, bounce);
         if (e) break;
-        if (hostCnt[HPT_Q_ERROR]) {
+        if (hostCnt[HPT_C_ERROR]) {
             (void) hipStreamSynchronize(s);
-            (void) hipHostFree(hostCnt);
             return setErr(c, HPT_EINVAL, "Lookup dimension exceeds the direction number table size! You may have "
                                          "to reduce the 'maxDepth' parameter of your integrator.");
         }
@@ -1030,7 +1052,6 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         c->stats.paths += w.nPaths;
     }
     hipError_t e2 = hipStreamSynchronize(s);
-    (void) hipHostFree(hostCnt);
     if (e != hipSuccess || e2 != hipSuccess)
         return setErr(c, HPT_EDEVICE, std::string("render failed: ") + hipGetErrorString(e ? e : e2));
     if (int rf = checkFault(c)) return rf;

@@ -8,21 +8,23 @@
 
 #include "../hpt_device.h"
 
-/* queue counter slots */
-#define HPT_Q_TRACE 0
-#define HPT_Q_SHADOW 1
-#define HPT_Q_SHADE_IN 2
-#define HPT_Q_SHADE_OUT 3
-#define HPT_Q_ERROR 4     /* set when a path runs out of Sobol dimensions */
-#define HPT_Q_TAIL_BOUNCES 5 /* path-bounces shaded inside k_tail */
-#define HPT_Q_COUNT 8
+/* Counter block (uint32 words).  Bounce b uses the slots of parity
+   p = b & 1 (the camera pass is bounce 0); k_clear zeroes the other parity's
+   slots once bounce b's trace launch has run. */
+#define HPT_C_TRACE(p) (0 + (p))  /* closest-hit rays of bounce b (traceQ[p]) */
+#define HPT_C_SHADOW(p) (2 + (p)) /* shadow rays of bounce b (shadowQ[p]) */
+#define HPT_C_SHADE(p) (4 + (p))  /* paths bounce b shades (shadeQ[p]: survivors of the previous post) */
+#define HPT_C_ERROR 12       /* set when a path runs out of Sobol dimensions */
+#define HPT_C_TAIL_BOUNCES 13 /* path-bounces shaded inside k_tail */
+#define HPT_C_TAIL_CURSOR 14  /* k_tail's work claims */
+#define HPT_Q_COUNT 16
 /* HptScene::fault bits: a traversal bound fired (the ray would otherwise end
    with whatever hit it had; the render / batch call fails instead) */
 #define HPT_FAULT_LEAVES 1u   /* more than 2^18 leaf rounds for one ray */
 #define HPT_FAULT_RESTARTS 2u /* more than HPT_MAX_RESTARTS kd-restarts for one ray */
 #define HPT_MAX_RESTARTS 1024
 /* k_trace work cursors (persistent waves claim rays from them), one per
-   128-byte line, stored after the queue counters in the same buffer */
+   128-byte line, stored after the counters in the same buffer */
 #define HPT_CURSORS 64
 #define HPT_CURSOR_STRIDE 32
 #define HPT_CURSOR_OFFSET 64
@@ -67,26 +69,30 @@ struct HptPaths {
 };
 
 
-/* launch wrappers (hpt_render.hip) */
+/* launch wrappers (hpt_render.hip).  Queue lengths are passed as device
+   pointers (the kernels read them; the host only bounds the grids). */
 hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPaths &P, uint32_t *traceQ,
-                             uint32_t *counters, hipStream_t s);
+                             uint32_t *nTrace, hipStream_t s);
+/* one persistent traversal launch: closest-hit rays traceQ[0, *nTrace), shadow rays shadowQ[0, *nShadow) */
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
-                            uint32_t *counters, uint32_t *stats, uint64_t maxItems, hipStream_t s);
+                            const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
+                            uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_env_filtered_batch(const HptScene &sc, int n, const float *d, const float *rx, const float *ry,
                                         float *out, hipStream_t s);
 /* closest-hit rays as 64-ray packets (coherent rays: the camera pass) */
-hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *counters,
-                                   uint32_t *stats, uint64_t maxItems, hipStream_t s);
-hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
-                              uint32_t *counters, uint64_t maxItems, hipStream_t s);
-hipError_t hpt_launch_shade(const HptScene &sc, const HptScene *scDev, const HptPaths &P, const uint32_t *shadeQ, uint32_t *traceQ,
-                            uint32_t *shadowQ, uint32_t *counters, uint64_t maxItems, hipStream_t s);
-/* the rest of every live path (shade queue) to termination in one launch */
-hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *counters,
-                           uint64_t maxItems, hipStream_t s);
-hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
-                           uint32_t *counters, uint64_t maxItems, hipStream_t s);
-hipError_t hpt_launch_rotate(uint32_t *counters, hipStream_t s);
+hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
+                                   uint32_t *cursors, uint32_t *stats, uint64_t maxItems, hipStream_t s);
+hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
+                              uint32_t *shadeQ, uint32_t *nShade, uint64_t maxItems, hipStream_t s);
+hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
+                            uint32_t *traceQ, uint32_t *nTrace, uint32_t *shadowQ, uint32_t *nShadow, uint32_t *counters,
+                            uint64_t maxItems, hipStream_t s);
+hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
+                           uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s);
+/* the rest of every live path (the shade queue) to termination in one launch */
+hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
+                           uint32_t *counters, uint64_t items, hipStream_t s);
+hipError_t hpt_launch_clear(uint32_t *counters, uint32_t parity, hipStream_t s);
 /* k_splat + k_gather; partial = (nPaths / nSpp) * 9 float4 of scratch */
 hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *partial, float4 *film,
                              hipStream_t s);

@@ -373,9 +373,10 @@ template <int STACK> HD uint32_t rayKey(const uint2 *stk, int stride) { return s
 HD uint32_t rayLeaves(const TraceRay &r) { return r.cnt & (HPT_CNT_RESTART - 1u); }
 HD uint32_t rayRestarts(const TraceRay &r) { return r.cnt / HPT_CNT_RESTART; }
 
-template <int STACK, bool STATS>
+template <int STACK, bool STATS, bool LAT = false>
 HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, TraceCounters &tc) {
     static_assert((STACK & (STACK - 1)) == 0, "the ring stack index is masked");
+    static_assert(!(LAT && STATS), "the latency-mode leaf pass keeps no traversal counters");
     const float4 *__restrict__ leafF = reinterpret_cast<const float4 *>(sc.leafF);
     /* the ray as plain values: selecting among struct members by axis would be
        folded into a dynamically addressed load and push the state to scratch */
@@ -499,6 +500,51 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
        prefetched records are dead by then, so the fp64 test's registers do
        not stack on top of them */
     const uint32_t first = leafFirst, last = leafLast;
+    if (LAT) {
+        /* latency mode (k_tail: few waves, registers to spare): every record of a
+           chunk of 8 is requested at once and each candidate's whole fp64 record in
+           one go, so a leaf costs two memory round trips instead of one per record
+           and three per exact test.  Same tests in the same order: identical hits. */
+        for (uint32_t c0 = first; c0 < last; c0 += 8) {
+            const uint32_t n = min(last - c0, 8u);
+            float4 ra[8], rb[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k)
+                if (k < n) {
+                    ra[k] = leafF[2 * (c0 + k)];
+                    rb[k] = leafF[2 * (c0 + k) + 1];
+                }
+            uint32_t mask = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k)
+                if (k < n && segMayHit(ra[k], rb[k], o, d, sc.maxRadius)) mask |= 1u << k;
+            uint32_t segOf[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) segOf[k] = __float_as_uint(rb[k].z);
+            while (mask) {
+                const uint32_t k = (uint32_t) (__ffs(mask) - 1);
+                mask &= mask - 1;
+                uint32_t s = segOf[0];
+#pragma unroll
+                for (uint32_t q = 1; q < 8; ++q) s = k == q ? segOf[q] : s;
+                const float rad = segRadius(sc, s);
+                const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
+                const double *src = reinterpret_cast<const double *>(sc.segs + s);
+                double rec[15];
+#pragma unroll
+                for (int q = 0; q < 15; ++q) rec[q] = src[q];
+                float t;
+                uint32_t far;
+                const float mint = __uint_as_float(stk[(STACK + HPT_ROW_MM) * stride].x);
+                if (segIntersectRec(rec, o, d, r2, mint, r.tHit, t, far)) {
+                    r.found = true;
+                    if (r.shadow) return true;
+                    r.tHit = t;
+                    r.segHit = s | (far << 31);
+                }
+            }
+        }
+    } else
     for (uint32_t c0 = first; c0 < last; c0 += 32) {
         const uint32_t c1 = min(last, c0 + 32);
         uint32_t mask = 0;
@@ -1918,7 +1964,7 @@ HD bool decodePath(const HptWave &w, uint32_t id, int &px, int &py, uint32_t &j)
 
 extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, HptWave w, HptPaths P,
                                                             uint32_t *__restrict__ traceQ,
-                                                            uint32_t *__restrict__ counters) {
+                                                            uint32_t *__restrict__ nTrace) {
     uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = id < w.nPaths;
     int px = 0, py = 0;
@@ -1950,7 +1996,7 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
         P.state[id] = 0xffffffffu; /* outside the image */
         P.li[id] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
-    qpushBlock<HPT_QBLOCK>(valid, id, traceQ, &counters[HPT_Q_TRACE]);
+    qpushBlock<HPT_QBLOCK>(valid, id, traceQ, nTrace);
 }
 
 /* k_trace: the wave's closest-hit rays (traceQ[0, nTrace)) then its any-hit
@@ -2015,21 +2061,24 @@ struct PathIO {
 #define HPT_TRACE_OCCUPANCY
 #endif
 
+/* the queue lengths come from device memory (the launch is enqueued before
+   the host knows them) */
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
-    uint32_t *__restrict__ counters, uint32_t *__restrict__ cursors) {
+    const uint32_t *__restrict__ nTrace, const uint32_t *__restrict__ nShadow, uint32_t *__restrict__ cursors) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    PathIO io{P, traceQ, shadowQ, counters[HPT_Q_TRACE], counters[HPT_Q_SHADOW], 0};
+    PathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0};
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(HptScene sc, HptPaths P,
                                                                               const uint32_t *__restrict__ traceQ,
                                                                               const uint32_t *__restrict__ shadowQ,
-                                                                              uint32_t *__restrict__ counters,
+                                                                              const uint32_t *__restrict__ nTrace,
+                                                                              const uint32_t *__restrict__ nShadow,
                                                                               uint32_t *__restrict__ cursors,
                                                                               uint32_t *stats) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    PathIO io{P, traceQ, shadowQ, counters[HPT_Q_TRACE], counters[HPT_Q_SHADOW], 0};
+    PathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0};
     tracePersistent<HPT_STACK, true>(sc, io, cursors, stk + threadIdx.x, stats);
 }
 
@@ -2041,17 +2090,17 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
 #define HPT_PACKET_BLOCK HPT_TRACE_BLOCK
 #endif
 extern "C" __global__ __launch_bounds__(HPT_PACKET_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_PACKET_WAVES))) void
-k_trace_packet(HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, uint32_t *__restrict__ counters,
+k_trace_packet(HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ nTrace,
                uint32_t *__restrict__ cursors) {
     __shared__ PacketLds lds[HPT_PACKET_BLOCK / 64];
-    PathIO io{P, traceQ, nullptr, counters[HPT_Q_TRACE], 0, 0};
+    PathIO io{P, traceQ, nullptr, *nTrace, 0, 0};
     tracePackets<false>(sc, io, cursors, lds[threadIdx.x >> 6], nullptr);
 }
 extern "C" __global__ __launch_bounds__(HPT_PACKET_BLOCK) void k_trace_packet_counted(
-    HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, uint32_t *__restrict__ counters,
+    HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ nTrace,
     uint32_t *__restrict__ cursors, uint32_t *stats) {
     __shared__ PacketLds lds[HPT_PACKET_BLOCK / 64];
-    PathIO io{P, traceQ, nullptr, counters[HPT_Q_TRACE], 0, 0};
+    PathIO io{P, traceQ, nullptr, *nTrace, 0, 0};
     tracePackets<true>(sc, io, cursors, lds[threadIdx.x >> 6], stats);
 }
 
@@ -2077,10 +2126,11 @@ HD void fillIts(const HptScene &sc, uint32_t seg, V3 hp, V3 rayD, V3 &p, Frame &
 /* primary hits / misses (path.cpp:128-143) */
 extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, HptPaths P,
                                                              const uint32_t *__restrict__ traceQ,
+                                                             const uint32_t *__restrict__ nTrace,
                                                              uint32_t *__restrict__ shadeQ,
-                                                             uint32_t *__restrict__ counters) {
+                                                             uint32_t *__restrict__ nShade) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = counters[HPT_Q_TRACE];
+    const uint32_t n = *nTrace;
     bool alive = false;
     uint32_t id = 0;
     if (tid < n) {
@@ -2101,7 +2151,7 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
             P.li[id] = make_float4(0.0f + c.x, 0.0f + c.y, 0.0f + c.z, 0.0f);
         }
     }
-    qpushBlock<HPT_QBLOCK>(alive, id, shadeQ, &counters[HPT_Q_SHADE_OUT]);
+    qpushBlock<HPT_QBLOCK>(alive, id, shadeQ, nShade);
 }
 
 /* one bounce of shading: path.cpp:145-232 up to the continuation ray cast.
@@ -2126,7 +2176,7 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__rest
                     (sc.strictNormals && dot(rayD, geo.n) * wi.z >= 0);
         if (!stop && dim + 3 >= HPT_SOBOL_DIMS) {
             /* sobol.cpp:236-238 raises "Lookup dimension exceeds the direction number table size" */
-            atomicOr(&counters[HPT_Q_ERROR], 1u);
+            atomicOr(&counters[HPT_C_ERROR], 1u);
             stop = true;
         }
         /* one inlined copy per BSDF source: the scene's own (kernel
@@ -2190,20 +2240,26 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__rest
         P.state[id] = (st & ~HPT_ST_DIM_MASK) | dim;
     }
 }
+/* where a shading launch reads and appends: its shade queue's length, the
+   next trace launch's queue lengths, and the counter block (error word) */
+struct HptShadeIO {
+    const uint32_t *nShade;
+    uint32_t *nTrace, *nShadow, *counters;
+};
 template <bool MULTI>
 __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
                                             uint32_t *__restrict__ traceQ, uint32_t *__restrict__ shadowQ,
-                                            uint32_t *__restrict__ counters) {
+                                            const HptShadeIO &q) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = counters[HPT_Q_SHADE_IN];
+    const uint32_t n = *q.nShade;
     bool cont = false, shadow = false;
     uint32_t id = 0;
     if (tid < n) {
         id = shadeQ[tid];
-        shadePath<MULTI>(sc, P, id, counters, cont, shadow);
+        shadePath<MULTI>(sc, P, id, q.counters, cont, shadow);
     }
-    qpushBlock<HPT_SHADE_BLOCK>(cont, id, traceQ, &counters[HPT_Q_TRACE]);
-    qpushBlock<HPT_SHADE_BLOCK>(shadow, id, shadowQ, &counters[HPT_Q_SHADOW]);
+    qpushBlock<HPT_SHADE_BLOCK>(cont, id, traceQ, q.nTrace);
+    qpushBlock<HPT_SHADE_BLOCK>(shadow, id, shadowQ, q.nShadow);
 }
 #ifndef HPT_SHADE_WAVES
 #define HPT_SHADE_WAVES 0 /* 0: natural allocation (100 VGPRs = 5 waves/SIMD) */
@@ -2216,60 +2272,14 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
 extern "C" __global__ __launch_bounds__(HPT_SHADE_BLOCK) HPT_SHADE_OCCUPANCY void k_shade(HptScene sc, HptPaths P,
                                                            const uint32_t *__restrict__ shadeQ,
                                                            uint32_t *__restrict__ traceQ,
-                                                           uint32_t *__restrict__ shadowQ,
-                                                           uint32_t *__restrict__ counters) {
-    shadeBounce<false>(sc, P, shadeQ, traceQ, shadowQ, counters);
+                                                           uint32_t *__restrict__ shadowQ, HptShadeIO q) {
+    shadeBounce<false>(sc, P, shadeQ, traceQ, shadowQ, q);
 }
-/* k_shade for a single Marschner hair shape with the lobe cdfs / sums staged
-   in LDS (51 KB): persistent blocks (two per CU, 10 waves each = 5 waves per
-   SIMD) stage the tables once and walk the shade queue in block-sized steps,
-   so the staging cost is paid per block, not per path */
-#ifndef HPT_SHADE_LDS_BLOCK
-#define HPT_SHADE_LDS_BLOCK 640
-#endif
-#ifndef HPT_SHADE_LDS_WAVES
-#define HPT_SHADE_LDS_WAVES 5
-#endif
-extern "C" __global__ __launch_bounds__(HPT_SHADE_LDS_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_SHADE_LDS_WAVES))) void k_shade_mlds(const HptScene *scg, HptPaths P,
-                                                                            const uint32_t *__restrict__ shadeQ,
-                                                                            uint32_t *__restrict__ traceQ,
-                                                                            uint32_t *__restrict__ shadowQ,
-                                                                            uint32_t *__restrict__ counters) {
-    /* the scene through a global pointer, not the kernel argument: the loop below would
-       hoist every argument field it touches into scalar registers (they spill) */
-    const HptScene &sc = *scg;
-    __shared__ MarschnerLds T;
-    /* lobe by lobe with uniform pointers (a per-lane index into the kernel argument's
-       pointer arrays would copy the argument to scratch) */
-#pragma unroll
-    for (int l = 0; l < 3; ++l) {
-        const float *cdf = l == 0 ? sc.bsdf.mar.cdf[0] : (l == 1 ? sc.bsdf.mar.cdf[1] : sc.bsdf.mar.cdf[2]);
-        const float *sums = l == 0 ? sc.bsdf.mar.sums[0] : (l == 1 ? sc.bsdf.mar.sums[1] : sc.bsdf.mar.sums[2]);
-        for (uint32_t i = threadIdx.x; i < HPT_CDF_WORDS; i += blockDim.x) T.cdf[l][i] = cdf[i];
-        for (uint32_t i = threadIdx.x; i < HPT_AZ_RES; i += blockDim.x) T.sums[l][i] = sums[i];
-    }
-    __syncthreads();
-    const uint32_t n = counters[HPT_Q_SHADE_IN];
-    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) { /* block-uniform */
-        asm volatile("" ::: "memory"); /* scene fields are re-read per step, not hoisted (scalar loads, cached) */
-        const uint32_t tid = base + threadIdx.x;
-        bool cont = false, shadow = false;
-        uint32_t id = 0;
-        if (tid < n) {
-            id = shadeQ[tid];
-            shadePath<false, true>(sc, P, id, counters, cont, shadow, &T);
-        }
-        qpushBlock<HPT_SHADE_LDS_BLOCK>(cont, id, traceQ, &counters[HPT_Q_TRACE]);
-        qpushBlock<HPT_SHADE_LDS_BLOCK>(shadow, id, shadowQ, &counters[HPT_Q_SHADOW]);
-    }
-}
-
 extern "C" __global__ __launch_bounds__(HPT_SHADE_BLOCK) void k_shade_multi(HptScene sc, HptPaths P,
                                                                  const uint32_t *__restrict__ shadeQ,
                                                                  uint32_t *__restrict__ traceQ,
-                                                                 uint32_t *__restrict__ shadowQ,
-                                                                 uint32_t *__restrict__ counters) {
-    shadeBounce<true>(sc, P, shadeQ, traceQ, shadowQ, counters);
+                                                                 uint32_t *__restrict__ shadowQ, HptShadeIO q) {
+    shadeBounce<true>(sc, P, shadeQ, traceQ, shadowQ, q);
 }
 
 /* continuation result: path.cpp:225-286; true when the path goes on */
@@ -2309,7 +2319,7 @@ HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__restr
             if (hit) {
                 alive = true;
                 if ((int) depth >= sc.rrDepth && dim >= HPT_SOBOL_DIMS) {
-                    atomicOr(&counters[HPT_Q_ERROR], 1u);
+                    atomicOr(&counters[HPT_C_ERROR], 1u);
                     alive = false;
                 } else if ((int) depth >= sc.rrDepth) {
                     float q = fminr(maxc(T) * 1.0f * 1.0f, 0.95f);
@@ -2326,83 +2336,171 @@ HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__restr
     }
     return alive;
 }
+/* continuation results of a bounce (the paths of its trace queue) */
 extern "C" __global__ __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc, HptPaths P,
                                                           const uint32_t *__restrict__ traceQ,
-                                                          uint32_t *__restrict__ shadeQ,
+                                                          const uint32_t *__restrict__ nTrace,
+                                                          uint32_t *__restrict__ shadeQ, uint32_t *__restrict__ nShade,
                                                           uint32_t *__restrict__ counters) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = counters[HPT_Q_TRACE];
+    const uint32_t n = *nTrace;
     bool alive = false;
     uint32_t id = 0;
     if (tid < n) {
         id = traceQ[tid];
         alive = postPath(sc, P, id, counters);
     }
-    qpushBlock<HPT_POST_BLOCK>(alive, id, shadeQ, &counters[HPT_Q_SHADE_OUT]);
+    qpushBlock<HPT_POST_BLOCK>(alive, id, shadeQ, nShade);
 }
 
-/* Tail of the frame (few live paths left, e.g. after Russian roulette
-   starts): one lane carries its path through every remaining bounce --
-   shade, shadow ray, continuation ray, post -- inside one launch, so the
-   tail costs the longest path's chain instead of one host-synchronised
-   launch sequence per bounce, each waiting on its own slowest ray.  Every
-   step is the wavefront kernels' own per-path function in the same order
-   (the shadow contribution is added before post's emitter term, as k_trace
-   finishes before k_post), so the film is bit-identical. */
+/* Tail of the frame (few live paths left, after Russian roulette has
+   culled most of them): a lane pair carries its path through every
+   remaining bounce -- shade, shadow ray, continuation ray, post -- inside
+   one launch, so the tail costs the longest path's chain instead of one
+   host-synchronised launch sequence per bounce, each waiting on its own
+   slowest ray.  The even lane shades, traces the shadow ray and runs post;
+   the odd lane traces the continuation ray at the same time.  Pairs take
+   their paths from the shade queue, and a pair whose path ends claims the
+   next one.  Every step is the
+   wavefront kernels' own per-path function in the same order (the shadow
+   contribution is added before post's emitter term, as k_trace finishes
+   before k_post), so the film is bit-identical.  The traversal runs in
+   latency mode (traceRound LAT): the tail is a chain of dependent memory
+   round trips, not a bandwidth problem. */
+struct HptTail {
+    const uint32_t *shadeQ, *nShade;
+    uint32_t pairs; /* lane pairs per wave that take paths (1..32) */
+};
+#ifdef HPT_TAIL_PROFILE
+/* timing instrumentation of k_tail (experiment builds only: make variant KFLAGS=-DHPT_TAIL_PROFILE):
+   per wave [iterations, shade, trace, post ticks, begin, end, sum over iterations of the wave's
+   longest ray in leaf rounds, items claimed]; 100 MHz s_memrealtime ticks */
+#define HPT_TAIL_PROFILE_WAVES 65536
+__device__ unsigned long long g_tailprof[HPT_TAIL_PROFILE_WAVES][8];
+#endif
 template <bool MULTI>
-__device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
+__device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const HptTail &T,
                                           uint32_t *__restrict__ counters, uint2 *stk) {
-    /* two lanes per path: the even lane shades, traces the shadow ray and runs
-       post; the odd lane traces the continuation ray at the same time */
-    const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x, lane = __lane_id(), partner = lane & ~1u;
-    const bool odd = (tid & 1u) != 0;
-    bool live = (tid >> 1) < counters[HPT_Q_SHADE_IN];
-    PathIO io{P, nullptr, nullptr, 0, 0, live ? shadeQ[tid >> 1] : 0u};
-    uint32_t nb = 0;
+    const uint32_t lane = __lane_id(), partner = lane & ~1u;
+    const bool odd = (lane & 1u) != 0;
+    const uint32_t total = *T.nShade;
+    uint32_t id = 0, nb = 0;
+    bool live = false, exhausted = false;
     TraceCounters tc;
+    PathIO io{P, nullptr, nullptr, 0, 0, 0};
+#ifdef HPT_TAIL_PROFILE
+    uint32_t rounds = 0;
+    unsigned long long pIt = 0, pS = 0, pT = 0, pP = 0, pR = 0, pItems = 0;
+    const unsigned long long pBegin = __builtin_amdgcn_s_memrealtime();
+#endif
     auto trace = [&](bool shadowRay) {
         TraceRay r;
-        const float4 ro = P.ro[io.id], rd = shadowRay ? P.sdir[io.id] : P.rd[io.id];
-        if (beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(rd.x, rd.y, rd.z), shadowRay ? kEpsilon : ro.w, rd.w, shadowRay) &&
-            (stashRay<HPT_STACK>(stk, (int) blockDim.x, r, io.id), true))
-            while (!traceRound<HPT_STACK, false>(sc, r, stk, (int) blockDim.x, tc)) {
+        const float4 ro = P.ro[id], rd = shadowRay ? P.sdir[id] : P.rd[id];
+        const bool act = beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(rd.x, rd.y, rd.z), shadowRay ? kEpsilon : ro.w, rd.w, shadowRay);
+        stashRay<HPT_STACK>(stk, (int) blockDim.x, r, id);
+        if (act)
+            while (!traceRound<HPT_STACK, false, true>(sc, r, stk, (int) blockDim.x, tc)) {
+#ifdef HPT_TAIL_PROFILE
+                ++rounds;
+#endif
             }
-        io.finish(sc, io.id, r);
+        io.finish(sc, id, r);
     };
-    while (__ballot(live) != 0) {
+    while (true) {
+        /* free pairs claim the next items (the even lane's rank, shared with the odd lane) */
+        /* only the first T.pairs pairs of a wave take paths: a wave waits each bounce for
+           its slowest ray, and the fewer paths share a wave, the shorter that wait is
+           (the host spreads few paths thinly over the resident waves) */
+        const uint64_t freeM = __ballot(!live && !odd && (lane >> 1) < T.pairs);
+        if (!exhausted && freeM != 0) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&counters[HPT_C_TAIL_CURSOR], (uint32_t) __popcll(freeM));
+            base = __shfl(base, 0);
+            if (base + (uint32_t) __popcll(freeM) >= total) exhausted = true;
+            const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t) (freeM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) freeM, 0u));
+            const uint32_t j = __shfl(base + rk, (int) partner);
+            if (!live && (lane >> 1) < T.pairs && j < total) { /* exactly the pairs counted in freeM */
+                id = T.shadeQ[j];
+                live = true;
+#ifdef HPT_TAIL_PROFILE
+                pItems += odd ? 0u : 1u;
+#endif
+            }
+        }
+        if (__ballot(live) == 0) {
+            if (exhausted) break;
+            continue;
+        }
+#ifdef HPT_TAIL_PROFILE
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        rounds = 0;
+#endif
         bool cont = false, shadow = false;
         if (live && !odd) {
             ++nb;
-            shadePath<MULTI>(sc, P, io.id, counters, cont, shadow);
+            shadePath<MULTI>(sc, P, id, counters, cont, shadow);
         }
         __threadfence_block(); /* the continuation ray is in HBM for the odd lane */
         const int f = __shfl((cont ? 1 : 0) | (shadow ? 2 : 0), (int) partner);
         cont = (f & 1) != 0;
         shadow = (f & 2) != 0;
-        if (live && !odd && shadow) trace(true);
-        if (live && odd && cont) trace(false);
+#ifdef HPT_TAIL_PROFILE
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+#endif
+        /* one call site: the shadow ray (even lane) and the continuation ray (odd
+           lane) are traced at the same time, not one after the other */
+        if (live && (odd ? cont : shadow)) trace(!odd);
         __threadfence_block(); /* the hit record is in HBM for the even lane */
+#ifdef HPT_TAIL_PROFILE
+        const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
+#endif
         bool alive = false;
-        if (live && !odd && cont) alive = postPath(sc, P, io.id, counters);
+        if (live && !odd && cont) alive = postPath(sc, P, id, counters);
         live = live && __shfl(alive ? 1 : 0, (int) partner) != 0;
+#ifdef HPT_TAIL_PROFILE
+        const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
+        uint32_t rm = rounds;
+        for (int off = 32; off > 0; off >>= 1) rm = max(rm, (uint32_t) __shfl_xor(rm, off));
+        ++pIt;
+        pS += t1 - t0;
+        pT += t2 - t1;
+        pP += t3 - t2;
+        pR += rm;
+#endif
     }
     for (int off = 32; off > 0; off >>= 1) nb += __shfl_down(nb, off);
-    if (__lane_id() == 0 && nb) atomicAdd(&counters[HPT_Q_TAIL_BOUNCES], nb);
-}
-#ifndef HPT_TAIL_WAVES
-#define HPT_TAIL_WAVES 4 /* register target: 4 waves/SIMD hold ~2.6e5 lanes = 1.3e5 paths resident */
+    if (__lane_id() == 0 && nb) atomicAdd(&counters[HPT_C_TAIL_BOUNCES], nb);
+#ifdef HPT_TAIL_PROFILE
+    for (int off = 32; off > 0; off >>= 1) pItems += __shfl_down(pItems, off);
+    const uint32_t wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (__lane_id() == 0 && wv < HPT_TAIL_PROFILE_WAVES) {
+        unsigned long long *rec = g_tailprof[wv];
+        rec[0] = pIt;
+        rec[1] = pS;
+        rec[2] = pT;
+        rec[3] = pP;
+        rec[4] = pBegin;
+        rec[5] = __builtin_amdgcn_s_memrealtime();
+        rec[6] = pR;
+        rec[7] = pItems;
+    }
 #endif
-extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void k_tail(HptScene sc, HptPaths P,
-                                                               const uint32_t *__restrict__ shadeQ,
-                                                               uint32_t *__restrict__ counters) {
-    __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    tailPaths<false>(sc, P, shadeQ, counters, stk + threadIdx.x);
 }
-extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void k_tail_multi(HptScene sc, HptPaths P,
-                                                                     const uint32_t *__restrict__ shadeQ,
-                                                                     uint32_t *__restrict__ counters) {
+/* persistent: pairs claim work, so any amount of it fits one launch.  No
+   occupancy target: the tail is latency-bound and the traversal keeps its
+   leaf records and exact-test records in registers (LAT) */
+#ifndef HPT_TAIL_WAVES
+#define HPT_TAIL_WAVES 2
+#endif
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void
+k_tail(HptScene sc, HptPaths P, HptTail T, uint32_t *__restrict__ counters) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    tailPaths<true>(sc, P, shadeQ, counters, stk + threadIdx.x);
+    tailPaths<false>(sc, P, T, counters, stk + threadIdx.x);
+}
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void
+k_tail_multi(HptScene sc, HptPaths P, HptTail T, uint32_t *__restrict__ counters) {
+    __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
+    tailPaths<true>(sc, P, T, counters, stk + threadIdx.x);
 }
 
 /* Deterministic film accumulation (imageblock.h:124-204 + renderproc.cpp:
@@ -2641,14 +2739,17 @@ extern "C" __global__ void k_env_filtered_batch(HptScene sc, int n, const float 
     out[3 * i + 2] = v.z;
 }
 
-/* tiny queue-rotation kernel: shade_in <- shade_out, reset the rest */
-extern "C" __global__ void k_rotate(uint32_t *counters, uint32_t *cursors) {
-    for (uint32_t i = threadIdx.x; i < HPT_CURSORS; i += blockDim.x) cursors[i * HPT_CURSOR_STRIDE] = 0;
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        counters[HPT_Q_SHADE_IN] = counters[HPT_Q_SHADE_OUT];
-        counters[HPT_Q_SHADE_OUT] = 0;
-        counters[HPT_Q_TRACE] = 0;
-        counters[HPT_Q_SHADOW] = 0;
+/* after bounce b's trace launch (parity p): zero the counts bounce b + 1
+   appends to (parity p ^ 1, consumed by bounce b - 1) and reset the trace
+   cursors */
+extern "C" __global__ void k_clear(uint32_t *counters, uint32_t p) {
+    uint32_t *cur = counters + HPT_CURSOR_OFFSET;
+    for (uint32_t i = threadIdx.x; i < HPT_CURSORS; i += blockDim.x) cur[i * HPT_CURSOR_STRIDE] = 0;
+    if (threadIdx.x == 0) {
+        const uint32_t q = p ^ 1u;
+        counters[HPT_C_TRACE(q)] = 0;
+        counters[HPT_C_SHADOW(q)] = 0;
+        counters[HPT_C_SHADE(q)] = 0;
     }
 }
 
@@ -2658,9 +2759,9 @@ extern "C" __global__ void k_rotate(uint32_t *counters, uint32_t *cursors) {
 static inline unsigned blocksFor(uint64_t n, unsigned bs) { return (unsigned) ((n + bs - 1) / bs); }
 
 hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPaths &P, uint32_t *traceQ,
-                             uint32_t *counters, hipStream_t s) {
+                             uint32_t *nTrace, hipStream_t s) {
     if (w.nPaths == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_camera, dim3(blocksFor(w.nPaths, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, w, P, traceQ, counters);
+    hipLaunchKernelGGL(k_camera, dim3(blocksFor(w.nPaths, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, w, P, traceQ, nTrace);
     return hipGetLastError();
 }
 /* persistent grid: as many one-wave blocks as can be resident at once
@@ -2698,83 +2799,84 @@ static unsigned persistentBlocks(const void *kernel, uint64_t items, int block =
 }
 
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
-                            uint32_t *counters, uint32_t *stats, uint64_t maxItems, hipStream_t s) {
+                            const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
+                            uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
     if (stats)
         hipLaunchKernelGGL(k_trace_counted, dim3(persistentBlocks((const void *) k_trace_counted, maxItems)),
-                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, counters,
-                           counters + HPT_CURSOR_OFFSET, stats);
+                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, stats);
     else
-        hipLaunchKernelGGL(k_trace, dim3(persistentBlocks((const void *) k_trace, maxItems)), dim3(HPT_TRACE_BLOCK),
-                           0, s, sc, P, traceQ, shadowQ, counters, counters + HPT_CURSOR_OFFSET);
+        hipLaunchKernelGGL(k_trace, dim3(persistentBlocks((const void *) k_trace, maxItems)), dim3(HPT_TRACE_BLOCK), 0, s,
+                           sc, P, traceQ, shadowQ, nTrace, nShadow, cursors);
     return hipGetLastError();
 }
-hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *counters,
-                                   uint32_t *stats, uint64_t maxItems, hipStream_t s) {
+hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
+                                   uint32_t *cursors, uint32_t *stats, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
     if (stats)
         hipLaunchKernelGGL(k_trace_packet_counted,
                            dim3(persistentBlocks((const void *) k_trace_packet_counted, maxItems, HPT_PACKET_BLOCK)),
-                           dim3(HPT_PACKET_BLOCK), 0, s, sc, P, traceQ, counters, counters + HPT_CURSOR_OFFSET, stats);
+                           dim3(HPT_PACKET_BLOCK), 0, s, sc, P, traceQ, nTrace, cursors, stats);
     else
         hipLaunchKernelGGL(k_trace_packet, dim3(persistentBlocks((const void *) k_trace_packet, maxItems, HPT_PACKET_BLOCK)),
-                           dim3(HPT_PACKET_BLOCK), 0, s, sc, P, traceQ, counters, counters + HPT_CURSOR_OFFSET);
+                           dim3(HPT_PACKET_BLOCK), 0, s, sc, P, traceQ, nTrace, cursors);
     return hipGetLastError();
 }
-hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
-                              uint32_t *counters, uint64_t maxItems, hipStream_t s) {
+hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
+                              uint32_t *shadeQ, uint32_t *nShade, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_primary, dim3(blocksFor(maxItems, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, P, traceQ, shadeQ, counters);
+    hipLaunchKernelGGL(k_primary, dim3(blocksFor(maxItems, HPT_QBLOCK)), dim3(HPT_QBLOCK), 0, s, sc, P, traceQ, nTrace,
+                       shadeQ, nShade);
     return hipGetLastError();
 }
-/* HAIRPT_SHADE_LDS=1 selects k_shade_mlds (Marschner cdfs / sums staged in LDS).  Measured on
-   MI355X at the headline (furball 512^2 @ 256, shade per frame): L2 tables 18.2 ms; LDS staging
-   19.4 ms (512-thread persistent blocks, 4 waves/SIMD) and 27.8 ms (640 threads, 5 waves): the
-   persistent loop needs 168 VGPRs and spills, which costs more than the L2-latency binary search
-   it saves.  Off by default; kept for the A/B. */
-static bool hptShadeLds() {
-    static const bool on = [] {
-        const char *e = getenv("HAIRPT_SHADE_LDS");
-        return e && e[0] == '1';
-    }();
-    return on;
-}
-
-hipError_t hpt_launch_shade(const HptScene &sc, const HptScene *scDev, const HptPaths &P, const uint32_t *shadeQ, uint32_t *traceQ,
-                            uint32_t *shadowQ, uint32_t *counters, uint64_t maxItems, hipStream_t s) {
+hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
+                            uint32_t *traceQ, uint32_t *nTrace, uint32_t *shadowQ, uint32_t *nShadow, uint32_t *counters,
+                            uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
+    const HptShadeIO q{nShade, nTrace, nShadow, counters};
     if (sc.nShapes > 1)
         hipLaunchKernelGGL(k_shade_multi, dim3(blocksFor(maxItems, HPT_SHADE_BLOCK)), dim3(HPT_SHADE_BLOCK), 0, s, sc, P, shadeQ,
-                           traceQ, shadowQ, counters);
-    else if (sc.bsdf.kind == HPT_BSDF_MARSCHNER && hptShadeLds())
-        hipLaunchKernelGGL(k_shade_mlds,
-                           dim3(persistentBlocks((const void *) k_shade_mlds, maxItems, HPT_SHADE_LDS_BLOCK)),
-                           dim3(HPT_SHADE_LDS_BLOCK), 0, s, scDev, P, shadeQ, traceQ, shadowQ, counters);
+                           traceQ, shadowQ, q);
     else
         hipLaunchKernelGGL(k_shade, dim3(blocksFor(maxItems, HPT_SHADE_BLOCK)), dim3(HPT_SHADE_BLOCK), 0, s, sc, P, shadeQ,
-                           traceQ, shadowQ, counters);
+                           traceQ, shadowQ, q);
     return hipGetLastError();
 }
-hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, uint32_t *shadeQ,
-                           uint32_t *counters, uint64_t maxItems, hipStream_t s) {
+hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
+                           uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_post, dim3(blocksFor(maxItems, HPT_POST_BLOCK)), dim3(HPT_POST_BLOCK), 0, s, sc, P, traceQ, shadeQ, counters);
+    hipLaunchKernelGGL(k_post, dim3(blocksFor(maxItems, HPT_POST_BLOCK)), dim3(HPT_POST_BLOCK), 0, s, sc, P, traceQ, nTrace,
+                       shadeQ, nShade, counters);
     return hipGetLastError();
 }
-hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, uint32_t *counters,
-                           uint64_t maxItems, hipStream_t s) {
-    if (maxItems == 0) return hipSuccess;
-    /* two lanes per path (a spill-free 2-waves/SIMD build measured slower at every tail size) */
+hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
+                           uint32_t *counters, uint64_t items, hipStream_t s) {
+    if (items == 0) return hipSuccess;
+    /* two lanes per path; persistent (pairs claim paths).  Paths are spread over all resident
+       waves: K pairs per wave, the fewest that still cover the work in one residency */
+    const void *kern = sc.nShapes > 1 ? (const void *) k_tail_multi : (const void *) k_tail;
+    const uint64_t residentWaves = (uint64_t) persistentBlocks(kern, ~0ull >> 8) * (HPT_TRACE_BLOCK / 64);
+    const uint32_t K = (uint32_t) std::min<uint64_t>(32, std::max<uint64_t>(1, (items + residentWaves - 1) / residentWaves));
+    const HptTail T{shadeQ, nShade, K};
+    const unsigned blocks = persistentBlocks(kern, (items + K - 1) / K * 64);
     if (sc.nShapes > 1)
-        hipLaunchKernelGGL(k_tail_multi, dim3(blocksFor(2 * maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc,
-                           P, shadeQ, counters);
+        hipLaunchKernelGGL(k_tail_multi, dim3(blocks), dim3(HPT_TRACE_BLOCK), 0, s, sc, P, T, counters);
     else
-        hipLaunchKernelGGL(k_tail, dim3(blocksFor(2 * maxItems, HPT_TRACE_BLOCK)), dim3(HPT_TRACE_BLOCK), 0, s, sc, P,
-                           shadeQ, counters);
+        hipLaunchKernelGGL(k_tail, dim3(blocks), dim3(HPT_TRACE_BLOCK), 0, s, sc, P, T, counters);
     return hipGetLastError();
 }
-hipError_t hpt_launch_rotate(uint32_t *counters, hipStream_t s) {
-    hipLaunchKernelGGL(k_rotate, dim3(1), dim3(64), 0, s, counters, counters + HPT_CURSOR_OFFSET);
+#ifdef HPT_TAIL_PROFILE
+/* copy out (and clear) the k_tail timing records of the last frame: n waves x 8 u64 */
+extern "C" int hpt_debug_tailprof(unsigned long long *out, int n) {
+    if (n > HPT_TAIL_PROFILE_WAVES) n = HPT_TAIL_PROFILE_WAVES;
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tailprof), (size_t) n * 64) != hipSuccess) return -1;
+    static unsigned long long zeros[HPT_TAIL_PROFILE_WAVES][8];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_tailprof), zeros, sizeof(zeros)) == hipSuccess ? n : -1;
+}
+#endif
+hipError_t hpt_launch_clear(uint32_t *counters, uint32_t parity, hipStream_t s) {
+    hipLaunchKernelGGL(k_clear, dim3(1), dim3(128), 0, s, counters, parity);
     return hipGetLastError();
 }
 hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *partial, float4 *film,

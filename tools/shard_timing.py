@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--config", default="furball_marschner")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--all-ranks", action="store_true", help="time every rank of each N (default: rank 0 and the slowest of a sample)")
+    ap.add_argument("--ns", default="2,4,8", help="shard counts to time (besides N=1)")
     a = ap.parse_args()
     cfg = scenes.CONFIGS[a.config]
     xml = scenes.make_scene(a.config, os.path.join(tempfile.gettempdir(), "hpt_shards"), n_strands=cfg["n"])
@@ -50,7 +51,7 @@ def main():
     r.render_device(film.data_ptr(), 0, spp)  # warm-up
     t1, _ = timed(0, 1)
     out = {"config": a.config, "N1_ms": round(t1 * 1e3, 3), "shards": {}}
-    for n in (2, 4, 8):
+    for n in [int(x) for x in a.ns.split(",")]:
         ranks = range(n) if a.all_ranks else sorted({0, n - 1})
         ts = {}
         for k in ranks:
