@@ -62,7 +62,9 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-spp", type=int, default=96, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="0 = this process's CPUs, at most 16 (the GPU box's CPU share per GPU)")
+                    help="0 = every CPU this process may run on (nproc, SURVEY.md 8(d))")
+    ap.add_argument("--cpu-share-threads", type=int, default=16,
+                    help="also time the sample on this many threads (the GPU box's CPU share per GPU); 0 = skip")
     ap.add_argument("--workdir", default=os.path.join(tempfile.gettempdir(), "hpt_bench"))
     return ap.parse_args()
 
@@ -81,11 +83,20 @@ def cpu_baseline(args, cfg, xml_defines, hair_src, env_rgb, nodes, idx):
     o.set_kdtree(nodes, idx)
     o.prepare()
     avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    threads = args.cpu_threads if args.cpu_threads > 0 else min(16, avail)
-    t0 = time.perf_counter()
-    o.render(0, args.cpu_spp, threads=threads, width=W, height=H)
-    dt = time.perf_counter() - t0
+    threads = args.cpu_threads if args.cpu_threads > 0 else avail
     paths = W * H * args.cpu_spp
+
+    def timed(n_threads):
+        t0 = time.perf_counter()
+        o.render(0, args.cpu_spp, threads=n_threads, width=W, height=H)
+        return time.perf_counter() - t0
+
+    dt = timed(threads)
+    share = None
+    if args.cpu_share_threads > 0 and args.cpu_share_threads < threads:
+        ds = timed(args.cpu_share_threads)
+        share = {"value": paths / ds / 1e6, "cores": args.cpu_share_threads,
+                 "note": "the same sample on the GPU box's 16-CPU share per GPU"}
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -94,8 +105,8 @@ def cpu_baseline(args, cfg, xml_defines, hair_src, env_rgb, nodes, idx):
         pass
     return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
             "cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": avail,
-            "threads_note": "one worker thread per core like mitsuba.cpp:135,281; capped at the GPU box's "
-                            "16-CPU share per GPU",
+            "threads_note": "one worker thread per CPU this process may run on (nproc), like mitsuba.cpp:135,281",
+            "cpu_share": share,
             "sample": "%dx%d @ %d spp of the same scene (%d paths), %.2f s, liboracle_ref.so "
                       "(-O3 -march=nocona -msse2 -funsafe-math-optimizations, config-ubuntu-20.04.py:8)"
                       % (W, H, args.cpu_spp, paths, dt)}
@@ -126,13 +137,17 @@ def timed_steps(step, steps, world, dist_mod, sync, device, after_step=None):
 def main():
     args = parse()
     rank = int(os.environ.get("RANK", "0"))
-    # ranks beyond the visible devices share them (a rehearsal of the N > 1 path on a
-    # one-GPU box); on a full node LOCAL_RANK < device count and this is the identity
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     world = int(os.environ.get("WORLD_SIZE", "1"))
     # HPT_BENCH_BACKEND=gloo only rehearses N > 1 on a one-GPU box (RCCL refuses two
     # ranks on one device): the film is reduced from a host copy.  Never the bench.
     backend = os.environ.get("HPT_BENCH_BACKEND", "nccl")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n_dev = max(1, torch.cuda.device_count())
+    if backend == "gloo":
+        local %= n_dev  # the rehearsal's ranks share the visible devices
+    elif local >= n_dev:
+        raise SystemExit("LOCAL_RANK %d but only %d visible GPU(s): one rank per GPU (HIP_VISIBLE_DEVICES too narrow?)"
+                         % (local, n_dev))
     if world > 1:
         dist.init_process_group(backend)  # "nccl" = RCCL over xGMI on ROCm
     torch.cuda.set_device(local)
@@ -209,9 +224,14 @@ def main():
     bytes_lay = io + BYTES_NODE4 * tot["nodes"] + BYTES_PRIM * tot["prims"] + BYTES_EXACT * tot["exact"]
     gbs = lambda b, ms: b / (ms * 1e-3) / 1e9 if ms > 0 else 0.0  # noqa: E731
     achieved, achieved_lay = gbs(bytes_alg, ms_trace), gbs(bytes_lay, ms_trace)
+    # the packet pass reads a node or a leaf record once per PACKET step (wave-uniform scalar
+    # loads), so 8(d)'s per-unit figures are charged per step (slots / 64), not per member
+    # lane; each lane still reads and writes its own ray (52 B)
     io_pk = BYTES_CLOSEST * tot["p_rays"]
-    bytes_pk = io_pk + B8D_NODE * tot["p_nodes"] + (B8D_REF + B8D_PRIM) * tot["p_prims"]
-    bytes_pk_lay = io_pk + BYTES_NODE2 * tot["p_nodes"] + BYTES_PRIM * tot["p_prims"] + BYTES_EXACT * tot["p_exact"]
+    pk_node_steps, pk_prim_steps = tot["p_node_slots"] / 64.0, tot["p_prim_slots"] / 64.0
+    bytes_pk = io_pk + B8D_NODE * pk_node_steps + (B8D_REF + B8D_PRIM) * pk_prim_steps
+    bytes_pk_lane = io_pk + B8D_NODE * tot["p_nodes"] + (B8D_REF + B8D_PRIM) * tot["p_prims"]
+    bytes_pk_lay = io_pk + BYTES_NODE2 * pk_node_steps + BYTES_PRIM * pk_prim_steps + BYTES_EXACT * tot["p_exact"]
     achieved_pk, achieved_pk_lay = gbs(bytes_pk, ms_packet), gbs(bytes_pk_lay, ms_packet)
     traffic, traffic_src, traffic_pk, limiter = None, None, None, None
     tj = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
@@ -256,6 +276,9 @@ def main():
             "roofline": {"bound": "hbm", "limiter": limiter, "kernel": "k_trace", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "traffic_source": traffic_src,
+                         "traffic_calibration": "profiles/r03_fetch_calibration.json: FETCH_SIZE is 64 B per 128-B "
+                                                "line for 8/16/32-B accesses, cold or Infinity-Cache resident (x2 = "
+                                                "line bytes); WRITE_SIZE is 32 B per lone 16-B store",
                          "achieved_hbm": round(traffic / (ms_trace / max(1, launches)) * 1e-6, 1) if traffic else None,
                          "frac_hbm": round(traffic / (ms_trace / max(1, launches)) * 1e-6 / HBM_PEAK_GBS, 4)
                          if traffic else None,
@@ -267,13 +290,16 @@ def main():
                          "avg_launch_ms": round(ms_trace / max(1, launches), 4), "launches": int(launches),
                          "bytes_per_step": int(bytes_alg // args.steps),
                          "rank0_trace_ms_per_step": round(ms_trace / args.steps, 3)},
-            # the camera pass's packet traversal (k_trace_packet), same byte model per member lane
+            # the camera pass's packet traversal (k_trace_packet): 8(d) bytes per packet step
             "roofline_packet": {"bound": "hbm", "kernel": "k_trace_packet", "achieved": round(achieved_pk, 1),
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_pk / HBM_PEAK_GBS, 4),
                                 "traffic": traffic_pk,
                                 "achieved_hbm": round(traffic_pk / (ms_packet / max(1, p_launches)) * 1e-6, 1)
                                 if traffic_pk else None,
+                                "algorithmic_model": "SURVEY.md 8(d) per packet step: 8 B per binary-node step, "
+                                                     "4+52 B per leaf-record step (wave-uniform), 52 B ray I/O per lane",
                                 "algorithmic_bytes_per_launch": int(bytes_pk // max(1, p_launches)),
+                                "lane_demand_bytes_per_launch": int(bytes_pk_lane // max(1, p_launches)),
                                 "achieved_layout": round(achieved_pk_lay, 1),
                                 "avg_launch_ms": round(ms_packet / max(1, p_launches), 4),
                                 "launches": int(p_launches)},

@@ -183,6 +183,11 @@ inline P3 xform(const float *M, const P3 &p) {
 
 } // namespace
 
+void sfmtULongs(uint64_t seed, size_t n, uint64_t *out) {
+    Sfmt19937 r(seed);
+    for (size_t i = 0; i < n; ++i) out[i] = r.nextULong();
+}
+
 HairData loadHair(const std::string &path, float radius, float angleThresholdDeg, float reduction,
                   const float *toWorld) {
     if (reduction < 0 || reduction >= 1)

@@ -144,6 +144,8 @@ struct HairData {
 };
 
 /* hair.cpp:609-785 (binary + ASCII).  to_world may be null. */
+/* the loader's SFMT19937 seeded like Random(seed) (random.cpp:497-526): n outputs of nextULong */
+void sfmtULongs(uint64_t seed, size_t n, uint64_t *out);
 HairData loadHair(const std::string &path, float radius, float angleThresholdDeg, float reduction,
                   const float *toWorld);
 

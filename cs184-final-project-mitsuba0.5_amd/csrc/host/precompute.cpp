@@ -901,6 +901,9 @@ bool cameraSampleToCamera(const SceneDesc &d, float s2c[16]) {
 }
 
 void setupCamera(const SceneDesc &d, HptCamera &cam) {
+    /* PerspectiveCamera::setXFov (sensor.cpp:285-288) on the final horizontal field of view */
+    const float xfov = cameraXFov(d);
+    if (xfov <= 0 || xfov >= 180) throw std::runtime_error("The horizontal field of view must be in the interval (0, 180)!");
     if (!cameraSampleToCamera(d, cam.s2c))
         throw std::runtime_error("Unable to invert singular matrix (perspective camera)");
     std::memcpy(cam.toWorld, d.toWorld, sizeof(cam.toWorld));

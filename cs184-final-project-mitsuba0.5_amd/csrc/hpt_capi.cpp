@@ -52,6 +52,7 @@ static bool defaultPackets() {
 struct hpt_context {
     int device = 0;
     uint32_t tailPaths = defaultTailPaths();
+    uint32_t maxLeafRounds = HPT_MAX_LEAF_ROUNDS, maxRestarts = HPT_MAX_RESTARTS; /* traversal bounds */
     bool packets = defaultPackets();
     hipStream_t stream = nullptr;
     uint32_t *hostCnt = nullptr; /* pinned copy of the counter block */
@@ -347,6 +348,21 @@ int hpt_set_sampler_scramble(hpt_context *c, uint64_t scramble) {
     if (!c) return HPT_EINVAL;
     c->desc.scramble = scramble;
     c->prepared = false;
+    return HPT_OK;
+}
+
+int hpt_debug_sfmt(uint64_t seed, uint64_t n, uint64_t *out) {
+    if (!out && n) return HPT_EINVAL;
+    sfmtULongs(seed, (size_t) n, out);
+    return HPT_OK;
+}
+
+int hpt_set_traversal_bounds(hpt_context *c, uint32_t max_leaf_rounds, uint32_t max_restarts) {
+    if (!c || max_leaf_rounds == 0) return HPT_EINVAL;
+    c->maxLeafRounds = std::min<uint32_t>(max_leaf_rounds, HPT_MAX_LEAF_ROUNDS);
+    c->maxRestarts = std::min<uint32_t>(max_restarts, HPT_MAX_RESTARTS);
+    c->sc.maxLeafRounds = c->maxLeafRounds;
+    c->sc.maxRestarts = c->maxRestarts;
     return HPT_OK;
 }
 
@@ -730,6 +746,8 @@ int hpt_prepare(hpt_context *c) {
     sc.hideEmitters = d.hideEmitters ? 1 : 0;
     if (sc.cam.logRes > (uint32_t) c->vdc.size() / HPT_SOBOL_BITS)
         return setErr(c, HPT_EINVAL, "image resolution exceeds the Sobol look-up tables");
+    c->sc.maxLeafRounds = c->maxLeafRounds;
+    c->sc.maxRestarts = c->maxRestarts;
     c->prepared = true;
     return HPT_OK;
 }

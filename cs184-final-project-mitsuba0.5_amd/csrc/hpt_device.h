@@ -210,6 +210,8 @@ struct HptScene {
     float tentScale;
     int maxDepth, rrDepth, strictNormals, hideEmitters;
     uint32_t *fault;            /* device word: HPT_FAULT_* bits set by the traversal bounds */
+    uint32_t maxLeafRounds;     /* traversal bounds of one ray (HPT_MAX_LEAF_ROUNDS / HPT_MAX_RESTARTS unless */
+    uint32_t maxRestarts;       /*  lowered through hpt_set_traversal_bounds, a test hook) */
 };
 
 #endif

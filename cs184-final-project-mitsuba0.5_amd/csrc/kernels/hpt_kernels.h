@@ -20,9 +20,10 @@
 #define HPT_Q_COUNT 16
 /* HptScene::fault bits: a traversal bound fired (the ray would otherwise end
    with whatever hit it had; the render / batch call fails instead) */
-#define HPT_FAULT_LEAVES 1u   /* more than 2^18 leaf rounds for one ray */
-#define HPT_FAULT_RESTARTS 2u /* more than HPT_MAX_RESTARTS kd-restarts for one ray */
-#define HPT_MAX_RESTARTS 1024
+#define HPT_FAULT_LEAVES 1u   /* more than HptScene::maxLeafRounds (2^18) leaf rounds for one ray */
+#define HPT_FAULT_RESTARTS 2u /* more than HptScene::maxRestarts (1024) kd-restarts for one ray */
+#define HPT_MAX_LEAF_ROUNDS (1u << 18)
+#define HPT_MAX_RESTARTS 1024u
 /* k_trace work cursors (persistent waves claim rays from them), one per
    128-byte line, stored after the counters in the same buffer */
 #define HPT_CURSORS 64

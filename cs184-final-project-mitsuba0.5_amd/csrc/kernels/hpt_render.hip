@@ -258,13 +258,6 @@ HD bool segMayHit(const float4 a, const float4 b, V3 o, V3 d, float r) {
     return wn <= r * __builtin_amdgcn_sqrtf(nn) * 1.000001f + 3e-6f * (r + fabsf(wx) + fabsf(wy) + fabsf(wz));
 }
 
-#ifdef HPT_EXPERIMENT_NO_EXACT
-/* register-pressure experiment only (never the product): no exact test */
-#define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, far) ((t = (mint)), (far = 0), (s) == 0xffffffffu)
-#else
-#define HPT_SEG_TEST(segs, s, o, d, r2, mint, maxt, t, far) segIntersect(segs, s, o, d, r2, mint, maxt, t, far)
-#endif
-
 /* adaptive ray epsilon: skdtree.cpp:126-129 (closest) / :213-216 (shadow) */
 HD float adaptiveMint(V3 o, float mint, bool shadow) {
     if (mint != kEpsilon) return mint;
@@ -338,31 +331,16 @@ HD bool waveLeader() { return __lane_id() == (uint32_t) (__ffsll((unsigned long 
      row STACK+0  rcp.x, rcp.y       read once per round
      row STACK+1  rcp.z, key         key: what the IO's finish() needs (path id / ray index)
      row STACK+2  mint, maxt         mint read by the exact tests, maxt at a kd-restart
-   With HPT_RCP_LDS=0 the reciprocal direction is recomputed at the start of
-   every round instead (1.0f / d, the same IEEE division beginRay does) and the
-   rows shrink to (key, -), (mint, maxt): 80 B of LDS per lane with the stack.
-   Row k of lane i is stk[k * stride]. */
-#ifndef HPT_RCP_LDS
-#define HPT_RCP_LDS 1
-#endif
-#if HPT_RCP_LDS
+   (recomputing rcp each round instead, 80 B of LDS per lane, measured
+   slower: DESIGN.md 5).  Row k of lane i is stk[k * stride]. */
 #define HPT_RAY_ROWS 3
 #define HPT_ROW_KEY 1 /* .y */
 #define HPT_ROW_MM 2
-#else
-#define HPT_RAY_ROWS 2
-#define HPT_ROW_KEY 0 /* .y */
-#define HPT_ROW_MM 1
-#endif
 #define HPT_CNT_RESTART (1u << 20)
 template <int STACK>
 HD void stashRay(uint2 *stk, int stride, TraceRay &r, uint32_t key) {
-#if HPT_RCP_LDS
     stk[STACK * stride] = make_uint2(__float_as_uint(r.rcp.x), __float_as_uint(r.rcp.y));
     stk[(STACK + 1) * stride] = make_uint2(__float_as_uint(r.rcp.z), key);
-#else
-    stk[STACK * stride] = make_uint2(0u, key);
-#endif
     stk[(STACK + HPT_ROW_MM) * stride] = make_uint2(__float_as_uint(r.mint), __float_as_uint(r.maxt));
     r.cnt = 0u;
     /* the rows must be re-read, not forwarded from these stores (forwarding keeps the values in registers) */
@@ -380,21 +358,13 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     const float4 *__restrict__ leafF = reinterpret_cast<const float4 *>(sc.leafF);
     /* the ray as plain values: selecting among struct members by axis would be
        folded into a dynamically addressed load and push the state to scratch */
-#if HPT_RCP_LDS
     const uint2 cr0 = stk[STACK * stride], cr1 = stk[(STACK + 1) * stride];
     const V3 o = r.o, d = r.d, rcp = v3(__uint_as_float(cr0.x), __uint_as_float(cr0.y), __uint_as_float(cr1.x));
-#else
-    const V3 o = r.o, d = r.d, rcp = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-#endif
     /* hard bound so every wave drains even on a malformed tree; the call fails loudly */
     {
         const uint32_t cnt = r.cnt + 1u;
         r.cnt = cnt;
-#ifdef HPT_EXPERIMENT_MAX_ROUNDS
-        /* timing experiment only (never the product): rays end after this many leaf rounds */
-        if ((cnt & (HPT_CNT_RESTART - 1u)) > HPT_EXPERIMENT_MAX_ROUNDS) return true;
-#endif
-        if ((cnt & (HPT_CNT_RESTART - 1u)) > (1u << 18)) {
+        if ((cnt & (HPT_CNT_RESTART - 1u)) > sc.maxLeafRounds) {
             atomicOr(sc.fault, HPT_FAULT_LEAVES);
             return true;
         }
@@ -572,7 +542,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
             float t;
             uint32_t far;
             const float mint = __uint_as_float(stk[(STACK + HPT_ROW_MM) * stride].x);
-            if (HPT_SEG_TEST(sc.segs, s, o, d, r2, mint, r.tHit, t, far)) {
+            if (segIntersect(sc.segs, s, o, d, r2, mint, r.tHit, t, far)) {
                 r.found = true;
                 if (r.shadow) return true;
                 r.tHit = t;
@@ -586,7 +556,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
         if (!r.lost || r.tmax >= maxt) return true;
         const uint32_t cnt = r.cnt + HPT_CNT_RESTART;
         r.cnt = cnt;
-        if (cnt / HPT_CNT_RESTART > HPT_MAX_RESTARTS) {
+        if (cnt / HPT_CNT_RESTART > sc.maxRestarts) {
             atomicOr(sc.fault, HPT_FAULT_RESTARTS);
             return true;
         }
@@ -610,9 +580,6 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
 HD uint32_t hitSegment(const TraceRay &r) { return r.segHit & 0x7fffffffu; }
 HD uint32_t hitFarRoot(const TraceRay &r) { return r.segHit >> 31; }
 
-#ifndef HPT_XCD_SHARDS
-#define HPT_XCD_SHARDS 0 /* 1: waves claim their own XCD's shards first */
-#endif
 #ifndef HPT_REFILL
 #define HPT_REFILL 16 /* idle lanes that trigger a refill of the wave */
 #endif
@@ -646,22 +613,8 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
         }
     };
     bool active = false, exhausted = false;
-#if HPT_XCD_SHARDS
-    /* XCD-aware claiming: the 64 shards are 8 groups of 8 contiguous
-       shards; a wave walks its own XCD's group first (HW_REG_XCC_ID,
-       placement used for L2 affinity only), then the other groups, so each
-       XCD's L2 mostly sees the tree region of one eighth of the queue
-       (queue order follows the image's block order) */
-    uint32_t xcc;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-    xcc &= 7u;
-    const uint32_t sub = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) / 8u;
-    int tried = 0;
-    uint32_t shard = xcc * 8u + sub % 8u;
-#else
     uint32_t shard = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % HPT_CURSORS;
     int tried = 0;
-#endif
     while (true) {
         const uint64_t idle = __ballot(!active);
         if (!exhausted && __popcll(idle) >= HPT_REFILL) {
@@ -682,11 +635,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
                     exhausted = true;
                     break;
                 }
-#if HPT_XCD_SHARDS
-                shard = ((xcc + (uint32_t) tried / 8u) % 8u) * 8u + (sub + (uint32_t) tried) % 8u;
-#else
                 shard = (shard + 1) % HPT_CURSORS;
-#endif
             }
             if (!active) {
                 /* idle lanes below this one (v_mbcnt: no 64-bit lane mask kept live across the loop) */
@@ -835,9 +784,6 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
     uint64_t done = ~__ballot(valid);
     uint64_t act = ~done;
     if (act == 0) return true;
-#ifdef HPT_PACKET_FORCE_FALLBACK
-    return false;
-#endif
     uint32_t node = 0;
     int sp = 0;
     uint32_t steps = 0;
@@ -909,7 +855,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
                 if (STATS) ++tc.exact;
                 float t;
                 uint32_t far;
-                if (HPT_SEG_TEST(sc.segs, sg, o, d, r2, r.mint, r.tHit, t, far)) {
+                if (segIntersect(sc.segs, sg, o, d, r2, r.mint, r.tHit, t, far)) {
                     r.found = true;
                     r.tHit = t;
                     r.segHit = sg | (far << 31);

@@ -75,6 +75,8 @@ SIGNATURES = {
     "hpt_set_camera": (C.c_int, [C.c_void_p, _f, C.c_float, C.c_int, C.c_int, C.c_float, C.c_float]),
     "hpt_set_sampler": (C.c_int, [C.c_void_p, C.c_int]),
     "hpt_set_sampler_scramble": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "hpt_set_traversal_bounds": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    "hpt_debug_sfmt": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
     "hpt_set_integrator": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
     "hpt_set_hair_file": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_float, _f]),
     "hpt_set_hair_reduction": (C.c_int, [C.c_void_p, C.c_float]),
@@ -140,7 +142,11 @@ def _f32(a, n=None):
 
 
 class HairPTError(RuntimeError):
-    pass
+    """A hairpt call failed: code is the C ABI's negative status (HPT_E*)."""
+
+    def __init__(self, msg, code=None):
+        super().__init__(msg)
+        self.code = code
 
 
 class Renderer:
@@ -168,7 +174,7 @@ class Renderer:
 
     def _check(self, rc):
         if rc != 0:
-            raise HairPTError("hairpt error %d: %s" % (rc, self.lib.hpt_last_error(self.h).decode()))
+            raise HairPTError("hairpt error %d: %s" % (rc, self.lib.hpt_last_error(self.h).decode()), rc)
         return rc
 
     # ---- scene ----
@@ -187,6 +193,10 @@ class Renderer:
 
     def set_scramble(self, scramble: int):
         self._check(self.lib.hpt_set_sampler_scramble(self.h, scramble))
+
+    def set_traversal_bounds(self, max_leaf_rounds=1 << 18, max_restarts=1024):
+        """test hook: lower the per-ray traversal bounds (a ray past them fails the call, code -5)"""
+        self._check(self.lib.hpt_set_traversal_bounds(self.h, max_leaf_rounds, max_restarts))
 
     def set_integrator(self, max_depth, rr_depth=5, strict_normals=True, hide_emitters=False):
         self._check(self.lib.hpt_set_integrator(self.h, max_depth, rr_depth, int(strict_normals), int(hide_emitters)))

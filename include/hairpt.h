@@ -63,6 +63,13 @@ int hpt_set_camera(hpt_context *ctx, const float to_world[16], float fov_x_deg, 
 int hpt_set_sampler(hpt_context *ctx, int sample_count);
 /* SobolSampler "scramble" (sobol.cpp:92-102); 0 = unscrambled (the default) */
 int hpt_set_sampler_scramble(hpt_context *ctx, uint64_t scramble);
+/* Test hook: the hair loader's SFMT19937 (`reduction` culling, hair.cpp:628) seeded like
+   Random(seed) (src/libcore/random.cpp:497-526), n outputs of Random::nextULong (:551-553);
+   pinned by the reference's known answers for Random(4321) (src/tests/test_random.cpp:434-507) */
+int hpt_debug_sfmt(uint64_t seed, uint64_t n, uint64_t *out);
+/* Test hook (no reference counterpart): lower the per-ray traversal bounds (leaf rounds, kd-restarts;
+   defaults and maxima 2^18 and 1024) past which a render or trace call fails with HPT_ETRAVERSAL */
+int hpt_set_traversal_bounds(hpt_context *ctx, uint32_t max_leaf_rounds, uint32_t max_restarts);
 /* MonteCarloIntegrator params (src/librender/integrator.cpp:190-203) */
 int hpt_set_integrator(hpt_context *ctx, int max_depth, int rr_depth, int strict_normals, int hide_emitters);
 /* HairShape(Properties) (src/shapes/hair.cpp:609-785); to_world may be NULL */

@@ -3160,6 +3160,11 @@ int orc_marschner_tables(orc_scene *s, float *nR, float *nTT, float *nTRT, float
     return 0;
 }
 
+void orc_sfmt(uint64_t seed, int n, uint64_t *out) {
+    OracleSfmt r(seed);
+    for (int i = 0; i < n; ++i) out[i] = r.nextULong();
+}
+
 void orc_gauss_legendre140(float *points, float *weights) {
     GaussLegendre<140> g;
     std::memcpy(points, g.points, sizeof(g.points));

@@ -136,6 +136,8 @@ int orc_marschner_tables(orc_scene *s, float *nR, float *nTT, float *nTRT, float
                          float *out_trans100, float *out_spec_weight);
 /* Gauss-Legendre<140> restatement (gausssexylingerie.hpp) */
 void orc_gauss_legendre140(float *points, float *weights);
+/* OracleSfmt seeded like Random(seed): n outputs of nextULong */
+void orc_sfmt(uint64_t seed, int n, uint64_t *out);
 /* InterpolatedDistribution1D restatement over 'weights' (size x ndist) */
 void orc_idist_warp(const float *weights, int size, int ndist, int n, const float *dist,
                     const float *u, int *out_x, float *out_u, float *out_pdf, float *out_sum);

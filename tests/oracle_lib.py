@@ -63,6 +63,7 @@ _SIG = {
     "orc_bsdf_sample": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f, _u32]),
     "orc_marschner_tables": (C.c_int, [C.c_void_p, _f, _f, _f, _f, _f, _f]),
     "orc_gauss_legendre140": (None, [_f, _f]),
+    "orc_sfmt": (None, [C.c_uint64, C.c_int, _u64]),
     "orc_idist_warp": (None, [_f, C.c_int, C.c_int, C.c_int, _f, _f, _i32, _f, _f, _f]),
     "orc_env_sample": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f, _f]),
     "orc_env_eval": (None, [C.c_void_p, C.c_int, _f, _f, _f]),
@@ -333,6 +334,12 @@ class Oracle:
         self.lib.orc_trace_paths(self.s, n, p(px, _u32), p(py, _u32), p(frame, _u32), p(rgb, _f), p(pos, _f),
                                  p(depth, _i32))
         return rgb, pos, depth
+
+
+def sfmt(seed, n):
+    out = np.zeros(n, np.uint64)
+    load().orc_sfmt(seed, n, p(out, _u64))
+    return out
 
 
 def gauss_legendre140():

@@ -135,8 +135,27 @@ def reference_flags_floor(name, n_strands, r, width, height, spp, radii=None, ma
 
 
 def l2_metrics(a, b):
-    """Per-pixel L2 on linear HDR RGB: RMSE of ||dRGB||, max, relative RMSE."""
+    """Per-pixel L2 on linear HDR RGB: RMSE of ||dRGB||, its max and 99th
+    percentile over pixels, relative RMSE, and the fraction of pixels whose L2 exceeds
+    north_star's 1e-3."""
     d = np.linalg.norm(a.astype(np.float64) - b.astype(np.float64), axis=-1)
     rmse = float(np.sqrt(np.mean(d * d)))
     lum = a.astype(np.float64) @ np.array([0.212671, 0.715160, 0.072169])
-    return {"rmse": rmse, "max": float(d.max()), "rel_rmse": rmse / max(float(lum.mean()), 1e-12)}
+    return {"rmse": rmse, "max": float(d.max()), "p99": float(np.percentile(d, 99)),
+            "rel_rmse": rmse / max(float(lum.mean()), 1e-12), "frac_gt_1e-3": float(np.mean(d > 1e-3))}
+
+
+def assert_at_floor(m, floor, same, floor_same, factor=2.0):
+    """The film-parity bar of every render test, per-pixel statistics against the same
+    statistics of the reference-flags noise floor (the strict oracle vs the oracle built
+    with the reference's own compiler flags):
+      - RMSE below north_star's 1e-3 and within `factor` of the floor's;
+      - the per-pixel maximum within `factor` of the floor's maximum (a single path that
+        flips a discrete event moves its pixel by O(radiance / spp), on either side);
+      - the fraction of pixels with L2 > 1e-3 at most `factor` x the floor's, + 0.2 %;
+      - bit-identical pixels no fewer than the floor's, - 5 %."""
+    assert m["rmse"] < 1e-3, m
+    assert m["rmse"] <= factor * floor["rmse"] + 1e-6, (m, floor)
+    assert m["max"] <= factor * floor["max"] + 1e-5, (m, floor)
+    assert m["frac_gt_1e-3"] <= factor * floor["frac_gt_1e-3"] + 2e-3, (m, floor)
+    assert same >= floor_same - 0.05, (same, floor_same)

@@ -274,3 +274,30 @@ def test_camera_rays_bit_exact(name, size):
     oo, od, omin, omax = o.camera_rays(pos)
     for a, b in ((go, oo), (gd, od), (gmin, omin), (gmax, omax)):
         np.testing.assert_array_equal(_bits(a), _bits(b))
+
+
+@pytest.mark.parametrize("fov_xml,size", [
+    ('<float name="fov" value="0"/>', (32, 32)),
+    ('<float name="fov" value="180"/>', (32, 32)),
+    ('<float name="fov" value="-10"/>', (32, 32)),
+    # a y fov of 150 on a 2:1 frame is an x fov of ~165.3: accepted; of 170 is ~175.0: accepted;
+    # a diagonal fov of 179.9 on a 4:1 frame stays below 180 too, so the failing case is x
+    ('<float name="fov" value="200"/><string name="fovAxis" value="x"/>', (64, 32)),
+    ('<string name="focalLength" value="0mm"/>', (32, 32)),
+])
+def test_xfov_outside_range_rejected(tmp_path, fov_xml, size):
+    """PerspectiveCamera::setXFov (sensor.cpp:285-288) rejects a final horizontal field of view
+    outside (0, 180) with its own message, whichever of fov / fovAxis / focalLength produced it."""
+    xml = _xml_with_fov(tmp_path, fov_xml)
+    r = native.Renderer(device=native.HOST_ONLY)
+    with pytest.raises(native.HairPTError, match=r"horizontal field of view must be in the interval \(0, 180\)"):
+        r.load_scene_xml(xml, {"width": size[0], "height": size[1], "spp": 4})
+        r.prepare()
+
+
+def test_xfov_inside_range_accepted(tmp_path):
+    """a y fov of 150 on a 2:1 frame is an x fov of ~165: inside (0, 180), prepared fine"""
+    xml = _xml_with_fov(tmp_path, '<float name="fov" value="150"/><string name="fovAxis" value="y"/>')
+    r = native.Renderer(device=native.HOST_ONLY)
+    r.load_scene_xml(xml, {"width": 64, "height": 32, "spp": 4})
+    r.prepare()

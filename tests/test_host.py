@@ -488,3 +488,40 @@ def test_ascii_hair_ragged_lines(tmp_path, reduction):
     assert len(pxyz) > 50
     np.testing.assert_array_equal(pxyz, oxyz)
     np.testing.assert_array_equal(pst, ost)
+
+
+def test_path_state_packing(tmp_path):
+    """HptPaths::state (hpt_kernels.h): dim in bits 0-10, depth in 11-23, sampled type in
+    24-30, 'scattered' in 31.  hptState rewrites depth and dim and must keep the type and
+    scattered bits for every depth a path can reach (maxDepth = -1 runs until Russian
+    roulette or the 1024 Sobol dimensions end it: depth < 8192) and every dim < 2048.
+    Compiled from the header the kernels use (the packing is host/device inline code)."""
+    import subprocess
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "cs184-final-project-mitsuba0.5_amd")
+    src = tmp_path / "state.cpp"
+    src.write_text(r'''
+#include "kernels/hpt_kernels.h"
+#include <cstdio>
+int main() {
+    unsigned bad = 0, n = 0;
+    for (unsigned type = 0; type < 128; type += 7)
+        for (unsigned sc = 0; sc < 2; ++sc)
+            for (unsigned depth = 0; depth < 8192; depth += (depth < 300 ? 1 : 97))
+                for (unsigned dim = 0; dim < 2048; dim += 13) {
+                    const unsigned old = (sc << 31) | (type << 24) | (((depth * 7919u) & 0x1fffu) << 11) | 5u;
+                    const unsigned st = hptState(old, depth, dim);
+                    ++n;
+                    if (HPT_ST_DIM(st) != dim || HPT_ST_DEPTH(st) != depth || ((st >> 24) & 0x7fu) != type ||
+                        (st >> 31) != sc)
+                        ++bad;
+                }
+    std::printf("%u %u\n", n, bad);
+    return bad != 0;
+}
+''')
+    exe = tmp_path / "state"
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                           "-I" + os.path.join(root, "csrc"), str(src), "-o", str(exe)])
+    out = subprocess.run([str(exe)], capture_output=True, text=True)
+    n, bad = (int(x) for x in out.stdout.split())
+    assert out.returncode == 0 and bad == 0 and n > 100000, out.stdout

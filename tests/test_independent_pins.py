@@ -16,6 +16,8 @@ within float32 rounding:
     vectors in test_oracle_golden.py).
 """
 import ctypes
+import json
+import os
 
 import numpy as np
 import pytest
@@ -318,7 +320,9 @@ def test_sunsky_bitmap_matches_float64_restatement(case):
 _M128 = (1 << 128) - 1
 
 
-def _sfmt_floats(count, seed=5489):
+def _sfmt_u64(count, seed=5489):
+    """SFMT19937 as Random(seed) (random.cpp:397-406 init_gen_rand, :330-360 gen_rand_all,
+    :296-304 gen_rand64), in Python's big integers: `count` outputs of nextULong."""
     n = 19937 // 128 + 1
     n64 = 2 * n
     lo = [0] * n64
@@ -344,11 +348,18 @@ def _sfmt_floats(count, seed=5489):
             b = w[(i + 122) % n]
             w[i] = (w[i] ^ ((w[i] << 8) & _M128) ^ (lanes_shr(b, 11) & msk) ^ (w[r1] >> 8) ^ lanes_shl(w[r2], 18))
             r1, r2 = r2, i
-        for k in range(n64):  # gen_rand64, then the single-precision nextFloat
-            u64 = (w[k // 2] >> (64 * (k % 2))) & ((1 << 64) - 1)
-            bits = ((u64 & 0xffffffff) >> 9) | 0x3f800000
-            out.append(np.float32(np.array([bits], np.uint32).view(np.float32)[0] - np.float32(1.0)))
-    return np.array(out[:count], np.float32)
+        for k in range(n64):  # gen_rand64
+            out.append((w[k // 2] >> (64 * (k % 2))) & ((1 << 64) - 1))
+    return out[:count]
+
+
+def _sfmt_floats(count, seed=5489):
+    """the single-precision nextFloat (random.cpp:630-640) over _sfmt_u64"""
+    out = []
+    for u64 in _sfmt_u64(count, seed):
+        bits = ((u64 & 0xffffffff) >> 9) | 0x3f800000
+        out.append(np.float32(np.array([bits], np.uint32).view(np.float32)[0] - np.float32(1.0)))
+    return np.array(out, np.float32)
 
 
 def test_sfmt_independent_pin_of_hair_reduction(tmp_path):
@@ -1800,3 +1811,22 @@ def test_diffuse_independent_pin_gpu(tmp_path):
         _, _, wo, w, sp, _ = r.bsdf(wi, np.zeros_like(wi), u)
         return wo, w, sp
     _diffuse_pin(ev, sm)
+
+
+def test_sfmt_reference_known_answers():
+    """The SFMT19937 that culls strands for the hair loader's `reduction` exists three
+    times -- the product (hair_io.cpp, through the hpt_debug_sfmt hook), the oracle and
+    the Python restatement above.  All three reproduce the reference's own known answers
+    for Random(4321) (src/tests/test_random.cpp:434-507, tests/golden/sfmt_4321.json), so
+    a shared misreading (word order of gen_rand64, the period certification) would show."""
+    import ctypes
+
+    g = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "sfmt_4321.json")))
+    ref = [int(v, 16) for v in g["next_ulong"]]
+    assert g["seed"] == 4321 and len(ref) == 192
+    assert _sfmt_u64(len(ref), g["seed"]) == ref
+    assert [int(x) for x in oracle_lib.sfmt(g["seed"], len(ref))] == ref
+    lib = native.load_library()
+    out = (ctypes.c_uint64 * len(ref))()
+    assert lib.hpt_debug_sfmt(g["seed"], len(ref), out) == 0
+    assert list(out) == ref
