@@ -59,7 +59,15 @@ struct FilmDesc {
     bool banner = true;
 };
 
-/* ---- one BSDF instance (constant textures) ---- */
+/* ---- a procedural 2-D texture: only `checkerboard` (checkerboard.cpp:47-80 over the uv
+   transform of Texture2D, texture.cpp:81-121) ---- */
+struct TextureDesc {
+    std::string type;                              /* "" = a constant colour (no texture) */
+    float color0[3] = {0.4f, 0.4f, 0.4f}, color1[3] = {0.2f, 0.2f, 0.2f};
+    float uoffset = 0.0f, voffset = 0.0f, uscale = 1.0f, vscale = 1.0f;
+};
+
+/* ---- one BSDF instance (constant colours, except a diffuse reflectance texture) ---- */
 struct BsdfDesc {
     std::string type = "diffuse";                  /* Shape::configure default (shape.cpp:99-110) */
     float intIOR = 1.5046f, extIOR = 1.000277f;   /* ior.h: bk7 / air defaults */
@@ -71,6 +79,18 @@ struct BsdfDesc {
     float exponent = 30.0f;
     bool nonlinear = false;
     bool sampleVisible = true, ensureEnergyConservation = true;
+    TextureDesc reflectanceTexture;                /* diffuse: 'reflectance' given as a texture */
+    std::vector<BsdfDesc> nested;                  /* twosided: the one or two nested BSDFs */
+};
+
+/* ---- a triangle-mesh shape (obj.cpp / rectangle.cpp).  The GPU path renders hair;
+   scenes with these shapes are parsed, exported and rendered by the CPU path (C1) ---- */
+struct MeshShapeDesc {
+    std::string type;                              /* obj | rectangle */
+    std::string file;                              /* obj: resolved against the scene directory */
+    float toWorld[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    bool faceNormals = false, flipNormals = false, flipTexCoords = true; /* obj.cpp:226-240 defaults */
+    int bsdf = 0;                                  /* index into SceneDesc::bsdfs */
 };
 
 /* ---- one hair shape ---- */
@@ -102,6 +122,7 @@ struct SceneDesc {
     std::string rfilter = "tent";
     /* hair shapes (hair.cpp:609-640), each referencing one of bsdfs */
     std::vector<HairShapeDesc> shapes;
+    std::vector<MeshShapeDesc> meshes;
     std::vector<BsdfDesc> bsdfs;
     KDBuildParams kd;                              /* from the first hair shape */
     /* emitter */
@@ -126,6 +147,8 @@ struct SceneDesc {
  * properties, <transform> with matrix/lookat/translate/rotate/scale).
  * Throws std::runtime_error with a message on failure. */
 SceneDesc parseSceneXML(const std::string &path, const std::map<std::string, std::string> &defines);
+/* the parsed description as JSON (defaults resolved, paths absolute): what hpt_export_scene_json returns */
+std::string sceneToJSON(const SceneDesc &d);
 
 /* ---- hair geometry ---- */
 struct HairData {

@@ -319,6 +319,26 @@ float lookupIOR(const Ctx &c, const XNode &nd, const Props &p, const char *key, 
     fail(c.file, nd.line, "Unable to find an IOR value for \"" + name + "\"");
 }
 
+/* <texture type="checkerboard"> (checkerboard.cpp:47-52, texture.cpp:81-95) */
+void parseTexture(const Ctx &c, const XNode &t, TextureDesc &x) {
+    x.type = attrS(c, t, "type");
+    if (x.type != "checkerboard")
+        fail(c.file, t.line, "texture \"" + x.type + "\" is outside this path (only \"checkerboard\")");
+    Props p;
+    collectProps(c, t, p);
+    for (int i = 0; i < 3; ++i) {
+        x.color0[i] = p.num.count("color0") ? p.num["color0"][i] : 0.4f;
+        x.color1[i] = p.num.count("color1") ? p.num["color1"][i] : 0.2f;
+    }
+    if (p.str.count("coordinates") && p.str["coordinates"] != "uv")
+        fail(c.file, t.line, "Only UV coordinates are supported at the moment!");
+    x.uoffset = num1(p, "uoffset", 0.0f);
+    x.voffset = num1(p, "voffset", 0.0f);
+    const float uvscale = num1(p, "uvscale", 1.0f);
+    x.uscale = num1(p, "uscale", uvscale);
+    x.vscale = num1(p, "vscale", uvscale);
+}
+
 void parseBSDF(const Ctx &c, const XNode &b, BsdfDesc &d) {
     std::string type = attrS(c, b, "type");
     Props p;
@@ -429,15 +449,109 @@ void parseBSDF(const Ctx &c, const XNode &b, BsdfDesc &d) {
         }
         d.ensureEnergyConservation = num1(p, "ensureEnergyConservation", 1.0f) != 0.0f;
     } else if (type == "diffuse") {
-        /* diffuse.cpp:62-69: 'reflectance' or 'diffuseReflectance' */
+        /* diffuse.cpp:62-69: 'reflectance' or 'diffuseReflectance', a colour or a texture */
         const char *key = p.num.count("reflectance") ? "reflectance" : "diffuseReflectance";
         for (int i = 0; i < 3; ++i) d.diffuse[i] = p.num.count(key) ? p.num[key][i] : 0.5f;
         d.ensureEnergyConservation = num1(p, "ensureEnergyConservation", 1.0f) != 0.0f;
+        for (auto &kp : b.kids)
+            if (kp->tag == "texture") {
+                const std::string name = attrS(c, *kp, "name", false);
+                if (name != "reflectance" && name != "diffuseReflectance")
+                    fail(c.file, kp->line, "diffuse: unexpected texture \"" + name + "\"");
+                parseTexture(c, *kp, d.reflectanceTexture);
+            }
+    } else if (type == "plastic") {
+        /* SmoothPlastic (plastic.cpp:146-165): constant colours */
+        d.intIOR = lookupIOR(c, b, p, "intIOR", "polypropylene");
+        d.extIOR = lookupIOR(c, b, p, "extIOR", "air");
+        if (d.intIOR < 0 || d.extIOR < 0)
+            fail(c.file, b.line, "The interior and exterior indices of refraction must be positive!");
+        for (int i = 0; i < 3; ++i) {
+            d.diffuse[i] = p.num.count("diffuseReflectance") ? p.num["diffuseReflectance"][i] : 0.5f;
+            d.specular[i] = p.num.count("specularReflectance") ? p.num["specularReflectance"][i] : 1.0f;
+        }
+        d.nonlinear = num1(p, "nonlinear", 0.0f) != 0.0f;
+        for (auto &kp : b.kids)
+            if (kp->tag == "texture")
+                fail(c.file, kp->line, "plastic: textured reflectances are outside this path (constant colours only)");
+    } else if (type == "twosided") {
+        /* TwoSidedBRDF (twosided.cpp:58-110): one or two nested BSDFs, no transmission */
+        for (auto &kp : b.kids) {
+            const XNode *nb = nullptr;
+            if (kp->tag == "bsdf") {
+                nb = kp.get();
+            } else if (kp->tag == "ref") {
+                auto it = c.ids.find(attrS(c, *kp, "id"));
+                if (it == c.ids.end()) fail(c.file, kp->line, "unknown reference \"" + attrS(c, *kp, "id") + "\"");
+                nb = it->second;
+            }
+            if (!nb) continue;
+            if (d.nested.size() == 2) fail(c.file, kp->line, "No more than two nested BRDFs can be added!");
+            BsdfDesc n;
+            parseBSDF(c, *nb, n);
+            if (n.type == "thindielectric" || n.type == "marschnerdielectric" || n.type == "marschner" ||
+                n.type == "kajiyakay")
+                fail(c.file, nb->line, "Only materials without a transmission component can be nested!");
+            d.nested.push_back(n);
+        }
+        if (d.nested.empty()) fail(c.file, b.line, "A nested one-sided material is required!");
     } else {
         fail(c.file, b.line, "BSDF plugin \"" + type +
-                                 "\" is outside the hair hot path (supported: marschner, kajiyakay, roughplastic, "
-                                 "marschnerdielectric, thindielectric, diffuse)");
+                                 "\" is outside this path (supported: marschner, kajiyakay, roughplastic, "
+                                 "marschnerdielectric, thindielectric, diffuse, plastic, twosided)");
     }
+}
+
+/* the BSDF of a shape: a <ref>, a nested <bsdf>, or Shape::configure's 0.5 Lambertian
+   (shape.cpp:48-64); one BsdfDesc per distinct XML node */
+int shapeBSDF(Ctx &c, const XNode &nd, SceneDesc &d) {
+    const XNode *bn = nullptr;
+    for (auto &kp : nd.kids) {
+        const XNode &k = *kp;
+        if (k.tag == "ref") {
+            std::string id = attrS(c, k, "id");
+            auto it = c.ids.find(id);
+            if (it == c.ids.end()) fail(c.file, k.line, "unknown reference \"" + id + "\"");
+            bn = it->second;
+        } else if (k.tag == "bsdf") {
+            bn = &k;
+        }
+    }
+    if (!bn) {
+        d.bsdfs.push_back(BsdfDesc());
+        return (int) d.bsdfs.size() - 1;
+    }
+    auto it = c.bsdfIndex.find(bn);
+    if (it == c.bsdfIndex.end()) {
+        BsdfDesc b;
+        parseBSDF(c, *bn, b);
+        d.bsdfs.push_back(b);
+        it = c.bsdfIndex.emplace(bn, (int) d.bsdfs.size() - 1).first;
+    }
+    return it->second;
+}
+
+/* WavefrontOBJ (obj.cpp:199-240) / Rectangle (rectangle.cpp:81-87) */
+void parseMeshShape(Ctx &c, const XNode &nd, const std::string &type, SceneDesc &d) {
+    Props p;
+    collectProps(c, nd, p);
+    MeshShapeDesc m;
+    m.type = type;
+    if (type == "obj") {
+        if (!p.str.count("filename")) fail(c.file, nd.line, "obj shape needs a filename");
+        m.file = p.str["filename"];
+        if (!m.file.empty() && m.file[0] != '/') m.file = d.sceneDir + "/" + m.file;
+        m.faceNormals = num1(p, "faceNormals", 0.0f) != 0.0f;
+        m.flipTexCoords = num1(p, "flipTexCoords", 1.0f) != 0.0f;
+        if (p.num.count("maxSmoothAngle"))
+            fail(c.file, nd.line, "obj: 'maxSmoothAngle' (mesh topology rebuild) is outside this path");
+        if (p.num.count("shapeIndex") || num1(p, "collapse", 0.0f) != 0.0f)
+            fail(c.file, nd.line, "obj: 'shapeIndex' / 'collapse' are outside this path");
+    }
+    m.flipNormals = num1(p, "flipNormals", 0.0f) != 0.0f;
+    if (p.xform.count("toWorld")) parseTransform(c, *p.xform["toWorld"], m.toWorld);
+    m.bsdf = shapeBSDF(c, nd, d);
+    d.meshes.push_back(m);
 }
 
 void parseObject(Ctx &c, const XNode &nd, SceneDesc &d) {
@@ -530,8 +644,12 @@ void parseObject(Ctx &c, const XNode &nd, SceneDesc &d) {
         parseBSDF(c, nd, unused);
     } else if (tag == "shape") {
         std::string type = attrS(c, nd, "type");
+        if (type == "obj" || type == "rectangle") {
+            parseMeshShape(c, nd, type, d);
+            return;
+        }
         if (type != "hair")
-            fail(c.file, nd.line, "shape \"" + type + "\" is outside the hair hot path (only \"hair\")");
+            fail(c.file, nd.line, "shape \"" + type + "\" is outside this path (hair; obj / rectangle on the CPU path)");
         Props p;
         collectProps(c, nd, p);
         if (!p.str.count("filename")) fail(c.file, nd.line, "hair shape needs a filename");
@@ -557,32 +675,7 @@ void parseObject(Ctx &c, const XNode &nd, SceneDesc &d) {
             parseTransform(c, *p.xform["toWorld"], h.toWorld);
             h.hasToWorld = true;
         }
-        const XNode *bn = nullptr;
-        for (auto &kp : nd.kids) {
-            const XNode &k = *kp;
-            if (k.tag == "ref") {
-                std::string id = attrS(c, k, "id");
-                auto it = c.ids.find(id);
-                if (it == c.ids.end()) fail(c.file, k.line, "unknown reference \"" + id + "\"");
-                bn = it->second;
-            } else if (k.tag == "bsdf") {
-                bn = &k;
-            }
-        }
-        if (bn) {
-            auto it = c.bsdfIndex.find(bn);
-            if (it == c.bsdfIndex.end()) {
-                BsdfDesc b;
-                parseBSDF(c, *bn, b);
-                d.bsdfs.push_back(b);
-                it = c.bsdfIndex.emplace(bn, (int) d.bsdfs.size() - 1).first;
-            }
-            h.bsdf = it->second;
-        } else {
-            /* Shape::configure (shape.cpp:48-64): a 0.5 Lambertian BRDF */
-            d.bsdfs.push_back(BsdfDesc());
-            h.bsdf = (int) d.bsdfs.size() - 1;
-        }
+        h.bsdf = shapeBSDF(c, nd, d);
         if (d.shapes.size() >= HPT_MAX_SHAPES) fail(c.file, nd.line, "too many hair shapes");
         d.shapes.push_back(h);
     } else if (tag == "emitter") {
@@ -657,7 +750,7 @@ SceneDesc parseSceneXML(const std::string &path, const std::map<std::string, std
     size_t slash = path.find_last_of('/');
     d.sceneDir = slash == std::string::npos ? "." : path.substr(0, slash);
     for (auto &kp : root->kids) parseObject(c, *kp, d);
-    if (d.shapes.empty()) fail(path, root->line, "scene has no hair shape");
+    if (d.shapes.empty() && d.meshes.empty()) fail(path, root->line, "scene has no shape");
     if (!d.envFile.empty() && d.envFile[0] != '/') d.envFile = d.sceneDir + "/" + d.envFile;
     if (d.emitter.empty()) {
         /* scene.cpp:358-372: no emitter -> default sun & sky */
@@ -666,6 +759,155 @@ SceneDesc parseSceneXML(const std::string &path, const std::map<std::string, std
         d.sunRadiusScale = 15.0f;
     }
     return d;
+}
+
+namespace {
+struct Json {
+    std::ostringstream o;
+    bool first = true;
+    void sep() {
+        if (!first) o << ",";
+        first = false;
+    }
+    void key(const char *k) {
+        sep();
+        o << "\"" << k << "\":";
+    }
+    static std::string esc(const std::string &s) {
+        std::string r;
+        for (char ch : s) {
+            if (ch == '"' || ch == '\\') r += '\\';
+            r += ch;
+        }
+        return r;
+    }
+    void str(const char *k, const std::string &v) {
+        key(k);
+        o << "\"" << esc(v) << "\"";
+    }
+    void num(const char *k, double v) {
+        key(k);
+        char b[40];
+        std::snprintf(b, sizeof(b), "%.9g", v);
+        o << b;
+    }
+    void boolean(const char *k, bool v) {
+        key(k);
+        o << (v ? "true" : "false");
+    }
+    void arr(const char *k, const float *v, int n) {
+        key(k);
+        o << "[";
+        for (int i = 0; i < n; ++i) {
+            char b[40];
+            std::snprintf(b, sizeof(b), "%.9g", (double) v[i]);
+            o << (i ? "," : "") << b;
+        }
+        o << "]";
+    }
+    void open(const char *k, char br) {
+        if (k) key(k);
+        else sep();
+        o << br;
+        first = true;
+    }
+    void close(char br) {
+        o << br;
+        first = false;
+    }
+};
+
+void bsdfJSON(Json &j, const BsdfDesc &b) {
+    j.open(nullptr, '{');
+    j.str("type", b.type);
+    j.num("intIOR", b.intIOR);
+    j.num("extIOR", b.extIOR);
+    j.str("distribution", b.distribution);
+    j.num("alpha", b.alpha);
+    j.arr("diffuse", b.diffuse, 3);
+    j.arr("specular", b.specular, 3);
+    j.arr("transmittance", b.transmittance, 3);
+    j.num("exponent", b.exponent);
+    j.boolean("nonlinear", b.nonlinear);
+    j.boolean("sampleVisible", b.sampleVisible);
+    if (!b.reflectanceTexture.type.empty()) {
+        const TextureDesc &t = b.reflectanceTexture;
+        j.open("reflectanceTexture", '{');
+        j.str("type", t.type);
+        j.arr("color0", t.color0, 3);
+        j.arr("color1", t.color1, 3);
+        j.num("uoffset", t.uoffset);
+        j.num("voffset", t.voffset);
+        j.num("uscale", t.uscale);
+        j.num("vscale", t.vscale);
+        j.close('}');
+    }
+    j.open("nested", '[');
+    for (const BsdfDesc &n : b.nested) bsdfJSON(j, n);
+    j.close(']');
+    j.close('}');
+}
+} // namespace
+
+std::string sceneToJSON(const SceneDesc &d) {
+    Json j;
+    j.open(nullptr, '{');
+    j.open("integrator", '{');
+    j.str("type", d.integrator);
+    j.num("maxDepth", d.maxDepth);
+    j.num("rrDepth", d.rrDepth);
+    j.boolean("strictNormals", d.strictNormals);
+    j.boolean("hideEmitters", d.hideEmitters);
+    j.close('}');
+    j.open("sensor", '{');
+    j.arr("toWorld", d.toWorld, 16);
+    j.num("fov", d.fov);
+    j.str("fovAxis", d.fovAxis);
+    j.num("xfov", cameraXFov(d));
+    j.num("nearClip", d.nearClip);
+    j.num("farClip", d.farClip);
+    j.num("width", d.width);
+    j.num("height", d.height);
+    j.num("sampleCount", d.spp);
+    j.str("film", d.film.type);
+    j.str("rfilter", d.rfilter);
+    j.close('}');
+    j.open("bsdfs", '[');
+    for (const BsdfDesc &b : d.bsdfs) bsdfJSON(j, b);
+    j.close(']');
+    j.open("hair", '[');
+    for (const HairShapeDesc &h : d.shapes) {
+        j.open(nullptr, '{');
+        j.str("filename", h.file);
+        j.num("radius", h.radius);
+        j.num("angleThreshold", h.angleThreshold);
+        j.num("reduction", h.reduction);
+        j.arr("toWorld", h.toWorld, 16);
+        j.num("bsdf", h.bsdf);
+        j.close('}');
+    }
+    j.close(']');
+    j.open("meshes", '[');
+    for (const MeshShapeDesc &m : d.meshes) {
+        j.open(nullptr, '{');
+        j.str("type", m.type);
+        j.str("filename", m.file);
+        j.arr("toWorld", m.toWorld, 16);
+        j.boolean("faceNormals", m.faceNormals);
+        j.boolean("flipNormals", m.flipNormals);
+        j.boolean("flipTexCoords", m.flipTexCoords);
+        j.num("bsdf", m.bsdf);
+        j.close('}');
+    }
+    j.close(']');
+    j.open("emitter", '{');
+    j.str("type", d.emitter);
+    j.str("filename", d.envFile);
+    j.num("scale", d.envScale);
+    j.arr("toWorld", d.emitterToWorld, 16);
+    j.close('}');
+    j.close('}');
+    return j.o.str();
 }
 
 } // namespace hpt

@@ -322,6 +322,17 @@ int hpt_load_scene_xml(hpt_context *c, const char *path, int n_defines, const ch
     return HPT_OK;
 }
 
+int hpt_export_scene_json(hpt_context *c, char *buf, size_t capacity, size_t *needed) {
+    if (!c) return HPT_EINVAL;
+    if (!c->hairFromFile) return setErr(c, HPT_ESTATE, "no scene loaded with hpt_load_scene_xml");
+    const std::string js = sceneToJSON(c->desc);
+    if (needed) *needed = js.size() + 1;
+    if (!buf) return HPT_OK;
+    if (capacity < js.size() + 1) return setErr(c, HPT_EINVAL, "buffer too small");
+    std::memcpy(buf, js.c_str(), js.size() + 1);
+    return HPT_OK;
+}
+
 int hpt_set_camera(hpt_context *c, const float to_world[16], float fov_x_deg, int width, int height,
                    float near_clip, float far_clip) {
     if (!c || !to_world || width <= 0 || height <= 0 || !(near_clip > 0) || !(near_clip < far_clip))
@@ -528,6 +539,9 @@ int hpt_prepare(hpt_context *c) {
     if (!c) return HPT_EINVAL;
     if (!c->haveCamera || !c->haveHair || !c->haveBSDF || !c->haveEnv)
         return setErr(c, HPT_ESTATE, "scene incomplete: need camera, hair, bsdf and emitter");
+    if (!c->desc.meshes.empty())
+        return setErr(c, HPT_EINVAL, "scene has obj/rectangle shapes: the device path renders hair only; "
+                                     "triangle scenes (C1) render on the CPU path from hpt_export_scene_json");
     const bool hostOnly = c->device == HPT_HOST_ONLY;
     if (!hostOnly) {
         HIPCHK(c, hipSetDevice(c->device));

@@ -72,6 +72,7 @@ SIGNATURES = {
     "hpt_last_error": (C.c_char_p, [C.c_void_p]),
     "hpt_set_data_dir": (C.c_int, [C.c_void_p, C.c_char_p]),
     "hpt_load_scene_xml": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]),
+    "hpt_export_scene_json": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "hpt_set_camera": (C.c_int, [C.c_void_p, _f, C.c_float, C.c_int, C.c_int, C.c_float, C.c_float]),
     "hpt_set_sampler": (C.c_int, [C.c_void_p, C.c_int]),
     "hpt_set_sampler_scramble": (C.c_int, [C.c_void_p, C.c_uint64]),
@@ -183,6 +184,15 @@ class Renderer:
         keys = (C.c_char_p * max(1, len(defines)))(*[k.encode() for k in defines])
         vals = (C.c_char_p * max(1, len(defines)))(*[str(v).encode() for v in defines.values()])
         self._check(self.lib.hpt_load_scene_xml(self.h, path.encode(), len(defines), keys, vals))
+
+    def scene_json(self) -> dict:
+        """The parsed scene (hpt_export_scene_json), defaults resolved."""
+        import json
+        need = C.c_size_t(0)
+        self._check(self.lib.hpt_export_scene_json(self.h, None, 0, C.byref(need)))
+        buf = C.create_string_buffer(need.value)
+        self._check(self.lib.hpt_export_scene_json(self.h, buf, need.value, C.byref(need)))
+        return json.loads(buf.value.decode())
 
     def set_camera(self, to_world, fov_x, width, height, near=1e-2, far=1e4):
         m = _f32(to_world).reshape(16)

@@ -51,9 +51,19 @@ int hpt_set_data_dir(hpt_context *ctx, const char *dir);
 /* Parse a Mitsuba scene XML (src/librender/scenehandler.cpp) with -D style
    defines: integrator "path", sensor "perspective" + sampler "sobol" + film,
    shape "hair", bsdf "marschner"/"kajiyakay"/"roughplastic"/"marschnerdielectric"/"thindielectric"/"diffuse"
+   (parsed too, CPU path only: shape "obj"/"rectangle", bsdf "plastic"/"twosided", texture "checkerboard")
    (one per hair shape; several shapes per scene), emitter "sunsky"/"envmap". */
 int hpt_load_scene_xml(hpt_context *ctx, const char *path, int n_defines, const char *const *keys,
                        const char *const *values);
+
+/* The parsed scene as JSON: defaults resolved, paths absolute, every shape
+   (hair and, for the C1 plumbing scene, obj / rectangle meshes) with its BSDF
+   (plastic, twosided, diffuse with a checkerboard texture ...).  Replaces
+   reading the SceneHandler's object graph (src/librender/scenehandler.cpp:
+   endElement) from C.  With buf == NULL only *needed (bytes incl. the NUL) is
+   set.  hpt_prepare refuses scenes with mesh shapes: triangles render on the
+   CPU path only (BASELINE.json configs[0]). */
+int hpt_export_scene_json(hpt_context *ctx, char *buf, size_t capacity, size_t *needed);
 
 /* ---- low-level scene setters (what a Mitsuba plugin shim would call) ---- */
 /* PerspectiveCameraImpl (src/sensors/perspective.cpp:108-165); row-major 4x4 */

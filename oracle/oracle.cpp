@@ -20,12 +20,15 @@
  */
 #include "oracle.h"
 #include "ref_core.h"
+#include "lobatto.h"
 
 #include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
+#include <functional>
+#include <map>
 #include <memory>
 #include <sstream>
 #include <stdexcept>
@@ -1209,74 +1212,110 @@ struct ThinDielectric {
     }
 };
 
+#include "mesh_bsdf.h"
+
 /* ------------------------------------------------------------------ */
-/* diffuse.cpp:60-140 (SmoothDiffuse, constant reflectance)            */
+/* diffuse.cpp:60-140 (SmoothDiffuse: a constant or checkerboard reflectance) */
 /* ------------------------------------------------------------------ */
 struct SmoothDiffuse {
     Spec reflectance{0.5f};
-    void configure() {
-        float mx = reflectance.max();
-        if (mx > 1.0f) reflectance *= 0.99f * (1.0f / mx);
+    bool textured = false;
+    Checkerboard tex;
+    void configure() { /* ensureEnergyConservation (bsdf.cpp:88-112): a ScalingTexture */
+        float mx = maxReflectance();
+        if (mx > 1.0f) {
+            const float scale = 0.99f * (1.0f / mx);
+            reflectance *= scale;
+            tex.color0 *= scale;
+            tex.color1 *= scale;
+        }
     }
-    Spec eval(const V3 &wi, const V3 &wo) const {
+    float maxReflectance() const { return textured ? tex.maximum().max() : reflectance.max(); }
+    Spec refl(const float *uv) const { return textured ? tex.eval(uv ? uv[0] : 0.0f, uv ? uv[1] : 0.0f) : reflectance; }
+    Spec eval(const V3 &wi, const V3 &wo, const float *uv = nullptr) const {
         if (wi.z <= 0 || wo.z <= 0) return Spec(0.0f);
-        return reflectance * (kInvPi * wo.z);
+        return refl(uv) * (kInvPi * wo.z);
     }
     float pdf(const V3 &wi, const V3 &wo) const {
         if (wi.z <= 0 || wo.z <= 0) return 0.0f;
         return kInvPi * wo.z;
     }
-    Spec sample(const V3 &wi, float sx, float sy, V3 &wo, float &pdfOut, uint32_t &type) const {
+    Spec sample(const V3 &wi, float sx, float sy, V3 &wo, float &pdfOut, uint32_t &type,
+                const float *uv = nullptr) const {
         pdfOut = 0;
         type = 0;
         if (wi.z <= 0) return Spec(0.0f);
         wo = squareToCosineHemisphere(sx, sy);
         type = EDiffuseReflection;
         pdfOut = kInvPi * wo.z;
-        return reflectance;
+        return refl(uv);
     }
 };
 
-/* One BSDF instance of a hair shape (the default is Shape::configure's 0.5
-   Lambertian, shape.cpp:57-64) */
+/* One BSDF instance: of a hair shape (the default is Shape::configure's 0.5
+   Lambertian, shape.cpp:57-64) or of a mesh shape.  uv = the intersection's
+   texture coordinates (only the checkerboard diffuse reads them; NULL = (0, 0)). */
 struct BsdfInst {
-    int kind = 5; /* 0 marschner, 1 kajiyakay, 2 roughplastic, 3 marschnerdielectric, 4 thindielectric, 5 diffuse */
+    int kind = 5; /* 0 marschner, 1 kajiyakay, 2 roughplastic, 3 marschnerdielectric, 4 thindielectric, 5 diffuse,
+                     6 plastic, 7 twosided */
     Marschner marschner;
     KajiyaKay kk;
     RoughPlastic rp;
     MarschnerDielectric md;
     ThinDielectric td;
     SmoothDiffuse df;
+    SmoothPlastic pl;
+    std::shared_ptr<BsdfInst> nested[2]; /* twosided.cpp:84-89: nested[1] = nested[0] when absent */
     /* the combined type has an ESmooth component (path.cpp:175 gate) */
-    bool smooth() const { return kind != 4 && !(kind == 5 && df.reflectance.max() <= 0); }
-    Spec eval(const V3 &wi, const V3 &wo) const {
+    bool smooth() const {
+        if (kind == 7) return nested[0]->smooth() || nested[1]->smooth();
+        return kind != 4 && !(kind == 5 && df.maxReflectance() <= 0);
+    }
+    Spec eval(const V3 &wi, const V3 &wo, const float *uv = nullptr) const {
         switch (kind) {
         case 0: return marschner.eval(wi, wo);
         case 1: return kk.eval(wi, wo);
         case 2: return rp.eval(wi, wo);
         case 3: return md.eval(wi, wo);
         case 4: return td.eval(wi, wo);
-        default: return df.eval(wi, wo);
+        case 6: return pl.eval(wi, wo);
+        case 7: /* twosided.cpp:108-120 */
+            if (wi.z > 0) return nested[0]->eval(wi, wo, uv);
+            return nested[1]->eval(V3(wi.x, wi.y, -wi.z), V3(wo.x, wo.y, -wo.z), uv);
+        default: return df.eval(wi, wo, uv);
         }
     }
-    float pdf(const V3 &wi, const V3 &wo) const {
+    float pdf(const V3 &wi, const V3 &wo, const float *uv = nullptr) const {
         switch (kind) {
         case 0: return marschner.pdf();
         case 1: return kk.pdf(wi, wo);
         case 2: return rp.pdf(wi, wo);
         case 3: return md.pdf(wi, wo);
         case 4: return td.pdf(wi, wo);
+        case 6: return pl.pdf(wi, wo);
+        case 7: /* :122-134 */
+            if (wi.z > 0) return nested[0]->pdf(wi, wo, uv);
+            return nested[1]->pdf(V3(wi.x, wi.y, -wi.z), V3(wo.x, wo.y, -wo.z), uv);
         default: return df.pdf(wi, wo);
         }
     }
-    Spec sample(const V3 &wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type) const {
+    Spec sample(const V3 &wi, float sx, float sy, V3 &wo, float &pdf, uint32_t &type,
+                const float *uv = nullptr) const {
         switch (kind) {
         case 0: return marschner.sample(wi, sx, sy, wo, pdf, type);
         case 1: return kk.sample(wi, sx, sy, wo, pdf, type);
         case 2: return rp.sample(wi, sx, sy, wo, pdf, type);
         case 3: return md.sample(wi, sx, sy, wo, pdf, type);
         case 4: return td.sample(wi, sx, sy, wo, pdf, type);
-        default: return df.sample(wi, sx, sy, wo, pdf, type);
+        case 6: return pl.sample(wi, sx, sy, wo, pdf, type);
+        case 7: { /* :161-183 */
+            const bool flipped = wi.z < 0;
+            const V3 w = flipped ? V3(wi.x, wi.y, -wi.z) : wi;
+            Spec result = nested[flipped ? 1 : 0]->sample(w, sx, sy, wo, pdf, type, uv);
+            if (flipped && !result.isZero() && pdf != 0) wo.z *= -1;
+            return result;
+        }
+        default: return df.sample(wi, sx, sy, wo, pdf, type, uv);
         }
     }
 };
@@ -1467,6 +1506,11 @@ struct Hit {
     float t = kInf;
     uint32_t iv = 0;
     V3 p;
+    /* mesh hits (mesh_geom.h): kind 1 = triangle (shape = mesh, prim = triangle, u/v = barycentrics),
+       kind 2 = rectangle (shape = rectangle, u/v = local x/y) */
+    int kind = 0;
+    uint32_t shape = 0, prim = 0;
+    float u = 0, v = 0;
     bool valid() const { return t < kInf; }
 };
 
@@ -1829,92 +1873,7 @@ struct EnvMap {
     }
 };
 
-} // namespace
-
-/* ------------------------------------------------------------------ */
-/* The scene                                                            */
-/* ------------------------------------------------------------------ */
-struct orc_scene {
-    std::string err;
-    /* sobol */
-    std::vector<uint32_t> m32;
-    uint64_t scramble = 0; /* after sampleTEA */
-    std::vector<uint64_t> vdc, vdcInv;
-    int vdcRows = 0, invRows = 0;
-    /* camera */
-    float toWorld[16];
-    float fov = 35, nearClip = 1e-2f, farClip = 1e4f;
-    int width = 0, height = 0;
-    float s2c[16]; /* sampleToCamera, row-major */
-    float dx[3], dy[3];
-    float invResX = 0, invResY = 0;
-    uint32_t logRes = 0;
-    float resolution = 1;
-    /* scene */
-    HairGeom hair;
-    KDTree tree;
-    AABB aabb;
-    std::vector<BsdfInst> bsdfs; /* one per hair shape (orc_set_* sets the last loaded shape's) */
-    EnvMap env;
-    bool hasEnv = false;
-    int maxDepth = -1, rrDepth = 5;
-    int sampleCount = 1; /* sampler->getSampleCount() for the ray-differential scale */
-    bool strictNormals = false, hideEmitters = false;
-    bool prepared = false;
-};
-
-namespace {
-
-/* ---------------- Sobol: sobolseq.h:43-58, 99-131; sobol.cpp:204-250 ---------------- */
-inline float sobolSample(const orc_scene *s, uint64_t index, uint32_t dim) {
-    uint32_t result = (uint32_t) s->scramble; /* sobolseq.h:43-58 with (uint32_t) scramble */
-    for (uint32_t i = dim * 52; index; index >>= 1, ++i)
-        if (index & 1)
-            result ^= s->m32[i];
-    return std::min(result * (1.0f / (1ULL << 32)), kOneMinusEps);
-}
-
-inline uint64_t sobolLookUp(const orc_scene *s, uint32_t m, uint32_t frame, uint32_t px, uint32_t py) {
-    const uint32_t m2 = m << 1;
-    uint64_t index = uint64_t(frame) << m2;
-    uint64_t delta = 0;
-    for (uint32_t c = 0; frame; frame >>= 1, ++c)
-        if (frame & 1)
-            delta ^= s->vdc[(m - 1) * 52 + c];
-    uint64_t scramble = (s->scramble & 0xFFFFFFFF) >> (32 - m); /* sobolseq.h:119-123 */
-    uint64_t b = (((uint64_t) (px ^ scramble) << m) | (py ^ scramble)) ^ delta;
-    for (uint32_t c = 0; b; b >>= 1, ++c)
-        if (b & 1)
-            index ^= s->vdcInv[(m - 1) * 52 + c];
-    return index;
-}
-
-struct Sampler {
-    const orc_scene *s;
-    uint64_t sobolIndex = 0, sampleIndex = 0;
-    uint32_t dimension = 0;
-    int px = 0, py = 0;
-    void setSampleIndex(uint64_t j) {
-        dimension = 0;
-        sampleIndex = j;
-        if (s->logRes > 1 && px >= 0)
-            sobolIndex = sobolLookUp(s, s->logRes, (uint32_t) j, px, py);
-        else
-            sobolIndex = j;
-    }
-    float next1D() { return sobolSample(s, sobolIndex, dimension++); }
-    void next2D(float &a, float &b) {
-        if (dimension == 0 && sobolIndex != sampleIndex) {
-            a = sobolSample(s, sobolIndex, dimension++) * s->resolution - px;
-            b = sobolSample(s, sobolIndex, dimension++) * s->resolution - py;
-        } else {
-            a = sobolSample(s, sobolIndex, dimension++);
-            b = sobolSample(s, sobolIndex, dimension++);
-        }
-    }
-};
-
-/* ---------------- camera: perspective.cpp:125-165, 271-298 ---------------- */
+/* ---------------- transforms (transform.h, matrix.h/.inl) ---------------- */
 inline V3 xformPoint(const float *M, const V3 &p) { /* transform.h:108-125 */
     float x = M[0] * p.x + M[1] * p.y + M[2] * p.z + M[3];
     float y = M[4] * p.x + M[5] * p.y + M[6] * p.z + M[7];
@@ -2005,6 +1964,101 @@ static Xform xformTranslate(float x, float y, float z) { /* transform.cpp:33-47 
                  {{{1, 0, 0, -x}, {0, 1, 0, -y}, {0, 0, 1, -z}, {0, 0, 0, 1}}}};
 }
 
+#include "mesh_geom.h"
+
+} // namespace
+
+/* ------------------------------------------------------------------ */
+/* The scene                                                            */
+/* ------------------------------------------------------------------ */
+struct orc_scene {
+    std::string err;
+    /* sobol */
+    std::vector<uint32_t> m32;
+    uint64_t scramble = 0; /* after sampleTEA */
+    std::vector<uint64_t> vdc, vdcInv;
+    int vdcRows = 0, invRows = 0;
+    /* camera */
+    float toWorld[16];
+    float fov = 35, nearClip = 1e-2f, farClip = 1e4f;
+    int width = 0, height = 0;
+    float s2c[16]; /* sampleToCamera, row-major */
+    float dx[3], dy[3];
+    float invResX = 0, invResY = 0;
+    uint32_t logRes = 0;
+    float resolution = 1;
+    /* scene */
+    HairGeom hair;
+    KDTree tree;
+    AABB aabb;                   /* hair AABB */
+    /* C1 mesh shapes (mesh_geom.h): CPU path only */
+    std::vector<TriMesh> meshes;
+    std::vector<RectShape> rects;
+    MeshBVH bvh;
+    AABB sceneAabb;              /* == aabb for hair-only scenes */
+    bool hasMeshes() const { return !meshes.empty() || !rects.empty(); }
+    bool hasHair() const { return !hair.shapeFirst.empty(); }
+    std::vector<BsdfInst> bsdfs; /* hair shapes: one each (orc_set_* sets the last one's); meshes index it */
+    EnvMap env;
+    bool hasEnv = false;
+    int maxDepth = -1, rrDepth = 5;
+    int sampleCount = 1; /* sampler->getSampleCount() for the ray-differential scale */
+    bool strictNormals = false, hideEmitters = false;
+    bool prepared = false;
+};
+
+namespace {
+
+/* ---------------- Sobol: sobolseq.h:43-58, 99-131; sobol.cpp:204-250 ---------------- */
+inline float sobolSample(const orc_scene *s, uint64_t index, uint32_t dim) {
+    uint32_t result = (uint32_t) s->scramble; /* sobolseq.h:43-58 with (uint32_t) scramble */
+    for (uint32_t i = dim * 52; index; index >>= 1, ++i)
+        if (index & 1)
+            result ^= s->m32[i];
+    return std::min(result * (1.0f / (1ULL << 32)), kOneMinusEps);
+}
+
+inline uint64_t sobolLookUp(const orc_scene *s, uint32_t m, uint32_t frame, uint32_t px, uint32_t py) {
+    const uint32_t m2 = m << 1;
+    uint64_t index = uint64_t(frame) << m2;
+    uint64_t delta = 0;
+    for (uint32_t c = 0; frame; frame >>= 1, ++c)
+        if (frame & 1)
+            delta ^= s->vdc[(m - 1) * 52 + c];
+    uint64_t scramble = (s->scramble & 0xFFFFFFFF) >> (32 - m); /* sobolseq.h:119-123 */
+    uint64_t b = (((uint64_t) (px ^ scramble) << m) | (py ^ scramble)) ^ delta;
+    for (uint32_t c = 0; b; b >>= 1, ++c)
+        if (b & 1)
+            index ^= s->vdcInv[(m - 1) * 52 + c];
+    return index;
+}
+
+struct Sampler {
+    const orc_scene *s;
+    uint64_t sobolIndex = 0, sampleIndex = 0;
+    uint32_t dimension = 0;
+    int px = 0, py = 0;
+    void setSampleIndex(uint64_t j) {
+        dimension = 0;
+        sampleIndex = j;
+        if (s->logRes > 1 && px >= 0)
+            sobolIndex = sobolLookUp(s, s->logRes, (uint32_t) j, px, py);
+        else
+            sobolIndex = j;
+    }
+    float next1D() { return sobolSample(s, sobolIndex, dimension++); }
+    void next2D(float &a, float &b) {
+        if (dimension == 0 && sobolIndex != sampleIndex) {
+            a = sobolSample(s, sobolIndex, dimension++) * s->resolution - px;
+            b = sobolSample(s, sobolIndex, dimension++) * s->resolution - py;
+        } else {
+            a = sobolSample(s, sobolIndex, dimension++);
+            b = sobolSample(s, sobolIndex, dimension++);
+        }
+    }
+};
+
+/* ---------------- camera: perspective.cpp:125-165, 271-298 ---------------- */
 /* PerspectiveCameraImpl::configure (perspective.cpp:125-165): m_cameraToSample =
    S(1/relSize) T(-relOffset) S(-0.5, -0.5 aspect, 1) T(-1, -1/aspect, 0) perspective(...),
    m_sampleToCamera = its inverse (the Transform's stored inverse matrix) */
@@ -2178,12 +2232,29 @@ bool rayIntersectBrute(const orc_scene *s, const Ray &ray, float mint, float max
     return found;
 }
 
+/* the hair shape inside the scene-level kd-tree (hair.cpp:200-217): clip to the hair AABB,
+   then HairKDTree::rayIntersect */
+bool hairIntersect(const orc_scene *s, const Ray &ray, float mint, float maxt, Hit &hit, Stats *st, bool brute) {
+    float m2, M2;
+    if (!s->aabb.rayIntersect(ray, m2, M2)) return false;
+    if (mint > m2) m2 = mint;
+    if (maxt < M2) M2 = maxt;
+    if (!(M2 > m2)) return false;
+    float t = kInf;
+    bool ok = brute ? rayIntersectBrute<false>(s, ray, m2, M2, t, &hit) : rayIntersectHavran<false>(s, ray, m2, M2, t, &hit, st);
+    if (ok) {
+        hit.t = t;
+        hit.kind = 0;
+    }
+    return ok;
+}
+
 /* skdtree.cpp:112-141 */
 bool sceneIntersect(const orc_scene *s, const Ray &ray, Hit &hit, Stats *st, bool brute = false) {
     hit.t = kInf;
     float mint, maxt;
     if (st) st->rays++;
-    if (s->aabb.rayIntersect(ray, mint, maxt)) {
+    if (s->sceneAabb.rayIntersect(ray, mint, maxt)) {
         float rayMinT = ray.mint;
         if (rayMinT == kEpsilon)
             rayMinT *= std::max(std::max(std::max(std::abs(ray.o.x), std::abs(ray.o.y)), std::abs(ray.o.z)),
@@ -2191,21 +2262,10 @@ bool sceneIntersect(const orc_scene *s, const Ray &ray, Hit &hit, Stats *st, boo
         if (rayMinT > mint) mint = rayMinT;
         if (ray.maxt < maxt) maxt = ray.maxt;
         if (maxt > mint) {
-            /* scene-level leaf -> HairShape::rayIntersect -> HairKDTree::rayIntersect (hair.cpp:200-217) */
-            float m2, M2;
-            if (s->aabb.rayIntersect(ray, m2, M2)) {
-                if (mint > m2) m2 = mint;
-                if (maxt < M2) M2 = maxt;
-                if (M2 > m2) {
-                    float t = kInf;
-                    bool ok = brute ? rayIntersectBrute<false>(s, ray, m2, M2, t, &hit)
-                                    : rayIntersectHavran<false>(s, ray, m2, M2, t, &hit, st);
-                    if (ok) {
-                        hit.t = t;
-                        return true;
-                    }
-                }
-            }
+            /* meshes first (any order gives the closest hit: maxt shrinks), then the hair shape */
+            bool found = s->hasMeshes() && meshIntersect<false>(s->meshes, s->rects, s->bvh, ray, mint, maxt, &hit, st);
+            if (s->hasHair() && hairIntersect(s, ray, mint, maxt, hit, st, brute)) found = true;
+            if (found) return true;
         }
     }
     hit.t = kInf;
@@ -2216,13 +2276,16 @@ bool sceneIntersect(const orc_scene *s, const Ray &ray, Hit &hit, Stats *st, boo
 bool sceneOccluded(const orc_scene *s, const Ray &ray, Stats *st, bool brute = false) {
     float mint, maxt, t = kInf;
     if (st) st->shadowRays++;
-    if (s->aabb.rayIntersect(ray, mint, maxt)) {
+    if (s->sceneAabb.rayIntersect(ray, mint, maxt)) {
         float rayMinT = ray.mint;
         if (rayMinT == kEpsilon)
             rayMinT *= std::max(std::max(std::abs(ray.o.x), std::abs(ray.o.y)), std::abs(ray.o.z));
         if (rayMinT > mint) mint = rayMinT;
         if (ray.maxt < maxt) maxt = ray.maxt;
         if (maxt > mint) {
+            if (s->hasMeshes() && meshIntersect<true>(s->meshes, s->rects, s->bvh, ray, mint, maxt, nullptr, st))
+                return true;
+            if (!s->hasHair()) return false;
             float m2, M2;
             if (s->aabb.rayIntersect(ray, m2, M2)) {
                 if (mint > m2) m2 = mint;
@@ -2244,12 +2307,67 @@ struct Intersection {
     V3 p;
     Frame geoFrame, shFrame;
     V3 wi;
+    float uv[2] = {0, 0};
+    int bsdf = 0; /* index into orc_scene::bsdfs */
     V3 toWorld(const V3 &v) const { return shFrame.toWorld(v); }
     V3 toLocal(const V3 &v) const { return shFrame.toLocal(v); }
 };
 
+/* skdtree.h:343-428 (fillIntersectionRecord<true>) for a triangle, rectangle.cpp:155-168 for a rectangle */
+void fillMeshIntersection(const orc_scene *s, const Ray &ray, const Hit &hit, Intersection &its) {
+    its.t = hit.t;
+    its.iv = 0;
+    V3 dpdu;
+    if (hit.kind == 1) {
+        const TriMesh &m = s->meshes[hit.shape];
+        const uint32_t i0 = m.idx[3 * hit.prim], i1 = m.idx[3 * hit.prim + 1], i2 = m.idx[3 * hit.prim + 2];
+        const V3 b(1 - hit.u - hit.v, hit.u, hit.v);
+        const V3 &p0 = m.p[i0], &p1 = m.p[i1], &p2 = m.p[i2];
+        its.p = p0 * b.x + p1 * b.y + p2 * b.z;
+        const V3 side1 = p1 - p0, side2 = p2 - p0;
+        V3 faceNormal = cross(side1, side2);
+        const float length = faceNormal.length();
+        if (!faceNormal.isZero()) faceNormal /= length;
+        dpdu = m.dpdu.empty() ? side1 : m.dpdu[hit.prim];
+        V3 shN;
+        if (!m.n.empty()) {
+            shN = normalize(m.n[i0] * b.x + m.n[i1] * b.y + m.n[i2] * b.z);
+            if (dot(faceNormal, shN) < 0) faceNormal = -faceNormal;
+        } else {
+            shN = faceNormal;
+        }
+        its.geoFrame = frameFromNormal(faceNormal);
+        if (!m.uv.empty()) {
+            its.uv[0] = m.uv[2 * i0] * b.x + m.uv[2 * i1] * b.y + m.uv[2 * i2] * b.z;
+            its.uv[1] = m.uv[2 * i0 + 1] * b.x + m.uv[2 * i1 + 1] * b.y + m.uv[2 * i2 + 1] * b.z;
+        } else {
+            its.uv[0] = b.y;
+            its.uv[1] = b.z;
+        }
+        its.shFrame.n = shN;
+        its.bsdf = m.bsdf;
+    } else {
+        const RectShape &r = s->rects[hit.shape];
+        its.geoFrame = r.frame;
+        its.shFrame = frameFromNormal(its.geoFrame.n);
+        dpdu = r.dpdu;
+        its.uv[0] = 0.5f * (hit.u + 1);
+        its.uv[1] = 0.5f * (hit.v + 1);
+        its.p = ray.at(its.t);
+        its.bsdf = r.bsdf;
+    }
+    computeShadingFrame(its.shFrame.n, dpdu, its.shFrame);
+    its.wi = its.toLocal(-ray.d);
+}
+
 /* hair.cpp:825-862 + skdtree.h:422-427 */
 void fillIntersection(const orc_scene *s, const Ray &ray, const Hit &hit, Intersection &its) {
+    if (hit.kind != 0) {
+        fillMeshIntersection(s, ray, hit, its);
+        return;
+    }
+    its.bsdf = s->hair.shapeBsdf[s->hair.shapeOf(hit.iv)];
+    its.uv[0] = its.uv[1] = 0;
     its.t = hit.t;
     its.iv = hit.iv;
     its.p = hit.p;
@@ -2346,7 +2464,7 @@ Spec Li(const orc_scene *s, const CamRay &cr, Sampler &sampler, Stats *st, int *
             (s->strictNormals && dot(ray.d, its.geoFrame.n) * its.wi.z >= 0))
             break;
         if (st) st->bounces++;
-        const BsdfInst &bsdf = bsdfOf(s, its.iv);
+        const BsdfInst &bsdf = s->bsdfs[its.bsdf];
         /* direct illumination, only for BSDFs with an ESmooth component (path.cpp:175) */
         float nx, ny;
         if (bsdf.smooth()) sampler.next2D(nx, ny);
@@ -2356,9 +2474,9 @@ Spec Li(const orc_scene *s, const CamRay &cr, Sampler &sampler, Stats *st, int *
             Spec value = sampleEmitterDirect(s, its.p, nx, ny, dRecD, dRecPdf, st);
             if (!value.isZero()) {
                 V3 wo = its.toLocal(dRecD);
-                const Spec bsdfVal = bsdf.eval(its.wi, wo);
+                const Spec bsdfVal = bsdf.eval(its.wi, wo, its.uv);
                 if (!bsdfVal.isZero() && (!s->strictNormals || dot(its.geoFrame.n, dRecD) * wo.z > 0)) {
-                    float bp = bsdf.pdf(its.wi, wo);
+                    float bp = bsdf.pdf(its.wi, wo, its.uv);
                     float weight = miWeight(dRecPdf, bp);
                     Li += throughput * value * bsdfVal * weight;
                 }
@@ -2370,7 +2488,7 @@ Spec Li(const orc_scene *s, const CamRay &cr, Sampler &sampler, Stats *st, int *
         float bsdfPdfV = 0;
         uint32_t sampledType = 0;
         V3 woLocal;
-        Spec bsdfWeight = bsdf.sample(its.wi, bx, by, woLocal, bsdfPdfV, sampledType);
+        Spec bsdfWeight = bsdf.sample(its.wi, bx, by, woLocal, bsdfPdfV, sampledType, its.uv);
         if (bsdfWeight.isZero())
             break;
         scattered |= sampledType != ENull;
@@ -2487,8 +2605,30 @@ void prepareScene(orc_scene *s) {
         s->aabb.expandBy(mn);
         s->aabb.expandBy(mx);
     }
-    /* scene.cpp:386-412 + envmap.cpp:336-347: bsphere of (hair AABB U camera position) * 1.5 */
-    AABB sc = s->aabb;
+    s->sceneAabb = s->aabb;
+    if (s->hasMeshes()) {
+        buildMeshBVH(s->meshes, s->rects, s->bvh);
+        AABB a;
+        if (s->hasHair()) {
+            a.expandBy(s->aabb.min);
+            a.expandBy(s->aabb.max);
+        }
+        for (const TriMesh &m : s->meshes) {
+            a.expandBy(m.aabb.min);
+            a.expandBy(m.aabb.max);
+        }
+        for (const RectShape &r : s->rects) {
+            a.expandBy(r.aabb.min);
+            a.expandBy(r.aabb.max);
+        }
+        /* the scene kd-tree's bounds, slightly enlarged (gkdtree.h:1213-1220; max uses the new min) */
+        const float eps = 1e-3f;
+        a.min -= (a.max - a.min) * eps + V3(eps);
+        a.max += (a.max - a.min) * eps + V3(eps);
+        s->sceneAabb = a;
+    }
+    /* scene.cpp:386-412 + envmap.cpp:336-347: bsphere of (scene AABB U camera position) * 1.5 */
+    AABB sc = s->sceneAabb;
     sc.expandBy(V3(s->toWorld[3], s->toWorld[7], s->toWorld[11]));
     V3 center = (sc.max + sc.min) * 0.5f;
     float radius = (center - sc.max).length();
@@ -2871,6 +3011,144 @@ int orc_set_diffuse(orc_scene *s, const float reflectance[3]) {
     return 0;
 }
 
+/* ---- C1 mesh scene (mesh_bsdf.h, mesh_geom.h) ---- */
+int orc_new_bsdf(orc_scene *s) {
+    s->bsdfs.emplace_back();
+    s->prepared = false;
+    return (int) s->bsdfs.size() - 1;
+}
+
+int orc_set_diffuse_checkerboard(orc_scene *s, const float color0[3], const float color1[3], float uoffset,
+                                 float voffset, float uscale, float vscale) {
+    BsdfInst &b = lastBsdf(s);
+    b.kind = 5;
+    b.df = SmoothDiffuse();
+    b.df.textured = true;
+    b.df.tex.color0 = Spec(color0[0], color0[1], color0[2]);
+    b.df.tex.color1 = Spec(color1[0], color1[1], color1[2]);
+    b.df.tex.uoffset = uoffset;
+    b.df.tex.voffset = voffset;
+    b.df.tex.uscale = uscale;
+    b.df.tex.vscale = vscale;
+    b.df.configure();
+    return 0;
+}
+
+int orc_set_plastic(orc_scene *s, float eta, int nonlinear, const float diffuse[3], const float specular[3]) {
+    BsdfInst &b = lastBsdf(s);
+    b.kind = 6;
+    b.pl = SmoothPlastic();
+    b.pl.eta = eta;
+    b.pl.nonlinear = nonlinear != 0;
+    b.pl.diffuse = Spec(diffuse[0], diffuse[1], diffuse[2]);
+    b.pl.specular = Spec(specular[0], specular[1], specular[2]);
+    b.pl.configure();
+    return 0;
+}
+
+int orc_set_twosided(orc_scene *s, int nested0, int nested1) {
+    const int n = (int) s->bsdfs.size();
+    if (nested0 < 0 || nested0 >= n - 1 || nested1 >= n - 1) { s->err = "twosided: bad nested bsdf index"; return -1; }
+    if (nested1 < 0) nested1 = nested0;
+    for (int k : {nested0, nested1}) {
+        const int kind = s->bsdfs[k].kind;
+        if (kind == 0 || kind == 1 || kind == 3 || kind == 4) {
+            s->err = "Only materials without a transmission component can be nested!";
+            return -1;
+        }
+    }
+    /* the nestable kinds (roughplastic, diffuse, plastic, twosided) are plain values */
+    auto copyOf = [&](int k) {
+        const BsdfInst &src = s->bsdfs[k];
+        auto p = std::make_shared<BsdfInst>();
+        p->kind = src.kind;
+        p->rp = src.rp;
+        p->df = src.df;
+        p->pl = src.pl;
+        p->nested[0] = src.nested[0];
+        p->nested[1] = src.nested[1];
+        return p;
+    };
+    BsdfInst &b = s->bsdfs.back();
+    b.nested[0] = copyOf(nested0);
+    b.nested[1] = copyOf(nested1);
+    b.kind = 7;
+    return 0;
+}
+
+int orc_add_obj(orc_scene *s, const char *path, const float *to_world, int face_normals, int flip_normals,
+                int flip_tex_coords, int bsdf) {
+    if (bsdf < 0 || bsdf >= (int) s->bsdfs.size()) { s->err = "obj: bad bsdf index"; return -1; }
+    try {
+        loadOBJ(path, to_world, face_normals != 0, flip_normals != 0, flip_tex_coords != 0, bsdf, s->meshes);
+    } catch (const std::exception &e) {
+        s->err = e.what();
+        return -1;
+    }
+    s->prepared = false;
+    return 0;
+}
+
+int orc_add_rectangle(orc_scene *s, const float *to_world, int flip_normals, int bsdf) {
+    if (bsdf < 0 || bsdf >= (int) s->bsdfs.size()) { s->err = "rectangle: bad bsdf index"; return -1; }
+    try {
+        s->rects.push_back(makeRectangle(to_world, flip_normals != 0, bsdf));
+    } catch (const std::exception &e) {
+        s->err = e.what();
+        return -1;
+    }
+    s->prepared = false;
+    return 0;
+}
+
+int orc_mesh_info(orc_scene *s, int64_t *out /* [4]: meshes, triangles, vertices, rectangles */) {
+    int64_t tris = 0, verts = 0;
+    for (const TriMesh &m : s->meshes) {
+        tris += (int64_t) m.triangles();
+        verts += (int64_t) m.p.size();
+    }
+    out[0] = (int64_t) s->meshes.size();
+    out[1] = tris;
+    out[2] = verts;
+    out[3] = (int64_t) s->rects.size();
+    return 0;
+}
+
+/* BSDF batch with texture coordinates (the last BSDF) */
+void orc_bsdf_eval_uv(orc_scene *s, int n, const float *wi, const float *wo, const float *uv, float *out_rgb,
+                      float *out_pdf) {
+    const BsdfInst &b = s->bsdfs.back();
+    for (int i = 0; i < n; ++i) {
+        const V3 a(wi[3 * i], wi[3 * i + 1], wi[3 * i + 2]), c(wo[3 * i], wo[3 * i + 1], wo[3 * i + 2]);
+        const Spec v = b.eval(a, c, uv + 2 * i);
+        for (int k = 0; k < 3; ++k) out_rgb[3 * i + k] = v.s[k];
+        out_pdf[i] = b.pdf(a, c, uv + 2 * i);
+    }
+}
+
+float orc_fresnel_diffuse_reflectance(float eta) { return fresnelDiffuseReflectance(eta); }
+
+/* trace a batch of rays through the whole scene (meshes and hair): t (inf on miss), the
+   hit record's shading normal, uv and bsdf index */
+void orc_trace_scene(orc_scene *s, int n, const float *o, const float *d, float *out_t, float *out_n,
+                     float *out_uv, int32_t *out_bsdf) {
+    if (!s->prepared) prepareScene(s);
+    for (int i = 0; i < n; ++i) {
+        Ray ray(V3(o[3 * i], o[3 * i + 1], o[3 * i + 2]), V3(d[3 * i], d[3 * i + 1], d[3 * i + 2]), kEpsilon, kInf);
+        Hit hit;
+        out_t[i] = kInf;
+        out_bsdf[i] = -1;
+        if (!sceneIntersect(s, ray, hit, nullptr)) continue;
+        Intersection its;
+        fillIntersection(s, ray, hit, its);
+        out_t[i] = its.t;
+        for (int k = 0; k < 3; ++k) out_n[3 * i + k] = its.shFrame.n[k];
+        out_uv[2 * i] = its.uv[0];
+        out_uv[2 * i + 1] = its.uv[1];
+        out_bsdf[i] = its.bsdf;
+    }
+}
+
 int orc_set_envmap(orc_scene *s, const float *rgb, int w, int h, float scale, const float *to_world) {
     s->env.w = w;
     s->env.h = h;
@@ -2921,7 +3199,7 @@ int orc_set_integrator(orc_scene *s, int max_depth, int rr_depth, int strict_nor
 int orc_prepare(orc_scene *s) {
     if (s->m32.empty()) { s->err = "sobol tables not set"; return -1; }
     if (s->width <= 0) { s->err = "camera not set"; return -1; }
-    if (s->hair.shapeFirst.empty()) { s->err = "no hair shape"; return -1; }
+    if (!s->hasHair() && !s->hasMeshes()) { s->err = "no shape"; return -1; }
     try {
         prepareScene(s);
     } catch (const std::exception &e) {
@@ -2948,7 +3226,7 @@ int orc_get_camera(orc_scene *s, float sample_to_camera[16], float dx[3], float 
 static int renderImpl(orc_scene *s, int spp_begin, int spp_end, int n_threads, int shard, int n_shards,
                       float *film, uint64_t *stats) {
     if (!s->prepared && orc_prepare(s) != 0) return -1;
-    if (s->tree.empty()) { s->err = "kd-tree not set"; return -1; }
+    if (s->hasHair() && s->tree.empty()) { s->err = "kd-tree not set"; return -1; }
     const int W = s->width, H = s->height, BS = 32;
     const int nbx = (W + BS - 1) / BS, nby = (H + BS - 1) / BS, nblocks = nbx * nby;
     /* shard ownership as the GPU renderer deals it (hpt_capi.cpp blockOrder): every

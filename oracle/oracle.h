@@ -85,6 +85,30 @@ int orc_set_marschnerdielectric(orc_scene *s, float eta, const float diffuse[3],
 /* thindielectric.cpp / diffuse.cpp */
 int orc_set_thindielectric(orc_scene *s, float eta, const float spec_r[3], const float spec_t[3]);
 int orc_set_diffuse(orc_scene *s, const float reflectance[3]);
+/* ---- C1 "teapot" plumbing scene (CPU path only; oracle/mesh_bsdf.h, mesh_geom.h) ----
+   orc_new_bsdf appends a BSDF (default 0.5 diffuse) and returns its index; the orc_set_*
+   calls configure the last one.  orc_set_twosided nests copies of two earlier BSDFs
+   (nested1 < 0: nested0 on both sides).  Mesh shapes reference BSDFs by index. */
+int orc_new_bsdf(orc_scene *s);
+/* diffuse.cpp with a checkerboard reflectance (checkerboard.cpp, texture.cpp:81-121) */
+int orc_set_diffuse_checkerboard(orc_scene *s, const float color0[3], const float color1[3], float uoffset,
+                                 float voffset, float uscale, float vscale);
+/* plastic.cpp (SmoothPlastic, constant reflectances): eta = intIOR/extIOR */
+int orc_set_plastic(orc_scene *s, float eta, int nonlinear, const float diffuse[3], const float specular[3]);
+int orc_set_twosided(orc_scene *s, int nested0, int nested1);
+/* obj.cpp WavefrontOBJ (to_world row-major, may be NULL) / rectangle.cpp */
+int orc_add_obj(orc_scene *s, const char *path, const float *to_world, int face_normals, int flip_normals,
+                int flip_tex_coords, int bsdf);
+int orc_add_rectangle(orc_scene *s, const float *to_world, int flip_normals, int bsdf);
+int orc_mesh_info(orc_scene *s, int64_t *out /* meshes, triangles, vertices, rectangles */);
+void orc_bsdf_eval_uv(orc_scene *s, int n, const float *wi, const float *wo, const float *uv, float *out_rgb,
+                      float *out_pdf);
+/* util.cpp:814-859 with fast = false */
+float orc_fresnel_diffuse_reflectance(float eta);
+/* closest hit over the whole scene: t (inf on miss), shading normal, uv, bsdf index (-1 on miss) */
+void orc_trace_scene(orc_scene *s, int n, const float *o, const float *d, float *out_t, float *out_n,
+                     float *out_uv, int32_t *out_bsdf);
+
 /* envmap.cpp: linear RGB float bitmap (w x h x 3), to_world may be NULL */
 int orc_set_envmap(orc_scene *s, const float *rgb, int w, int h, float scale,
                    const float *to_world);

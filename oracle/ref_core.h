@@ -95,6 +95,8 @@ struct Spec {
     Spec operator*(const Spec &o) const { return Spec(s[0] * o.s[0], s[1] * o.s[1], s[2] * o.s[2]); }
     Spec operator*(float f) const { return Spec(s[0] * f, s[1] * f, s[2] * f); }
     Spec operator/(float f) const { float r = 1.0f / f; return Spec(s[0] * r, s[1] * r, s[2] * r); }
+    Spec operator-(const Spec &o) const { return Spec(s[0] - o.s[0], s[1] - o.s[1], s[2] - o.s[2]); }
+    Spec &operator/=(const Spec &o) { for (int i = 0; i < 3; ++i) s[i] /= o.s[i]; return *this; } /* spectrum.h:170-175 */
     Spec &operator+=(const Spec &o) { for (int i = 0; i < 3; ++i) s[i] += o.s[i]; return *this; }
     Spec &operator*=(const Spec &o) { for (int i = 0; i < 3; ++i) s[i] *= o.s[i]; return *this; }
     Spec &operator*=(float f) { for (int i = 0; i < 3; ++i) s[i] *= f; return *this; }

@@ -70,6 +70,17 @@ _SIG = {
     "orc_env_eval_filtered": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f]),
     "orc_env_level": (C.c_int, [C.c_void_p, C.c_int, _f, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "orc_trace_paths": (None, [C.c_void_p, C.c_int, _u32, _u32, _u32, _f, _f, _i32]),
+    # C1 mesh scene (oracle/mesh_bsdf.h, mesh_geom.h)
+    "orc_new_bsdf": (C.c_int, [C.c_void_p]),
+    "orc_set_diffuse_checkerboard": (C.c_int, [C.c_void_p, _f, _f, C.c_float, C.c_float, C.c_float, C.c_float]),
+    "orc_set_plastic": (C.c_int, [C.c_void_p, C.c_float, C.c_int, _f, _f]),
+    "orc_set_twosided": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "orc_add_obj": (C.c_int, [C.c_void_p, C.c_char_p, _f, C.c_int, C.c_int, C.c_int, C.c_int]),
+    "orc_add_rectangle": (C.c_int, [C.c_void_p, _f, C.c_int, C.c_int]),
+    "orc_mesh_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
+    "orc_bsdf_eval_uv": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f]),
+    "orc_fresnel_diffuse_reflectance": (C.c_float, [C.c_float]),
+    "orc_trace_scene": (None, [C.c_void_p, C.c_int, _f, _f, _f, _f, _f, _i32]),
 }
 
 _libs = {}
@@ -334,6 +345,84 @@ class Oracle:
         self.lib.orc_trace_paths(self.s, n, p(px, _u32), p(py, _u32), p(frame, _u32), p(rgb, _f), p(pos, _f),
                                  p(depth, _i32))
         return rgb, pos, depth
+
+
+class MeshOracle(Oracle):
+    """An oracle scene built from the product's parsed scene (hpt_export_scene_json): the
+    C1 plumbing configuration -- triangle meshes, rectangles, plastic / twosided / checkerboard
+    diffuse BSDFs and an RGBE envmap.  The CPU path renders it; the device path is hair only."""
+
+    def new_bsdf(self, b):
+        """Append one BSDF described like the scene JSON; returns its index."""
+        nested = [self.new_bsdf(n) for n in b.get("nested", [])]
+        idx = self.lib.orc_new_bsdf(self.s)
+        kind = b["type"]
+        if kind == "twosided":
+            self.check(self.lib.orc_set_twosided(self.s, nested[0], nested[1] if len(nested) > 1 else -1))
+        elif kind == "plastic":
+            self.check(self.lib.orc_set_plastic(self.s, b["intIOR"] / b["extIOR"], int(b["nonlinear"]),
+                                                p(f32(b["diffuse"]), _f), p(f32(b["specular"]), _f)))
+        elif kind == "diffuse":
+            t = b.get("reflectanceTexture")
+            if t:
+                self.check(self.lib.orc_set_diffuse_checkerboard(
+                    self.s, p(f32(t["color0"]), _f), p(f32(t["color1"]), _f), t["uoffset"], t["voffset"],
+                    t["uscale"], t["vscale"]))
+            else:
+                self.check(self.lib.orc_set_diffuse(self.s, p(f32(b["diffuse"]), _f)))
+        else:
+            raise ValueError("MeshOracle: bsdf %r is not part of the C1 scene" % kind)
+        return idx
+
+    def setup_scene(self, js, env_rgb, width, height, spp):
+        sen, it, em = js["sensor"], js["integrator"], js["emitter"]
+        cam = f32(sen["toWorld"])
+        self.check(self.lib.orc_set_sample_count(self.s, spp))
+        self.check(self.lib.orc_set_camera(self.s, p(cam, _f), sen["xfov"], width, height, sen["nearClip"],
+                                           sen["farClip"]))
+        table = [self.new_bsdf(b) for b in js["bsdfs"]]
+        for m in js["meshes"]:
+            tw = f32(m["toWorld"])
+            if m["type"] == "obj":
+                self.check(self.lib.orc_add_obj(self.s, m["filename"].encode(), p(tw, _f), int(m["faceNormals"]),
+                                                int(m["flipNormals"]), int(m["flipTexCoords"]), table[m["bsdf"]]))
+            else:
+                self.check(self.lib.orc_add_rectangle(self.s, p(tw, _f), int(m["flipNormals"]), table[m["bsdf"]]))
+        env = f32(env_rgb)
+        etw = f32(em["toWorld"])
+        self.check(self.lib.orc_set_envmap(self.s, p(env, _f), env.shape[1], env.shape[0], em["scale"], p(etw, _f)))
+        self.check(self.lib.orc_set_integrator(self.s, it["maxDepth"], it["rrDepth"], int(it["strictNormals"]),
+                                               int(it["hideEmitters"])))
+        self.prepare()
+        return table
+
+    def mesh_info(self):
+        out = (C.c_int64 * 4)()
+        self.check(self.lib.orc_mesh_info(self.s, out))
+        return dict(zip(("meshes", "triangles", "vertices", "rectangles"), list(out)))
+
+    def bsdf_eval_uv(self, wi, wo, uv):
+        wi, wo = f32(wi).reshape(-1, 3), f32(wo).reshape(-1, 3)
+        uv = f32(uv).reshape(-1, 2)
+        n = wi.shape[0]
+        rgb = np.zeros((n, 3), np.float32)
+        pdf = np.zeros(n, np.float32)
+        self.lib.orc_bsdf_eval_uv(self.s, n, p(wi, _f), p(wo, _f), p(uv, _f), p(rgb, _f), p(pdf, _f))
+        return rgb, pdf
+
+    def trace_scene(self, o, d):
+        o, d = f32(o).reshape(-1, 3), f32(d).reshape(-1, 3)
+        n = o.shape[0]
+        t = np.zeros(n, np.float32)
+        nrm = np.zeros((n, 3), np.float32)
+        uv = np.zeros((n, 2), np.float32)
+        b = np.zeros(n, np.int32)
+        self.lib.orc_trace_scene(self.s, n, p(o, _f), p(d, _f), p(t, _f), p(nrm, _f), p(uv, _f), p(b, _i32))
+        return t, nrm, uv, b
+
+
+def fresnel_diffuse_reflectance(eta):
+    return float(load().orc_fresnel_diffuse_reflectance(eta))
 
 
 def sfmt(seed, n):
