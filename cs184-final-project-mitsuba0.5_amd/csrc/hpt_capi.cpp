@@ -20,6 +20,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <map>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -294,11 +296,29 @@ int hpt_set_data_dir(hpt_context *c, const char *dir) {
     return HPT_OK;
 }
 
+/* the process-wide -D table (hpt_set_default_defines) */
+static std::mutex gDefinesMutex;
+static std::map<std::string, std::string> gDefaultDefines;
+
+int hpt_set_default_defines(int n_defines, const char *const *keys, const char *const *values) {
+    if (n_defines < 0 || (n_defines > 0 && (!keys || !values))) return HPT_EINVAL;
+    for (int i = 0; i < n_defines; ++i)
+        if (!keys[i] || !values[i]) return HPT_EINVAL;
+    std::lock_guard<std::mutex> lock(gDefinesMutex);
+    gDefaultDefines.clear();
+    for (int i = 0; i < n_defines; ++i) gDefaultDefines[keys[i]] = values[i];
+    return HPT_OK;
+}
+
 int hpt_load_scene_xml(hpt_context *c, const char *path, int n_defines, const char *const *keys,
                        const char *const *values) {
     if (!c || !path) return HPT_EINVAL;
     std::map<std::string, std::string> defs;
-    for (int i = 0; i < n_defines; ++i) defs[keys[i]] = values[i];
+    {
+        std::lock_guard<std::mutex> lock(gDefinesMutex);
+        defs = gDefaultDefines;
+    }
+    for (int i = 0; i < n_defines; ++i) defs[keys[i]] = values[i]; /* explicit defines win */
     try {
         c->desc = parseSceneXML(path, defs);
     } catch (const std::exception &e) {

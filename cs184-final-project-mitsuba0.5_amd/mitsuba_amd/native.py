@@ -72,6 +72,7 @@ SIGNATURES = {
     "hpt_last_error": (C.c_char_p, [C.c_void_p]),
     "hpt_set_data_dir": (C.c_int, [C.c_void_p, C.c_char_p]),
     "hpt_load_scene_xml": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]),
+    "hpt_set_default_defines": (C.c_int, [C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_char_p)]),
     "hpt_export_scene_json": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "hpt_set_camera": (C.c_int, [C.c_void_p, _f, C.c_float, C.c_int, C.c_int, C.c_float, C.c_float]),
     "hpt_set_sampler": (C.c_int, [C.c_void_p, C.c_int]),

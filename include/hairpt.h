@@ -55,6 +55,13 @@ int hpt_set_data_dir(hpt_context *ctx, const char *dir);
    (one per hair shape; several shapes per scene), emitter "sunsky"/"envmap". */
 int hpt_load_scene_xml(hpt_context *ctx, const char *path, int n_defines, const char *const *keys,
                        const char *const *values);
+/* Process-wide -D defines, merged under the explicit ones by every later
+   hpt_load_scene_xml (replaces the previous table; n_defines = 0 clears it).
+   The reference keeps its -D map local to main() (src/mitsuba/mitsuba.cpp:
+   143-175) and hands it to SceneHandler (:354); a binding calls this right
+   there, so a plugin shim that re-parses the scene file sees the job's defines
+   (INTEGRATION.md section 1). */
+int hpt_set_default_defines(int n_defines, const char *const *keys, const char *const *values);
 
 /* The parsed scene as JSON: defaults resolved, paths absolute, every shape
    (hair and, for the C1 plumbing scene, obj / rectangle meshes) with its BSDF
