@@ -55,6 +55,7 @@ struct hpt_context {
     int device = 0;
     uint32_t tailPaths = defaultTailPaths();
     uint32_t maxLeafRounds = HPT_MAX_LEAF_ROUNDS, maxRestarts = HPT_MAX_RESTARTS; /* traversal bounds */
+    uint32_t packetStack = 0;      /* 0 = the kernel's packet stack depth */
     bool packets = defaultPackets();
     hipStream_t stream = nullptr;
     uint32_t *hostCnt = nullptr; /* pinned copy of the counter block */
@@ -394,6 +395,13 @@ int hpt_set_traversal_bounds(hpt_context *c, uint32_t max_leaf_rounds, uint32_t 
     c->maxRestarts = std::min<uint32_t>(max_restarts, HPT_MAX_RESTARTS);
     c->sc.maxLeafRounds = c->maxLeafRounds;
     c->sc.maxRestarts = c->maxRestarts;
+    return HPT_OK;
+}
+
+int hpt_set_packet_stack(hpt_context *c, uint32_t entries) {
+    if (!c) return HPT_EINVAL;
+    c->packetStack = entries;
+    c->sc.packetStack = entries;
     return HPT_OK;
 }
 
@@ -782,6 +790,7 @@ int hpt_prepare(hpt_context *c) {
         return setErr(c, HPT_EINVAL, "image resolution exceeds the Sobol look-up tables");
     c->sc.maxLeafRounds = c->maxLeafRounds;
     c->sc.maxRestarts = c->maxRestarts;
+    c->sc.packetStack = c->packetStack;
     c->prepared = true;
     return HPT_OK;
 }
@@ -1032,8 +1041,10 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         /* the camera pass is bounce 0 (parity 0) */
         e = timed(0, [&] { return hpt_launch_camera(sc, w, c->P, c->qTrace, C + HPT_C_TRACE(0), s); });
         if (e) break;
+        /* the camera pass has no shadow rays: qShadow / C[SHADOW(0)] take the rays of overflowing packets */
         e = c->packets ? timed(6, [&] {
-            return hpt_launch_trace_packet(sc, c->P, c->qTrace, C + HPT_C_TRACE(0), cur, dst, w.nPaths, s);
+            return hpt_launch_trace_packet(sc, c->P, c->qTrace, C + HPT_C_TRACE(0), cur, dst, w.nPaths, c->qShadow,
+                                           C + HPT_C_SHADOW(0), s);
         })
                        : timed(-1, [&] {
                              return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(0),
@@ -1043,6 +1054,13 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         reportLaunch("camera");
         e = hpt_launch_clear(C, 0, s);
         if (e) break;
+        if (c->packets) {
+            /* overflowing packets' rays (none at the shipped configs), then fresh cursors again */
+            e = hpt_launch_trace_overflow(sc, c->P, c->qShadow, C + HPT_C_SHADOW(0), cur,
+                                          std::min<uint64_t>(w.nPaths, 1u << 16), s);
+            if (e == hipSuccess) e = hpt_launch_clear(C, 0, s);
+            if (e) break;
+        }
         e = timed(1, [&] {
             return hpt_launch_primary(sc, c->P, c->qTrace, C + HPT_C_TRACE(0), c->qShade[1], C + HPT_C_SHADE(1), w.nPaths, s);
         });

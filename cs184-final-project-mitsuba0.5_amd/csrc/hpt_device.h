@@ -212,6 +212,7 @@ struct HptScene {
     uint32_t *fault;            /* device word: HPT_FAULT_* bits set by the traversal bounds */
     uint32_t maxLeafRounds;     /* traversal bounds of one ray (HPT_MAX_LEAF_ROUNDS / HPT_MAX_RESTARTS unless */
     uint32_t maxRestarts;       /*  lowered through hpt_set_traversal_bounds, a test hook) */
+    uint32_t packetStack;       /* camera packets' stack entries (0 = the build's; hpt_set_packet_stack, a test hook) */
 };
 
 #endif

@@ -80,9 +80,14 @@ hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_
                             uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_env_filtered_batch(const HptScene &sc, int n, const float *d, const float *rx, const float *ry,
                                         float *out, hipStream_t s);
-/* closest-hit rays as 64-ray packets (coherent rays: the camera pass) */
+/* closest-hit rays as 64-ray packets (coherent rays: the camera pass); the rays of a packet whose
+   stack overflows are appended to overflowQ / *nOverflow for hpt_launch_trace_overflow */
 hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
-                                   uint32_t *cursors, uint32_t *stats, uint64_t maxItems, hipStream_t s);
+                                   uint32_t *cursors, uint32_t *stats, uint64_t maxItems, uint32_t *overflowQ,
+                                   uint32_t *nOverflow, hipStream_t s);
+/* those rays, one lane each (persistent; maxItems only sizes the grid) */
+hipError_t hpt_launch_trace_overflow(const HptScene &sc, const HptPaths &P, const uint32_t *overflowQ,
+                                     const uint32_t *nOverflow, uint32_t *cursors, uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
                               uint32_t *shadeQ, uint32_t *nShade, uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,

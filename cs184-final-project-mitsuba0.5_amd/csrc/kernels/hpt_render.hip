@@ -30,6 +30,7 @@
 #include <map>
 #include <mutex>
 #include <utility>
+#include <vector>
 
 #include "../hpt_device.h"
 #include "hpt_kernels.h"
@@ -595,9 +596,23 @@ HD uint32_t hitFarRoot(const TraceRay &r) { return r.segHit >> 31; }
    key() (after begin: what finish needs, kept in LDS while the ray is
    traced) and finish(key, r).  Every wave exits once all shards are exhausted and its
    lanes have drained, so the grid always completes. */
+#ifdef HPT_TRACE_PROFILE
+/* timing instrumentation of the persistent traversal (experiment builds only: make variant
+   KFLAGS=-DHPT_TRACE_PROFILE): per launch (host-set slot) and wave [begin, the moment its
+   claims found every shard empty, end, rays claimed, rays still in flight when it found
+   them empty, 0, 0, 0]; 100 MHz s_memrealtime ticks */
+#define HPT_TRACE_PROFILE_LAUNCHES 16
+#define HPT_TRACE_PROFILE_WAVES 16384
+__device__ unsigned long long g_traceprof[HPT_TRACE_PROFILE_LAUNCHES][HPT_TRACE_PROFILE_WAVES][8];
+__device__ uint32_t g_traceprof_slot;
+#endif
 template <int STACK, bool STATS, class IO>
 __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint32_t *cursors, uint2 *stk,
                                                 uint32_t *stats) {
+#ifdef HPT_TRACE_PROFILE
+    const unsigned long long prBegin = __builtin_amdgcn_s_memrealtime();
+    unsigned long long prExhausted = 0, prClaimed = 0, prInFlight = 0;
+#endif
     const uint32_t total = io.count();
     const uint32_t lane = __lane_id();
     TraceRay r;
@@ -633,10 +648,17 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
                 }
                 if (++tried >= HPT_CURSORS) {
                     exhausted = true;
+#ifdef HPT_TRACE_PROFILE
+                    prExhausted = __builtin_amdgcn_s_memrealtime();
+                    prInFlight = (unsigned long long) (64 - n);
+#endif
                     break;
                 }
                 shard = (shard + 1) % HPT_CURSORS;
             }
+#ifdef HPT_TRACE_PROFILE
+            prClaimed += got;
+#endif
             if (!active) {
                 /* idle lanes below this one (v_mbcnt: no 64-bit lane mask kept live across the loop) */
                 const uint32_t rank =
@@ -663,12 +685,29 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             if (exhausted) break;
             continue;
         }
+#ifdef HPT_TRACE_PROFILE
+        if (exhausted && prExhausted == 0) prExhausted = __builtin_amdgcn_s_memrealtime();
+#endif
         if (active && traceRound<STACK, STATS>(sc, r, stk, (int) blockDim.x, tc)) {
             nU += io.finish(sc, rayKey<STACK>(stk, (int) blockDim.x), r);
             if (STATS) rayDone(rayLeaves(r), rayRestarts(r));
             active = false;
         }
     }
+#ifdef HPT_TRACE_PROFILE
+    {
+        const uint32_t wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        const uint32_t slot = g_traceprof_slot;
+        if (lane == 0 && wv < HPT_TRACE_PROFILE_WAVES && slot < HPT_TRACE_PROFILE_LAUNCHES) {
+            unsigned long long *rec = g_traceprof[slot][wv];
+            rec[0] = prBegin;
+            rec[1] = prExhausted;
+            rec[2] = __builtin_amdgcn_s_memrealtime();
+            rec[3] = prClaimed;
+            rec[4] = prInFlight;
+        }
+    }
+#endif
     if (STATS) {
         /* traversal counters for the algorithmic byte model:
            [0] node visits [1] primitive tests [2] closest rays [3] shadow rays
@@ -781,6 +820,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
     auto leaf = [&](uint32_t i) { return leafP[i]; };
 #endif
     const V3 o = r.o, d = r.d, rcp = r.rcp;
+    const int spMax = sc.packetStack ? min((int) sc.packetStack, HPT_PACKET_STACK) : HPT_PACKET_STACK;
     uint64_t done = ~__ballot(valid);
     uint64_t act = ~done;
     if (act == 0) return true;
@@ -809,7 +849,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
             const uint64_t mBelow = __ballot(me & below);
             if (mBelow != 0 && mBelow != act) {
                 /* the lanes disagree on the front-to-back order: the others revisit this node later */
-                if (sp == HPT_PACKET_STACK) return false;
+                if (sp == spMax) return false;
                 if (lane == 0) L.ent[sp] = PacketEntry{node, 1u, act & ~mBelow, 0ull};
                 ++sp;
                 act = mBelow;
@@ -825,7 +865,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
                 continue;
             }
             if ((mBoth | mFar) != 0) {
-                if (sp == HPT_PACKET_STACK) return false;
+                if (sp == spMax) return false;
                 if (in & both) L.saved[sp][lane] = r.tmax;
                 if (lane == 0) L.ent[sp] = PacketEntry{second, 0u, mBoth, mFar};
                 ++sp;
@@ -892,10 +932,15 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
 
 /* Persistent packet tracer: each wave claims 64 consecutive closest-hit rays
    (the camera queue keeps a pixel's samples together), traces them as one
-   packet and writes the hits; the shard cursors are k_trace's. */
-template <bool STATS, class IO>
+   packet and writes the hits; the shard cursors are k_trace's.  A packet whose
+   stack overflows is finished lane by lane: INLINE, right here (the batch entry
+   point), or else its rays are appended to overflowQ for a k_trace_overflow launch
+   (the camera pass), which keeps the per-lane traversal and its registers out of
+   this kernel. */
+template <bool STATS, bool INLINE, class IO>
 __device__ __forceinline__ void tracePackets(const HptScene &sc, IO &io, uint32_t *cursors, PacketLds &L,
-                                             uint32_t *stats) {
+                                             uint32_t *stats, uint32_t *overflowQ = nullptr,
+                                             uint32_t *nOverflow = nullptr) {
     const uint32_t total = io.count();
     const uint32_t lane = __lane_id();
     TraceCounters tc;
@@ -935,15 +980,21 @@ __device__ __forceinline__ void tracePackets(const HptScene &sc, IO &io, uint32_
         r.shadow = false;
         if (lane < got) valid = io.begin(sc, k, r);
         if (STATS) nC += lane < got ? 1u : 0u;
-        if (!tracePacket<STATS>(sc, r, valid, L, tc)) {
+        const bool ok = tracePacket<STATS>(sc, r, valid, L, tc);
+        if (!ok) {
             /* packet stack overflow: every lane re-traces its ray alone (same result) */
             if (STATS) fallbacks += lane == 0 ? 1u : 0u;
-            uint2 *stk = reinterpret_cast<uint2 *>(&L) + lane;
-            if (lane < got && io.begin(sc, k, r) && (stashRay<8>(stk, 64, r, io.key()), true))
-                while (!traceRound<8, STATS>(sc, r, stk, 64, tc)) {
-                }
+            if (INLINE) {
+                uint2 *stk = reinterpret_cast<uint2 *>(&L) + lane;
+                if (lane < got && io.begin(sc, k, r) && (stashRay<8>(stk, 64, r, io.key()), true))
+                    while (!traceRound<8, STATS>(sc, r, stk, 64, tc)) {
+                    }
+            } else if (lane < got && valid) {
+                overflowQ[atomicAdd(nOverflow, 1u)] = io.key();
+            }
         }
-        if (lane < got) io.finish(sc, io.key(), r);
+        /* lanes handed to the overflow launch are finished there */
+        if (lane < got && (ok || INLINE || !valid)) io.finish(sc, io.key(), r);
     }
     if (STATS) {
         for (int off = 32; off > 0; off >>= 1) {
@@ -2037,17 +2088,26 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
 #endif
 extern "C" __global__ __launch_bounds__(HPT_PACKET_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_PACKET_WAVES))) void
 k_trace_packet(HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ nTrace,
-               uint32_t *__restrict__ cursors) {
+               uint32_t *__restrict__ cursors, uint32_t *__restrict__ overflowQ, uint32_t *__restrict__ nOverflow) {
     __shared__ PacketLds lds[HPT_PACKET_BLOCK / 64];
     PathIO io{P, traceQ, nullptr, *nTrace, 0, 0};
-    tracePackets<false>(sc, io, cursors, lds[threadIdx.x >> 6], nullptr);
+    tracePackets<false, false>(sc, io, cursors, lds[threadIdx.x >> 6], nullptr, overflowQ, nOverflow);
 }
 extern "C" __global__ __launch_bounds__(HPT_PACKET_BLOCK) void k_trace_packet_counted(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ nTrace,
-    uint32_t *__restrict__ cursors, uint32_t *stats) {
+    uint32_t *__restrict__ cursors, uint32_t *stats, uint32_t *__restrict__ overflowQ, uint32_t *__restrict__ nOverflow) {
     __shared__ PacketLds lds[HPT_PACKET_BLOCK / 64];
     PathIO io{P, traceQ, nullptr, *nTrace, 0, 0};
-    tracePackets<true>(sc, io, cursors, lds[threadIdx.x >> 6], stats);
+    tracePackets<true, false>(sc, io, cursors, lds[threadIdx.x >> 6], stats, overflowQ, nOverflow);
+}
+/* the camera rays of packets whose stack overflowed, one lane per ray (k_trace's traversal;
+   a separate symbol so the profiles keep k_trace's launches apart) */
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace_overflow(
+    HptScene sc, HptPaths P, const uint32_t *__restrict__ overflowQ, const uint32_t *__restrict__ nOverflow,
+    uint32_t *__restrict__ cursors) {
+    __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
+    PathIO io{P, overflowQ, nullptr, *nOverflow, 0, 0};
+    tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
 
 /* fill the intersection record: hair.cpp:825-862 + skdtree.h:422-427 */
@@ -2613,7 +2673,7 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptS
     __shared__ PacketLds lds[HPT_TRACE_BLOCK / 64];
     BatchIO io{o, d, mint, maxt, outT, outP, outSeg, outHit, (uint32_t) n, (flags & 1) != 0, 0u};
     if ((flags & 4) && !(flags & 1))
-        tracePackets<false>(sc, io, cursor, lds[threadIdx.x >> 6], nullptr);
+        tracePackets<false, true>(sc, io, cursor, lds[threadIdx.x >> 6], nullptr);
     else if (flags & 2)
         tracePersistent<2, false>(sc, io, cursor, stk + threadIdx.x, nullptr);
     else
@@ -2744,10 +2804,32 @@ static unsigned persistentBlocks(const void *kernel, uint64_t items, int block =
     return (unsigned) std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t) resident));
 }
 
+#ifdef HPT_TRACE_PROFILE
+static uint32_t g_traceprofHostSlot = 0;
+/* copy out (and clear) the k_trace timing records of the launches since the last call:
+   launches x HPT_TRACE_PROFILE_WAVES x 8 u64; returns the number of launches recorded */
+extern "C" int hpt_debug_traceprof(unsigned long long *out, int maxLaunches) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    const int n = (int) std::min<uint32_t>(g_traceprofHostSlot, (uint32_t) std::min(maxLaunches, HPT_TRACE_PROFILE_LAUNCHES));
+    if (n > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_traceprof), (size_t) n * HPT_TRACE_PROFILE_WAVES * 64) != hipSuccess)
+        return -1;
+    std::vector<unsigned long long> zeros((size_t) HPT_TRACE_PROFILE_LAUNCHES * HPT_TRACE_PROFILE_WAVES * 8, 0ull);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_traceprof), zeros.data(), zeros.size() * 8) != hipSuccess) return -1;
+    g_traceprofHostSlot = 0;
+    return n;
+}
+#endif
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
                             uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
+#ifdef HPT_TRACE_PROFILE
+    {
+        const uint32_t slot = g_traceprofHostSlot++;
+        (void) hipMemcpyToSymbolAsync(HIP_SYMBOL(g_traceprof_slot), &slot, 4, 0, hipMemcpyHostToDevice, s);
+        (void) hipStreamSynchronize(s); /* the slot word is read by the launch below */
+    }
+#endif
     if (stats)
         hipLaunchKernelGGL(k_trace_counted, dim3(persistentBlocks((const void *) k_trace_counted, maxItems)),
                            dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, stats);
@@ -2757,15 +2839,23 @@ hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_
     return hipGetLastError();
 }
 hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
-                                   uint32_t *cursors, uint32_t *stats, uint64_t maxItems, hipStream_t s) {
+                                   uint32_t *cursors, uint32_t *stats, uint64_t maxItems, uint32_t *overflowQ,
+                                   uint32_t *nOverflow, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
     if (stats)
         hipLaunchKernelGGL(k_trace_packet_counted,
                            dim3(persistentBlocks((const void *) k_trace_packet_counted, maxItems, HPT_PACKET_BLOCK)),
-                           dim3(HPT_PACKET_BLOCK), 0, s, sc, P, traceQ, nTrace, cursors, stats);
+                           dim3(HPT_PACKET_BLOCK), 0, s, sc, P, traceQ, nTrace, cursors, stats, overflowQ, nOverflow);
     else
         hipLaunchKernelGGL(k_trace_packet, dim3(persistentBlocks((const void *) k_trace_packet, maxItems, HPT_PACKET_BLOCK)),
-                           dim3(HPT_PACKET_BLOCK), 0, s, sc, P, traceQ, nTrace, cursors);
+                           dim3(HPT_PACKET_BLOCK), 0, s, sc, P, traceQ, nTrace, cursors, overflowQ, nOverflow);
+    return hipGetLastError();
+}
+hipError_t hpt_launch_trace_overflow(const HptScene &sc, const HptPaths &P, const uint32_t *overflowQ,
+                                     const uint32_t *nOverflow, uint32_t *cursors, uint64_t maxItems, hipStream_t s) {
+    if (maxItems == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_trace_overflow, dim3(persistentBlocks((const void *) k_trace_overflow, maxItems)),
+                       dim3(HPT_TRACE_BLOCK), 0, s, sc, P, overflowQ, nOverflow, cursors);
     return hipGetLastError();
 }
 hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,

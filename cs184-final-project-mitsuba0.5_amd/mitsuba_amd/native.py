@@ -78,6 +78,7 @@ SIGNATURES = {
     "hpt_set_sampler": (C.c_int, [C.c_void_p, C.c_int]),
     "hpt_set_sampler_scramble": (C.c_int, [C.c_void_p, C.c_uint64]),
     "hpt_set_traversal_bounds": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    "hpt_set_packet_stack": (C.c_int, [C.c_void_p, C.c_uint32]),
     "hpt_debug_sfmt": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
     "hpt_set_integrator": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
     "hpt_set_hair_file": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_float, _f]),
@@ -208,6 +209,10 @@ class Renderer:
     def set_traversal_bounds(self, max_leaf_rounds=1 << 18, max_restarts=1024):
         """test hook: lower the per-ray traversal bounds (a ray past them fails the call, code -5)"""
         self._check(self.lib.hpt_set_traversal_bounds(self.h, max_leaf_rounds, max_restarts))
+
+    def set_packet_stack(self, entries=0):
+        """test hook: limit the camera packets' stack (0 = the build's depth) to force the overflow path"""
+        self._check(self.lib.hpt_set_packet_stack(self.h, entries))
 
     def set_integrator(self, max_depth, rr_depth=5, strict_normals=True, hide_emitters=False):
         self._check(self.lib.hpt_set_integrator(self.h, max_depth, rr_depth, int(strict_normals), int(hide_emitters)))

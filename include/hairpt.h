@@ -87,6 +87,10 @@ int hpt_debug_sfmt(uint64_t seed, uint64_t n, uint64_t *out);
 /* Test hook (no reference counterpart): lower the per-ray traversal bounds (leaf rounds, kd-restarts;
    defaults and maxima 2^18 and 1024) past which a render or trace call fails with HPT_ETRAVERSAL */
 int hpt_set_traversal_bounds(hpt_context *ctx, uint32_t max_leaf_rounds, uint32_t max_restarts);
+/* Test hook (no reference counterpart): limit the camera pass's packet stack to `entries` (0 = the
+   build's 23; larger values are clamped) so that packets overflow and their rays take the
+   per-lane fallback launch -- hits, and so the film, are unchanged */
+int hpt_set_packet_stack(hpt_context *ctx, uint32_t entries);
 /* MonteCarloIntegrator params (src/librender/integrator.cpp:190-203) */
 int hpt_set_integrator(hpt_context *ctx, int max_depth, int rr_depth, int strict_normals, int hide_emitters);
 /* HairShape(Properties) (src/shapes/hair.cpp:609-785); to_world may be NULL */

@@ -149,6 +149,23 @@ def test_traversal_bound_fails_loudly_and_recovers():
     assert np.isfinite(r2.render(0, 4)).all()
 
 
+def test_packet_overflow_launch_is_bit_identical():
+    """Camera packets whose stack overflows hand their rays to k_trace_overflow (one lane per
+    ray, k_trace's traversal) instead of tracing them inside the packet kernel.  With the
+    packet stack limited to 1 and 3 entries (test hook) most packets overflow; the film must
+    equal the default render bit for bit, and the counted frame must see the overflows."""
+    _, r, _ = scene_util.make("furball_marschner", 40000, 64, 48, 8, device=0)
+    ref = r.render(0, 8)
+    for entries in (1, 3):
+        r.set_packet_stack(entries)
+        film = r.render(0, 8, collect_stats=2)
+        assert r.stats().packet_fallbacks > 0
+        np.testing.assert_array_equal(film, ref)
+    r.set_packet_stack(0)
+    np.testing.assert_array_equal(r.render(0, 8, collect_stats=2), ref)
+    assert r.stats().packet_fallbacks == 0
+
+
 def test_curly_full_size():
     """C4 at full size: 10,000 helical strands (~2.7e6 segments), 1024x1024 @ 256 spp."""
     si = _full_size("curly_marschner", 10000, 1024, 1024, 256, 65)
