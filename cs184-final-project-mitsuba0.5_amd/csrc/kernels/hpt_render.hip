@@ -1150,23 +1150,12 @@ HD float sampleM(float v, float sinThetaI, float cosThetaI, float xi1, float xi2
 }
 
 /* Where MarschnerDiffuse::sample reads the per-lobe InterpolatedDistribution1D
-   cdfs and sums: GlobalTabs = the scene's HBM arrays (through L2), LdsTabs =
-   a copy staged in LDS by k_shade_mlds (the binary search of azSample is a
-   chain of dependent reads: LDS latency instead of L2 latency). */
+   cdfs and sums: the scene's HBM arrays, through L2 (an LDS-staged copy was
+   measured slower: DESIGN.md section 5, k_shade) */
 struct GlobalTabs {
     const HptMarschner &m;
     HD const float *cdf(int l) const { return l == 0 ? m.cdf[0] : (l == 1 ? m.cdf[1] : m.cdf[2]); }
     HD const float *sums(int l) const { return l == 0 ? m.sums[0] : (l == 1 ? m.sums[1] : m.sums[2]); }
-};
-#define HPT_CDF_WORDS (HPT_AZ_RES * (HPT_AZ_RES + 1))
-struct MarschnerLds {
-    float cdf[3][HPT_CDF_WORDS];
-    float sums[3][HPT_AZ_RES];
-};
-struct LdsTabs {
-    const MarschnerLds &t;
-    HD const float *cdf(int l) const { return t.cdf[l]; }
-    HD const float *sums(int l) const { return t.sums[l]; }
 };
 
 /* MarschnerDiffuse::sample (:594-744); pdf() == 1 (:517-520) */
@@ -2164,9 +2153,9 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
    MULTI: several hair shapes, the hit shape's BSDF comes from sc.bsdfs (a
    separate kernel, so the single-shape one never mixes a kernel-argument
    pointer with a global one -- that would copy the scene to scratch) */
-template <bool MULTI, bool LDS = false>
+template <bool MULTI>
 HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__restrict__ counters, bool &cont,
-                  bool &shadow, const MarschnerLds *ldsTabs = nullptr) {
+                  bool &shadow) {
     {
         uint32_t st = P.state[id];
         uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st);
@@ -2223,8 +2212,7 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__rest
             float bpdf = 0.0f;
             uint32_t type = 0;
             V3 w;
-            if constexpr (LDS) w = bsdfSampleT(B, LdsTabs{*ldsTabs}, wi, bx, by, woL, bpdf, type);
-            else w = bsdfSample(B, wi, bx, by, woL, bpdf, type);
+            w = bsdfSample(B, wi, bx, by, woL, bpdf, type);
             if (!isZero(w)) {
                 V3 wo = sh.toWorld(woL);
                 float woDotGeoN = dot(geo.n, wo);
