@@ -103,8 +103,14 @@ def cpu_baseline(args, cfg, xml_defines, hair_src, env_rgb, nodes, idx):
             model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model)
     except OSError:
         pass
+    quota = None  # the cgroup's CPU bandwidth limit (cgroup v2 cpu.max "quota period"), in CPUs
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
     return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
-            "cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": avail,
+            "cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": avail, "cgroup_cpu_quota": quota,
             "threads_note": "one worker thread per CPU this process may run on (nproc), like mitsuba.cpp:135,281",
             "cpu_share": share,
             "sample": "%dx%d @ %d spp of the same scene (%d paths), %.2f s, liboracle_ref.so "
