@@ -773,6 +773,9 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
    later).  A lane therefore tests the same leaves in the same order with
    the same intervals as its own traversal, and its result is bit-identical.
    A packet whose stack would overflow finishes lane by lane (traceRound). */
+#ifndef HPT_PACKET_LEAF_BATCH
+#define HPT_PACKET_LEAF_BATCH 2 /* leaf records per round trip in the packet traversal: 1 / 2 / 4 / 6 gave 30.98 / 29.53 / 30.54 / 30.55 ms per headline frame */
+#endif
 #ifndef HPT_PACKET_STACK
 #define HPT_PACKET_STACK 23 /* 6.4 KB of LDS per wave: 6 waves/SIMD fit the 160 KB (24 entries did not) */
 #endif
@@ -882,14 +885,36 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
             if (lane == 0) tc.nodeSlots += 64;
         }
         const uint32_t lf = nd.w0 & 0x7fffffffu, ll = nd.w1;
-        for (uint32_t e = lf; e < ll; ++e) {
-            const float4 fa = leaf(2 * e), fb = leaf(2 * e + 1);
-            if (STATS) {
-                tc.prims += me ? 1u : 0u;
-                if (lane == 0) tc.primSlots += 64;
+        /* HPT_PACKET_LEAF_BATCH records per round trip (wave-uniform scalar loads issued
+           together), pre-test into a candidate mask, then the exact tests in record order:
+           the same tests in the same order as one record at a time (the pre-test does not
+           read tHit), so the hits are identical */
+        for (uint32_t c0 = lf; c0 < ll; c0 += HPT_PACKET_LEAF_BATCH) {
+            const uint32_t n = min(ll - c0, (uint32_t) HPT_PACKET_LEAF_BATCH);
+            float4 ra[HPT_PACKET_LEAF_BATCH], rb[HPT_PACKET_LEAF_BATCH];
+#pragma unroll
+            for (uint32_t k = 0; k < HPT_PACKET_LEAF_BATCH; ++k) {
+                const uint32_t e = c0 + (k < n ? k : 0u);
+                ra[k] = leaf(2 * e);
+                rb[k] = leaf(2 * e + 1);
             }
-            if (me && segMayHit(fa, fb, o, d, sc.maxRadius)) {
-                const uint32_t sg = __float_as_uint(fb.z);
+            uint32_t mask = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < HPT_PACKET_LEAF_BATCH; ++k) {
+                if (k < n) {
+                    if (STATS) {
+                        tc.prims += me ? 1u : 0u;
+                        if (lane == 0) tc.primSlots += 64;
+                    }
+                    if (me && segMayHit(ra[k], rb[k], o, d, sc.maxRadius)) mask |= 1u << k;
+                }
+            }
+            while (mask) {
+                const uint32_t k = (uint32_t) (__ffs(mask) - 1);
+                mask &= mask - 1;
+                uint32_t sg = __float_as_uint(rb[0].z);
+#pragma unroll
+                for (uint32_t q = 1; q < HPT_PACKET_LEAF_BATCH; ++q) sg = k == q ? __float_as_uint(rb[q].z) : sg;
                 const float rad = segRadius(sc, sg);
                 const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
                 if (STATS) ++tc.exact;
