@@ -189,7 +189,9 @@ int ensureWave(hpt_context *c, uint64_t n) {
     r |= alloc(n * 4, (void **) &c->P.state);
     r |= alloc(n * 16, (void **) &c->P.thr);
     r |= alloc(n * 16, (void **) &c->P.li);
-    r |= alloc(n * 16, (void **) &c->P.hit);
+    r |= alloc(n * 4, (void **) &c->P.hit);
+    r |= alloc(n * 4, (void **) &c->P.hitQ);
+    r |= alloc(n * 4, (void **) &c->P.hitS);
     r |= alloc(n * 16, (void **) &c->P.bw);
     r |= alloc(n * 16, (void **) &c->P.sdir);
     r |= alloc(n * 16, (void **) &c->P.scontrib);
@@ -1056,7 +1058,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         if (e) break;
         if (c->packets) {
             /* overflowing packets' rays (none at the shipped configs), then fresh cursors again */
-            e = hpt_launch_trace_overflow(sc, c->P, c->qShadow, C + HPT_C_SHADOW(0), cur,
+            e = hpt_launch_trace_overflow(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_SHADOW(0), cur,
                                           std::min<uint64_t>(w.nPaths, 1u << 16), s);
             if (e == hipSuccess) e = hpt_launch_clear(C, 0, s);
             if (e) break;

@@ -63,12 +63,17 @@ struct HptPaths {
     uint32_t *state;   /* dim[0:11) | depth[11:24) | sampledType[24:31) | scattered[31] */
     float4 *thr;       /* throughput rgb                             */
     float4 *li;        /* accumulated radiance rgb                   */
-    float4 *hit;       /* segment id (int bits, -1 = miss), t, far-root flag (uint bits) */
+    uint32_t *hit;     /* k_tail's hit records by path: segment id | far root << 31, HPT_MISS = miss */
+    uint32_t *hitQ;    /* a trace launch's hit records by trace-queue position (k_primary / k_post read them in queue order) */
+    uint32_t *hitS;    /* the next shade queue's hit records by shade-queue position (written with the queue) */
     float4 *bw;        /* bsdf weight rgb, bsdf pdf                  */
     float4 *sdir;      /* shadow ray direction xyz, maxt             */
     float4 *scontrib;  /* NEE contribution rgb (added if unoccluded) */
 };
 
+
+/* hit record of a miss (a segment id never has all 31 bits set) */
+#define HPT_MISS 0xffffffffu
 
 /* launch wrappers (hpt_render.hip).  Queue lengths are passed as device
    pointers (the kernels read them; the host only bounds the grids). */
@@ -86,7 +91,7 @@ hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const 
                                    uint32_t *cursors, uint32_t *stats, uint64_t maxItems, uint32_t *overflowQ,
                                    uint32_t *nOverflow, hipStream_t s);
 /* those rays, one lane each (persistent; maxItems only sizes the grid) */
-hipError_t hpt_launch_trace_overflow(const HptScene &sc, const HptPaths &P, const uint32_t *overflowQ,
+hipError_t hpt_launch_trace_overflow(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *overflowQ,
                                      const uint32_t *nOverflow, uint32_t *cursors, uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
                               uint32_t *shadeQ, uint32_t *nShade, uint64_t maxItems, hipStream_t s);

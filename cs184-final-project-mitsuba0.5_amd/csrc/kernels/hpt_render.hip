@@ -585,6 +585,53 @@ HD uint32_t hitFarRoot(const TraceRay &r) { return r.segHit >> 31; }
 #define HPT_REFILL 16 /* idle lanes that trigger a refill of the wave */
 #endif
 
+/* Drain splitting.  Once a persistent wave's claims find the queue empty, its
+   finished lanes would idle until the wave's slowest ray ends, and the launch
+   ends with the slowest wave.  Instead an idle lane takes over the far part of
+   a running ray's remaining interval: the ray (donor) keeps [its start, m] and
+   the helper traces [m, end] from the root, the way a kd-restart resumes an
+   interval.  The members of a split ray (same key, same kind) each know their
+   interval's start (the LDS mint row, also the lower bound of their exact
+   tests); the ray's answer is the hit of the member with the lowest start that
+   found one, once every member below it has finished without one (shadow ray:
+   any member's hit; no hit: every member finished).  Primitive tests accept
+   t in [start, best] per member, so the union over members finds the same
+   closest hit as one traversal over [mint, maxt] (hair.cpp:485-548: the root
+   accepted for a segment depends only on which of its roots lie in the
+   interval, and a root below a member's start is in a lower member's). */
+#ifndef HPT_DRAIN_SPLIT
+#define HPT_DRAIN_SPLIT 1
+#endif
+#ifndef HPT_SPLIT_MIN
+#define HPT_SPLIT_MIN 8 /* idle lanes that trigger a split step (or as many idle as running) */
+#endif
+/* v of lane src (ds_bpermute; unlike __shfl no lane-id arithmetic, which would keep the
+   lane id live through the traversal) */
+HD int fromLane(int v, uint32_t src) { return __builtin_amdgcn_ds_bpermute((int) (src << 2), v); }
+HD uint32_t fromLane(uint32_t v, uint32_t src) { return (uint32_t) fromLane((int) v, src); }
+HD float fromLane(float v, uint32_t src) { return __int_as_float(fromLane(__float_as_int(v), src)); }
+/* position of the k-th (0-based) set bit of m (k < popcount(m)) */
+HD uint32_t selectBit(uint64_t m, uint32_t k) {
+    uint32_t pos = 0, c = (uint32_t) __popc((uint32_t) m), x;
+    if (k >= c) {
+        k -= c;
+        x = (uint32_t) (m >> 32);
+        pos = 32;
+    } else {
+        x = (uint32_t) m;
+    }
+#pragma unroll
+    for (int w = 16; w >= 1; w >>= 1) {
+        c = (uint32_t) __popc(x & ((1u << w) - 1u));
+        if (k >= c) {
+            k -= c;
+            x >>= w;
+            pos += (uint32_t) w;
+        }
+    }
+    return pos;
+}
+
 /* Persistent traversal: each wave keeps its 64 lanes busy by claiming new
    rays whenever HPT_REFILL lanes have finished.  The work range is split
    into HPT_CURSORS contiguous shards, each with its own cursor on its own
@@ -630,6 +677,147 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
     bool active = false, exhausted = false;
     uint32_t shard = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % HPT_CURSORS;
     int tried = 0;
+    /* drain splitting (HPT_DRAIN_SPLIT): lanes of split rays, and those of them that have
+       finished their interval while the ray's answer is still open (wave-uniform masks) */
+    constexpr bool SPLIT = !STATS && HPT_DRAIN_SPLIT;
+    uint64_t splitM = 0, waitM = 0;
+    const int stride = (int) blockDim.x;
+    /* the j-th of n pieces of [a, b] starts here (the same expression on the donor and the helper) */
+    auto pieceStart = [](float a, float b, uint32_t j, uint32_t n) {
+        return j >= n ? b : a + (b - a) * ((float) j / (float) n);
+    };
+    uint32_t rot = 0; /* rotates which running rays get helpers first */
+    /* the lane index, recomputed where it is needed (kept live from the top it costs the
+       traversal a register) */
+    auto laneNow = []() {
+        uint32_t l;
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+        return l;
+    };
+    auto splitStep = [&](TraceRay &r, bool &active) {
+        const uint32_t lane = laneNow();
+        const uint64_t actM = __ballot(active), idleM = ~(actM | waitM);
+        const float end = __uint_as_float(stk[(STACK + HPT_ROW_MM) * stride].y);
+        const float b = fminr(r.tHit, end);
+        /* what a helper takes: the bottom stack entry (the farthest pending subtree, entered at
+           t0 = the end of the entry above it) and everything after it, or with an empty stack
+           the far half of the remaining interval, from the root */
+        const bool fromStack = r.sp > 0;
+        uint32_t node = 0;
+        float t0, t1 = end;
+        if (fromStack) {
+            const uint32_t bot = r.top - (uint32_t) r.sp;
+            const uint2 e = stk[(bot & (STACK - 1)) * stride];
+            node = e.x;
+            t1 = __uint_as_float(e.y);
+            t0 = r.sp > 1 ? __uint_as_float(stk[((bot + 1u) & (STACK - 1)) * stride].y) : r.tmax;
+        } else {
+            t0 = pieceStart(r.tmin, b, 1u, 2u);
+        }
+        const bool elig = active && t0 < b && t0 > r.tmin;
+        const uint64_t eM = __ballot(elig);
+        const uint32_t nE = (uint32_t) __popcll(eM), nI = (uint32_t) __popcll(idleM);
+        if (nE == 0 || nI == 0 || (nI < HPT_SPLIT_MIN && nI < nE)) return;
+        const uint32_t nS = min(nE, nI); /* helpers this step, one per donor */
+        const uint32_t rE = __builtin_amdgcn_mbcnt_hi((uint32_t) (eM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) eM, 0u));
+        const uint32_t rI =
+            __builtin_amdgcn_mbcnt_hi((uint32_t) (idleM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) idleM, 0u));
+        const uint32_t rr = rot % nE;
+        const bool give = elig && (rE + nE - rr) % nE < nS;
+        const bool take = ((idleM >> lane) & 1u) && rI < nS;
+        const uint32_t donor = take ? selectBit(eM, (rI + rr) % nE) : lane;
+        const uint2 cr0 = stk[STACK * stride], cr1 = stk[(STACK + 1) * stride];
+        const uint32_t dnode = (uint32_t) fromLane((int) node, donor);
+        const float dt0 = fromLane(t0, donor), dt1 = fromLane(t1, donor), de = fromLane(end, donor);
+        const int dflags = fromLane((r.shadow ? 1 : 0) | (fromStack ? 2 : 0) | (r.lost ? 4 : 0), donor);
+        const float ox = fromLane(r.o.x, donor), oy = fromLane(r.o.y, donor), oz = fromLane(r.o.z, donor);
+        const float dx = fromLane(r.d.x, donor), dy = fromLane(r.d.y, donor), dz = fromLane(r.d.z, donor);
+        const uint32_t c0 = (uint32_t) fromLane((int) cr0.x, donor), c1 = (uint32_t) fromLane((int) cr0.y, donor);
+        const uint32_t c2 = (uint32_t) fromLane((int) cr1.x, donor), key = (uint32_t) fromLane((int) cr1.y, donor);
+        if (give) {
+            /* the donor keeps [its start, t0] */
+            if (fromStack) {
+                r.sp -= 1;
+                r.lost = false; /* entries lost beyond the bottom one are now the helper's */
+            }
+            stk[(STACK + HPT_ROW_MM) * stride].y = __float_as_uint(t0);
+            r.maxt = t0;
+            if (!(r.found && r.tHit <= t0)) {
+                r.found = false;
+                r.tHit = t0;
+            }
+        }
+        if (take) {
+            /* the helper: [t0, the donor's end]; the last part ends at the ray's own end, not at
+               a hit found beyond t0 (that t is the fp64 root rounded to float, maybe below it) */
+            const bool stackPart = (dflags & 2) != 0;
+            r.o = v3(ox, oy, oz);
+            r.d = v3(dx, dy, dz);
+            r.rcp = v3(__uint_as_float(c0), __uint_as_float(c1), __uint_as_float(c2));
+            r.shadow = (dflags & 1) != 0;
+            r.found = false;
+            r.segHit = 0;
+            r.node = stackPart ? dnode : 0u;
+            r.mint = r.tmin = dt0;
+            r.tmax = stackPart ? dt1 : de;
+            r.maxt = r.tHit = de;
+            /* a kd-restart covers what follows the stolen subtree */
+            r.lost = stackPart && ((dflags & 4) != 0 || dt1 < de);
+            r.top = 0;
+            r.sp = 0;
+            r.cnt = 0;
+            stk[STACK * stride] = make_uint2(c0, c1);
+            stk[(STACK + 1) * stride] = make_uint2(c2, key);
+            stk[(STACK + HPT_ROW_MM) * stride] = make_uint2(__float_as_uint(dt0), __float_as_uint(de));
+            active = true;
+        }
+        splitM |= __ballot(give) | __ballot(take);
+        rot += nS;
+        asm volatile("" ::: "memory"); /* traceRound re-reads the rows (see stashRay) */
+    };
+    /* newW: split lanes that finished their interval this round */
+    auto decideSplit = [&](TraceRay &r, bool &active, uint64_t newW) {
+        const uint32_t lane = laneNow();
+        waitM |= newW;
+        const uint2 kr = stk[(STACK + 1) * stride], mm = stk[(STACK + HPT_ROW_MM) * stride];
+        const uint32_t myKey = kr.y;
+        const float lo = __uint_as_float(mm.x);
+        const int myKind = r.shadow ? 1 : 0;
+        while (newW) { /* wave-uniform: one split ray per pass */
+            const int L = __ffsll((unsigned long long) newW) - 1;
+            const uint32_t K = (uint32_t) __builtin_amdgcn_readlane((int) myKey, L);
+            const int S = __builtin_amdgcn_readlane(myKind, L);
+            const bool mem = ((splitM >> lane) & 1u) && myKey == K && myKind == S;
+            const uint64_t memM = __ballot(mem);
+            const bool w = (waitM >> lane) & 1u;
+            const uint64_t fnd = __ballot(mem && w && r.found);
+            int F = -1;
+            float minLo = finf();
+            for (uint64_t m = fnd; m; m &= m - 1) {
+                const int l = __ffsll((unsigned long long) m) - 1;
+                const float v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lo), l));
+                if (v < minLo) {
+                    minLo = v;
+                    F = l;
+                }
+            }
+            /* shadow ray: any hit decides; closest: no running member below the lowest hit */
+            const bool decided = S ? (fnd != 0 || (memM & ~waitM) == 0) : __ballot(mem && !w && lo < minLo) == 0;
+            if (decided) {
+                if ((int) lane == (F >= 0 ? F : L)) nU += io.finish(sc, K, r);
+                if (mem) active = false;
+                splitM &= ~memM;
+                waitM &= ~memM;
+            } else if (F >= 0) {
+                /* members above the lowest hit cannot give the answer */
+                const uint64_t dropM = __ballot(mem && lo > minLo);
+                if ((dropM >> lane) & 1u) active = false;
+                splitM &= ~dropM;
+                waitM &= ~dropM;
+            }
+            newW &= ~memM;
+        }
+    };
     while (true) {
         const uint64_t idle = __ballot(!active);
         if (!exhausted && __popcll(idle) >= HPT_REFILL) {
@@ -681,6 +869,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
                 }
             }
         }
+        if (SPLIT && exhausted) break; /* the drain loop below */
         if (__ballot(active) == 0) {
             if (exhausted) break;
             continue;
@@ -692,6 +881,22 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             nU += io.finish(sc, rayKey<STACK>(stk, (int) blockDim.x), r);
             if (STATS) rayDone(rayLeaves(r), rayRestarts(r));
             active = false;
+        }
+    }
+    if (SPLIT) {
+#ifdef HPT_TRACE_PROFILE
+        if (prExhausted == 0) prExhausted = __builtin_amdgcn_s_memrealtime();
+#endif
+        while (true) {
+            splitStep(r, active);
+            if (__ballot(active) == 0) break;
+            bool fin = false;
+            if (active && traceRound<STACK, STATS>(sc, r, stk, (int) blockDim.x, tc)) {
+                fin = true;
+                if (!((splitM >> laneNow()) & 1u)) nU += io.finish(sc, rayKey<STACK>(stk, (int) blockDim.x), r);
+                active = false;
+            }
+            if (splitM) decideSplit(r, active, __ballot(fin) & splitM);
         }
     }
 #ifdef HPT_TRACE_PROFILE
@@ -1927,6 +2132,35 @@ __device__ __forceinline__ void qpushBlock(bool pred, uint32_t value, uint32_t *
     __syncthreads(); /* waveCount / blockBase may be reused by a second push */
 }
 
+/* qpushBlock that also stores value2 at the same position of a parallel array */
+template <int BLOCK>
+__device__ __forceinline__ void qpushBlock2(bool pred, uint32_t value, uint32_t *queue, uint32_t value2,
+                                            uint32_t *array2, uint32_t *counter) {
+    constexpr int NW = BLOCK / 64;
+    __shared__ uint32_t waveCount[NW];
+    __shared__ uint32_t blockBase;
+    const uint64_t mask = __ballot(pred);
+    const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+    if (lane == 0) waveCount[wave] = (uint32_t) __popcll(mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t c = waveCount[w];
+            waveCount[w] = tot;
+            tot += c;
+        }
+        blockBase = tot ? atomicAdd(counter, tot) : 0u;
+    }
+    __syncthreads();
+    if (pred) {
+        const uint32_t pos = blockBase + waveCount[wave] + (uint32_t) __popcll(mask & ((1ull << lane) - 1ull));
+        queue[pos] = value;
+        array2[pos] = value2;
+    }
+    __syncthreads();
+}
+
 /* append to a queue: one atomic per wave (wave64 ballot + mbcnt) */
 HD void qpush(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
     uint64_t mask = __ballot(pred);
@@ -2013,15 +2247,26 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
 /* k_trace: the wave's closest-hit rays (traceQ[0, nTrace)) then its any-hit
    shadow rays (shadowQ) as one persistent grid; k_trace_counted adds the
    traversal counters of the byte model (one counted frame per bench run) */
+/* Closest-hit records go to P.hitQ by trace-queue position (the wavefront
+   kernels; k_primary / k_post read them in queue order), or to P.hit by path
+   (byQueue false: k_tail).  A record is 4 bytes (segment | far root << 31, or
+   HPT_MISS) and consecutive queue positions belong to the rays one wave
+   claimed together, so a launch's record writes fill whole lines in L2
+   instead of a 32-byte sector per lone path-indexed 16-byte store.
+   posQ (k_trace_overflow): the queue positions of the rays to trace. */
 struct PathIO {
     HptPaths P;
     const uint32_t *traceQ, *shadowQ;
     uint32_t nTrace, nShadow, id;
+    bool byQueue;
+    const uint32_t *posQ;
     HD uint32_t count() const { return nTrace + nShadow; }
     HD bool begin(const HptScene &sc, uint32_t k, TraceRay &r) {
         if (k < nTrace) {
-            id = traceQ[k];
-            const float4 ro = P.ro[id], rd = P.rd[id];
+            const uint32_t q = posQ ? posQ[k] : k;
+            const uint32_t path = traceQ[q];
+            id = byQueue ? q : path; /* the key: where finish() writes the record */
+            const float4 ro = P.ro[path], rd = P.rd[path];
             return beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(rd.x, rd.y, rd.z), ro.w, rd.w, false);
         }
         id = shadowQ[k - nTrace];
@@ -2029,16 +2274,12 @@ struct PathIO {
         return beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(sd.x, sd.y, sd.z), kEpsilon, sd.w, true);
     }
     HD uint32_t key() const { return id; }
-    /* id: the path; returns 1 for an unoccluded shadow ray */
+    /* id: the record's queue position / path (closest), the path (shadow ray);
+       returns 1 for an unoccluded shadow ray */
     HD uint32_t finish(const HptScene &sc, uint32_t id, const TraceRay &r) {
         if (!r.shadow) {
-            /* hit record: segment (-1: miss), t, accepted root (the shading kernel re-derives the point) */
-            /* the miss constants are materialised here, not hoisted out of the trace loop (no
-               literal operands on VOP3 here: a hoisted +inf would hold a register for the loop) */
-            uint32_t missT;
-            asm volatile("v_mov_b32 %0, 0x7f800000" : "=v"(missT));
-            P.hit[id] = make_float4(__int_as_float(r.found ? (int32_t) hitSegment(r) : -1),
-                                    r.found ? r.tHit : __uint_as_float(missT), __uint_as_float(hitFarRoot(r)), 0.0f);
+            /* the shading kernel re-derives the point from the segment and the accepted root */
+            (byQueue ? P.hitQ : P.hit)[id] = r.found ? r.segHit : HPT_MISS;
             return 0;
         }
         if (r.found) return 0;
@@ -2078,7 +2319,7 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY voi
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
     const uint32_t *__restrict__ nTrace, const uint32_t *__restrict__ nShadow, uint32_t *__restrict__ cursors) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    PathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0};
+    PathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0, true, nullptr};
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(HptScene sc, HptPaths P,
@@ -2089,7 +2330,7 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
                                                                               uint32_t *__restrict__ cursors,
                                                                               uint32_t *stats) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    PathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0};
+    PathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0, true, nullptr};
     tracePersistent<HPT_STACK, true>(sc, io, cursors, stk + threadIdx.x, stats);
 }
 
@@ -2104,23 +2345,24 @@ extern "C" __global__ __launch_bounds__(HPT_PACKET_BLOCK) __attribute__((amdgpu_
 k_trace_packet(HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ nTrace,
                uint32_t *__restrict__ cursors, uint32_t *__restrict__ overflowQ, uint32_t *__restrict__ nOverflow) {
     __shared__ PacketLds lds[HPT_PACKET_BLOCK / 64];
-    PathIO io{P, traceQ, nullptr, *nTrace, 0, 0};
+    PathIO io{P, traceQ, nullptr, *nTrace, 0, 0, true, nullptr};
     tracePackets<false, false>(sc, io, cursors, lds[threadIdx.x >> 6], nullptr, overflowQ, nOverflow);
 }
 extern "C" __global__ __launch_bounds__(HPT_PACKET_BLOCK) void k_trace_packet_counted(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ nTrace,
     uint32_t *__restrict__ cursors, uint32_t *stats, uint32_t *__restrict__ overflowQ, uint32_t *__restrict__ nOverflow) {
     __shared__ PacketLds lds[HPT_PACKET_BLOCK / 64];
-    PathIO io{P, traceQ, nullptr, *nTrace, 0, 0};
+    PathIO io{P, traceQ, nullptr, *nTrace, 0, 0, true, nullptr};
     tracePackets<true, false>(sc, io, cursors, lds[threadIdx.x >> 6], stats, overflowQ, nOverflow);
 }
 /* the camera rays of packets whose stack overflowed, one lane per ray (k_trace's traversal;
    a separate symbol so the profiles keep k_trace's launches apart) */
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace_overflow(
-    HptScene sc, HptPaths P, const uint32_t *__restrict__ overflowQ, const uint32_t *__restrict__ nOverflow,
-    uint32_t *__restrict__ cursors) {
+    HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ overflowQ,
+    const uint32_t *__restrict__ nOverflow, uint32_t *__restrict__ cursors) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    PathIO io{P, overflowQ, nullptr, *nOverflow, 0, 0};
+    /* overflowQ holds camera-queue positions (the packet kernel's keys) */
+    PathIO io{P, traceQ, nullptr, *nOverflow, 0, 0, true, overflowQ};
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
 
@@ -2153,10 +2395,11 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
     const uint32_t n = *nTrace;
     bool alive = false;
     uint32_t id = 0;
+    uint32_t seg = HPT_MISS;
     if (tid < n) {
         id = traceQ[tid];
-        float4 h = P.hit[id];
-        if (__float_as_int(h.x) >= 0) {
+        seg = P.hitQ[tid];
+        if (seg != HPT_MISS) {
             alive = true;
         } else if (!sc.hideEmitters) {
             /* a camera ray keeps its differentials: EWA-filtered lookup (envmap.cpp:394-406) */
@@ -2171,7 +2414,7 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
             P.li[id] = make_float4(0.0f + c.x, 0.0f + c.y, 0.0f + c.z, 0.0f);
         }
     }
-    qpushBlock<HPT_QBLOCK>(alive, id, shadeQ, nShade);
+    qpushBlock2<HPT_QBLOCK>(alive, id, shadeQ, seg, P.hitS, nShade);
 }
 
 /* one bounce of shading: path.cpp:145-232 up to the continuation ray cast.
@@ -2179,18 +2422,18 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
    separate kernel, so the single-shape one never mixes a kernel-argument
    pointer with a global one -- that would copy the scene to scratch) */
 template <bool MULTI>
-HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__restrict__ counters, bool &cont,
-                  bool &shadow) {
+HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec, uint32_t *__restrict__ counters,
+                  bool &cont, bool &shadow) {
     {
         uint32_t st = P.state[id];
         uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st);
-        float4 h = P.hit[id], ro = P.ro[id], rd = P.rd[id];
+        float4 ro = P.ro[id], rd = P.rd[id];
         V3 rayD = v3(rd.x, rd.y, rd.z);
         V3 p, wi;
         Frame geo, sh;
-        const uint32_t seg = (uint32_t) __float_as_int(h.x);
+        const uint32_t seg = hitRec & 0x7fffffffu;
         /* the traced ray is still in ro / rd: the hit point from the accepted root (hair.cpp:519-541) */
-        const V3 hp = segHitPoint(sc, seg, v3(ro.x, ro.y, ro.z), rayD, __float_as_uint(h.z));
+        const V3 hp = segHitPoint(sc, seg, v3(ro.x, ro.y, ro.z), rayD, hitRec >> 31);
         fillIts(sc, seg, hp, rayD, p, geo, sh, wi);
         bool stop = ((int) depth >= sc.maxDepth && sc.maxDepth > 0) ||
                     (sc.strictNormals && dot(rayD, geo.n) * wi.z >= 0);
@@ -2275,7 +2518,7 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
     uint32_t id = 0;
     if (tid < n) {
         id = shadeQ[tid];
-        shadePath<MULTI>(sc, P, id, q.counters, cont, shadow);
+        shadePath<MULTI>(sc, P, id, P.hitS[tid], q.counters, cont, shadow);
     }
     qpushBlock<HPT_SHADE_BLOCK>(cont, id, traceQ, q.nTrace);
     qpushBlock<HPT_SHADE_BLOCK>(shadow, id, shadowQ, q.nShadow);
@@ -2302,14 +2545,13 @@ extern "C" __global__ __launch_bounds__(HPT_SHADE_BLOCK) void k_shade_multi(HptS
 }
 
 /* continuation result: path.cpp:225-286; true when the path goes on */
-HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t *__restrict__ counters) {
+HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, bool hit, uint32_t *__restrict__ counters) {
     bool alive = false;
     {
         uint32_t st = P.state[id];
         uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st), type = (st >> 24) & 0x7fu;
         const bool scattered = (st >> 31) != 0;
-        float4 h = P.hit[id], bw = P.bw[id], thr = P.thr[id], rd = P.rd[id];
-        bool hit = __float_as_int(h.x) >= 0;
+        float4 bw = P.bw[id], thr = P.thr[id], rd = P.rd[id];
         V3 T = v3(thr.x, thr.y, thr.z);
         bool done = false, hitEmitter = false;
         V3 value = v3(0, 0, 0);
@@ -2365,11 +2607,14 @@ extern "C" __global__ __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc,
     const uint32_t n = *nTrace;
     bool alive = false;
     uint32_t id = 0;
+    uint32_t seg = HPT_MISS;
     if (tid < n) {
         id = traceQ[tid];
-        alive = postPath(sc, P, id, counters);
+        seg = P.hitQ[tid];
+        alive = postPath(sc, P, id, seg != HPT_MISS, counters);
     }
-    qpushBlock<HPT_POST_BLOCK>(alive, id, shadeQ, nShade);
+    /* the survivors' hit records travel with the shade queue, in its order */
+    qpushBlock2<HPT_POST_BLOCK>(alive, id, shadeQ, seg, P.hitS, nShade);
 }
 
 /* Tail of the frame (few live paths left, after Russian roulette has
@@ -2403,10 +2648,10 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
     const uint32_t lane = __lane_id(), partner = lane & ~1u;
     const bool odd = (lane & 1u) != 0;
     const uint32_t total = *T.nShade;
-    uint32_t id = 0, nb = 0;
+    uint32_t id = 0, nb = 0, hitRec = 0;
     bool live = false, exhausted = false;
     TraceCounters tc;
-    PathIO io{P, nullptr, nullptr, 0, 0, 0};
+    PathIO io{P, nullptr, nullptr, 0, 0, 0, false, nullptr};
 #ifdef HPT_TAIL_PROFILE
     uint32_t rounds = 0;
     unsigned long long pIt = 0, pS = 0, pT = 0, pP = 0, pR = 0, pItems = 0;
@@ -2440,6 +2685,7 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
             const uint32_t j = __shfl(base + rk, (int) partner);
             if (!live && (lane >> 1) < T.pairs && j < total) { /* exactly the pairs counted in freeM */
                 id = T.shadeQ[j];
+                hitRec = P.hitS[j];
                 live = true;
 #ifdef HPT_TAIL_PROFILE
                 pItems += odd ? 0u : 1u;
@@ -2457,7 +2703,7 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
         bool cont = false, shadow = false;
         if (live && !odd) {
             ++nb;
-            shadePath<MULTI>(sc, P, id, counters, cont, shadow);
+            shadePath<MULTI>(sc, P, id, hitRec, counters, cont, shadow);
         }
         __threadfence_block(); /* the continuation ray is in HBM for the odd lane */
         const int f = __shfl((cont ? 1 : 0) | (shadow ? 2 : 0), (int) partner);
@@ -2474,7 +2720,10 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
         const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
 #endif
         bool alive = false;
-        if (live && !odd && cont) alive = postPath(sc, P, id, counters);
+        if (live && !odd && cont) {
+            hitRec = P.hit[id];
+            alive = postPath(sc, P, id, hitRec != HPT_MISS, counters);
+        }
         live = live && __shfl(alive ? 1 : 0, (int) partner) != 0;
 #ifdef HPT_TAIL_PROFILE
         const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
@@ -2864,11 +3113,11 @@ hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const 
                            dim3(HPT_PACKET_BLOCK), 0, s, sc, P, traceQ, nTrace, cursors, overflowQ, nOverflow);
     return hipGetLastError();
 }
-hipError_t hpt_launch_trace_overflow(const HptScene &sc, const HptPaths &P, const uint32_t *overflowQ,
+hipError_t hpt_launch_trace_overflow(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *overflowQ,
                                      const uint32_t *nOverflow, uint32_t *cursors, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
     hipLaunchKernelGGL(k_trace_overflow, dim3(persistentBlocks((const void *) k_trace_overflow, maxItems)),
-                       dim3(HPT_TRACE_BLOCK), 0, s, sc, P, overflowQ, nOverflow, cursors);
+                       dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, overflowQ, nOverflow, cursors);
     return hipGetLastError();
 }
 hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
