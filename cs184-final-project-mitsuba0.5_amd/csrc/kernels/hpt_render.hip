@@ -653,7 +653,7 @@ HD uint32_t selectBit(uint64_t m, uint32_t k) {
 __device__ unsigned long long g_traceprof[HPT_TRACE_PROFILE_LAUNCHES][HPT_TRACE_PROFILE_WAVES][8];
 __device__ uint32_t g_traceprof_slot;
 #endif
-template <int STACK, bool STATS, class IO>
+template <int STACK, bool STATS, bool SPLIT = (!STATS && HPT_DRAIN_SPLIT), class IO>
 __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint32_t *cursors, uint2 *stk,
                                                 uint32_t *stats) {
 #ifdef HPT_TRACE_PROFILE
@@ -677,9 +677,10 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
     bool active = false, exhausted = false;
     uint32_t shard = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % HPT_CURSORS;
     int tried = 0;
-    /* drain splitting (HPT_DRAIN_SPLIT): lanes of split rays, and those of them that have
-       finished their interval while the ray's answer is still open (wave-uniform masks) */
-    constexpr bool SPLIT = !STATS && HPT_DRAIN_SPLIT;
+    /* drain splitting (HPT_DRAIN_SPLIT; never in the counted kernels, whose counts price the
+       unsplit traversal): lanes of split rays, and those of them that have finished their
+       interval while the ray's answer is still open (wave-uniform masks) */
+    static_assert(!(SPLIT && STATS), "the counted traversal is not split");
     uint64_t splitM = 0, waitM = 0;
     const int stride = (int) blockDim.x;
     /* the j-th of n pieces of [a, b] starts here (the same expression on the donor and the helper) */
@@ -2894,7 +2895,8 @@ extern "C" __global__ void k_camera_batch(HptScene sc, int n, const float *pos, 
 /* Batch trace through the production traversal (tracePersistent).  flags:
    bit 0 = any-hit shadow query, bit 1 = 2-entry stack (exercises the
    kd-restart path for the parity tests), bit 2 = closest hits through the
-   packet traversal (tracePackets, 64 consecutive rays per packet) */
+   packet traversal (tracePackets, 64 consecutive rays per packet), bit 3 = no
+   drain splitting (the parity tests compare both) */
 struct BatchIO {
     const float *o, *d, *mint, *maxt;
     float *outT, *outP;
@@ -2938,6 +2940,8 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptS
         tracePackets<false, true>(sc, io, cursor, lds[threadIdx.x >> 6], nullptr);
     else if (flags & 2)
         tracePersistent<2, false>(sc, io, cursor, stk + threadIdx.x, nullptr);
+    else if (flags & 8)
+        tracePersistent<HPT_STACK, false, false>(sc, io, cursor, stk + threadIdx.x, nullptr);
     else
         tracePersistent<HPT_STACK, false>(sc, io, cursor, stk + threadIdx.x, nullptr);
 }

@@ -388,7 +388,7 @@ class Renderer:
                                               _p(maxt, _f)))
         return o, d, mint, maxt
 
-    def trace(self, o, d, mint, maxt, shadow=False, tiny_stack=False, packet=False):
+    def trace(self, o, d, mint, maxt, shadow=False, tiny_stack=False, packet=False, split=True):
         o = _f32(o).reshape(-1, 3)
         d = _f32(d).reshape(-1, 3)
         n = o.shape[0]
@@ -399,7 +399,8 @@ class Renderer:
         op = np.zeros((n, 3), np.float32)
         oh = np.zeros(n, np.uint8)
         self._check(self.lib.hpt_trace_batch(self.h, n, _p(o, _f), _p(d, _f), _p(mint, _f), _p(maxt, _f),
-                                             (1 if shadow else 0) | (2 if tiny_stack else 0) | (4 if packet else 0),
+                                             (1 if shadow else 0) | (2 if tiny_stack else 0) | (4 if packet else 0)
+                                             | (0 if split else 8),
                                              _p(ot, _f), _p(oiv, _i32), _p(op, _f), _p(oh, _u8)))
         return oh.astype(bool) if shadow else (ot, oiv, op)
 

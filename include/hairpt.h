@@ -255,6 +255,7 @@ int hpt_camera_batch(hpt_context *ctx, int n, const float *pos, float *out_o, fl
 #define HPT_TRACE_SHADOW 1      /* any-hit query (out_hit) instead of closest hit */
 #define HPT_TRACE_TINY_STACK 2  /* test hook: 2-entry traversal stack, forces kd-restarts */
 #define HPT_TRACE_PACKET 4      /* closest hits through the 64-ray packet traversal (camera pass) */
+#define HPT_TRACE_NO_SPLIT 8    /* test hook: no drain splitting (idle lanes wait for their wave's last ray) */
 int hpt_trace_batch(hpt_context *ctx, int n, const float *o, const float *d, const float *mint, const float *maxt,
                     int flags, float *out_t, int32_t *out_iv, float *out_p, uint8_t *out_hit);
 /* BSDF::eval / pdf / sample for the scene's hair BSDF (local frame) */

@@ -132,6 +132,13 @@ def test_trace_bit_exact(fixture, kind, request):
     np.testing.assert_array_equal(tiv, oiv)
     np.testing.assert_array_equal(tt, ot)
     np.testing.assert_array_equal(r.trace(orig, dirs, mint, sm, shadow=True, tiny_stack=True), osh)
+    # drain splitting (every batch ends in a drain: idle lanes take over the farthest pending
+    # subtrees of running rays) gives the answers of the unsplit traversal
+    ut, uiv, up = r.trace(orig, dirs, mint, maxt, split=False)
+    np.testing.assert_array_equal(uiv, oiv)
+    np.testing.assert_array_equal(ut, ot)
+    np.testing.assert_array_equal(up, op)
+    np.testing.assert_array_equal(r.trace(orig, dirs, mint, sm, shadow=True, split=False), osh)
 
 
 HAIRCURL_RADII = [0.02, 0.035, 0.05, 0.028]
