@@ -141,6 +141,29 @@ def test_trace_bit_exact(fixture, kind, request):
     np.testing.assert_array_equal(r.trace(orig, dirs, mint, sm, shadow=True, split=False), osh)
 
 
+@pytest.mark.parametrize("n", [1, 7, 63, 65, 300])
+def test_trace_small_batches_split(furball, n):
+    """Drain splitting at its most aggressive: a batch of n rays leaves most lanes of
+    every wave idle from the start, so running rays are split again and again (stack
+    steals and, once a ray's stack is empty, interval halves from the root) -- the
+    closest hits, the far roots and the any-hit answers must still be the oracle's and
+    the unsplit traversal's (tiny-stack rays split too: lost entries go to the helper)."""
+    _, r, o = furball
+    # camera rays and random chords (_rays: n // 2 of each), then n grazing rays
+    a = _rays(o, n, 100 + n)
+    g = _grazing_rays(r, n, 200 + n, float(scene_util.scenes.CONFIGS["furball_marschner"]["radius"]))
+    orig, dirs, mint, maxt = (np.concatenate([x, y]).astype(np.float32) for x, y in zip(a, g))
+    ot, oiv, op = o.trace(orig, dirs, mint, maxt)
+    sm = np.minimum(maxt, 3.0).astype(np.float32)
+    osh = o.trace(orig, dirs, mint, sm, shadow=True)
+    for kw in ({}, {"split": False}, {"tiny_stack": True}):
+        gt, giv, gp = r.trace(orig, dirs, mint, maxt, **kw)
+        np.testing.assert_array_equal(giv, oiv, err_msg=str(kw))
+        np.testing.assert_array_equal(gt, ot, err_msg=str(kw))
+        np.testing.assert_array_equal(gp, op, err_msg=str(kw))
+        np.testing.assert_array_equal(r.trace(orig, dirs, mint, sm, shadow=True, **kw), osh, err_msg=str(kw))
+
+
 HAIRCURL_RADII = [0.02, 0.035, 0.05, 0.028]
 
 
