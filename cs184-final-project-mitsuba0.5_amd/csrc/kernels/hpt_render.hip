@@ -2248,6 +2248,14 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
 /* k_trace: the wave's closest-hit rays (traceQ[0, nTrace)) then its any-hit
    shadow rays (shadowQ) as one persistent grid; k_trace_counted adds the
    traversal counters of the byte model (one counted frame per bench run) */
+#ifdef HPT_COST_PROBE
+/* experiment builds only: leaf rounds of each path's closest / shadow ray per trace launch
+   (host-set slot), to see whether a ray's cost predicts its path's next ray's */
+#define HPT_COST_LAUNCHES 6
+#define HPT_COST_PATHS (1 << 21)
+__device__ uint16_t g_costprof[HPT_COST_LAUNCHES][2][HPT_COST_PATHS];
+__device__ uint32_t g_cost_slot;
+#endif
 /* Closest-hit records go to P.hitQ by trace-queue position (the wavefront
    kernels; k_primary / k_post read them in queue order), or to P.hit by path
    (byQueue false: k_tail).  A record is 4 bytes (segment | far root << 31, or
@@ -2278,6 +2286,14 @@ struct PathIO {
     /* id: the record's queue position / path (closest), the path (shadow ray);
        returns 1 for an unoccluded shadow ray */
     HD uint32_t finish(const HptScene &sc, uint32_t id, const TraceRay &r) {
+#ifdef HPT_COST_PROBE
+        {
+            const uint32_t path = r.shadow ? id : (byQueue && traceQ && !posQ ? traceQ[id] : HPT_COST_PATHS);
+            const uint32_t slot = g_cost_slot;
+            if (path < HPT_COST_PATHS && slot < HPT_COST_LAUNCHES)
+                g_costprof[slot][r.shadow ? 1 : 0][path] = (uint16_t) min(rayLeaves(r) + 1u, 65535u);
+        }
+#endif
         if (!r.shadow) {
             /* the shading kernel re-derives the point from the segment and the accepted root */
             (byQueue ? P.hitQ : P.hit)[id] = r.found ? r.segHit : HPT_MISS;
@@ -3070,6 +3086,19 @@ static unsigned persistentBlocks(const void *kernel, uint64_t items, int block =
     return (unsigned) std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t) resident));
 }
 
+#ifdef HPT_COST_PROBE
+static uint32_t g_costHostSlot = 0;
+extern "C" int hpt_debug_costprof(uint16_t *out) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    const int n = (int) std::min<uint32_t>(g_costHostSlot, HPT_COST_LAUNCHES);
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_costprof), sizeof(uint16_t) * HPT_COST_LAUNCHES * 2 * HPT_COST_PATHS) != hipSuccess)
+        return -1;
+    std::vector<uint16_t> zeros((size_t) HPT_COST_LAUNCHES * 2 * HPT_COST_PATHS, 0);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_costprof), zeros.data(), zeros.size() * 2) != hipSuccess) return -1;
+    g_costHostSlot = 0;
+    return n;
+}
+#endif
 #ifdef HPT_TRACE_PROFILE
 static uint32_t g_traceprofHostSlot = 0;
 /* copy out (and clear) the k_trace timing records of the launches since the last call:
@@ -3089,6 +3118,13 @@ hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
                             uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
+#ifdef HPT_COST_PROBE
+    {
+        const uint32_t slot = g_costHostSlot++;
+        (void) hipMemcpyToSymbolAsync(HIP_SYMBOL(g_cost_slot), &slot, 4, 0, hipMemcpyHostToDevice, s);
+        (void) hipStreamSynchronize(s);
+    }
+#endif
 #ifdef HPT_TRACE_PROFILE
     {
         const uint32_t slot = g_traceprofHostSlot++;
