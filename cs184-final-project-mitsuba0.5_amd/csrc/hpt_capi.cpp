@@ -192,6 +192,7 @@ int ensureWave(hpt_context *c, uint64_t n) {
     r |= alloc(n * 4, (void **) &c->P.hit);
     r |= alloc(n * 4, (void **) &c->P.hitQ);
     r |= alloc(n * 4, (void **) &c->P.hitS);
+    r |= alloc(n * 32, (void **) &c->P.postRec);
     r |= alloc(n * 16, (void **) &c->P.bw);
     r |= alloc(n * 16, (void **) &c->P.sdir);
     r |= alloc(n * 16, (void **) &c->P.scontrib);

@@ -66,6 +66,8 @@ struct HptPaths {
     uint32_t *hit;     /* k_tail's hit records by path: segment id | far root << 31, HPT_MISS = miss */
     uint32_t *hitQ;    /* a trace launch's hit records by trace-queue position (k_primary / k_post read them in queue order) */
     uint32_t *hitS;    /* the next shade queue's hit records by shade-queue position (written with the queue) */
+    float4 *postRec;   /* what k_post needs of a continuation ray, by trace-queue position (written by k_shade
+                          with the queue): [2k] bsdf weight rgb, pdf; [2k+1] throughput rgb, state bits */
     float4 *bw;        /* bsdf weight rgb, bsdf pdf                  */
     float4 *sdir;      /* shadow ray direction xyz, maxt             */
     float4 *scontrib;  /* NEE contribution rgb (added if unoccluded) */

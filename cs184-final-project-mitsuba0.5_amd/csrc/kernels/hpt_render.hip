@@ -2162,6 +2162,36 @@ __device__ __forceinline__ void qpushBlock2(bool pred, uint32_t value, uint32_t 
     __syncthreads();
 }
 
+/* qpushBlock that also stores a two-float4 record at the same position of recs */
+template <int BLOCK>
+__device__ __forceinline__ void qpushBlockRec(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter,
+                                              float4 *recs, float4 r0, float4 r1) {
+    constexpr int NW = BLOCK / 64;
+    __shared__ uint32_t waveCount[NW];
+    __shared__ uint32_t blockBase;
+    const uint64_t mask = __ballot(pred);
+    const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+    if (lane == 0) waveCount[wave] = (uint32_t) __popcll(mask);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t c = waveCount[w];
+            waveCount[w] = tot;
+            tot += c;
+        }
+        blockBase = tot ? atomicAdd(counter, tot) : 0u;
+    }
+    __syncthreads();
+    if (pred) {
+        const uint32_t pos = blockBase + waveCount[wave] + (uint32_t) __popcll(mask & ((1ull << lane) - 1ull));
+        queue[pos] = value;
+        recs[2 * pos] = r0;
+        recs[2 * pos + 1] = r1;
+    }
+    __syncthreads();
+}
+
 /* append to a queue: one atomic per wave (wave64 ballot + mbcnt) */
 HD void qpush(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
     uint64_t mask = __ballot(pred);
@@ -2438,9 +2468,12 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
    MULTI: several hair shapes, the hit shape's BSDF comes from sc.bsdfs (a
    separate kernel, so the single-shape one never mixes a kernel-argument
    pointer with a global one -- that would copy the scene to scratch) */
-template <bool MULTI>
+/* REC (the wavefront k_shade): the continuation's bsdf weight, throughput and state go to
+   rec0 / rec1 for the post record (k_post reads them in queue order) instead of P.bw / P.state;
+   k_tail keeps them by path */
+template <bool MULTI, bool REC = false>
 HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec, uint32_t *__restrict__ counters,
-                  bool &cont, bool &shadow) {
+                  bool &cont, bool &shadow, float4 &rec0, float4 &rec1) {
     {
         uint32_t st = P.state[id];
         uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st);
@@ -2465,6 +2498,7 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
         auto shadeWith = [&](const HptBsdf &B) {
             const uint64_t sidx = P.sobol[id];
             float4 thr = P.thr[id];
+            rec1 = thr;
             V3 T = v3(thr.x, thr.y, thr.z);
             /* ---- direct illumination (path.cpp:175, scene.cpp:828-852, envmap.cpp:516-543) ---- */
             if (B.smooth) {
@@ -2504,7 +2538,8 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
                 if (!(sc.strictNormals && woDotGeoN * woL.z <= 0)) {
                     P.ro[id] = make_float4(p.x, p.y, p.z, kEpsilon);
                     P.rd[id] = make_float4(wo.x, wo.y, wo.z, finf());
-                    P.bw[id] = make_float4(w.x, w.y, w.z, bpdf);
+                    rec0 = make_float4(w.x, w.y, w.z, bpdf);
+                    if (!REC) P.bw[id] = rec0;
                     cont = true;
                     /* bits 24-30: sampled type; bit 31: 'scattered' (path.cpp:205) */
                     st = (st & 0x80ffffffu) | (type << 24) | (type != HPT_ENULL ? 0x80000000u : 0u);
@@ -2516,7 +2551,9 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
             if (MULTI) shadeWith(sc.bsdfs[sc.shapes[sc.segs[seg].shape].bsdf]);
             else shadeWith(sc.bsdf);
         }
-        P.state[id] = (st & ~HPT_ST_DIM_MASK) | dim;
+        st = (st & ~HPT_ST_DIM_MASK) | dim;
+        rec1.w = __uint_as_float(st);
+        if (!REC || !cont) P.state[id] = st;
     }
 }
 /* where a shading launch reads and appends: its shade queue's length, the
@@ -2533,11 +2570,12 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
     const uint32_t n = *q.nShade;
     bool cont = false, shadow = false;
     uint32_t id = 0;
+    float4 rec0, rec1;
     if (tid < n) {
         id = shadeQ[tid];
-        shadePath<MULTI>(sc, P, id, P.hitS[tid], q.counters, cont, shadow);
+        shadePath<MULTI, true>(sc, P, id, P.hitS[tid], q.counters, cont, shadow, rec0, rec1);
     }
-    qpushBlock<HPT_SHADE_BLOCK>(cont, id, traceQ, q.nTrace);
+    qpushBlockRec<HPT_SHADE_BLOCK>(cont, id, traceQ, q.nTrace, P.postRec, rec0, rec1);
     qpushBlock<HPT_SHADE_BLOCK>(shadow, id, shadowQ, q.nShadow);
 }
 #ifndef HPT_SHADE_WAVES
@@ -2562,18 +2600,24 @@ extern "C" __global__ __launch_bounds__(HPT_SHADE_BLOCK) void k_shade_multi(HptS
 }
 
 /* continuation result: path.cpp:225-286; true when the path goes on */
-HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, bool hit, uint32_t *__restrict__ counters) {
+/* REC: bsdf weight, throughput and state from the post record (rec0 / rec1, k_post) instead of
+   by path (k_tail) */
+template <bool REC = false>
+HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, bool hit, uint32_t *__restrict__ counters,
+                 float4 rec0 = float4(), float4 rec1 = float4()) {
     bool alive = false;
     {
-        uint32_t st = P.state[id];
+        uint32_t st = REC ? __float_as_uint(rec1.w) : P.state[id];
         uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st), type = (st >> 24) & 0x7fu;
         const bool scattered = (st >> 31) != 0;
-        float4 bw = P.bw[id], thr = P.thr[id], rd = P.rd[id];
+        float4 bw = REC ? rec0 : P.bw[id], thr = REC ? rec1 : P.thr[id];
         V3 T = v3(thr.x, thr.y, thr.z);
         bool done = false, hitEmitter = false;
         V3 value = v3(0, 0, 0);
-        V3 d = v3(rd.x, rd.y, rd.z);
+        V3 d = v3(0, 0, 0);
         if (!hit) {
+            const float4 rd = P.rd[id]; /* the direction matters only for a miss */
+            d = v3(rd.x, rd.y, rd.z);
             /* path.cpp:238-240: only a pass-through (ENull) chain from the camera is unscattered */
             value = envEval(sc.env, d);
             float4 ro = P.ro[id];
@@ -2628,7 +2672,7 @@ extern "C" __global__ __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc,
     if (tid < n) {
         id = traceQ[tid];
         seg = P.hitQ[tid];
-        alive = postPath(sc, P, id, seg != HPT_MISS, counters);
+        alive = postPath<true>(sc, P, id, seg != HPT_MISS, counters, P.postRec[2 * tid], P.postRec[2 * tid + 1]);
     }
     /* the survivors' hit records travel with the shade queue, in its order */
     qpushBlock2<HPT_POST_BLOCK>(alive, id, shadeQ, seg, P.hitS, nShade);
@@ -2720,7 +2764,8 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
         bool cont = false, shadow = false;
         if (live && !odd) {
             ++nb;
-            shadePath<MULTI>(sc, P, id, hitRec, counters, cont, shadow);
+            float4 rec0, rec1;
+            shadePath<MULTI>(sc, P, id, hitRec, counters, cont, shadow, rec0, rec1);
         }
         __threadfence_block(); /* the continuation ray is in HBM for the odd lane */
         const int f = __shfl((cont ? 1 : 0) | (shadow ? 2 : 0), (int) partner);
