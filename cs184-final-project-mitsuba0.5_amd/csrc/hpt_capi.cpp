@@ -192,7 +192,9 @@ int ensureWave(hpt_context *c, uint64_t n) {
     r |= alloc(n * 4, (void **) &c->P.hit);
     r |= alloc(n * 4, (void **) &c->P.hitQ);
     r |= alloc(n * 4, (void **) &c->P.hitS);
-    r |= alloc(n * 32, (void **) &c->P.postRec);
+    r |= alloc(n * 64, (void **) &c->P.postRec);
+    r |= alloc(n * 48, (void **) &c->P.shadowRec);
+    r |= alloc(n * 48, (void **) &c->P.shadeRec);
     r |= alloc(n * 16, (void **) &c->P.bw);
     r |= alloc(n * 16, (void **) &c->P.sdir);
     r |= alloc(n * 16, (void **) &c->P.scontrib);

@@ -66,8 +66,20 @@ struct HptPaths {
     uint32_t *hit;     /* k_tail's hit records by path: segment id | far root << 31, HPT_MISS = miss */
     uint32_t *hitQ;    /* a trace launch's hit records by trace-queue position (k_primary / k_post read them in queue order) */
     uint32_t *hitS;    /* the next shade queue's hit records by shade-queue position (written with the queue) */
-    float4 *postRec;   /* what k_post needs of a continuation ray, by trace-queue position (written by k_shade
-                          with the queue): [2k] bsdf weight rgb, pdf; [2k+1] throughput rgb, state bits */
+    /* Queue-ordered path records: a bounce's kernels read and write a path's state at its
+       position in the queue they consume / fill (coalesced), not at its path id (a gather
+       over scattered ids), so the state travels with the queues:
+       postRec   by trace-queue position, written by k_shade with the queue, read by k_trace and
+                 k_post: [4k] origin xyz | Sobol index bits 0-31, [4k+1] direction xyz | bits
+                 32-63, [4k+2] bsdf weight rgb, pdf, [4k+3] throughput rgb, state bits
+       shadowRec by shadow-queue position (k_shade -> k_trace): [3k] origin xyz, [3k+1]
+                 direction xyz, maxt, [3k+2] NEE contribution rgb
+       shadeRec  by shade-queue position (k_primary / k_post -> k_shade / k_tail): [3k] traced
+                 origin xyz | Sobol bits 0-31, [3k+1] traced direction xyz | bits 32-63,
+                 [3k+2] throughput rgb, state bits
+       The by-path arrays above (ro, rd, thr, state, bw, sdir, scontrib) are k_camera's and
+       k_tail's. */
+    float4 *postRec, *shadowRec, *shadeRec;
     float4 *bw;        /* bsdf weight rgb, bsdf pdf                  */
     float4 *sdir;      /* shadow ray direction xyz, maxt             */
     float4 *scontrib;  /* NEE contribution rgb (added if unoccluded) */

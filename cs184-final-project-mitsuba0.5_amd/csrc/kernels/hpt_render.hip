@@ -2162,10 +2162,12 @@ __device__ __forceinline__ void qpushBlock2(bool pred, uint32_t value, uint32_t 
     __syncthreads();
 }
 
-/* qpushBlock that also stores a two-float4 record at the same position of recs */
-template <int BLOCK>
+/* qpushBlock that also stores an NR-float4 record at the same position of recs and, with
+   array2, a word there */
+template <int BLOCK, int NR>
 __device__ __forceinline__ void qpushBlockRec(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter,
-                                              float4 *recs, float4 r0, float4 r1) {
+                                              float4 *recs, const float4 *rec, uint32_t *array2 = nullptr,
+                                              uint32_t value2 = 0u) {
     constexpr int NW = BLOCK / 64;
     __shared__ uint32_t waveCount[NW];
     __shared__ uint32_t blockBase;
@@ -2186,8 +2188,9 @@ __device__ __forceinline__ void qpushBlockRec(bool pred, uint32_t value, uint32_
     if (pred) {
         const uint32_t pos = blockBase + waveCount[wave] + (uint32_t) __popcll(mask & ((1ull << lane) - 1ull));
         queue[pos] = value;
-        recs[2 * pos] = r0;
-        recs[2 * pos + 1] = r1;
+#pragma unroll
+        for (int i = 0; i < NR; ++i) recs[NR * pos + i] = rec[i];
+        if (array2) array2[pos] = value2;
     }
     __syncthreads();
 }
@@ -2299,8 +2302,19 @@ struct PathIO {
     uint32_t nTrace, nShadow, id;
     bool byQueue;
     const uint32_t *posQ;
+    bool recs; /* bounce launches: rays from the queue-ordered records, keys are queue positions */
     HD uint32_t count() const { return nTrace + nShadow; }
     HD bool begin(const HptScene &sc, uint32_t k, TraceRay &r) {
+        if (recs) { /* a bounce ray leaves the hit point at kEpsilon (path.cpp:213, scene.cpp:838) */
+            if (k < nTrace) {
+                id = k;
+                const float4 o = P.postRec[4 * k], d = P.postRec[4 * k + 1];
+                return beginRay(sc, r, v3(o.x, o.y, o.z), v3(d.x, d.y, d.z), kEpsilon, finf(), false);
+            }
+            id = k - nTrace;
+            const float4 o = P.shadowRec[3 * id], d = P.shadowRec[3 * id + 1];
+            return beginRay(sc, r, v3(o.x, o.y, o.z), v3(d.x, d.y, d.z), kEpsilon, d.w, true);
+        }
         if (k < nTrace) {
             const uint32_t q = posQ ? posQ[k] : k;
             const uint32_t path = traceQ[q];
@@ -2318,7 +2332,7 @@ struct PathIO {
     HD uint32_t finish(const HptScene &sc, uint32_t id, const TraceRay &r) {
 #ifdef HPT_COST_PROBE
         {
-            const uint32_t path = r.shadow ? id : (byQueue && traceQ && !posQ ? traceQ[id] : HPT_COST_PATHS);
+            const uint32_t path = r.shadow ? (recs ? shadowQ[id] : id) : (byQueue && traceQ && !posQ ? traceQ[id] : HPT_COST_PATHS);
             const uint32_t slot = g_cost_slot;
             if (path < HPT_COST_PATHS && slot < HPT_COST_LAUNCHES)
                 g_costprof[slot][r.shadow ? 1 : 0][path] = (uint16_t) min(rayLeaves(r) + 1u, 65535u);
@@ -2330,8 +2344,9 @@ struct PathIO {
             return 0;
         }
         if (r.found) return 0;
-        const float4 c = P.scontrib[id], l = P.li[id];
-        P.li[id] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
+        const uint32_t path = recs ? shadowQ[id] : id;
+        const float4 c = recs ? P.shadowRec[3 * id + 2] : P.scontrib[id], l = P.li[path];
+        P.li[path] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
         return 1;
     }
 };
@@ -2366,7 +2381,7 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY voi
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
     const uint32_t *__restrict__ nTrace, const uint32_t *__restrict__ nShadow, uint32_t *__restrict__ cursors) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    PathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0, true, nullptr};
+    PathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0, true, nullptr, true};
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(HptScene sc, HptPaths P,
@@ -2377,7 +2392,7 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
                                                                               uint32_t *__restrict__ cursors,
                                                                               uint32_t *stats) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    PathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0, true, nullptr};
+    PathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0, true, nullptr, true};
     tracePersistent<HPT_STACK, true>(sc, io, cursors, stk + threadIdx.x, stats);
 }
 
@@ -2392,14 +2407,14 @@ extern "C" __global__ __launch_bounds__(HPT_PACKET_BLOCK) __attribute__((amdgpu_
 k_trace_packet(HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ nTrace,
                uint32_t *__restrict__ cursors, uint32_t *__restrict__ overflowQ, uint32_t *__restrict__ nOverflow) {
     __shared__ PacketLds lds[HPT_PACKET_BLOCK / 64];
-    PathIO io{P, traceQ, nullptr, *nTrace, 0, 0, true, nullptr};
+    PathIO io{P, traceQ, nullptr, *nTrace, 0, 0, true, nullptr, false};
     tracePackets<false, false>(sc, io, cursors, lds[threadIdx.x >> 6], nullptr, overflowQ, nOverflow);
 }
 extern "C" __global__ __launch_bounds__(HPT_PACKET_BLOCK) void k_trace_packet_counted(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ nTrace,
     uint32_t *__restrict__ cursors, uint32_t *stats, uint32_t *__restrict__ overflowQ, uint32_t *__restrict__ nOverflow) {
     __shared__ PacketLds lds[HPT_PACKET_BLOCK / 64];
-    PathIO io{P, traceQ, nullptr, *nTrace, 0, 0, true, nullptr};
+    PathIO io{P, traceQ, nullptr, *nTrace, 0, 0, true, nullptr, false};
     tracePackets<true, false>(sc, io, cursors, lds[threadIdx.x >> 6], stats, overflowQ, nOverflow);
 }
 /* the camera rays of packets whose stack overflowed, one lane per ray (k_trace's traversal;
@@ -2409,7 +2424,7 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY voi
     const uint32_t *__restrict__ nOverflow, uint32_t *__restrict__ cursors) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     /* overflowQ holds camera-queue positions (the packet kernel's keys) */
-    PathIO io{P, traceQ, nullptr, *nOverflow, 0, 0, true, overflowQ};
+    PathIO io{P, traceQ, nullptr, *nOverflow, 0, 0, true, overflowQ, false};
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
 
@@ -2443,11 +2458,18 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
     bool alive = false;
     uint32_t id = 0;
     uint32_t seg = HPT_MISS;
+    float4 sOut[3];
     if (tid < n) {
         id = traceQ[tid];
         seg = P.hitQ[tid];
         if (seg != HPT_MISS) {
             alive = true;
+            /* the shade record (hpt_kernels.h): the camera ray, its Sobol index, throughput 1, state */
+            const float4 ro = P.ro[id], rd = P.rd[id], thr = P.thr[id];
+            const uint64_t sidx = P.sobol[id];
+            sOut[0] = make_float4(ro.x, ro.y, ro.z, __uint_as_float((uint32_t) sidx));
+            sOut[1] = make_float4(rd.x, rd.y, rd.z, __uint_as_float((uint32_t) (sidx >> 32)));
+            sOut[2] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(P.state[id]));
         } else if (!sc.hideEmitters) {
             /* a camera ray keeps its differentials: EWA-filtered lookup (envmap.cpp:394-406) */
             const float4 rd = P.rd[id];
@@ -2461,23 +2483,24 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
             P.li[id] = make_float4(0.0f + c.x, 0.0f + c.y, 0.0f + c.z, 0.0f);
         }
     }
-    qpushBlock2<HPT_QBLOCK>(alive, id, shadeQ, seg, P.hitS, nShade);
+    qpushBlockRec<HPT_QBLOCK, 3>(alive, id, shadeQ, nShade, P.shadeRec, sOut, P.hitS, seg);
 }
 
 /* one bounce of shading: path.cpp:145-232 up to the continuation ray cast.
    MULTI: several hair shapes, the hit shape's BSDF comes from sc.bsdfs (a
    separate kernel, so the single-shape one never mixes a kernel-argument
    pointer with a global one -- that would copy the scene to scratch) */
-/* REC (the wavefront k_shade): the continuation's bsdf weight, throughput and state go to
-   rec0 / rec1 for the post record (k_post reads them in queue order) instead of P.bw / P.state;
-   k_tail keeps them by path */
+/* REC (the wavefront k_shade): the path comes from its shade record in[0..2] and the
+   continuation / shadow ray go to the post record cOut[0..3] / shadow record sOut[0..2]
+   (hpt_kernels.h), which the caller appends with the queues; k_tail (REC false) keeps
+   everything by path */
 template <bool MULTI, bool REC = false>
 HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec, uint32_t *__restrict__ counters,
-                  bool &cont, bool &shadow, float4 &rec0, float4 &rec1) {
+                  bool &cont, bool &shadow, const float4 *in, float4 *cOut, float4 *sOut) {
     {
-        uint32_t st = P.state[id];
+        uint32_t st = REC ? __float_as_uint(in[2].w) : P.state[id];
         uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st);
-        float4 ro = P.ro[id], rd = P.rd[id];
+        const float4 ro = REC ? in[0] : P.ro[id], rd = REC ? in[1] : P.rd[id];
         V3 rayD = v3(rd.x, rd.y, rd.z);
         V3 p, wi;
         Frame geo, sh;
@@ -2496,9 +2519,8 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
            argument, scalar loads) or, with several hair shapes, the hit
            shape's entry of sc.bsdfs */
         auto shadeWith = [&](const HptBsdf &B) {
-            const uint64_t sidx = P.sobol[id];
-            float4 thr = P.thr[id];
-            rec1 = thr;
+            const uint64_t sidx = REC ? ((uint64_t) __float_as_uint(rd.w) << 32) | __float_as_uint(ro.w) : P.sobol[id];
+            const float4 thr = REC ? in[2] : P.thr[id];
             V3 T = v3(thr.x, thr.y, thr.z);
             /* ---- direct illumination (path.cpp:175, scene.cpp:828-852, envmap.cpp:516-543) ---- */
             if (B.smooth) {
@@ -2518,8 +2540,16 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
                         float bp = bsdfPdf(B, wi, wo);
                         float weight = miWeight(pdf, bp);
                         V3 c = mul(mul(T, val), bsdfVal) * weight;
-                        P.sdir[id] = make_float4(dW.x, dW.y, dW.z, farT * (1 - kShadowEpsilon));
-                        P.scontrib[id] = make_float4(c.x, c.y, c.z, 0.0f);
+                        const float4 sd = make_float4(dW.x, dW.y, dW.z, farT * (1 - kShadowEpsilon));
+                        const float4 sc4 = make_float4(c.x, c.y, c.z, 0.0f);
+                        if (REC) {
+                            sOut[0] = make_float4(p.x, p.y, p.z, 0.0f);
+                            sOut[1] = sd;
+                            sOut[2] = sc4;
+                        } else {
+                            P.sdir[id] = sd;
+                            P.scontrib[id] = sc4;
+                        }
                         shadow = true;
                     }
                 }
@@ -2536,24 +2566,31 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
                 V3 wo = sh.toWorld(woL);
                 float woDotGeoN = dot(geo.n, wo);
                 if (!(sc.strictNormals && woDotGeoN * woL.z <= 0)) {
-                    P.ro[id] = make_float4(p.x, p.y, p.z, kEpsilon);
-                    P.rd[id] = make_float4(wo.x, wo.y, wo.z, finf());
-                    rec0 = make_float4(w.x, w.y, w.z, bpdf);
-                    if (!REC) P.bw[id] = rec0;
+                    const float4 bw = make_float4(w.x, w.y, w.z, bpdf);
+                    if (REC) {
+                        cOut[0] = make_float4(p.x, p.y, p.z, ro.w); /* the Sobol index travels in .w */
+                        cOut[1] = make_float4(wo.x, wo.y, wo.z, rd.w);
+                        cOut[2] = bw;
+                        cOut[3] = thr;
+                    } else {
+                        P.ro[id] = make_float4(p.x, p.y, p.z, kEpsilon);
+                        P.rd[id] = make_float4(wo.x, wo.y, wo.z, finf());
+                        P.bw[id] = bw;
+                    }
                     cont = true;
                     /* bits 24-30: sampled type; bit 31: 'scattered' (path.cpp:205) */
                     st = (st & 0x80ffffffu) | (type << 24) | (type != HPT_ENULL ? 0x80000000u : 0u);
                 }
             }
-            if (shadow && !cont) P.ro[id] = make_float4(p.x, p.y, p.z, kEpsilon);
+            if (!REC && shadow && !cont) P.ro[id] = make_float4(p.x, p.y, p.z, kEpsilon);
         };
         if (!stop) {
             if (MULTI) shadeWith(sc.bsdfs[sc.shapes[sc.segs[seg].shape].bsdf]);
             else shadeWith(sc.bsdf);
         }
         st = (st & ~HPT_ST_DIM_MASK) | dim;
-        rec1.w = __uint_as_float(st);
-        if (!REC || !cont) P.state[id] = st;
+        if (REC) cOut[3].w = __uint_as_float(st);
+        else P.state[id] = st;
     }
 }
 /* where a shading launch reads and appends: its shade queue's length, the
@@ -2570,13 +2607,15 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
     const uint32_t n = *q.nShade;
     bool cont = false, shadow = false;
     uint32_t id = 0;
-    float4 rec0, rec1;
+    float4 in[3], cOut[4], sOut[3];
     if (tid < n) {
         id = shadeQ[tid];
-        shadePath<MULTI, true>(sc, P, id, P.hitS[tid], q.counters, cont, shadow, rec0, rec1);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) in[i] = P.shadeRec[3 * tid + i];
+        shadePath<MULTI, true>(sc, P, id, P.hitS[tid], q.counters, cont, shadow, in, cOut, sOut);
     }
-    qpushBlockRec<HPT_SHADE_BLOCK>(cont, id, traceQ, q.nTrace, P.postRec, rec0, rec1);
-    qpushBlock<HPT_SHADE_BLOCK>(shadow, id, shadowQ, q.nShadow);
+    qpushBlockRec<HPT_SHADE_BLOCK, 4>(cont, id, traceQ, q.nTrace, P.postRec, cOut);
+    qpushBlockRec<HPT_SHADE_BLOCK, 3>(shadow, id, shadowQ, q.nShadow, P.shadowRec, sOut);
 }
 #ifndef HPT_SHADE_WAVES
 #define HPT_SHADE_WAVES 0 /* 0: natural allocation (100 VGPRs = 5 waves/SIMD) */
@@ -2600,27 +2639,28 @@ extern "C" __global__ __launch_bounds__(HPT_SHADE_BLOCK) void k_shade_multi(HptS
 }
 
 /* continuation result: path.cpp:225-286; true when the path goes on */
-/* REC: bsdf weight, throughput and state from the post record (rec0 / rec1, k_post) instead of
-   by path (k_tail) */
+/* REC (k_post): the path from its post record rec[0..3], and a survivor's throughput and
+   state go to sOut[2] of its next shade record (sOut[0..1] = the traced ray = rec[0..1]);
+   k_tail (REC false) keeps everything by path */
 template <bool REC = false>
 HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, bool hit, uint32_t *__restrict__ counters,
-                 float4 rec0 = float4(), float4 rec1 = float4()) {
+                 const float4 *rec = nullptr, float4 *sOut = nullptr) {
     bool alive = false;
     {
-        uint32_t st = REC ? __float_as_uint(rec1.w) : P.state[id];
+        uint32_t st = REC ? __float_as_uint(rec[3].w) : P.state[id];
         uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st), type = (st >> 24) & 0x7fu;
         const bool scattered = (st >> 31) != 0;
-        float4 bw = REC ? rec0 : P.bw[id], thr = REC ? rec1 : P.thr[id];
+        float4 bw = REC ? rec[2] : P.bw[id], thr = REC ? rec[3] : P.thr[id];
         V3 T = v3(thr.x, thr.y, thr.z);
         bool done = false, hitEmitter = false;
         V3 value = v3(0, 0, 0);
         V3 d = v3(0, 0, 0);
         if (!hit) {
-            const float4 rd = P.rd[id]; /* the direction matters only for a miss */
+            const float4 rd = REC ? rec[1] : P.rd[id]; /* the direction matters only for a miss */
             d = v3(rd.x, rd.y, rd.z);
             /* path.cpp:238-240: only a pass-through (ENull) chain from the camera is unscattered */
             value = envEval(sc.env, d);
-            float4 ro = P.ro[id];
+            float4 ro = REC ? rec[0] : P.ro[id];
             float nearT, farT;
             if ((sc.hideEmitters && !scattered) ||
                 !bsphereIntersect(sc.env, v3(ro.x, ro.y, ro.z), d, nearT, farT) || nearT > 0 || farT < 0) {
@@ -2645,14 +2685,22 @@ HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, bool hit, uint32_
                     alive = false;
                 } else if ((int) depth >= sc.rrDepth) {
                     float q = fminr(maxc(T) * 1.0f * 1.0f, 0.95f);
-                    float u = sobolSampleUniform(sc, P.sobol[id], dim);
+                    const uint64_t sidx =
+                        REC ? ((uint64_t) __float_as_uint(rec[1].w) << 32) | __float_as_uint(rec[0].w) : P.sobol[id];
+                    float u = sobolSampleUniform(sc, sidx, dim);
                     dim += 1;
                     if (u >= q) alive = false;
                     else T = divs(T, q);
                 }
                 depth += 1;
-                P.thr[id] = make_float4(T.x, T.y, T.z, 0.0f);
-                P.state[id] = hptState(st, depth, dim);
+                if (REC) {
+                    sOut[0] = rec[0];
+                    sOut[1] = rec[1];
+                    sOut[2] = make_float4(T.x, T.y, T.z, __uint_as_float(hptState(st, depth, dim)));
+                } else {
+                    P.thr[id] = make_float4(T.x, T.y, T.z, 0.0f);
+                    P.state[id] = hptState(st, depth, dim);
+                }
             }
         }
     }
@@ -2669,13 +2717,16 @@ extern "C" __global__ __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc,
     bool alive = false;
     uint32_t id = 0;
     uint32_t seg = HPT_MISS;
+    float4 rec[4], sOut[3];
     if (tid < n) {
         id = traceQ[tid];
         seg = P.hitQ[tid];
-        alive = postPath<true>(sc, P, id, seg != HPT_MISS, counters, P.postRec[2 * tid], P.postRec[2 * tid + 1]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rec[i] = P.postRec[4 * tid + i];
+        alive = postPath<true>(sc, P, id, seg != HPT_MISS, counters, rec, sOut);
     }
-    /* the survivors' hit records travel with the shade queue, in its order */
-    qpushBlock2<HPT_POST_BLOCK>(alive, id, shadeQ, seg, P.hitS, nShade);
+    /* the survivors' shade records and hit records travel with the shade queue, in its order */
+    qpushBlockRec<HPT_POST_BLOCK, 3>(alive, id, shadeQ, nShade, P.shadeRec, sOut, P.hitS, seg);
 }
 
 /* Tail of the frame (few live paths left, after Russian roulette has
@@ -2712,7 +2763,7 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
     uint32_t id = 0, nb = 0, hitRec = 0;
     bool live = false, exhausted = false;
     TraceCounters tc;
-    PathIO io{P, nullptr, nullptr, 0, 0, 0, false, nullptr};
+    PathIO io{P, nullptr, nullptr, 0, 0, 0, false, nullptr, false};
 #ifdef HPT_TAIL_PROFILE
     uint32_t rounds = 0;
     unsigned long long pIt = 0, pS = 0, pT = 0, pP = 0, pR = 0, pItems = 0;
@@ -2747,6 +2798,13 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
             if (!live && (lane >> 1) < T.pairs && j < total) { /* exactly the pairs counted in freeM */
                 id = T.shadeQ[j];
                 hitRec = P.hitS[j];
+                if (!odd) { /* the shade record to the by-path arrays k_tail works on */
+                    const float4 a = P.shadeRec[3 * j], b = P.shadeRec[3 * j + 1], c = P.shadeRec[3 * j + 2];
+                    P.ro[id] = make_float4(a.x, a.y, a.z, kEpsilon);
+                    P.rd[id] = make_float4(b.x, b.y, b.z, finf());
+                    P.thr[id] = make_float4(c.x, c.y, c.z, 0.0f);
+                    P.state[id] = __float_as_uint(c.w);
+                }
                 live = true;
 #ifdef HPT_TAIL_PROFILE
                 pItems += odd ? 0u : 1u;
@@ -2764,8 +2822,7 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
         bool cont = false, shadow = false;
         if (live && !odd) {
             ++nb;
-            float4 rec0, rec1;
-            shadePath<MULTI>(sc, P, id, hitRec, counters, cont, shadow, rec0, rec1);
+            shadePath<MULTI>(sc, P, id, hitRec, counters, cont, shadow, nullptr, nullptr, nullptr);
         }
         __threadfence_block(); /* the continuation ray is in HBM for the odd lane */
         const int f = __shfl((cont ? 1 : 0) | (shadow ? 2 : 0), (int) partner);
