@@ -2798,11 +2798,13 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
             if (!live && (lane >> 1) < T.pairs && j < total) { /* exactly the pairs counted in freeM */
                 id = T.shadeQ[j];
                 hitRec = P.hitS[j];
-                if (!odd) { /* the shade record to the by-path arrays k_tail works on */
+                /* the shade record to the by-path arrays k_tail works on (both lanes of the
+                   pair store the same values) */
+                {
                     const float4 a = P.shadeRec[3 * j], b = P.shadeRec[3 * j + 1], c = P.shadeRec[3 * j + 2];
-                    P.ro[id] = make_float4(a.x, a.y, a.z, kEpsilon);
-                    P.rd[id] = make_float4(b.x, b.y, b.z, finf());
-                    P.thr[id] = make_float4(c.x, c.y, c.z, 0.0f);
+                    P.ro[id] = a;
+                    P.rd[id] = b;
+                    P.thr[id] = c;
                     P.state[id] = __float_as_uint(c.w);
                 }
                 live = true;
