@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -51,9 +52,37 @@ static bool defaultPackets() {
     return v ? std::atoi(v) != 0 : true;
 }
 
+/* device-side bounce control (launch a wave's bounces ahead without reading queue lengths
+   back); HPT_BOUNCE_AHEAD=0 reads every bounce's queue length on the host */
+static bool defaultBounceAhead() {
+    const char *v = std::getenv("HPT_BOUNCE_AHEAD");
+    return v ? std::atoi(v) != 0 : true;
+}
+
+/* the bounce schedule of a wave of paths: the shade-queue length of each wavefront bounce,
+   and whether a k_tail launch took the rest */
+struct BounceSchedule {
+    std::vector<uint32_t> shade;
+    bool tail = false;
+};
+
+/* test hook: HPT_SCHEDULE_TEST=1 records schedules with half the queue lengths (the bounces
+   launched ahead outgrow their grids: the wave is rendered again), =2 ends them one wavefront
+   bounce early (the tail launched ahead finds too many live paths and leaves the bounce to
+   k_shade: the host goes on bounce by bounce) */
+static int scheduleTestHook() {
+    const char *v = std::getenv("HPT_SCHEDULE_TEST");
+    return v ? std::atoi(v) : 0;
+}
+
 struct hpt_context {
     int device = 0;
     uint32_t tailPaths = defaultTailPaths();
+    bool bounceAhead = defaultBounceAhead();
+    int scheduleTest = scheduleTestHook();
+    /* schedules of the waves rendered since the last prepare, by (spp begin, spp count,
+       shard, shards): a repeated wave launches its bounces ahead on that schedule */
+    std::map<std::array<int64_t, 4>, BounceSchedule> schedules;
     uint32_t maxLeafRounds = HPT_MAX_LEAF_ROUNDS, maxRestarts = HPT_MAX_RESTARTS; /* traversal bounds */
     uint32_t packetStack = 0;      /* 0 = the kernel's packet stack depth */
     bool packets = defaultPackets();
@@ -796,6 +825,7 @@ int hpt_prepare(hpt_context *c) {
     c->sc.maxLeafRounds = c->maxLeafRounds;
     c->sc.maxRestarts = c->maxRestarts;
     c->sc.packetStack = c->packetStack;
+    c->schedules.clear();
     c->prepared = true;
     return HPT_OK;
 }
@@ -1070,51 +1100,103 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             return hpt_launch_primary(sc, c->P, c->qTrace, C + HPT_C_TRACE(0), c->qShade[1], C + HPT_C_SHADE(1), w.nPaths, s);
         });
         if (e) break;
-        /* bounce b (parity p): shade -> trace -> clear -> post, one host sync per bounce for
-           the queue length (grid sizes, the switch to k_tail) */
-        int bounce = 0;
-        for (int b = 1; e == hipSuccess; ++b) {
-            const uint32_t p = (uint32_t) b & 1u, q = p ^ 1u;
-            e = hipMemcpyAsync(hostCnt, C, HPT_Q_COUNT * 4, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e) break;
-            const uint32_t n = hostCnt[HPT_C_SHADE(p)];
-            if (n == 0) break;
-            ++bounce;
-            if (n < c->tailPaths) {
-                /* few live paths: finish them all in one launch (k_tail) */
-                e = timed(5, [&] { return hpt_launch_tail(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), C, n, s); });
-                if (e) break;
-                e = hipMemcpyAsync(hostCnt, C, HPT_Q_COUNT * 4, hipMemcpyDeviceToHost, s);
-                if (e == hipSuccess) e = hipStreamSynchronize(s);
-                if (e) break;
-                bounces += hostCnt[HPT_C_TAIL_BOUNCES]; /* k_tail counts its first bounce too */
-                c->stats.tail_paths += n;
-                break;
-            }
-            bounces += n;
-            e = timed(2, [&] {
-                return hpt_launch_shade(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), c->qTrace, C + HPT_C_TRACE(p), c->qShadow,
-                                        C + HPT_C_SHADOW(p), C, n, s);
+        /* bounce b (parity p): shade -> trace -> clear -> post.  A wave whose schedule is known
+           (the same spp range and shard rendered since the last prepare) launches its bounces
+           ahead, each kernel reading its queue length on the device, and the k_tail launch
+           that ended it; the device decides whether the tail takes its bounce (the queue is
+           shorter than tailPaths) or leaves it to k_shade.  The host reads the counters back
+           once, at the end of the schedule, and goes on bounce by bounce from there if paths
+           are still live -- a schedule that does not fit costs launches, never paths.  A wave
+           without a schedule reads each bounce's queue length back (grid sizes, the switch
+           to k_tail) and records its schedule. */
+        const std::array<int64_t, 4> key{(int64_t) w.sppBegin, (int64_t) w.nSpp, shard, nShards};
+        auto known = c->schedules.find(key);
+        bool ahead = c->bounceAhead && !perLaunch && !bounceReport && known != c->schedules.end();
+        const bool learn = c->bounceAhead && !ahead;
+        BounceSchedule seen;
+        int b = 1, bounce = 0;
+        auto wavefrontBounce = [&](uint32_t p, uint64_t grid, uint32_t tailFrom) -> hipError_t {
+            const uint32_t q = p ^ 1u;
+            hipError_t e1 = timed(2, [&] {
+                return hpt_launch_shade(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), c->qTrace, C + HPT_C_TRACE(p),
+                                        c->qShadow, C + HPT_C_SHADOW(p), C, grid, tailFrom, s);
             });
-            if (e) break;
-            e = timed(-1, [&] {
+            if (e1) return e1;
+            e1 = timed(-1, [&] {
                 return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(p), C + HPT_C_SHADOW(p), cur, dst,
-                                        2ull * n, s);
+                                        2ull * grid, s);
             });
-            if (e) break;
+            if (e1) return e1;
             reportLaunch("bounce");
             if (bounceReport && st && !evTrace.empty()) {
                 float ms = 0;
                 (void) hipStreamSynchronize(s);
                 (void) hipEventElapsedTime(&ms, evTrace.back().first, evTrace.back().second);
-                std::fprintf(stderr, "[bounce %d] shade %u -> trace %.3f ms\n", b, n, ms);
+                std::fprintf(stderr, "[bounce %d] shade %llu -> trace %.3f ms\n", b, (unsigned long long) grid, ms);
             }
-            e = hpt_launch_clear(C, p, s);
-            if (e) break;
-            e = timed(3, [&] {
-                return hpt_launch_post(sc, c->P, c->qTrace, C + HPT_C_TRACE(p), c->qShade[q], C + HPT_C_SHADE(q), C, n, s);
+            e1 = hpt_launch_clear(C, p, s);
+            if (e1) return e1;
+            return timed(3, [&] {
+                return hpt_launch_post(sc, c->P, c->qTrace, C + HPT_C_TRACE(p), c->qShade[q], C + HPT_C_SHADE(q), C, grid, s);
             });
+        };
+        if (ahead) {
+            const BounceSchedule &k = known->second;
+            for (size_t i = 0; i < k.shade.size() && e == hipSuccess; ++i, ++b)
+                e = wavefrontBounce((uint32_t) b & 1u, k.shade[i], 0u);
+            if (e == hipSuccess && k.tail)
+                e = timed(5, [&] {
+                    const uint32_t p = (uint32_t) b & 1u;
+                    return hpt_launch_tail(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), C, HPT_ITEMS_ON_DEVICE,
+                                           c->tailPaths, s);
+                });
+            if (e) break;
+        }
+        for (; e == hipSuccess; ++b) {
+            const uint32_t p = (uint32_t) b & 1u;
+            e = hipMemcpyAsync(hostCnt, C, HPT_Q_COUNT * 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e) break;
+            const uint32_t n = hostCnt[HPT_C_SHADE(p)];
+            if (n == 0 || hostCnt[HPT_C_TAIL_PATHS] != 0) break; /* no live path, or k_tail took the rest */
+            if (ahead) c->schedules.erase(key), ahead = false;    /* the schedule did not fit: re-record */
+            if (n < c->tailPaths) {
+                /* few live paths: finish them all in one launch (k_tail) */
+                seen.tail = true;
+                e = timed(5, [&] { return hpt_launch_tail(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), C, n, ~0u, s); });
+                if (e) break;
+                e = hipMemcpyAsync(hostCnt, C, HPT_Q_COUNT * 4, hipMemcpyDeviceToHost, s);
+                if (e == hipSuccess) e = hipStreamSynchronize(s);
+                break;
+            }
+            seen.shade.push_back(n);
+            e = wavefrontBounce(p, n, 0u);
+        }
+        if (e) break;
+        if (hostCnt[HPT_C_OVERFLOW]) {
+            /* a bounce launched ahead had more live paths than its schedule's grid: drop the
+               schedule and render the wave again, reading every queue length back (the
+               film takes a wave's paths only at its gather) */
+            c->schedules.erase(key);
+            c->stats.waves--;
+            c->stats.schedule_misses++;
+            j0 -= (int) nSpp;
+            continue;
+        }
+        if (learn) {
+            if (c->scheduleTest == 1)
+                for (auto &n : seen.shade) n = std::max<uint32_t>(1, n / 2);
+            if (c->scheduleTest == 2 && seen.tail && !seen.shade.empty()) seen.shade.pop_back();
+            c->schedules[key] = seen;
+        }
+        if (ahead) c->stats.waves_ahead++;
+        /* the wave's bounce statistics, counted on the device */
+        {
+            uint64_t shaded = 0;
+            std::memcpy(&shaded, hostCnt + HPT_C_BOUNCES, 8);
+            bounces += shaded + hostCnt[HPT_C_TAIL_BOUNCES]; /* k_tail counts its first bounce too */
+            c->stats.tail_paths += hostCnt[HPT_C_TAIL_PATHS];
+            bounce = (int) hostCnt[HPT_C_LAUNCHES];
         }
         maxB = std::max(maxB, bounce);
         if (e) break;

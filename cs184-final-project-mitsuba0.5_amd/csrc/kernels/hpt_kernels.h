@@ -14,6 +14,10 @@
 #define HPT_C_TRACE(p) (0 + (p))  /* closest-hit rays of bounce b (traceQ[p]) */
 #define HPT_C_SHADOW(p) (2 + (p)) /* shadow rays of bounce b (shadowQ[p]) */
 #define HPT_C_SHADE(p) (4 + (p))  /* paths bounce b shades (shadeQ[p]: survivors of the previous post) */
+#define HPT_C_BOUNCES 6      /* u64 (words 6-7): path-bounces shaded by k_shade */
+#define HPT_C_LAUNCHES 8     /* bounces that shaded live paths (k_shade or k_tail launches with work) */
+#define HPT_C_TAIL_PATHS 9   /* paths k_tail took over */
+#define HPT_C_OVERFLOW 10    /* a k_shade grid (sized from a schedule) was shorter than its queue */
 #define HPT_C_ERROR 12       /* set when a path runs out of Sobol dimensions */
 #define HPT_C_TAIL_BOUNCES 13 /* path-bounces shaded inside k_tail */
 #define HPT_C_TAIL_CURSOR 14  /* k_tail's work claims */
@@ -109,14 +113,19 @@ hipError_t hpt_launch_trace_overflow(const HptScene &sc, const HptPaths &P, cons
                                      const uint32_t *nOverflow, uint32_t *cursors, uint64_t maxItems, hipStream_t s);
 hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
                               uint32_t *shadeQ, uint32_t *nShade, uint64_t maxItems, hipStream_t s);
+/* tailFrom: the launch leaves a queue shorter than this to the tail launch of the same
+   bounce (0: always shade); a queue longer than the grid (maxItems) sets HPT_C_OVERFLOW */
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
                             uint32_t *traceQ, uint32_t *nTrace, uint32_t *shadowQ, uint32_t *nShadow, uint32_t *counters,
-                            uint64_t maxItems, hipStream_t s);
+                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s);
 hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
                            uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s);
-/* the rest of every live path (the shade queue) to termination in one launch */
+/* the rest of every live path (the shade queue) to termination in one launch, when the queue
+   is shorter than tailFrom (~0u: always); items = HPT_ITEMS_ON_DEVICE when the host has not
+   read the queue length (the launch then sizes its work from it on the device) */
+#define HPT_ITEMS_ON_DEVICE (~0ull)
 hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
-                           uint32_t *counters, uint64_t items, hipStream_t s);
+                           uint32_t *counters, uint64_t items, uint32_t tailFrom, hipStream_t s);
 hipError_t hpt_launch_clear(uint32_t *counters, uint32_t parity, hipStream_t s);
 /* k_splat + k_gather; partial = (nPaths / nSpp) * 9 float4 of scratch */
 hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *partial, float4 *film,

@@ -2598,13 +2598,22 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
 struct HptShadeIO {
     const uint32_t *nShade;
     uint32_t *nTrace, *nShadow, *counters;
+    uint32_t tailFrom; /* a queue shorter than this is k_tail's (device-side bounce control); 0: always shade */
 };
 template <bool MULTI>
 __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
                                             uint32_t *__restrict__ traceQ, uint32_t *__restrict__ shadowQ,
                                             const HptShadeIO &q) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = *q.nShade;
+    const uint32_t n0 = *q.nShade;
+    const uint32_t n = n0 < q.tailFrom ? 0u : n0; /* a short queue is the tail launch's bounce */
+    if (blockIdx.x == 0 && threadIdx.x == 0 && n != 0) {
+        atomicAdd((unsigned long long *) (q.counters + HPT_C_BOUNCES), (unsigned long long) n);
+        atomicAdd(&q.counters[HPT_C_LAUNCHES], 1u);
+        /* a grid sized from a schedule (bounces launched ahead) that is too small for the queue:
+           the host renders the wave again, reading every queue length back */
+        if (n > gridDim.x * blockDim.x) atomicOr(&q.counters[HPT_C_OVERFLOW], 1u);
+    }
     bool cont = false, shadow = false;
     uint32_t id = 0;
     float4 in[3], cOut[4], sOut[3];
@@ -2713,7 +2722,7 @@ extern "C" __global__ __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc,
                                                           uint32_t *__restrict__ shadeQ, uint32_t *__restrict__ nShade,
                                                           uint32_t *__restrict__ counters) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t n = *nTrace;
+    const uint32_t n = *nTrace; /* <= the bounce's shade queue, which k_shade checked against the grid */
     bool alive = false;
     uint32_t id = 0;
     uint32_t seg = HPT_MISS;
@@ -2745,7 +2754,8 @@ extern "C" __global__ __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc,
    round trips, not a bandwidth problem. */
 struct HptTail {
     const uint32_t *shadeQ, *nShade;
-    uint32_t pairs; /* lane pairs per wave that take paths (1..32) */
+    uint32_t pairs;    /* lane pairs per wave that take paths (1..32); 0: from the queue length, on the device */
+    uint32_t tailFrom; /* the launch takes the queue only when it is shorter than this (device-side bounce control) */
 };
 #ifdef HPT_TAIL_PROFILE
 /* timing instrumentation of k_tail (experiment builds only: make variant KFLAGS=-DHPT_TAIL_PROFILE):
@@ -2759,7 +2769,18 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
                                           uint32_t *__restrict__ counters, uint2 *stk) {
     const uint32_t lane = __lane_id(), partner = lane & ~1u;
     const bool odd = (lane & 1u) != 0;
-    const uint32_t total = *T.nShade;
+    const uint32_t n0 = *T.nShade;
+    const uint32_t total = n0 < T.tailFrom ? n0 : 0u;
+    /* nothing to take (k_shade has the bounce, or no path is live): leave the claim cursor
+       alone for a later tail launch of the same wave of paths */
+    if (total == 0) return;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        atomicAdd(&counters[HPT_C_TAIL_PATHS], total);
+        atomicAdd(&counters[HPT_C_LAUNCHES], 1u);
+    }
+    /* pairs per wave: the fewest that still cover the work in one residency of this grid */
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    const uint32_t pairs = T.pairs ? T.pairs : min(32u, max(1u, (total + waves - 1) / waves));
     uint32_t id = 0, nb = 0, hitRec = 0;
     bool live = false, exhausted = false;
     TraceCounters tc;
@@ -2784,10 +2805,10 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
     };
     while (true) {
         /* free pairs claim the next items (the even lane's rank, shared with the odd lane) */
-        /* only the first T.pairs pairs of a wave take paths: a wave waits each bounce for
+        /* only the first `pairs` pairs of a wave take paths: a wave waits each bounce for
            its slowest ray, and the fewer paths share a wave, the shorter that wait is
            (the host spreads few paths thinly over the resident waves) */
-        const uint64_t freeM = __ballot(!live && !odd && (lane >> 1) < T.pairs);
+        const uint64_t freeM = __ballot(!live && !odd && (lane >> 1) < pairs);
         if (!exhausted && freeM != 0) {
             uint32_t base = 0;
             if (lane == 0) base = atomicAdd(&counters[HPT_C_TAIL_CURSOR], (uint32_t) __popcll(freeM));
@@ -2795,7 +2816,7 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
             if (base + (uint32_t) __popcll(freeM) >= total) exhausted = true;
             const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t) (freeM >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) freeM, 0u));
             const uint32_t j = __shfl(base + rk, (int) partner);
-            if (!live && (lane >> 1) < T.pairs && j < total) { /* exactly the pairs counted in freeM */
+            if (!live && (lane >> 1) < pairs && j < total) { /* exactly the pairs counted in freeM */
                 id = T.shadeQ[j];
                 hitRec = P.hitS[j];
                 /* the shade record to the by-path arrays k_tail works on (both lanes of the
@@ -3273,9 +3294,9 @@ hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint3
 }
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
                             uint32_t *traceQ, uint32_t *nTrace, uint32_t *shadowQ, uint32_t *nShadow, uint32_t *counters,
-                            uint64_t maxItems, hipStream_t s) {
+                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
-    const HptShadeIO q{nShade, nTrace, nShadow, counters};
+    const HptShadeIO q{nShade, nTrace, nShadow, counters, tailFrom};
     if (sc.nShapes > 1)
         hipLaunchKernelGGL(k_shade_multi, dim3(blocksFor(maxItems, HPT_SHADE_BLOCK)), dim3(HPT_SHADE_BLOCK), 0, s, sc, P, shadeQ,
                            traceQ, shadowQ, q);
@@ -3292,15 +3313,21 @@ hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t
     return hipGetLastError();
 }
 hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
-                           uint32_t *counters, uint64_t items, hipStream_t s) {
+                           uint32_t *counters, uint64_t items, uint32_t tailFrom, hipStream_t s) {
     if (items == 0) return hipSuccess;
     /* two lanes per path; persistent (pairs claim paths).  Paths are spread over all resident
-       waves: K pairs per wave, the fewest that still cover the work in one residency */
+       waves: K pairs per wave, the fewest that still cover the work in one residency.  With
+       items = HPT_ITEMS_ON_DEVICE the host has not read the queue length: the whole resident
+       grid is launched and K comes from the length on the device (the same K, the same
+       number of waves with work) */
     const void *kern = sc.nShapes > 1 ? (const void *) k_tail_multi : (const void *) k_tail;
-    const uint64_t residentWaves = (uint64_t) persistentBlocks(kern, ~0ull >> 8) * (HPT_TRACE_BLOCK / 64);
-    const uint32_t K = (uint32_t) std::min<uint64_t>(32, std::max<uint64_t>(1, (items + residentWaves - 1) / residentWaves));
-    const HptTail T{shadeQ, nShade, K};
-    const unsigned blocks = persistentBlocks(kern, (items + K - 1) / K * 64);
+    const unsigned residentBlocks = persistentBlocks(kern, ~0ull >> 8);
+    const uint64_t residentWaves = (uint64_t) residentBlocks * (HPT_TRACE_BLOCK / 64);
+    const uint32_t K = items == HPT_ITEMS_ON_DEVICE
+                           ? 0u
+                           : (uint32_t) std::min<uint64_t>(32, std::max<uint64_t>(1, (items + residentWaves - 1) / residentWaves));
+    const HptTail T{shadeQ, nShade, K, tailFrom};
+    const unsigned blocks = K ? persistentBlocks(kern, (items + K - 1) / K * 64) : residentBlocks;
     if (sc.nShapes > 1)
         hipLaunchKernelGGL(k_tail_multi, dim3(blocks), dim3(HPT_TRACE_BLOCK), 0, s, sc, P, T, counters);
     else

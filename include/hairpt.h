@@ -191,6 +191,10 @@ typedef struct hpt_stats {
     /* counted frames: binary kd-node visits of k_trace (inner nodes entered + leaves, the count of
        rayIntersectHavran, sahkdtree3.h:178-308; `nodes` counts the two-level HptNode4 fetches) */
     uint64_t binary_nodes;
+    /* device-side bounce control: waves whose bounces were launched ahead on the schedule of an
+       earlier render of the same spp range and shard (no queue length read back per bounce), and
+       waves rendered again because a bounce outgrew its schedule (HPT_BOUNCE_AHEAD=0: neither) */
+    uint64_t waves_ahead, schedule_misses;
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 
