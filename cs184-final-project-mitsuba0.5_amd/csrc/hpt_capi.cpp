@@ -1187,6 +1187,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             if (c->scheduleTest == 1)
                 for (auto &n : seen.shade) n = std::max<uint32_t>(1, n / 2);
             if (c->scheduleTest == 2 && seen.tail && !seen.shade.empty()) seen.shade.pop_back();
+            if (c->schedules.size() >= 4096) c->schedules.clear(); /* e.g. a long run of -r passes */
             c->schedules[key] = seen;
         }
         if (ahead) c->stats.waves_ahead++;
