@@ -1111,7 +1111,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
            to k_tail) and records its schedule. */
         const std::array<int64_t, 4> key{(int64_t) w.sppBegin, (int64_t) w.nSpp, shard, nShards};
         auto known = c->schedules.find(key);
-        bool ahead = c->bounceAhead && !perLaunch && !bounceReport && known != c->schedules.end();
+        const bool ahead = c->bounceAhead && !perLaunch && !bounceReport && known != c->schedules.end();
+        bool fits = true; /* the schedule launched ahead was the whole wave */
         const bool learn = c->bounceAhead && !ahead;
         BounceSchedule seen;
         int b = 1, bounce = 0;
@@ -1159,7 +1160,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             if (e) break;
             const uint32_t n = hostCnt[HPT_C_SHADE(p)];
             if (n == 0 || hostCnt[HPT_C_TAIL_PATHS] != 0) break; /* no live path, or k_tail took the rest */
-            if (ahead) c->schedules.erase(key), ahead = false;    /* the schedule did not fit: re-record */
+            if (ahead && fits) c->schedules.erase(key), fits = false; /* the schedule did not fit: re-record */
             if (n < c->tailPaths) {
                 /* few live paths: finish them all in one launch (k_tail) */
                 seen.tail = true;
@@ -1173,6 +1174,10 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             e = wavefrontBounce(p, n, 0u);
         }
         if (e) break;
+        if (hostCnt[HPT_C_OVERFLOW] && !ahead) {
+            (void) hipStreamSynchronize(s);
+            return setErr(c, HPT_EDEVICE, "internal error: a shade grid sized from its read-back queue overflowed");
+        }
         if (hostCnt[HPT_C_OVERFLOW]) {
             /* a bounce launched ahead had more live paths than its schedule's grid: drop the
                schedule and render the wave again, reading every queue length back (the
@@ -1190,7 +1195,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             if (c->schedules.size() >= 4096) c->schedules.clear(); /* e.g. a long run of -r passes */
             c->schedules[key] = seen;
         }
-        if (ahead) c->stats.waves_ahead++;
+        if (ahead && fits) c->stats.waves_ahead++;
         /* the wave's bounce statistics, counted on the device */
         {
             uint64_t shaded = 0;

@@ -2612,7 +2612,7 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
         atomicAdd(&q.counters[HPT_C_LAUNCHES], 1u);
         /* a grid sized from a schedule (bounces launched ahead) that is too small for the queue:
            the host renders the wave again, reading every queue length back */
-        if (n > gridDim.x * blockDim.x) atomicOr(&q.counters[HPT_C_OVERFLOW], 1u);
+        if ((uint64_t) n > (uint64_t) gridDim.x * blockDim.x) atomicOr(&q.counters[HPT_C_OVERFLOW], 1u);
     }
     bool cont = false, shadow = false;
     uint32_t id = 0;
