@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--all-ranks", action="store_true", help="time every rank of each N (default: rank 0 and the slowest of a sample)")
     ap.add_argument("--ns", default="2,4,8", help="shard counts to time (besides N=1)")
+    ap.add_argument("--split", choices=["blocks", "spp"], default="blocks",
+                    help="rank r of N: its Hilbert-cyclic blocks (bench.py) or spp range [r*spp/N, (r+1)*spp/N) of every pixel")
     a = ap.parse_args()
     cfg = scenes.CONFIGS[a.config]
     xml = scenes.make_scene(a.config, os.path.join(tempfile.gettempdir(), "hpt_shards"), n_strands=cfg["n"])
@@ -43,7 +45,10 @@ def main():
         for _ in range(a.reps):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            r.render_device(film.data_ptr(), 0, spp, shard=shard, n_shards=n, collect_stats=1)
+            if a.split == "spp":
+                r.render_device(film.data_ptr(), shard * spp // n, (shard + 1) * spp // n, collect_stats=1)
+            else:
+                r.render_device(film.data_ptr(), 0, spp, shard=shard, n_shards=n, collect_stats=1)
             torch.cuda.synchronize()
             best = min(best, time.perf_counter() - t0)
         return best, r.stats()
