@@ -62,9 +62,10 @@ def parse():
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-spp", type=int, default=96, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--cpu-threads", type=int, default=0,
-                    help="0 = every CPU this process may run on (nproc, SURVEY.md 8(d))")
-    ap.add_argument("--cpu-share-threads", type=int, default=16,
-                    help="also time the sample on this many threads (the GPU box's CPU share per GPU); 0 = skip")
+                    help="0 = the CPUs this process can actually use: min(affinity CPUs, cgroup CPU quota)")
+    ap.add_argument("--cpu-nproc-run", choices=["auto", "off"], default="auto",
+                    help="also time the sample on one thread per affinity CPU (nproc, SURVEY.md 8(d)) when that "
+                         "differs from the effective CPUs")
     ap.add_argument("--workdir", default=os.path.join(tempfile.gettempdir(), "hpt_bench"))
     return ap.parse_args()
 
@@ -83,7 +84,16 @@ def cpu_baseline(args, cfg, xml_defines, hair_src, env_rgb, nodes, idx):
     o.set_kdtree(nodes, idx)
     o.prepare()
     avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    threads = args.cpu_threads if args.cpu_threads > 0 else avail
+    quota = None  # the cgroup's CPU bandwidth limit (cgroup v2 cpu.max "quota period"), in CPUs
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    # the CPUs the process can actually use: the affinity set, capped by the cgroup quota (on the
+    # GPU box 256 affinity CPUs share a 16-CPU quota: 256 threads are time-sliced onto 16)
+    effective = max(1, min(avail, int(quota))) if quota else avail
+    threads = args.cpu_threads if args.cpu_threads > 0 else effective
     paths = W * H * args.cpu_spp
 
     def timed(n_threads):
@@ -92,29 +102,26 @@ def cpu_baseline(args, cfg, xml_defines, hair_src, env_rgb, nodes, idx):
         return time.perf_counter() - t0
 
     dt = timed(threads)
-    share = None
-    if args.cpu_share_threads > 0 and args.cpu_share_threads < threads:
-        ds = timed(args.cpu_share_threads)
-        share = {"value": paths / ds / 1e6, "cores": args.cpu_share_threads,
-                 "note": "the same sample on the GPU box's 16-CPU share per GPU"}
+    nproc_run = None
+    if args.cpu_nproc_run == "auto" and avail != threads:
+        dn = timed(avail)
+        nproc_run = {"value": paths / dn / 1e6, "threads": avail,
+                     "note": "one worker per affinity CPU (nproc, like mitsuba.cpp:135,281), time-sliced onto "
+                             "the cgroup quota"}
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
             model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), model)
     except OSError:
         pass
-    quota = None  # the cgroup's CPU bandwidth limit (cgroup v2 cpu.max "quota period"), in CPUs
-    try:
-        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        quota = None if q == "max" else round(int(q) / int(per), 2)
-    except (OSError, ValueError):
-        pass
-    return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": threads, "kind": "port",
-            "cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": avail, "cgroup_cpu_quota": quota,
-            "threads_note": "one worker thread per CPU this process may run on (nproc), like mitsuba.cpp:135,281",
-            "cpu_share": share,
+    return {"value": paths / dt / 1e6, "unit": "Mpaths/s", "cores": min(threads, effective), "threads": threads,
+            "kind": "port", "cpu_model": model, "host_cpus": os.cpu_count(), "affinity_cpus": avail,
+            "cgroup_cpu_quota": quota,
+            "cores_note": "cores = the CPUs the run could use, min(threads, affinity CPUs, cgroup quota)",
+            "nproc_run": nproc_run,
             "sample": "%dx%d @ %d spp of the same scene (%d paths), %.2f s, liboracle_ref.so "
-                      "(-O3 -march=nocona -msse2 -funsafe-math-optimizations, config-ubuntu-20.04.py:8)"
+                      "(-O3 -march=nocona -msse2 -funsafe-math-optimizations, config-ubuntu-20.04.py:8; "
+                      "the oracle adds -ftree-vectorize -ffp-contract=off and traverses the product's kd-tree)"
                       % (W, H, args.cpu_spp, paths, dt)}
 
 
@@ -217,6 +224,12 @@ def main():
             acc["kernels"][k] = acc["kernels"].get(k, 0.0) + getattr(s, "ms_" + k)
 
     dt = timed_steps(lambda: step(1), args.steps, world, dist, torch.cuda.synchronize, "cuda:%d" % local, collect)
+    # the same frame once more with no recorded bounce schedule (what a render of a new spp range
+    # or the CLI's first pass does: every bounce's queue length read back); not
+    # part of `value`, which times repeated frames of the same spp range
+    r.clear_schedules()
+    first_ms = 1e3 * timed_steps(lambda: step(1), 1, world, dist, torch.cuda.synchronize, "cuda:%d" % local)
+    assert r.stats().waves_ahead == 0
     ms_trace, ms_packet, launches, p_launches = acc["ms_trace"], acc["ms_packet"], acc["launches"], acc["p_launches"]
     ms_kernels = acc["kernels"]
     tot = {k: v * args.steps for k, v in frame.items()}
@@ -239,6 +252,16 @@ def main():
     bytes_pk_lane = io_pk + B8D_NODE * tot["p_nodes"] + (B8D_REF + B8D_PRIM) * tot["p_prims"]
     bytes_pk_lay = io_pk + BYTES_NODE2 * pk_node_steps + BYTES_PRIM * pk_prim_steps + BYTES_EXACT * tot["p_exact"]
     achieved_pk, achieved_pk_lay = gbs(bytes_pk, ms_packet), gbs(bytes_pk_lay, ms_packet)
+    # the whole frame on SURVEY.md 8(d)'s B_path: camera ray + state 40 B per path; per path-bounce
+    # the state queue read + write 2 x 80, the hit record 40, the BSDF's table reads (Marschner
+    # ~430 B, Kajiya-Kay 0) and NEE's envmap reads 108; per shadow ray its record 80; every
+    # traversal at 8 B per binary node + 56 B per primitive test (camera rays per lane); the film
+    # gather 9 x 16 B read + 16 B written per pixel
+    b_bsdf = 430 if "marschner" in args.config else 0
+    bytes_frame = (40 * paths_total + (2 * 80 + 40 + b_bsdf + 108) * tot["bounces"] + 80 * tot["shadow"]
+                   + bytes_alg - io + B8D_NODE * tot["p_nodes"] + (B8D_REF + B8D_PRIM) * tot["p_prims"]
+                   + (9 * 16 + 16) * W * H * args.steps)
+    achieved_frame = bytes_frame / dt / 1e9
     traffic, traffic_src, traffic_pk, limiter = None, None, None, None
     tj = os.path.join(ROOT, "profiles", "traffic_%s.json" % args.config)
     if os.path.exists(tj):
@@ -309,6 +332,17 @@ def main():
                                 "achieved_layout": round(achieved_pk_lay, 1),
                                 "avg_launch_ms": round(ms_packet / max(1, p_launches), 4),
                                 "launches": int(p_launches)},
+            # every kernel of the frame on the same byte model, over the whole timed step
+            "roofline_frame": {"bound": "hbm", "achieved": round(achieved_frame, 1), "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(achieved_frame / HBM_PEAK_GBS, 4),
+                               "bytes_per_step": int(bytes_frame // args.steps),
+                               "algorithmic_model": "SURVEY.md 8(d) B_path summed over the frame: camera 40 B/path; "
+                                                    "per path-bounce 2x80 state + 40 hit + BSDF tables (%d) + NEE 108; "
+                                                    "80 B per shadow ray; traversal 8 B/binary node, 56 B/primitive "
+                                                    "test (camera rays per lane); film 160 B/pixel" % b_bsdf},
+            # value times repeated frames of one spp range, whose bounces are launched ahead on the
+            # schedule recorded by the first render; this is that first render (one frame)
+            "first_render_ms": round(first_ms, 3),
             "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in ms_kernels.items()},
             "cpu_baseline": cpu,
             "stats": {"bounces_per_path": round(tot["bounces"] / max(1, paths_total / world), 4),

@@ -4,9 +4,12 @@
  * Mirrors src/mitsuba/mitsuba.cpp:52-400 for the hair path: parse options,
  * load each scene XML, render, develop the film and write it next to the
  * scene (or to -o).  Rendering runs on MI355X devices through libhairpt.so;
- * with --gpus N the 32x32 blocks are dealt over N devices (Hilbert-cyclic,
- * one host thread + one hpt_context each) and the per-device films are
- * summed -- the single-node analogue of the reference's -c remote workers.
+ * with --gpus N the scene is parsed, loaded and its kd-tree built ONCE and
+ * shared with N device contexts (hpt_context_share_scene, uploaded in
+ * parallel, like mitsuba.cpp:281-329 hands one scene to every worker); the
+ * 32x32 blocks are dealt over the devices (Hilbert-cyclic) and the films are
+ * combined on the first device over xGMI (hpt_render_multi) -- the
+ * single-node analogue of the reference's -c remote workers.
  * -r sec writes the partial image every `sec` seconds like the reference's
  * flush timer (mitsuba.cpp:300-330): the samples are rendered in chunks and
  * the film accumulated so far is developed between chunks.
@@ -18,6 +21,7 @@
  *     -b/-z/-v (accepted)
  *     --spp N --width W --height H --max-depth D   overrides
  *     --device i   first device                    --gpus N   devices to use
+ *     --devices a,b,...  explicit device of each shard (a device may repeat)
  *     --stats      print timing / traversal statistics
  */
 #include <chrono>
@@ -48,6 +52,7 @@ void usage() {
         "   -r sec      Write (partial) output images every 'sec' seconds\n"
         "   --spp N --width W --height H --max-depth D   override scene parameters\n"
         "   --device I --gpus N   render on N devices starting at I\n"
+        "   --devices a,b,...     the device of each shard (a device may repeat)\n"
         "   --stats     print per-kernel timing and traversal counters\n");
 }
 
@@ -57,6 +62,7 @@ struct Opts {
     bool quiet = false, skipExisting = false, stats = false;
     int spp = 0, width = 0, height = 0, maxDepth = -2, device = 0, gpus = 1;
     double flushSec = 0; /* -r */
+    std::vector<int> devices; /* --devices */
     std::vector<std::string> scenes;
 };
 
@@ -99,6 +105,17 @@ int main(int argc, char **argv) {
         else if (a == "--max-depth") o.maxDepth = std::atoi(next("--max-depth").c_str());
         else if (a == "--device") o.device = std::atoi(next("--device").c_str());
         else if (a == "--gpus") o.gpus = std::max(1, std::atoi(next("--gpus").c_str()));
+        else if (a == "--devices") {
+            const std::string list = next("--devices");
+            o.devices.clear();
+            for (size_t i = 0; i < list.size();) {
+                size_t j = list.find(',', i);
+                if (j == std::string::npos) j = list.size();
+                o.devices.push_back(std::atoi(list.substr(i, j - i).c_str()));
+                i = j + 1;
+            }
+            if (o.devices.empty()) { std::fprintf(stderr, "--devices needs a list\n"); return 1; }
+        }
         else if (a == "--stats") o.stats = true;
         else if (!a.empty() && a[0] == '-') { std::fprintf(stderr, "unknown option %s\n", a.c_str()); usage(); return 1; }
         else o.scenes.push_back(a);
@@ -136,47 +153,63 @@ int main(int argc, char **argv) {
             if (!o.quiet) std::printf("Skipping \"%s\": output exists\n", scene.c_str());
             continue;
         }
-        const int G = o.gpus;
+        std::vector<int> devs = o.devices;
+        if (devs.empty())
+            for (int g = 0; g < o.gpus; ++g) devs.push_back(o.device + g);
+        const int G = (int) devs.size();
         std::vector<hpt_context *> ctx(G, nullptr);
         int W = 0, H = 0, spp = 0;
-        for (int g = 0; g < G; ++g) {
-            int rc = hpt_context_create(o.device + g, &ctx[g]);
-            if (rc) { std::fprintf(stderr, "cannot create a gfx950 context on device %d (%d)\n", o.device + g, rc); return 3; }
-            rc = hpt_load_scene_xml(ctx[g], scene.c_str(), (int) keys.size(), keys.data(), vals.data());
-            if (rc) { std::fprintf(stderr, "%s\n", hpt_last_error(ctx[g])); return 2; }
+        /* the scene once: parse, hair, kd-tree, tables on the first device's context ... */
+        const auto tLoad = std::chrono::steady_clock::now();
+        {
+            int rc = hpt_context_create(devs[0], &ctx[0]);
+            if (rc) { std::fprintf(stderr, "cannot create a gfx950 context on device %d (%d)\n", devs[0], rc); return 3; }
+            rc = hpt_load_scene_xml(ctx[0], scene.c_str(), (int) keys.size(), keys.data(), vals.data());
+            if (rc) { std::fprintf(stderr, "%s\n", hpt_last_error(ctx[0])); return 2; }
             hpt_scene_info info;
-            hpt_get_scene_info(ctx[g], &info);
+            hpt_get_scene_info(ctx[0], &info);
             if (o.width || o.height || o.maxDepth != -2) {
                 /* re-issue the camera / integrator with overrides */
                 W = o.width ? o.width : info.width;
                 H = o.height ? o.height : info.height;
-                hpt_set_camera(ctx[g], desc.toWorld, desc.fov, W, H, desc.nearClip, desc.farClip);
-                hpt_set_integrator(ctx[g], o.maxDepth != -2 ? o.maxDepth : info.max_depth, info.rr_depth,
+                hpt_set_camera(ctx[0], desc.toWorld, desc.fov, W, H, desc.nearClip, desc.farClip);
+                hpt_set_integrator(ctx[0], o.maxDepth != -2 ? o.maxDepth : info.max_depth, info.rr_depth,
                                    info.strict_normals, info.hide_emitters);
             }
-            if (o.spp) hpt_set_sampler(ctx[g], o.spp);
-            rc = hpt_prepare(ctx[g]);
-            if (rc) { std::fprintf(stderr, "%s\n", hpt_last_error(ctx[g])); return 2; }
-            hpt_get_scene_info(ctx[g], &info);
+            if (o.spp) hpt_set_sampler(ctx[0], o.spp);
+            rc = hpt_prepare(ctx[0]);
+            if (rc) { std::fprintf(stderr, "%s\n", hpt_last_error(ctx[0])); return 2; }
+            hpt_get_scene_info(ctx[0], &info);
             W = info.width;
             H = info.height;
             spp = info.spp;
-            if (g == 0 && !o.quiet)
+            if (!o.quiet)
                 std::printf("Scene \"%s\": %dx%d @ %d spp, %llu hair segments, kd-tree %llu nodes (depth %d, %.2f s)\n",
                             scene.c_str(), W, H, spp, (unsigned long long) info.segments,
                             (unsigned long long) info.kd_nodes, info.kd_depth, info.kd_build_seconds);
         }
-        std::vector<std::vector<float>> films(G, std::vector<float>((size_t) W * H * 4, 0.0f));
-        std::vector<int> rcs(G, 0);
+        const double loadSec = std::chrono::duration<double>(std::chrono::steady_clock::now() - tLoad).count();
+        /* ... then uploaded to the other devices in parallel (no second parse or build) */
+        if (G > 1) {
+            const auto tShare = std::chrono::steady_clock::now();
+            std::vector<int> rcs(G, 0);
+            std::vector<std::thread> th;
+            for (int g = 1; g < G; ++g) th.emplace_back([&, g] { rcs[g] = hpt_context_share_scene(ctx[0], devs[g], &ctx[g]); });
+            for (auto &t : th) t.join();
+            for (int g = 1; g < G; ++g)
+                if (rcs[g]) { std::fprintf(stderr, "device %d: %s\n", devs[g], hpt_last_error(ctx[0])); return 3; }
+            if (!o.quiet)
+                std::printf("Scene loaded once (%.2f s) and shared with %d more device context%s (%.2f s)\n", loadSec,
+                            G - 1, G > 2 ? "s" : "",
+                            std::chrono::duration<double>(std::chrono::steady_clock::now() - tShare).count());
+        }
+        std::vector<float> film((size_t) W * H * 4, 0.0f);
         hpt_film_params fp;
         hpt_get_film_params(ctx[0], &fp);
         char written[4096];
-        /* film combine (renderproc.cpp:142-145) + develop (Film::develop) */
+        /* develop (Film::develop); the device films are combined by hpt_render_multi */
         auto develop = [&]() -> bool {
-            std::vector<float> sum((size_t) W * H * 4, 0.0f);
-            for (int g = 0; g < G; ++g)
-                for (size_t i = 0; i < sum.size(); ++i) sum[i] += films[g][i];
-            if (hpt_write_film(ctx[0], out.c_str(), sum.data(), W, H, &fp, written, sizeof(written))) {
+            if (hpt_write_film(ctx[0], out.c_str(), film.data(), W, H, &fp, written, sizeof(written))) {
                 std::fprintf(stderr, "%s\n", hpt_last_error(ctx[0]));
                 return false;
             }
@@ -187,21 +220,15 @@ int main(int argc, char **argv) {
         auto t0 = std::chrono::steady_clock::now(), lastFlush = t0;
         for (int j0 = 0; j0 < spp; j0 += chunk) {
             const int j1 = std::min(spp, j0 + chunk);
-            std::vector<std::thread> th;
-            for (int g = 0; g < G; ++g)
-                th.emplace_back([&, g] {
-                    hpt_render_params p;
-                    std::memset(&p, 0, sizeof(p));
-                    p.spp_begin = j0;
-                    p.spp_end = j1;
-                    p.shard = g;
-                    p.n_shards = G;
-                    p.collect_stats = o.stats ? 2 : 0;
-                    rcs[g] = hpt_render(ctx[g], &p, films[g].data());
-                });
-            for (auto &t : th) t.join();
-            for (int g = 0; g < G; ++g)
-                if (rcs[g]) { std::fprintf(stderr, "render failed on device %d: %s\n", o.device + g, hpt_last_error(ctx[g])); return 4; }
+            hpt_render_params p;
+            std::memset(&p, 0, sizeof(p));
+            p.spp_begin = j0;
+            p.spp_end = j1;
+            p.collect_stats = o.stats ? 2 : 0;
+            if (hpt_render_multi(ctx.data(), G, &p, film.data())) {
+                std::fprintf(stderr, "render failed: %s\n", hpt_last_error(ctx[0]));
+                return 4;
+            }
             const auto now = std::chrono::steady_clock::now();
             if (j1 < spp && o.flushSec > 0 && std::chrono::duration<double>(now - lastFlush).count() >= o.flushSec) {
                 if (!develop()) return 5;

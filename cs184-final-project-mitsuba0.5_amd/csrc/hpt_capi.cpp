@@ -23,6 +23,7 @@
 #include <fstream>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -59,6 +60,12 @@ static bool defaultBounceAhead() {
     return v ? std::atoi(v) != 0 : true;
 }
 
+/* claim-order buckets (hpt_kernels.h HPT_BUCKETS): bounce rays claimed longest first;
+   HPT_CLAIM_BUCKETS=0/1 overrides the default */
+static bool defaultClaimBuckets() {
+    const char *v = std::getenv("HPT_CLAIM_BUCKETS");
+    return v ? std::atoi(v) != 0 : false;
+}
 /* the bounce schedule of a wave of paths: the shade-queue length of each wavefront bounce,
    and whether a k_tail launch took the rest */
 struct BounceSchedule {
@@ -114,6 +121,8 @@ struct hpt_context {
     HptPaths P;
     /* rays of the bounce; paths to shade by bounce parity (shadeQ[p] is post's output for p ^ 1) */
     uint32_t *qTrace = nullptr, *qShadow = nullptr, *qShade[2] = {nullptr, nullptr};
+    uint32_t *bucketBuf = nullptr;
+    bool claimBuckets = defaultClaimBuckets();
     uint32_t *counters = nullptr;
     uint64_t *dstats = nullptr;
     float4 *partial = nullptr;     /* film splat partials: slots x 9 (k_splat -> k_gather) */
@@ -124,6 +133,10 @@ struct hpt_context {
     int ownW = -1, ownH = -1, ownShard = -1, ownShards = -1, ownCap = 0, ownLocal = 0;
     hpt_stats stats;
     std::vector<hipEvent_t> evPool;
+    /* hpt_render_multi: this context's shard film, and (on the receiving context) the staging
+       buffer the other devices' films are copied into */
+    float4 *mfilm = nullptr, *mstage = nullptr;
+    size_t mfilmPixels = 0, mstagePixels = 0;
 };
 
 namespace {
@@ -231,8 +244,9 @@ int ensureWave(hpt_context *c, uint64_t n) {
     r |= alloc(n * 4, (void **) &c->qShadow);
     r |= alloc(n * 4, (void **) &c->qShade[0]);
     r |= alloc(n * 4, (void **) &c->qShade[1]);
+    r |= alloc((size_t) HPT_BUCKETS * 2 * n * 4, (void **) &c->bucketBuf); /* claim-order buckets: all rays of a bounce fit one */
     r |= alloc(HPT_COUNTER_WORDS * 4, (void **) &c->counters);
-    r |= alloc(24 * 8, (void **) &c->dstats);
+    r |= alloc(2 * 24 * 8, (void **) &c->dstats); /* the counters, and a snapshot at the start of a wave */
     if (r) return HPT_EDEVICE;
     c->capacity = n;
     return HPT_OK;
@@ -317,6 +331,8 @@ void hpt_context_destroy(hpt_context *c) {
     if (c->dBlockOf) (void) hipFree(c->dBlockOf);
     if (c->dLocalOf) (void) hipFree(c->dLocalOf);
     if (c->scDev) (void) hipFree(c->scDev);
+    if (c->mfilm) (void) hipFree(c->mfilm);
+    if (c->mstage) (void) hipFree(c->mstage);
     for (auto e : c->evPool) (void) hipEventDestroy(e);
     (void) hipHostFree(c->hostCnt);
     (void) hipStreamDestroy(c->stream);
@@ -348,6 +364,11 @@ int hpt_set_default_defines(int n_defines, const char *const *keys, const char *
 int hpt_load_scene_xml(hpt_context *c, const char *path, int n_defines, const char *const *keys,
                        const char *const *values) {
     if (!c || !path) return HPT_EINVAL;
+    /* the same argument checks as hpt_set_default_defines, before the context is touched */
+    if (n_defines < 0 || (n_defines > 0 && (!keys || !values)))
+        return setErr(c, HPT_EINVAL, "bad defines: n_defines < 0 or NULL key / value arrays");
+    for (int i = 0; i < n_defines; ++i)
+        if (!keys[i] || !values[i]) return setErr(c, HPT_EINVAL, "bad defines: NULL key or value");
     std::map<std::string, std::string> defs;
     {
         std::lock_guard<std::mutex> lock(gDefinesMutex);
@@ -436,6 +457,12 @@ int hpt_set_packet_stack(hpt_context *c, uint32_t entries) {
     if (!c) return HPT_EINVAL;
     c->packetStack = entries;
     c->sc.packetStack = entries;
+    return HPT_OK;
+}
+
+int hpt_clear_schedules(hpt_context *c) {
+    if (!c) return HPT_EINVAL;
+    c->schedules.clear();
     return HPT_OK;
 }
 
@@ -597,6 +624,8 @@ int hpt_set_sunsky(hpt_context *c, const float sun_direction[3], float turbidity
     return HPT_OK;
 }
 
+static int uploadScene(hpt_context *c);
+
 int hpt_prepare(hpt_context *c) {
     if (!c) return HPT_EINVAL;
     if (!c->haveCamera || !c->haveHair || !c->haveBSDF || !c->haveEnv)
@@ -604,12 +633,7 @@ int hpt_prepare(hpt_context *c) {
     if (!c->desc.meshes.empty())
         return setErr(c, HPT_EINVAL, "scene has obj/rectangle shapes: the device path renders hair only; "
                                      "triangle scenes (C1) render on the CPU path from hpt_export_scene_json");
-    const bool hostOnly = c->device == HPT_HOST_ONLY;
-    if (!hostOnly) {
-        HIPCHK(c, hipSetDevice(c->device));
-        HIPCHK(c, hipStreamSynchronize(c->stream));
-        freeBufs(c->sceneBufs);
-    }
+    c->prepared = false;
     const SceneDesc &d = c->desc;
     try {
         /* Sobol tables (data/sobol, extracted from src/samplers/sobolseq.cpp) */
@@ -673,6 +697,19 @@ int hpt_prepare(hpt_context *c) {
         buildEnvMipmap(c->env);
     } catch (const std::exception &e) {
         return setErr(c, HPT_EIO, e.what());
+    }
+    return uploadScene(c);
+}
+
+/* the device half of hpt_prepare: the host-built scene (kd-tree, tables, envmap) to this
+   context's device and the kernels' HptScene record.  hpt_context_share_scene runs it alone on a
+   context that copied another's host scene */
+static int uploadScene(hpt_context *c) {
+    const SceneDesc &d = c->desc;
+    if (c->device != HPT_HOST_ONLY) {
+        HIPCHK(c, hipSetDevice(c->device));
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        freeBufs(c->sceneBufs);
     }
     HptScene &sc = c->sc;
     std::memset(&sc, 0, sizeof(sc));
@@ -999,6 +1036,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         c->partialSlots = slots;
     }
     hipStream_t s = c->stream;
+    c->P.bucketQ = c->claimBuckets ? c->bucketBuf : nullptr;
+    c->P.bucketCap = (uint32_t) std::min<uint64_t>(2 * c->capacity, 0xffffffffull);
     if (!c->scDev) HIPCHK(c, hipMalloc((void **) &c->scDev, sizeof(HptScene)));
     if (c->scShadow.size() != sizeof(HptScene) || std::memcmp(c->scShadow.data(), &c->sc, sizeof(HptScene)) != 0) {
         HIPCHK(c, hipMemcpy(c->scDev, &c->sc, sizeof(HptScene), hipMemcpyHostToDevice));
@@ -1071,6 +1110,12 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         w.blockOf = c->dBlockOf;
         w.localOf = c->dLocalOf;
         c->stats.waves++;
+        /* a wave rendered again after its schedule overflowed must not count twice: the timing
+           events and traversal counters of the discarded attempt are rolled back to here */
+        const size_t evMark = evTrace.size();
+        size_t evMarkOther[7];
+        for (int i = 0; i < 7; ++i) evMarkOther[i] = evOther[i].size();
+        if (counted) HIPCHK(c, hipMemcpyAsync(c->dstats + 24, c->dstats, 24 * 8, hipMemcpyDeviceToDevice, s));
         HIPCHK(c, hipMemsetAsync(c->counters, 0, HPT_COUNTER_WORDS * 4, s));
         uint32_t *C = c->counters, *dst = counted ? (uint32_t *) c->dstats : nullptr, *cur = C + HPT_CURSOR_OFFSET;
         /* the camera pass is bounce 0 (parity 0) */
@@ -1113,19 +1158,19 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         auto known = c->schedules.find(key);
         const bool ahead = c->bounceAhead && !perLaunch && !bounceReport && known != c->schedules.end();
         bool fits = true; /* the schedule launched ahead was the whole wave */
-        const bool learn = c->bounceAhead && !ahead;
+        bool learn = c->bounceAhead && !ahead, extended = false;
         BounceSchedule seen;
         int b = 1, bounce = 0;
         auto wavefrontBounce = [&](uint32_t p, uint64_t grid, uint32_t tailFrom) -> hipError_t {
             const uint32_t q = p ^ 1u;
             hipError_t e1 = timed(2, [&] {
                 return hpt_launch_shade(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), c->qTrace, C + HPT_C_TRACE(p),
-                                        c->qShadow, C + HPT_C_SHADOW(p), C, grid, tailFrom, s);
+                                        c->qShadow, C + HPT_C_SHADOW(p), C, grid, tailFrom, s, C + HPT_C_BUCKET(p, 0));
             });
             if (e1) return e1;
             e1 = timed(-1, [&] {
                 return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(p), C + HPT_C_SHADOW(p), cur, dst,
-                                        2ull * grid, s);
+                                        2ull * grid, s, c->P.bucketQ ? C + HPT_C_BUCKET(p, 0) : nullptr);
             });
             if (e1) return e1;
             reportLaunch("bounce");
@@ -1160,7 +1205,16 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             if (e) break;
             const uint32_t n = hostCnt[HPT_C_SHADE(p)];
             if (n == 0 || hostCnt[HPT_C_TAIL_PATHS] != 0) break; /* no live path, or k_tail took the rest */
-            if (ahead && fits) c->schedules.erase(key), fits = false; /* the schedule did not fit: re-record */
+            if (ahead && fits) {
+                /* the schedule did not cover the wave (its tail declined, or bounces ran past it):
+                   re-record it as the part launched ahead plus the bounces read back from here */
+                seen.shade = known->second.shade;
+                seen.tail = false;
+                c->schedules.erase(key);
+                fits = false;
+                learn = extended = true;
+                c->stats.schedule_extensions++;
+            }
             if (n < c->tailPaths) {
                 /* few live paths: finish them all in one launch (k_tail) */
                 seen.tail = true;
@@ -1185,13 +1239,21 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             c->schedules.erase(key);
             c->stats.waves--;
             c->stats.schedule_misses++;
+            for (size_t i = evMark; i < evTrace.size(); ++i) evUsed -= 2; /* events back to the pool */
+            evTrace.resize(evMark);
+            for (int i = 0; i < 7; ++i) {
+                for (size_t k = evMarkOther[i]; k < evOther[i].size(); ++k) evUsed -= 2;
+                evOther[i].resize(evMarkOther[i]);
+            }
+            if (counted) HIPCHK(c, hipMemcpyAsync(c->dstats, c->dstats + 24, 24 * 8, hipMemcpyDeviceToDevice, s));
             j0 -= (int) nSpp;
             continue;
         }
         if (learn) {
-            if (c->scheduleTest == 1)
+            /* (the test hooks shorten first recordings only, so an extended schedule is whole) */
+            if (c->scheduleTest == 1 && !extended)
                 for (auto &n : seen.shade) n = std::max<uint32_t>(1, n / 2);
-            if (c->scheduleTest == 2 && seen.tail && !seen.shade.empty()) seen.shade.pop_back();
+            if (c->scheduleTest == 2 && !extended && seen.tail && !seen.shade.empty()) seen.shade.pop_back();
             if (c->schedules.size() >= 4096) c->schedules.clear(); /* e.g. a long run of -r passes */
             c->schedules[key] = seen;
         }
@@ -1288,6 +1350,108 @@ int hpt_render(hpt_context *c, const hpt_render_params *prm, float *film) {
     (void) hipFree(d);
     if (r) return r;
     if (e != hipSuccess) return setErr(c, HPT_EDEVICE, hipGetErrorString(e));
+    return HPT_OK;
+}
+
+int hpt_context_share_scene(hpt_context *src, int device, hpt_context **out) {
+    if (!src || !out) return HPT_EINVAL;
+    *out = nullptr;
+    if (!src->prepared) return setErr(src, HPT_ESTATE, "hpt_context_share_scene: the source context is not prepared");
+    hpt_context *c = nullptr;
+    int rc = hpt_context_create(device, &c);
+    if (rc) return setErr(src, rc, "hpt_context_share_scene: no gfx950 context on device " + std::to_string(device));
+    /* the host-built scene, as hpt_prepare left it on src (read-only there: several threads may
+       share one source at once) */
+    c->dataDir = src->dataDir;
+    c->desc = src->desc;
+    c->haveCamera = src->haveCamera, c->haveHair = src->haveHair, c->haveBSDF = src->haveBSDF;
+    c->haveEnv = src->haveEnv, c->hairFromFile = src->hairFromFile, c->envFromSunsky = src->envFromSunsky;
+    c->hair = src->hair;
+    c->tree = src->tree;
+    c->mar = src->mar;
+    c->rp = src->rp;
+    c->bsdfRec = src->bsdfRec;
+    c->env = src->env;
+    c->sobol32 = src->sobol32;
+    c->vdc = src->vdc;
+    c->vdcInv = src->vdcInv;
+    c->maxLeafRounds = src->maxLeafRounds, c->maxRestarts = src->maxRestarts, c->packetStack = src->packetStack;
+    c->tailPaths = src->tailPaths, c->bounceAhead = src->bounceAhead, c->packets = src->packets;
+    c->claimBuckets = src->claimBuckets;
+    rc = uploadScene(c);
+    if (rc) {
+        setErr(src, rc, c->err);
+        hpt_context_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return HPT_OK;
+}
+
+int hpt_render_multi(hpt_context *const *ctxs, int n, const hpt_render_params *prm, float *film) {
+    if (!ctxs || n <= 0 || !prm || !film) return HPT_EINVAL;
+    hpt_context *c0 = ctxs[0];
+    for (int g = 0; g < n; ++g) {
+        if (!ctxs[g]) return HPT_EINVAL;
+        if (ctxs[g]->device == HPT_HOST_ONLY) return setErr(c0, HPT_EDEVICE, "host-only context cannot render");
+        if (!ctxs[g]->prepared) return setErr(c0, HPT_ESTATE, "hpt_render_multi: a context is not prepared");
+        if (ctxs[g]->sc.cam.width != c0->sc.cam.width || ctxs[g]->sc.cam.height != c0->sc.cam.height)
+            return setErr(c0, HPT_EINVAL, "hpt_render_multi: contexts render different film sizes");
+    }
+    const size_t pixels = (size_t) c0->sc.cam.width * c0->sc.cam.height;
+    /* every context renders its shard into its own device film; the receiving context's film
+       starts as the caller's (hpt_render accumulates), the others at zero */
+    std::vector<int> rcs(n, HPT_OK);
+    auto shard = [&](int g) {
+        hpt_context *c = ctxs[g];
+        auto fail = [&](hipError_t e) { rcs[g] = setErr(c, HPT_EDEVICE, hipGetErrorString(e)); };
+        hipError_t e = hipSetDevice(c->device);
+        if (e == hipSuccess && c->mfilmPixels < pixels) {
+            if (c->mfilm) (void) hipFree(c->mfilm);
+            c->mfilm = nullptr;
+            c->mfilmPixels = 0;
+            e = hipMalloc((void **) &c->mfilm, pixels * 16);
+            if (e == hipSuccess) c->mfilmPixels = pixels;
+        }
+        if (e == hipSuccess)
+            e = g == 0 ? hipMemcpyAsync(c->mfilm, film, pixels * 16, hipMemcpyHostToDevice, c->stream)
+                       : hipMemsetAsync(c->mfilm, 0, pixels * 16, c->stream);
+        if (e != hipSuccess) return fail(e);
+        hpt_render_params p = *prm;
+        p.shard = g;
+        p.n_shards = n;
+        rcs[g] = renderImpl(c, &p, c->mfilm);
+    };
+    {
+        std::vector<std::thread> th;
+        for (int g = 1; g < n; ++g) th.emplace_back(shard, g);
+        shard(0);
+        for (auto &t : th) t.join();
+    }
+    for (int g = 0; g < n; ++g)
+        if (rcs[g]) {
+            if (g) setErr(c0, rcs[g], "device " + std::to_string(ctxs[g]->device) + ": " + ctxs[g]->err);
+            return rcs[g];
+        }
+    /* the film combine (renderproc.cpp:142-145) on the receiving device: each other film over
+       xGMI (peer copy) into a staging buffer, added in shard order, so the sum is the host sum
+       f0 + f1 + ... of the same films */
+    HIPCHK(c0, hipSetDevice(c0->device));
+    if (n > 1 && c0->mstagePixels < pixels) {
+        if (c0->mstage) (void) hipFree(c0->mstage);
+        c0->mstage = nullptr;
+        c0->mstagePixels = 0;
+        HIPCHK(c0, hipMalloc((void **) &c0->mstage, pixels * 16));
+        c0->mstagePixels = pixels;
+    }
+    for (int g = 1; g < n; ++g) {
+        if (ctxs[g]->device != c0->device) (void) hipDeviceEnablePeerAccess(ctxs[g]->device, 0); /* once; later calls report it done */
+        (void) hipGetLastError();
+        HIPCHK(c0, hipMemcpyPeerAsync(c0->mstage, c0->device, ctxs[g]->mfilm, ctxs[g]->device, pixels * 16, c0->stream));
+        HIPCHK(c0, hpt_launch_film_add(c0->mfilm, c0->mstage, pixels, c0->stream));
+    }
+    HIPCHK(c0, hipMemcpyAsync(film, c0->mfilm, pixels * 16, hipMemcpyDeviceToHost, c0->stream));
+    HIPCHK(c0, hipStreamSynchronize(c0->stream));
     return HPT_OK;
 }
 

@@ -22,6 +22,11 @@
 #define HPT_C_TAIL_BOUNCES 13 /* path-bounces shaded inside k_tail */
 #define HPT_C_TAIL_CURSOR 14  /* k_tail's work claims */
 #define HPT_Q_COUNT 16
+/* claim-order buckets of a bounce's trace launch (parity p): rays appended by k_shade to
+   HptPaths::bucketQ by the length of their interval inside the scene box, and claimed by
+   k_trace longest first, so that the rays still running when its queue runs dry are short */
+#define HPT_BUCKETS 4
+#define HPT_C_BUCKET(p, b) (16 + HPT_BUCKETS * (p) + (b))
 /* HptScene::fault bits: a traversal bound fired (the ray would otherwise end
    with whatever hit it had; the render / batch call fails instead) */
 #define HPT_FAULT_LEAVES 1u   /* more than HptScene::maxLeafRounds (2^18) leaf rounds for one ray */
@@ -84,12 +89,17 @@ struct HptPaths {
        The by-path arrays above (ro, rd, thr, state, bw, sdir, scontrib) are k_camera's and
        k_tail's. */
     float4 *postRec, *shadowRec, *shadeRec;
+    /* claim-order buckets (nullptr: off): bucket b holds bucketCap entries from b * bucketCap,
+       each a trace-queue position, or a shadow-queue position | HPT_BUCKET_SHADOW */
+    uint32_t *bucketQ;
+    uint32_t bucketCap;
     float4 *bw;        /* bsdf weight rgb, bsdf pdf                  */
     float4 *sdir;      /* shadow ray direction xyz, maxt             */
     float4 *scontrib;  /* NEE contribution rgb (added if unoccluded) */
 };
 
 
+#define HPT_BUCKET_SHADOW 0x80000000u
 /* hit record of a miss (a segment id never has all 31 bits set) */
 #define HPT_MISS 0xffffffffu
 
@@ -98,9 +108,10 @@ struct HptPaths {
 hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPaths &P, uint32_t *traceQ,
                              uint32_t *nTrace, hipStream_t s);
 /* one persistent traversal launch: closest-hit rays traceQ[0, *nTrace), shadow rays shadowQ[0, *nShadow) */
+/* nBucket (nullptr: queue order): the launch's HPT_BUCKETS claim-order bucket lengths (P.bucketQ) */
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
-                            uint64_t maxItems, hipStream_t s);
+                            uint64_t maxItems, hipStream_t s, const uint32_t *nBucket = nullptr);
 hipError_t hpt_launch_env_filtered_batch(const HptScene &sc, int n, const float *d, const float *rx, const float *ry,
                                         float *out, hipStream_t s);
 /* closest-hit rays as 64-ray packets (coherent rays: the camera pass); the rays of a packet whose
@@ -117,7 +128,7 @@ hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint3
    bounce (0: always shade); a queue longer than the grid (maxItems) sets HPT_C_OVERFLOW */
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
                             uint32_t *traceQ, uint32_t *nTrace, uint32_t *shadowQ, uint32_t *nShadow, uint32_t *counters,
-                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s);
+                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s, uint32_t *nBucket = nullptr);
 hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
                            uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s);
 /* the rest of every live path (the shade queue) to termination in one launch, when the queue
@@ -127,6 +138,8 @@ hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t
 hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
                            uint32_t *counters, uint64_t items, uint32_t tailFrom, hipStream_t s);
 hipError_t hpt_launch_clear(uint32_t *counters, uint32_t parity, hipStream_t s);
+/* dst[i] += src[i] over n RGBW pixels (hpt_render_multi's film combine) */
+hipError_t hpt_launch_film_add(float4 *dst, const float4 *src, size_t n, hipStream_t s);
 /* k_splat + k_gather; partial = (nPaths / nSpp) * 9 float4 of scratch */
 hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *partial, float4 *film,
                              hipStream_t s);

@@ -275,6 +275,9 @@ HD float adaptiveMint(V3 o, float mint, bool shadow) {
 /* 275-297), so the closest hit does not depend on the tree or on the   */
 /* traversal order.                                                      */
 /* ------------------------------------------------------------------ */
+/* first item of cursor shard s when n items are split over HPT_CURSORS contiguous shards */
+HD uint32_t shardLo(uint32_t n, uint32_t s) { return (uint32_t) ((uint64_t) n * s / HPT_CURSORS); }
+
 struct TraceRay {
     V3 o, d, rcp;
     float mint, maxt;   /* ray interval after the scene-AABB clip and adaptive epsilon */
@@ -643,24 +646,11 @@ HD uint32_t selectBit(uint64_t m, uint32_t k) {
    key() (after begin: what finish needs, kept in LDS while the ray is
    traced) and finish(key, r).  Every wave exits once all shards are exhausted and its
    lanes have drained, so the grid always completes. */
-#ifdef HPT_TRACE_PROFILE
-/* timing instrumentation of the persistent traversal (experiment builds only: make variant
-   KFLAGS=-DHPT_TRACE_PROFILE): per launch (host-set slot) and wave [begin, the moment its
-   claims found every shard empty, end, rays claimed, rays still in flight when it found
-   them empty, 0, 0, 0]; 100 MHz s_memrealtime ticks */
-#define HPT_TRACE_PROFILE_LAUNCHES 16
-#define HPT_TRACE_PROFILE_WAVES 16384
-__device__ unsigned long long g_traceprof[HPT_TRACE_PROFILE_LAUNCHES][HPT_TRACE_PROFILE_WAVES][8];
-__device__ uint32_t g_traceprof_slot;
-#endif
+#include "hpt_probes.h"
 template <int STACK, bool STATS, bool SPLIT = (!STATS && HPT_DRAIN_SPLIT), class IO>
 __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint32_t *cursors, uint2 *stk,
                                                 uint32_t *stats) {
-#ifdef HPT_TRACE_PROFILE
-    const unsigned long long prBegin = __builtin_amdgcn_s_memrealtime();
-    unsigned long long prExhausted = 0, prClaimed = 0, prInFlight = 0;
-#endif
-    const uint32_t total = io.count();
+    TraceProbe probe;
     const uint32_t lane = __lane_id();
     TraceRay r;
     TraceCounters tc;
@@ -825,36 +815,31 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             const uint32_t n = (uint32_t) __popcll(idle);
             uint32_t start = 0, got = 0;
             while (true) { /* wave-uniform */
-                const uint32_t lo = (uint32_t) ((uint64_t) total * shard / HPT_CURSORS);
-                const uint32_t size = (uint32_t) ((uint64_t) total * (shard + 1) / HPT_CURSORS) - lo;
+                const uint32_t lo = IO::kContiguous ? shardLo(io.count(), shard) : 0u;
+                const uint32_t size = IO::kContiguous ? shardLo(io.count(), shard + 1) - lo : io.shardSize(shard);
                 uint32_t base = 0;
                 if (lane == 0) base = atomicAdd(&cursors[shard * HPT_CURSOR_STRIDE], n);
                 base = __shfl(base, 0);
                 if (base < size) {
+                    /* contiguous shards: the first item claimed; buckets: the offset in the shard */
                     start = lo + base;
                     got = min(n, size - base);
                     break;
                 }
                 if (++tried >= HPT_CURSORS) {
                     exhausted = true;
-#ifdef HPT_TRACE_PROFILE
-                    prExhausted = __builtin_amdgcn_s_memrealtime();
-                    prInFlight = (unsigned long long) (64 - n);
-#endif
+                    probe.onExhausted(n);
                     break;
                 }
                 shard = (shard + 1) % HPT_CURSORS;
             }
-#ifdef HPT_TRACE_PROFILE
-            prClaimed += got;
-#endif
+            probe.onClaim(got);
             if (!active) {
                 /* idle lanes below this one (v_mbcnt: no 64-bit lane mask kept live across the loop) */
                 const uint32_t rank =
                     __builtin_amdgcn_mbcnt_hi((uint32_t) (idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) idle, 0u));
-                const uint32_t k = start + rank;
                 if (rank < got) {
-                    active = io.begin(sc, k, r);
+                    active = io.begin(sc, IO::kContiguous ? start + rank : io.item(shard, start + rank), r);
                     if (STATS) {
                         nC += r.shadow ? 0u : 1u;
                         nS += r.shadow ? 1u : 0u;
@@ -875,9 +860,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             if (exhausted) break;
             continue;
         }
-#ifdef HPT_TRACE_PROFILE
-        if (exhausted && prExhausted == 0) prExhausted = __builtin_amdgcn_s_memrealtime();
-#endif
+        if (exhausted) probe.onDrainStart();
         if (active && traceRound<STACK, STATS>(sc, r, stk, (int) blockDim.x, tc)) {
             nU += io.finish(sc, rayKey<STACK>(stk, (int) blockDim.x), r);
             if (STATS) rayDone(rayLeaves(r), rayRestarts(r));
@@ -885,12 +868,11 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
         }
     }
     if (SPLIT) {
-#ifdef HPT_TRACE_PROFILE
-        if (prExhausted == 0) prExhausted = __builtin_amdgcn_s_memrealtime();
-#endif
+        probe.onDrainStart();
         while (true) {
             splitStep(r, active);
             if (__ballot(active) == 0) break;
+            probe.onDrainRound(__ballot(active));
             bool fin = false;
             if (active && traceRound<STACK, STATS>(sc, r, stk, (int) blockDim.x, tc)) {
                 fin = true;
@@ -900,20 +882,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             if (splitM) decideSplit(r, active, __ballot(fin) & splitM);
         }
     }
-#ifdef HPT_TRACE_PROFILE
-    {
-        const uint32_t wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-        const uint32_t slot = g_traceprof_slot;
-        if (lane == 0 && wv < HPT_TRACE_PROFILE_WAVES && slot < HPT_TRACE_PROFILE_LAUNCHES) {
-            unsigned long long *rec = g_traceprof[slot][wv];
-            rec[0] = prBegin;
-            rec[1] = prExhausted;
-            rec[2] = __builtin_amdgcn_s_memrealtime();
-            rec[3] = prClaimed;
-            rec[4] = prInFlight;
-        }
-    }
-#endif
+    probe.finish();
     if (STATS) {
         /* traversal counters for the algorithmic byte model:
            [0] node visits [1] primitive tests [2] closest rays [3] shadow rays
@@ -2165,9 +2134,9 @@ __device__ __forceinline__ void qpushBlock2(bool pred, uint32_t value, uint32_t 
 /* qpushBlock that also stores an NR-float4 record at the same position of recs and, with
    array2, a word there */
 template <int BLOCK, int NR>
-__device__ __forceinline__ void qpushBlockRec(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter,
-                                              float4 *recs, const float4 *rec, uint32_t *array2 = nullptr,
-                                              uint32_t value2 = 0u) {
+__device__ __forceinline__ uint32_t qpushBlockRec(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter,
+                                                  float4 *recs, const float4 *rec, uint32_t *array2 = nullptr,
+                                                  uint32_t value2 = 0u) {
     constexpr int NW = BLOCK / 64;
     __shared__ uint32_t waveCount[NW];
     __shared__ uint32_t blockBase;
@@ -2185,14 +2154,63 @@ __device__ __forceinline__ void qpushBlockRec(bool pred, uint32_t value, uint32_
         blockBase = tot ? atomicAdd(counter, tot) : 0u;
     }
     __syncthreads();
+    const uint32_t pos = blockBase + waveCount[wave] + (uint32_t) __popcll(mask & ((1ull << lane) - 1ull));
     if (pred) {
-        const uint32_t pos = blockBase + waveCount[wave] + (uint32_t) __popcll(mask & ((1ull << lane) - 1ull));
         queue[pos] = value;
 #pragma unroll
         for (int i = 0; i < NR; ++i) recs[NR * pos + i] = rec[i];
         if (array2) array2[pos] = value2;
     }
     __syncthreads();
+    return pos; /* the entry's queue position (meaningful where pred) */
+}
+
+/* Claim-order buckets (hpt_kernels.h HPT_BUCKETS): append value to bucket b (0 = shortest
+   rays) of P.bucketQ, one atomic per non-empty bucket per block.  Every thread of the block
+   must call it. */
+template <int BLOCK>
+__device__ __forceinline__ void qpushBucket(bool pred, uint32_t b, uint32_t value, uint32_t *bucketQ, uint32_t cap,
+                                            uint32_t *counts) {
+    constexpr int NW = BLOCK / 64;
+    __shared__ uint32_t waveCount[HPT_BUCKETS][NW];
+    __shared__ uint32_t blockBase[HPT_BUCKETS];
+    const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+    uint64_t mine = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < HPT_BUCKETS; ++k) {
+        const uint64_t m = __ballot(pred && b == k);
+        if (lane == 0) waveCount[k][wave] = (uint32_t) __popcll(m);
+        if (b == k) mine = m;
+    }
+    __syncthreads();
+    if (threadIdx.x < HPT_BUCKETS) {
+        const uint32_t k = threadIdx.x;
+        uint32_t tot = 0;
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t c = waveCount[k][w];
+            waveCount[k][w] = tot;
+            tot += c;
+        }
+        blockBase[k] = tot ? atomicAdd(&counts[k], tot) : 0u;
+    }
+    __syncthreads();
+    if (pred)
+        bucketQ[(size_t) b * cap + blockBase[b] + waveCount[b][wave] + (uint32_t) __popcll(mine & ((1ull << lane) - 1ull))] =
+            value;
+    __syncthreads();
+}
+
+/* a ray's claim-order bucket: the length of its interval inside the scene box against the box
+   diagonal (rays that leave the hair's box soon are short; the thresholds are the quartiles of
+   the headline frame's bounce rays, tools/ray_order_probe.py) */
+HD uint32_t claimBucket(const HptScene &sc, V3 o, V3 d, float maxt) {
+    float nearT, farT;
+    const V3 rcp = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    if (!aabbIntersect(sc, o, d, rcp, nearT, farT)) return 0u;
+    const float len = fminr(farT, maxt) - fmaxr(nearT, 0.0f);
+    const float ex = sc.aabbMax[0] - sc.aabbMin[0], ey = sc.aabbMax[1] - sc.aabbMin[1], ez = sc.aabbMax[2] - sc.aabbMin[2];
+    const float rel2 = len * len / (ex * ex + ey * ey + ez * ez);
+    return (rel2 > 0.24f * 0.24f ? 1u : 0u) + (rel2 > 0.33f * 0.33f ? 1u : 0u) + (rel2 > 0.45f * 0.45f ? 1u : 0u);
 }
 
 /* append to a queue: one atomic per wave (wave64 ballot + mbcnt) */
@@ -2281,14 +2299,6 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
 /* k_trace: the wave's closest-hit rays (traceQ[0, nTrace)) then its any-hit
    shadow rays (shadowQ) as one persistent grid; k_trace_counted adds the
    traversal counters of the byte model (one counted frame per bench run) */
-#ifdef HPT_COST_PROBE
-/* experiment builds only: leaf rounds of each path's closest / shadow ray per trace launch
-   (host-set slot), to see whether a ray's cost predicts its path's next ray's */
-#define HPT_COST_LAUNCHES 6
-#define HPT_COST_PATHS (1 << 21)
-__device__ uint16_t g_costprof[HPT_COST_LAUNCHES][2][HPT_COST_PATHS];
-__device__ uint32_t g_cost_slot;
-#endif
 /* Closest-hit records go to P.hitQ by trace-queue position (the wavefront
    kernels; k_primary / k_post read them in queue order), or to P.hit by path
    (byQueue false: k_tail).  A record is 4 bytes (segment | far root << 31, or
@@ -2296,14 +2306,41 @@ __device__ uint32_t g_cost_slot;
    claimed together, so a launch's record writes fill whole lines in L2
    instead of a 32-byte sector per lone path-indexed 16-byte store.
    posQ (k_trace_overflow): the queue positions of the rays to trace. */
-struct PathIO {
+template <bool BUCKETS>
+struct PathIOT {
     HptPaths P;
     const uint32_t *traceQ, *shadowQ;
     uint32_t nTrace, nShadow, id;
     bool byQueue;
     const uint32_t *posQ;
+    static constexpr bool kContiguous = !BUCKETS; /* a shard's items are consecutive work indices */
     bool recs; /* bounce launches: rays from the queue-ordered records, keys are queue positions */
+    const uint32_t *bq; /* claim-order buckets (P.bucketQ), longest rays first; nullptr: queue order */
+    uint32_t nb[BUCKETS ? HPT_BUCKETS : 1];
     HD uint32_t count() const { return nTrace + nShadow; }
+    /* cursor shard s of HPT_CURSORS: its length, and its j-th work item (a work index k: closest
+       rays [0, nTrace), then shadow rays).  With buckets a shard walks the s-th part of every
+       bucket, longest bucket first, so every shard claims long rays before short ones */
+    HD uint32_t shardSize(uint32_t s) const {
+        if (!BUCKETS || !bq) return shardLo(count(), s + 1) - shardLo(count(), s);
+        uint32_t n = 0;
+#pragma unroll
+        for (int b = 0; b < HPT_BUCKETS; ++b) n += shardLo(nb[b], s + 1) - shardLo(nb[b], s);
+        return n;
+    }
+    HD uint32_t item(uint32_t s, uint32_t j) const {
+        if (!BUCKETS || !bq) return shardLo(count(), s) + j;
+#pragma unroll
+        for (int b = HPT_BUCKETS - 1; b >= 0; --b) {
+            const uint32_t lo = shardLo(nb[b], s), sz = shardLo(nb[b], s + 1) - lo;
+            if (j < sz || b == 0) {
+                const uint32_t e = bq[(size_t) b * P.bucketCap + lo + j];
+                return (e & HPT_BUCKET_SHADOW) ? nTrace + (e & ~HPT_BUCKET_SHADOW) : e;
+            }
+            j -= sz;
+        }
+        return 0;
+    }
     HD bool begin(const HptScene &sc, uint32_t k, TraceRay &r) {
         if (recs) { /* a bounce ray leaves the hit point at kEpsilon (path.cpp:213, scene.cpp:838) */
             if (k < nTrace) {
@@ -2330,14 +2367,10 @@ struct PathIO {
     /* id: the record's queue position / path (closest), the path (shadow ray);
        returns 1 for an unoccluded shadow ray */
     HD uint32_t finish(const HptScene &sc, uint32_t id, const TraceRay &r) {
-#ifdef HPT_COST_PROBE
-        {
-            const uint32_t path = r.shadow ? (recs ? shadowQ[id] : id) : (byQueue && traceQ && !posQ ? traceQ[id] : HPT_COST_PATHS);
-            const uint32_t slot = g_cost_slot;
-            if (path < HPT_COST_PATHS && slot < HPT_COST_LAUNCHES)
-                g_costprof[slot][r.shadow ? 1 : 0][path] = (uint16_t) min(rayLeaves(r) + 1u, 65535u);
+        if (HPT_PROBE_WANTS_PATH) {
+            const uint32_t path = r.shadow ? (recs ? shadowQ[id] : id) : (byQueue && traceQ && !posQ ? traceQ[id] : HPT_MISS);
+            probeRayFinished(r, path, r.shadow ? nTrace + id : id, recs);
         }
-#endif
         if (!r.shadow) {
             /* the shading kernel re-derives the point from the segment and the accepted root */
             (byQueue ? P.hitQ : P.hit)[id] = r.found ? r.segHit : HPT_MISS;
@@ -2350,6 +2383,9 @@ struct PathIO {
         return 1;
     }
 };
+
+using PathIO = PathIOT<false>;       /* queue order */
+using BouncePathIO = PathIOT<true>;  /* queue order or claim-order buckets (k_trace) */
 
 /* k_trace launch shape (measured on MI355X, furball 512^2 @ 256 spp):
    persistent 256-thread blocks (64 and 128 are within 1.5%); an 8-entry ring
@@ -2377,11 +2413,23 @@ struct PathIO {
 
 /* the queue lengths come from device memory (the launch is enqueued before
    the host knows them) */
+/* a bounce launch's work: its queue lengths and, with claim-order buckets, their lengths */
+HD BouncePathIO bouncePathIO(const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ, const uint32_t *nTrace,
+                             const uint32_t *nShadow, const uint32_t *nBucket) {
+    BouncePathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0, true, nullptr, true};
+    if (nBucket && P.bucketQ) {
+        io.bq = P.bucketQ;
+#pragma unroll
+        for (int b = 0; b < HPT_BUCKETS; ++b) io.nb[b] = nBucket[b];
+    }
+    return io;
+}
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
-    const uint32_t *__restrict__ nTrace, const uint32_t *__restrict__ nShadow, uint32_t *__restrict__ cursors) {
+    const uint32_t *__restrict__ nTrace, const uint32_t *__restrict__ nShadow, uint32_t *__restrict__ cursors,
+    const uint32_t *__restrict__ nBucket) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    PathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0, true, nullptr, true};
+    BouncePathIO io = bouncePathIO(P, traceQ, shadowQ, nTrace, nShadow, nBucket);
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(HptScene sc, HptPaths P,
@@ -2390,9 +2438,10 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
                                                                               const uint32_t *__restrict__ nTrace,
                                                                               const uint32_t *__restrict__ nShadow,
                                                                               uint32_t *__restrict__ cursors,
+                                                                              const uint32_t *__restrict__ nBucket,
                                                                               uint32_t *stats) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    PathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0, true, nullptr, true};
+    BouncePathIO io = bouncePathIO(P, traceQ, shadowQ, nTrace, nShadow, nBucket);
     tracePersistent<HPT_STACK, true>(sc, io, cursors, stk + threadIdx.x, stats);
 }
 
@@ -2599,6 +2648,7 @@ struct HptShadeIO {
     const uint32_t *nShade;
     uint32_t *nTrace, *nShadow, *counters;
     uint32_t tailFrom; /* a queue shorter than this is k_tail's (device-side bounce control); 0: always shade */
+    uint32_t *nBucket; /* the next trace launch's claim-order bucket lengths (nullptr: no buckets) */
 };
 template <bool MULTI>
 __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
@@ -2623,8 +2673,14 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
         for (int i = 0; i < 3; ++i) in[i] = P.shadeRec[3 * tid + i];
         shadePath<MULTI, true>(sc, P, id, P.hitS[tid], q.counters, cont, shadow, in, cOut, sOut);
     }
-    qpushBlockRec<HPT_SHADE_BLOCK, 4>(cont, id, traceQ, q.nTrace, P.postRec, cOut);
-    qpushBlockRec<HPT_SHADE_BLOCK, 3>(shadow, id, shadowQ, q.nShadow, P.shadowRec, sOut);
+    const uint32_t cpos = qpushBlockRec<HPT_SHADE_BLOCK, 4>(cont, id, traceQ, q.nTrace, P.postRec, cOut);
+    const uint32_t spos = qpushBlockRec<HPT_SHADE_BLOCK, 3>(shadow, id, shadowQ, q.nShadow, P.shadowRec, sOut);
+    if (q.nBucket) { /* uniform: the launch's claim-order buckets */
+        const uint32_t bc = cont ? claimBucket(sc, v3(cOut[0].x, cOut[0].y, cOut[0].z), v3(cOut[1].x, cOut[1].y, cOut[1].z), finf()) : 0u;
+        qpushBucket<HPT_SHADE_BLOCK>(cont, bc, cpos, P.bucketQ, P.bucketCap, q.nBucket);
+        const uint32_t bs = shadow ? claimBucket(sc, v3(sOut[0].x, sOut[0].y, sOut[0].z), v3(sOut[1].x, sOut[1].y, sOut[1].z), sOut[1].w) : 0u;
+        qpushBucket<HPT_SHADE_BLOCK>(shadow, bs, spos | HPT_BUCKET_SHADOW, P.bucketQ, P.bucketCap, q.nBucket);
+    }
 }
 #ifndef HPT_SHADE_WAVES
 #define HPT_SHADE_WAVES 0 /* 0: natural allocation (100 VGPRs = 5 waves/SIMD) */
@@ -2757,13 +2813,6 @@ struct HptTail {
     uint32_t pairs;    /* lane pairs per wave that take paths (1..32); 0: from the queue length, on the device */
     uint32_t tailFrom; /* the launch takes the queue only when it is shorter than this (device-side bounce control) */
 };
-#ifdef HPT_TAIL_PROFILE
-/* timing instrumentation of k_tail (experiment builds only: make variant KFLAGS=-DHPT_TAIL_PROFILE):
-   per wave [iterations, shade, trace, post ticks, begin, end, sum over iterations of the wave's
-   longest ray in leaf rounds, items claimed]; 100 MHz s_memrealtime ticks */
-#define HPT_TAIL_PROFILE_WAVES 65536
-__device__ unsigned long long g_tailprof[HPT_TAIL_PROFILE_WAVES][8];
-#endif
 template <bool MULTI>
 __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const HptTail &T,
                                           uint32_t *__restrict__ counters, uint2 *stk) {
@@ -2785,22 +2834,14 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
     bool live = false, exhausted = false;
     TraceCounters tc;
     PathIO io{P, nullptr, nullptr, 0, 0, 0, false, nullptr, false};
-#ifdef HPT_TAIL_PROFILE
-    uint32_t rounds = 0;
-    unsigned long long pIt = 0, pS = 0, pT = 0, pP = 0, pR = 0, pItems = 0;
-    const unsigned long long pBegin = __builtin_amdgcn_s_memrealtime();
-#endif
+    TailProbe probe;
     auto trace = [&](bool shadowRay) {
         TraceRay r;
         const float4 ro = P.ro[id], rd = shadowRay ? P.sdir[id] : P.rd[id];
         const bool act = beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(rd.x, rd.y, rd.z), shadowRay ? kEpsilon : ro.w, rd.w, shadowRay);
         stashRay<HPT_STACK>(stk, (int) blockDim.x, r, id);
         if (act)
-            while (!traceRound<HPT_STACK, false, true>(sc, r, stk, (int) blockDim.x, tc)) {
-#ifdef HPT_TAIL_PROFILE
-                ++rounds;
-#endif
-            }
+            while (!traceRound<HPT_STACK, false, true>(sc, r, stk, (int) blockDim.x, tc)) probe.onRound();
         io.finish(sc, id, r);
     };
     while (true) {
@@ -2829,19 +2870,14 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
                     P.state[id] = __float_as_uint(c.w);
                 }
                 live = true;
-#ifdef HPT_TAIL_PROFILE
-                pItems += odd ? 0u : 1u;
-#endif
+                probe.onItem(!odd);
             }
         }
         if (__ballot(live) == 0) {
             if (exhausted) break;
             continue;
         }
-#ifdef HPT_TAIL_PROFILE
-        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-        rounds = 0;
-#endif
+        probe.phase(0);
         bool cont = false, shadow = false;
         if (live && !odd) {
             ++nb;
@@ -2851,50 +2887,23 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
         const int f = __shfl((cont ? 1 : 0) | (shadow ? 2 : 0), (int) partner);
         cont = (f & 1) != 0;
         shadow = (f & 2) != 0;
-#ifdef HPT_TAIL_PROFILE
-        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-#endif
+        probe.phase(1);
         /* one call site: the shadow ray (even lane) and the continuation ray (odd
            lane) are traced at the same time, not one after the other */
         if (live && (odd ? cont : shadow)) trace(!odd);
         __threadfence_block(); /* the hit record is in HBM for the even lane */
-#ifdef HPT_TAIL_PROFILE
-        const unsigned long long t2 = __builtin_amdgcn_s_memrealtime();
-#endif
+        probe.phase(2);
         bool alive = false;
         if (live && !odd && cont) {
             hitRec = P.hit[id];
             alive = postPath(sc, P, id, hitRec != HPT_MISS, counters);
         }
         live = live && __shfl(alive ? 1 : 0, (int) partner) != 0;
-#ifdef HPT_TAIL_PROFILE
-        const unsigned long long t3 = __builtin_amdgcn_s_memrealtime();
-        uint32_t rm = rounds;
-        for (int off = 32; off > 0; off >>= 1) rm = max(rm, (uint32_t) __shfl_xor(rm, off));
-        ++pIt;
-        pS += t1 - t0;
-        pT += t2 - t1;
-        pP += t3 - t2;
-        pR += rm;
-#endif
+        probe.phase(3);
     }
     for (int off = 32; off > 0; off >>= 1) nb += __shfl_down(nb, off);
     if (__lane_id() == 0 && nb) atomicAdd(&counters[HPT_C_TAIL_BOUNCES], nb);
-#ifdef HPT_TAIL_PROFILE
-    for (int off = 32; off > 0; off >>= 1) pItems += __shfl_down(pItems, off);
-    const uint32_t wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (__lane_id() == 0 && wv < HPT_TAIL_PROFILE_WAVES) {
-        unsigned long long *rec = g_tailprof[wv];
-        rec[0] = pIt;
-        rec[1] = pS;
-        rec[2] = pT;
-        rec[3] = pP;
-        rec[4] = pBegin;
-        rec[5] = __builtin_amdgcn_s_memrealtime();
-        rec[6] = pR;
-        rec[7] = pItems;
-    }
-#endif
+    probe.finish();
 }
 /* persistent: pairs claim work, so any amount of it fits one launch.  No
    occupancy target: the tail is latency-bound and the traversal keeps its
@@ -3046,7 +3055,10 @@ struct BatchIO {
     uint32_t n;
     bool shadow;
     uint32_t cur;
+    static constexpr bool kContiguous = true;
     HD uint32_t count() const { return n; }
+    HD uint32_t shardSize(uint32_t s) const { return shardLo(n, s + 1) - shardLo(n, s); }
+    HD uint32_t item(uint32_t s, uint32_t j) const { return shardLo(n, s) + j; }
     HD uint32_t key() const { return cur; }
     HD bool begin(const HptScene &sc, uint32_t i, TraceRay &r) {
         cur = i;
@@ -3163,6 +3175,7 @@ extern "C" __global__ void k_clear(uint32_t *counters, uint32_t p) {
         counters[HPT_C_TRACE(q)] = 0;
         counters[HPT_C_SHADOW(q)] = 0;
         counters[HPT_C_SHADE(q)] = 0;
+        for (int b = 0; b < HPT_BUCKETS; ++b) counters[HPT_C_BUCKET(q, b)] = 0;
     }
 }
 
@@ -3211,58 +3224,17 @@ static unsigned persistentBlocks(const void *kernel, uint64_t items, int block =
     return (unsigned) std::max<uint64_t>(1, std::min<uint64_t>(need, (uint64_t) resident));
 }
 
-#ifdef HPT_COST_PROBE
-static uint32_t g_costHostSlot = 0;
-extern "C" int hpt_debug_costprof(uint16_t *out) {
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    const int n = (int) std::min<uint32_t>(g_costHostSlot, HPT_COST_LAUNCHES);
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_costprof), sizeof(uint16_t) * HPT_COST_LAUNCHES * 2 * HPT_COST_PATHS) != hipSuccess)
-        return -1;
-    std::vector<uint16_t> zeros((size_t) HPT_COST_LAUNCHES * 2 * HPT_COST_PATHS, 0);
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_costprof), zeros.data(), zeros.size() * 2) != hipSuccess) return -1;
-    g_costHostSlot = 0;
-    return n;
-}
-#endif
-#ifdef HPT_TRACE_PROFILE
-static uint32_t g_traceprofHostSlot = 0;
-/* copy out (and clear) the k_trace timing records of the launches since the last call:
-   launches x HPT_TRACE_PROFILE_WAVES x 8 u64; returns the number of launches recorded */
-extern "C" int hpt_debug_traceprof(unsigned long long *out, int maxLaunches) {
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    const int n = (int) std::min<uint32_t>(g_traceprofHostSlot, (uint32_t) std::min(maxLaunches, HPT_TRACE_PROFILE_LAUNCHES));
-    if (n > 0 && hipMemcpyFromSymbol(out, HIP_SYMBOL(g_traceprof), (size_t) n * HPT_TRACE_PROFILE_WAVES * 64) != hipSuccess)
-        return -1;
-    std::vector<unsigned long long> zeros((size_t) HPT_TRACE_PROFILE_LAUNCHES * HPT_TRACE_PROFILE_WAVES * 8, 0ull);
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_traceprof), zeros.data(), zeros.size() * 8) != hipSuccess) return -1;
-    g_traceprofHostSlot = 0;
-    return n;
-}
-#endif
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
-                            uint64_t maxItems, hipStream_t s) {
+                            uint64_t maxItems, hipStream_t s, const uint32_t *nBucket) {
     if (maxItems == 0) return hipSuccess;
-#ifdef HPT_COST_PROBE
-    {
-        const uint32_t slot = g_costHostSlot++;
-        (void) hipMemcpyToSymbolAsync(HIP_SYMBOL(g_cost_slot), &slot, 4, 0, hipMemcpyHostToDevice, s);
-        (void) hipStreamSynchronize(s);
-    }
-#endif
-#ifdef HPT_TRACE_PROFILE
-    {
-        const uint32_t slot = g_traceprofHostSlot++;
-        (void) hipMemcpyToSymbolAsync(HIP_SYMBOL(g_traceprof_slot), &slot, 4, 0, hipMemcpyHostToDevice, s);
-        (void) hipStreamSynchronize(s); /* the slot word is read by the launch below */
-    }
-#endif
+    hptProbeBeforeTraceLaunch(s);
     if (stats)
         hipLaunchKernelGGL(k_trace_counted, dim3(persistentBlocks((const void *) k_trace_counted, maxItems)),
-                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, stats);
+                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, nBucket, stats);
     else
         hipLaunchKernelGGL(k_trace, dim3(persistentBlocks((const void *) k_trace, maxItems)), dim3(HPT_TRACE_BLOCK), 0, s,
-                           sc, P, traceQ, shadowQ, nTrace, nShadow, cursors);
+                           sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, nBucket);
     return hipGetLastError();
 }
 hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
@@ -3294,9 +3266,9 @@ hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint3
 }
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
                             uint32_t *traceQ, uint32_t *nTrace, uint32_t *shadowQ, uint32_t *nShadow, uint32_t *counters,
-                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s) {
+                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s, uint32_t *nBucket) {
     if (maxItems == 0) return hipSuccess;
-    const HptShadeIO q{nShade, nTrace, nShadow, counters, tailFrom};
+    const HptShadeIO q{nShade, nTrace, nShadow, counters, tailFrom, P.bucketQ ? nBucket : nullptr};
     if (sc.nShapes > 1)
         hipLaunchKernelGGL(k_shade_multi, dim3(blocksFor(maxItems, HPT_SHADE_BLOCK)), dim3(HPT_SHADE_BLOCK), 0, s, sc, P, shadeQ,
                            traceQ, shadowQ, q);
@@ -3334,16 +3306,19 @@ hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t
         hipLaunchKernelGGL(k_tail, dim3(blocks), dim3(HPT_TRACE_BLOCK), 0, s, sc, P, T, counters);
     return hipGetLastError();
 }
-#ifdef HPT_TAIL_PROFILE
-/* copy out (and clear) the k_tail timing records of the last frame: n waves x 8 u64 */
-extern "C" int hpt_debug_tailprof(unsigned long long *out, int n) {
-    if (n > HPT_TAIL_PROFILE_WAVES) n = HPT_TAIL_PROFILE_WAVES;
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tailprof), (size_t) n * 64) != hipSuccess) return -1;
-    static unsigned long long zeros[HPT_TAIL_PROFILE_WAVES][8];
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_tailprof), zeros, sizeof(zeros)) == hipSuccess ? n : -1;
+extern "C" __global__ __launch_bounds__(256) void k_film_add(float4 *__restrict__ dst, const float4 *__restrict__ src,
+                                                             uint64_t n) {
+    const uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const float4 a = dst[i], b = src[i];
+        dst[i] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+    }
 }
-#endif
+hipError_t hpt_launch_film_add(float4 *dst, const float4 *src, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_film_add, dim3(blocksFor(n, 256)), dim3(256), 0, s, dst, src, (uint64_t) n);
+    return hipGetLastError();
+}
 hipError_t hpt_launch_clear(uint32_t *counters, uint32_t parity, hipStream_t s) {
     hipLaunchKernelGGL(k_clear, dim3(1), dim3(128), 0, s, counters, parity);
     return hipGetLastError();

@@ -63,7 +63,7 @@ class Stats(C.Structure):
                 ("packet_exact", C.c_uint64), ("packet_node_slots", C.c_uint64), ("packet_prim_slots", C.c_uint64),
                 ("packet_fallbacks", C.c_uint64), ("max_leaf_rounds", C.c_uint64), ("max_restarts", C.c_uint64),
                 ("restarted_rays", C.c_uint64), ("binary_nodes", C.c_uint64), ("waves_ahead", C.c_uint64),
-                ("schedule_misses", C.c_uint64)]
+                ("schedule_misses", C.c_uint64), ("schedule_extensions", C.c_uint64)]
 
 
 # every symbol declared in include/hairpt.h: (restype, argtypes)
@@ -80,6 +80,7 @@ SIGNATURES = {
     "hpt_set_sampler_scramble": (C.c_int, [C.c_void_p, C.c_uint64]),
     "hpt_set_traversal_bounds": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
     "hpt_set_packet_stack": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "hpt_clear_schedules": (C.c_int, [C.c_void_p]),
     "hpt_debug_sfmt": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
     "hpt_set_integrator": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
     "hpt_set_hair_file": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_float, _f]),
@@ -96,6 +97,8 @@ SIGNATURES = {
     "hpt_get_scene_info": (C.c_int, [C.c_void_p, C.POINTER(SceneInfo)]),
     "hpt_render": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), _f]),
     "hpt_render_device": (C.c_int, [C.c_void_p, C.POINTER(RenderParams), C.c_void_p]),
+    "hpt_context_share_scene": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    "hpt_render_multi": (C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(RenderParams), _f]),
     "hpt_get_stats": (C.c_int, [C.c_void_p, C.POINTER(Stats)]),
     "hpt_get_film_params": (C.c_int, [C.c_void_p, C.POINTER(FilmParams)]),
     "hpt_write_film": (C.c_int, [C.c_void_p, C.c_char_p, _f, C.c_int, C.c_int, C.POINTER(FilmParams), C.c_char_p,
@@ -156,14 +159,24 @@ class HairPTError(RuntimeError):
 class Renderer:
     """One HIP context on one MI355X (the drop-in for a Mitsuba render job)."""
 
-    def __init__(self, device: int = 0, data_dir: str = DATA_DIR):
+    def __init__(self, device: int = 0, data_dir: str = DATA_DIR, _handle=None):
         self.lib = load_library()
+        if _handle is not None:  # share_scene
+            self.h = _handle
+            return
         h = C.c_void_p()
         rc = self.lib.hpt_context_create(device, C.byref(h))
         if rc != 0:
             raise HairPTError("hpt_context_create(%d) failed (%d): no gfx950 device?" % (device, rc))
         self.h = h
         self._check(self.lib.hpt_set_data_dir(self.h, data_dir.encode()))
+
+    def share_scene(self, device: int) -> "Renderer":
+        """a context on `device` rendering this prepared context's scene (parsed, loaded and built
+        once, uploaded again: hpt_context_share_scene)"""
+        h = C.c_void_p()
+        self._check(self.lib.hpt_context_share_scene(self.h, device, C.byref(h)))
+        return Renderer(device, _handle=h)
 
     def close(self):
         if getattr(self, "h", None):
@@ -214,6 +227,10 @@ class Renderer:
     def set_packet_stack(self, entries=0):
         """test hook: limit the camera packets' stack (0 = the build's depth) to force the overflow path"""
         self._check(self.lib.hpt_set_packet_stack(self.h, entries))
+
+    def clear_schedules(self):
+        """forget the recorded bounce schedules: the next render of each wave reads every bounce back"""
+        self._check(self.lib.hpt_clear_schedules(self.h))
 
     def set_integrator(self, max_depth, rr_depth=5, strict_normals=True, hide_emitters=False):
         self._check(self.lib.hpt_set_integrator(self.h, max_depth, rr_depth, int(strict_normals), int(hide_emitters)))
@@ -290,6 +307,21 @@ class Renderer:
             spp_end = si.spp
         p = RenderParams(spp_begin, spp_end, shard, n_shards, max_wave_paths, int(collect_stats))
         self._check(self.lib.hpt_render_device(self.h, C.byref(p), C.c_void_p(device_ptr)))
+
+    @staticmethod
+    def render_multi(renderers, spp_begin=0, spp_end=None, max_wave_paths=0, collect_stats=False, film=None):
+        """shard g of len(renderers) on renderers[g], films combined on renderers[0]'s device
+        (hpt_render_multi); accumulates into film"""
+        r0 = renderers[0]
+        si = r0.info()
+        if spp_end is None:
+            spp_end = si.spp
+        if film is None:
+            film = np.zeros((si.height, si.width, 4), dtype=np.float32)
+        hs = (C.c_void_p * len(renderers))(*[r.h for r in renderers])
+        p = RenderParams(spp_begin, spp_end, 0, 1, max_wave_paths, int(collect_stats))
+        r0._check(r0.lib.hpt_render_multi(hs, len(renderers), C.byref(p), _p(film, _f)))
+        return film
 
     def stats(self) -> Stats:
         s = Stats()

@@ -91,6 +91,10 @@ int hpt_set_traversal_bounds(hpt_context *ctx, uint32_t max_leaf_rounds, uint32_
    build's 23; larger values are clamped) so that packets overflow and their rays take the
    per-lane fallback launch -- hits, and so the film, are unchanged */
 int hpt_set_packet_stack(hpt_context *ctx, uint32_t entries);
+/* Drop the bounce schedules recorded by earlier renders (no reference counterpart: the
+   reference has no wavefront).  The next render of each wave of paths then reads every
+   bounce's queue length back, as a first render does -- bench.py's first_render_ms */
+int hpt_clear_schedules(hpt_context *ctx);
 /* MonteCarloIntegrator params (src/librender/integrator.cpp:190-203) */
 int hpt_set_integrator(hpt_context *ctx, int max_depth, int rr_depth, int strict_normals, int hide_emitters);
 /* HairShape(Properties) (src/shapes/hair.cpp:609-785); to_world may be NULL */
@@ -164,6 +168,16 @@ int hpt_render(hpt_context *ctx, const hpt_render_params *params, float *film_rg
 /* Same, accumulating into a device buffer of W*H float4 on this context's device. */
 int hpt_render_device(hpt_context *ctx, const hpt_render_params *params, void *device_film_rgbw);
 
+/* One process, several devices (src/mitsuba/mitsuba.cpp:281-329: the scene is loaded once and
+   every worker renders from it).  hpt_context_share_scene makes a context on `device` from a
+   prepared context's host-built scene -- the XML is not parsed, the hair not loaded and the
+   kd-tree not built again, only uploaded -- and hpt_render_multi renders shard g of n on
+   ctxs[g] (on their own threads), combines the films on ctxs[0]'s device (peer copies over
+   xGMI, added in shard order: the same sum as adding the n host films) and ACCUMULATES the
+   result into film_rgbw.  params->shard / n_shards are ignored. */
+int hpt_context_share_scene(hpt_context *src, int device, hpt_context **out);
+int hpt_render_multi(hpt_context *const *ctxs, int n, const hpt_render_params *params, float *film_rgbw);
+
 typedef struct hpt_stats {
     double ms_total;               /* host wall time of the render call */
     double ms_camera, ms_trace, ms_primary, ms_shade, ms_post, ms_gather; /* HIP event sums */
@@ -195,6 +209,9 @@ typedef struct hpt_stats {
        earlier render of the same spp range and shard (no queue length read back per bounce), and
        waves rendered again because a bounce outgrew its schedule (HPT_BOUNCE_AHEAD=0: neither) */
     uint64_t waves_ahead, schedule_misses;
+    /* waves whose schedule was launched ahead but did not cover them (the tail declined, or
+       bounces ran past it): finished bounce by bounce and their schedule re-recorded */
+    uint64_t schedule_extensions;
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 

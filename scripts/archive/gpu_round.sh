@@ -2,7 +2,7 @@
 # One GPU call of the build/measure loop (run on the box from the repo root through gpurun):
 #   1. the gpu-marked tests (parity, configs)
 #   2. the headline bench with the default library, then with every libv_<V> variant named in $VARIANTS
-# Usage: TAG=r02a VARIANTS="w4" scripts/gpu_round.sh [pytest selection]
+# Usage: TAG=r02a VARIANTS="w4" scripts/archive/gpu_round.sh [pytest selection]
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B kd-tree build parameters (hair shape kd* properties) on the bench workload.
-# Usage: scripts/kd_variants.sh "k=v,k=v" "k=v" ...
+# Usage: scripts/archive/kd_variants.sh "k=v,k=v" "k=v" ...
 set -o pipefail
 mkdir -p gpurun_out
 for kd in "" "$@"; do

@@ -3,7 +3,7 @@
 # for each config, a rocprofv3 kernel trace + stats, the FETCH_SIZE and WRITE_SIZE PMC passes,
 # a committed-style summary (tools/rocpd_summary.py -> profiles/), then the bench line with
 # roofline + cpu_baseline (which reads the traffic JSON just written).
-# Usage: scripts/r03_configs.sh <config> [<config> ...]
+# Usage: scripts/archive/r03_configs.sh <config> [<config> ...]
 #   C2 straight_kk, C3 furball_marschner (headline), C4 curly_marschner, C5 furball_1m
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -1,5 +1,5 @@
 # A/B of kernel variant builds (make variant V=<name>): headline bench per build
-# usage: scripts/r03_variants.sh name1 name2 ...   ("main" = the default build)
+# usage: scripts/archive/r03_variants.sh name1 name2 ...   ("main" = the default build)
 set -o pipefail
 mkdir -p gpurun_out/var
 for V in "$@"; do

@@ -22,13 +22,13 @@ pytestmark = pytest.mark.gpu
 HAIRCURL_RADII = (0.0025, 0.0025)
 
 
-def _render_twice(name, n, radii, monkeypatch, ahead, hook, tail, max_wave=0):
+def _render_twice(name, n, radii, monkeypatch, ahead, hook, tail, max_wave=0, times=2):
     monkeypatch.setenv("HPT_BOUNCE_AHEAD", ahead)
     monkeypatch.setenv("HPT_SCHEDULE_TEST", hook)
     monkeypatch.setenv("HPT_TAIL_PATHS", tail)
     _, r, _ = scene_util.make(name, n, 64, 48, 16, device=0, radii=radii)
     out = []
-    for _ in range(2):
+    for _ in range(times):
         film = r.render(0, 16, max_wave_paths=max_wave, collect_stats=True)
         out.append((film, r.stats()))
     r.close()
@@ -42,9 +42,10 @@ def test_bounce_ahead_bit_identical(name, n, radii, tail, monkeypatch):
     (ref, s0), _ = _render_twice(name, n, radii, monkeypatch, "0", "0", tail)
     assert s0.waves_ahead == 0 and s0.schedule_misses == 0
     for hook in ("0", "1", "2"):
-        (first, s1), (second, s2) = _render_twice(name, n, radii, monkeypatch, "1", hook, tail)
+        (first, s1), (second, s2), (third, s3) = _render_twice(name, n, radii, monkeypatch, "1", hook, tail, times=3)
         np.testing.assert_array_equal(first, ref)
         np.testing.assert_array_equal(second, ref)
+        np.testing.assert_array_equal(third, ref)
         # the per-path work is the same whatever the schedule
         for s in (s1, s2):
             assert (s.bounces, s.tail_paths, s.max_bounces) == (s0.bounces, s0.tail_paths, s0.max_bounces), hook
@@ -58,8 +59,10 @@ def test_bounce_ahead_bit_identical(name, n, radii, tail, monkeypatch):
             assert s2.paths == s0.paths and s2.waves == s0.waves
         elif tail != "0":
             # one wavefront bounce short: the tail launched ahead declines its bounce (too many
-            # live paths) and the host finishes bounce by bounce
-            assert s2.schedule_misses == 0 and s2.waves_ahead == 0
+            # live paths) and the host finishes bounce by bounce, re-recording the schedule as the
+            # part launched ahead plus the bounces it read back: the third render runs ahead
+            assert s2.schedule_misses == 0 and s2.waves_ahead == 0 and s2.schedule_extensions == 1
+            assert (s3.waves_ahead, s3.schedule_misses, s3.schedule_extensions) == (1, 0, 0)
         else:
             # no tail in the schedule: the hook leaves it whole
             assert (s2.waves_ahead, s2.schedule_misses) == (1, 0)

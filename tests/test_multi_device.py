@@ -1,0 +1,93 @@
+"""One process, several devices (hpt_context_share_scene / hpt_render_multi; the reference loads
+the scene once and hands it to every worker, src/mitsuba/mitsuba.cpp:281-329).
+
+CPU: a host-only context shares a prepared scene without parsing, loading or building it again
+(the kd-tree and every table are the source's: the build time is the source's own figure).
+GPU: two contexts on device 0 (the box has one GPU; the shards time-share it) render the
+Hilbert-cyclic halves of a frame and combine them on the device; the film equals the one-context
+render up to the order of the per-pixel sums, and bit-for-bit the host sum of the two shard films.
+The CLI's --devices 0,0 renders through the same path."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import scene_util
+from mitsuba_amd import native
+
+
+def _host_ctx(xml, defines):
+    r = native.Renderer(device=native.HOST_ONLY)
+    r.load_scene_xml(xml, defines)
+    r.prepare()
+    return r
+
+
+def test_share_scene_host_only(tmp_path):
+    xml = scene_util.scenes.make_scene("furball_marschner", str(tmp_path), n_strands=600)
+    src = _host_ctx(xml, {"spp": 4, "width": 40, "height": 24})
+    dst = src.share_scene(native.HOST_ONLY)
+    a, b = src.info(), dst.info()
+    for f in ("width", "height", "spp", "max_depth", "segments", "kd_nodes", "kd_indices", "kd_depth", "bsdf"):
+        assert getattr(a, f) == getattr(b, f), f
+    # not rebuilt: the shared tree carries the source build's own timing
+    assert a.kd_build_seconds == b.kd_build_seconds
+    na, ia, _ = src.kdtree()
+    nb, ib, _ = dst.kdtree()
+    np.testing.assert_array_equal(na, nb)
+    np.testing.assert_array_equal(ia, ib)
+    assert src.scene_json() == dst.scene_json()
+    dst.close()
+    src.close()
+
+
+def test_share_scene_needs_a_prepared_source(tmp_path):
+    xml = scene_util.scenes.make_scene("furball_marschner", str(tmp_path), n_strands=100)
+    r = native.Renderer(device=native.HOST_ONLY)
+    r.load_scene_xml(xml, {})
+    with pytest.raises(native.HairPTError):
+        r.share_scene(native.HOST_ONLY)
+    r.close()
+
+
+@pytest.mark.gpu
+def test_render_multi_two_contexts_one_device(tmp_path):
+    xml = scene_util.scenes.make_scene("furball_marschner", str(tmp_path), n_strands=1500)
+    defs = {"spp": 8, "width": 96, "height": 64}
+    r0 = native.Renderer(device=0)
+    r0.load_scene_xml(xml, defs)
+    r0.prepare()
+    r1 = r0.share_scene(0)
+    single = r0.render(0, 8)
+    multi = native.Renderer.render_multi([r0, r1], 0, 8)
+    # the same shards rendered separately and summed on the host, in shard order
+    f0 = r0.render(0, 8, shard=0, n_shards=2)
+    f1 = r1.render(0, 8, shard=1, n_shards=2)
+    np.testing.assert_array_equal(multi, f0 + f1)
+    np.testing.assert_allclose(multi, single, rtol=1e-5, atol=1e-5)
+    # accumulating into a film (the CLI's -r chunks)
+    acc = native.Renderer.render_multi([r0, r1], 0, 4)
+    acc = native.Renderer.render_multi([r0, r1], 4, 8, film=acc)
+    np.testing.assert_allclose(acc, single, rtol=1e-5, atol=1e-5)
+    r1.close()
+    r0.close()
+
+
+@pytest.mark.gpu
+def test_cli_devices_share_one_scene(tmp_path):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
+    import film as ref
+    cli = os.path.join(os.path.dirname(native.__file__), "..", "bin", "mitsuba")
+    xml = scene_util.scenes.make_scene("furball_marschner", str(tmp_path), n_strands=800)
+    base = [cli, "-D", "spp=8", "-D", "width=64", "-D", "height=48"]
+    one = subprocess.run(base + ["-o", str(tmp_path / "one.png"), xml], capture_output=True, text=True, timeout=300)
+    assert one.returncode == 0, one.stderr
+    two = subprocess.run(base + ["--devices", "0,0", "-o", str(tmp_path / "two.png"), xml], capture_output=True,
+                         text=True, timeout=300)
+    assert two.returncode == 0, two.stderr
+    assert two.stdout.count("Scene \"") == 1 and "shared with 1 more device context" in two.stdout
+    a = ref.read_png(str(tmp_path / "one.png")).astype(int)
+    b = ref.read_png(str(tmp_path / "two.png")).astype(int)
+    assert np.abs(a - b).max() <= 1

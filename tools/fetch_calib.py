@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Summarise the FETCH_SIZE / WRITE_SIZE calibration (tools/fetch_calib.hip under
-rocprofv3 --pmc, scripts/r03_fetch_calib.sh): per launch, the counter in bytes
+rocprofv3 --pmc, scripts/archive/r03_fetch_calib.sh): per launch, the counter in bytes
 divided by the lines the launch touched and by the bytes it requested.
 
 Usage: python tools/fetch_calib.py <dir with fetch/ and write/ rocpd outputs> <program stdout>

@@ -58,17 +58,19 @@ def main():
     out = {"config": a.config, "N1_ms": round(t1 * 1e3, 3), "shards": {}}
     for n in [int(x) for x in a.ns.split(",")]:
         ranks = range(n) if a.all_ranks else sorted({0, n - 1})
-        ts = {}
+        ts, work = {}, {}
         for k in ranks:
             t, s = timed(k, n)
             ts[k] = (round(t * 1e3, 3), round(s.ms_trace, 3), round(s.ms_tail, 3))
+            work[k] = (int(s.bounces), int(s.paths), round(s.ms_trace_packet, 3))
             if k == 0:
                 kern = {n: round(getattr(s, "ms_" + n), 3) for n in
                         ("camera", "trace_packet", "primary", "trace", "shade", "post", "tail", "gather")}
                 print("N=%d rank 0 kernels (ms): %s; sum %.2f of %.2f wall" % (n, kern, sum(kern.values()), t * 1e3),
                       flush=True)
         worst = max(v[0] for v in ts.values())
-        out["shards"][n] = {"per_rank_ms_trace_tail": ts, "max_ms": worst, "efficiency": round(t1 * 1e3 / (n * worst), 4)}
+        out["shards"][n] = {"per_rank_ms_trace_tail": ts, "per_rank_bounces_paths_packet_ms": work, "max_ms": worst,
+                            "efficiency": round(t1 * 1e3 / (n * worst), 4)}
         print("N=%d ranks %s -> max %.2f ms, strong-scaling efficiency %.3f" % (n, ts, worst, t1 * 1e3 / (n * worst)),
               flush=True)
     print(json.dumps(out))

@@ -55,6 +55,7 @@ def main():
             rec = buf[li]
             rec = rec[rec[:, 2] > 0].astype(np.float64)
             beg, ex, end, claimed, infl = rec[:, 0], rec[:, 1], rec[:, 2], rec[:, 3], rec[:, 4]
+            drounds, dlanes = rec[:, 5], rec[:, 6]
             t0 = beg.min()
             tdry = ex[ex > 0].min() if (ex > 0).any() else end.max()
             tick = 0.01  # us per tick (100 MHz)
@@ -67,7 +68,14 @@ def main():
                         "start_spread_us": round((np.percentile(beg, 99) - t0) * tick, 1),
                         "in_flight_at_dry": int(infl.sum()),
                         "rays_per_us_main": round(claimed.sum() / max(main_us, 1e-9), 1),
-                        "wave_end_pct_us": {p: round(float(np.percentile(ends, p)), 1) for p in (50, 90, 99, 99.9)}})
+                        "wave_end_pct_us": {p: round(float(np.percentile(ends, p)), 1) for p in (50, 90, 99, 99.9)},
+                        # drain phase (after the first dry point): wave exits, drain-loop rounds and lane use
+                        "exit_after_dry_pct_us": {p: round(float(np.percentile((end - tdry) * tick, p)), 1)
+                                                  for p in (10, 25, 50, 75, 90, 99, 100)},
+                        "waves_alive_after_dry_us": {t: int(((end - tdry) * tick > t).sum())
+                                                     for t in (0, 50, 100, 200, 300, 400, 500)},
+                        "drain_rounds_pct": {p: round(float(np.percentile(drounds, p)), 1) for p in (50, 90, 99, 100)},
+                        "drain_lane_use": round(float(dlanes.sum() / max(64.0 * drounds.sum(), 1.0)), 3)})
     for o in out:
         print(json.dumps(o))
     r.close()
