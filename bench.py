@@ -66,6 +66,9 @@ def parse():
     ap.add_argument("--cpu-nproc-run", choices=["auto", "off"], default="auto",
                     help="also time the sample on one thread per affinity CPU (nproc, SURVEY.md 8(d)) when that "
                          "differs from the effective CPUs")
+    ap.add_argument("--balance", choices=["on", "off"], default="on",
+                    help="N > 1: after the warm-up, re-deal the blocks by the work each shaded (path-bounces "
+                         "summed over ranks, hpt_set_block_weights); off: the Hilbert-cyclic deal")
     ap.add_argument("--workdir", default=os.path.join(tempfile.gettempdir(), "hpt_bench"))
     return ap.parse_args()
 
@@ -203,6 +206,14 @@ def main():
 
     for _ in range(args.warmup):
         step(1)
+    balanced = False
+    if world > 1 and args.balance == "on":
+        # the warm-up frame's per-block path-bounces, summed over the ranks, deal the blocks
+        # longest-first (the same deal on every rank); one more frame records its schedules
+        distributed.balance_blocks(r, ((W + 31) // 32) * ((H + 31) // 32), world, dist,
+                                   "cuda:%d" % local if backend == "nccl" else "cpu")
+        step(1)
+        balanced = True
     # one untimed counted frame: traversal counters for the byte model (the
     # render is deterministic, so every frame has exactly these counts)
     step(2)
@@ -296,6 +307,8 @@ def main():
             "data": "synthetic hair (seeded, BINARY_HAIR; reference hair blobs absent) lit by the scene's sunsky (Hosek-Wilkie sky + Preetham sun rasterised like sunsky.cpp)",
             "config": {"workload": workload,
                        "paths_per_step": W * H * spp, "parallelism": "tiles%d" % world,
+                       "deal": "work-balanced (warm-up frame's path-bounces per block)" if balanced
+                       else "Hilbert-cyclic 32x32 blocks",
                        **({"rehearsal": "HPT_BENCH_BACKEND=gloo: ranks share GPUs, host-copy reduce"}
                           if host_film is not None and world > 1 else {}),
                        "kd_nodes": int(info.kd_nodes), "kd_depth": int(info.kd_depth),

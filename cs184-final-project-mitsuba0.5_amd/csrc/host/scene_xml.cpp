@@ -471,6 +471,8 @@ void parseBSDF(const Ctx &c, const XNode &b, BsdfDesc &d) {
             d.specular[i] = p.num.count("specularReflectance") ? p.num["specularReflectance"][i] : 1.0f;
         }
         d.nonlinear = num1(p, "nonlinear", 0.0f) != 0.0f;
+        /* BSDF::BSDF (bsdf.cpp:30-31): reflectances above 1 are scaled unless disabled */
+        d.ensureEnergyConservation = num1(p, "ensureEnergyConservation", 1.0f) != 0.0f;
         for (auto &kp : b.kids)
             if (kp->tag == "texture")
                 fail(c.file, kp->line, "plastic: textured reflectances are outside this path (constant colours only)");
@@ -830,6 +832,7 @@ void bsdfJSON(Json &j, const BsdfDesc &b) {
     j.num("exponent", b.exponent);
     j.boolean("nonlinear", b.nonlinear);
     j.boolean("sampleVisible", b.sampleVisible);
+    j.boolean("ensureEnergyConservation", b.ensureEnergyConservation);
     if (!b.reflectanceTexture.type.empty()) {
         const TextureDesc &t = b.reflectanceTexture;
         j.open("reflectanceTexture", '{');

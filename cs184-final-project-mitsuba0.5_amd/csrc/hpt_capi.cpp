@@ -131,6 +131,11 @@ struct hpt_context {
     uint32_t *dBlockOf = nullptr;
     int32_t *dLocalOf = nullptr;
     int ownW = -1, ownH = -1, ownShard = -1, ownShards = -1, ownCap = 0, ownLocal = 0;
+    uint64_t ownWeights = 0;            /* weightsVersion the ownership tables were dealt with */
+    std::vector<uint32_t> ownBlocks;    /* the image blocks of dBlockOf, on the host */
+    uint32_t *dBlockCost = nullptr;     /* path-bounces shaded per owned block (HptPaths::blockCost) */
+    std::vector<double> blockWeights;   /* hpt_set_block_weights (empty: Hilbert-cyclic deal) */
+    uint64_t weightsVersion = 0;
     hpt_stats stats;
     std::vector<hipEvent_t> evPool;
     /* hpt_render_multi: this context's shard film, and (on the receiving context) the staging
@@ -330,6 +335,7 @@ void hpt_context_destroy(hpt_context *c) {
     if (c->partial) (void) hipFree(c->partial);
     if (c->dBlockOf) (void) hipFree(c->dBlockOf);
     if (c->dLocalOf) (void) hipFree(c->dLocalOf);
+    if (c->dBlockCost) (void) hipFree(c->dBlockCost);
     if (c->scDev) (void) hipFree(c->scDev);
     if (c->mfilm) (void) hipFree(c->mfilm);
     if (c->mstage) (void) hipFree(c->mstage);
@@ -978,31 +984,66 @@ static std::vector<uint32_t> blockOrder(int nbx, int nby) {
     return order;
 }
 
-/* upload this shard's block ownership tables (cached per frame shape and shard) */
-static int ensureOwnership(hpt_context *c, int W, int H, int nbx, int nby, int shard, int nShards) {
-    if (c->ownW == W && c->ownH == H && c->ownShard == shard && c->ownShards == nShards) return HPT_OK;
+/* The shard of every image block.  Without weights: position i of the Hilbert order goes to
+   shard i mod N (compact patches of N blocks, one block each).  With weights (the measured
+   work of each block, hpt_set_block_weights): longest-processing-time first -- blocks in
+   descending weight (ties in Hilbert order) each to the shard with the least weight so far
+   (ties to the lowest shard) -- the same deal on every rank given the same weights. */
+static std::vector<int> dealBlocks(int nbx, int nby, int nShards, const std::vector<double> &weights) {
     const std::vector<uint32_t> order = blockOrder(nbx, nby);
+    std::vector<int> shardOf(order.size(), 0);
+    if (weights.size() != order.size()) {
+        for (size_t i = 0; i < order.size(); ++i) shardOf[order[i]] = (int) (i % (size_t) nShards);
+        return shardOf;
+    }
+    std::vector<size_t> byWeight(order.size());
+    for (size_t i = 0; i < order.size(); ++i) byWeight[i] = i; /* Hilbert positions */
+    std::stable_sort(byWeight.begin(), byWeight.end(),
+                     [&](size_t a, size_t b) { return weights[order[a]] > weights[order[b]]; });
+    std::vector<double> load((size_t) nShards, 0.0);
+    for (size_t k : byWeight) {
+        const int r = (int) (std::min_element(load.begin(), load.end()) - load.begin());
+        shardOf[order[k]] = r;
+        load[(size_t) r] += weights[order[k]];
+    }
+    return shardOf;
+}
+
+/* upload this shard's block ownership tables (cached per frame shape, shard and deal) */
+static int ensureOwnership(hpt_context *c, int W, int H, int nbx, int nby, int shard, int nShards) {
+    if (c->ownW == W && c->ownH == H && c->ownShard == shard && c->ownShards == nShards &&
+        c->ownWeights == c->weightsVersion)
+        return HPT_OK;
+    const std::vector<uint32_t> order = blockOrder(nbx, nby);
+    const std::vector<int> shardOf = dealBlocks(nbx, nby, nShards, c->blockWeights);
     std::vector<uint32_t> blockOf;
     std::vector<int32_t> localOf(order.size(), -1);
-    for (size_t i = (size_t) shard; i < order.size(); i += (size_t) nShards) {
-        localOf[order[i]] = (int32_t) blockOf.size();
-        blockOf.push_back(order[i]);
-    }
+    for (size_t i = 0; i < order.size(); ++i) /* a shard's blocks in Hilbert order (locality) */
+        if (shardOf[order[i]] == shard) {
+            localOf[order[i]] = (int32_t) blockOf.size();
+            blockOf.push_back(order[i]);
+        }
     const int n = (int) order.size();
     if (n > c->ownCap) {
         if (c->dBlockOf) (void) hipFree(c->dBlockOf);
         if (c->dLocalOf) (void) hipFree(c->dLocalOf);
+        if (c->dBlockCost) (void) hipFree(c->dBlockCost);
         c->dBlockOf = nullptr;
         c->dLocalOf = nullptr;
+        c->dBlockCost = nullptr;
         c->ownCap = 0;
         HIPCHK(c, hipMalloc((void **) &c->dBlockOf, n * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc((void **) &c->dLocalOf, n * sizeof(int32_t)));
+        HIPCHK(c, hipMalloc((void **) &c->dBlockCost, 2 * n * sizeof(uint32_t))); /* + a snapshot per wave */
         c->ownCap = n;
     }
     if (!blockOf.empty())
         HIPCHK(c, hipMemcpy(c->dBlockOf, blockOf.data(), blockOf.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->dLocalOf, localOf.data(), localOf.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIPCHK(c, hipMemset(c->dBlockCost, 0, n * sizeof(uint32_t))); /* costs are per ownership */
     c->ownW = W, c->ownH = H, c->ownShard = shard, c->ownShards = nShards, c->ownLocal = (int) blockOf.size();
+    c->ownWeights = c->weightsVersion;
+    c->ownBlocks.assign(blockOf.begin(), blockOf.end());
     return HPT_OK;
 }
 
@@ -1037,6 +1078,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     }
     hipStream_t s = c->stream;
     c->P.bucketQ = c->claimBuckets ? c->bucketBuf : nullptr;
+    c->P.blockCost = c->dBlockCost;
     c->P.bucketCap = (uint32_t) std::min<uint64_t>(2 * c->capacity, 0xffffffffull);
     if (!c->scDev) HIPCHK(c, hipMalloc((void **) &c->scDev, sizeof(HptScene)));
     if (c->scShadow.size() != sizeof(HptScene) || std::memcmp(c->scShadow.data(), &c->sc, sizeof(HptScene)) != 0) {
@@ -1108,6 +1150,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         w.shard = shard;
         w.nShards = nShards;
         w.blockOf = c->dBlockOf;
+        c->P.costSpp = w.nSpp;
         w.localOf = c->dLocalOf;
         c->stats.waves++;
         /* a wave rendered again after its schedule overflowed must not count twice: the timing
@@ -1116,29 +1159,28 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         size_t evMarkOther[7];
         for (int i = 0; i < 7; ++i) evMarkOther[i] = evOther[i].size();
         if (counted) HIPCHK(c, hipMemcpyAsync(c->dstats + 24, c->dstats, 24 * 8, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->dBlockCost + c->ownCap, c->dBlockCost, localBlocks * 4, hipMemcpyDeviceToDevice, s));
         HIPCHK(c, hipMemsetAsync(c->counters, 0, HPT_COUNTER_WORDS * 4, s));
-        uint32_t *C = c->counters, *dst = counted ? (uint32_t *) c->dstats : nullptr, *cur = C + HPT_CURSOR_OFFSET;
+        uint32_t *C = c->counters, *dst = counted ? (uint32_t *) c->dstats : nullptr;
+        uint32_t *curPacket = C + HPT_CURSOR_SET(2), *curOverflow = C + HPT_CURSOR_SET(3);
         /* the camera pass is bounce 0 (parity 0) */
         e = timed(0, [&] { return hpt_launch_camera(sc, w, c->P, c->qTrace, C + HPT_C_TRACE(0), s); });
         if (e) break;
         /* the camera pass has no shadow rays: qShadow / C[SHADOW(0)] take the rays of overflowing packets */
         e = c->packets ? timed(6, [&] {
-            return hpt_launch_trace_packet(sc, c->P, c->qTrace, C + HPT_C_TRACE(0), cur, dst, w.nPaths, c->qShadow,
+            return hpt_launch_trace_packet(sc, c->P, c->qTrace, C + HPT_C_TRACE(0), curPacket, dst, w.nPaths, c->qShadow,
                                            C + HPT_C_SHADOW(0), s);
         })
                        : timed(-1, [&] {
                              return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(0),
-                                                     C + HPT_C_SHADOW(0), cur, dst, w.nPaths, s);
+                                                     C + HPT_C_SHADOW(0), curPacket, dst, w.nPaths, s);
                          });
         if (e) break;
         reportLaunch("camera");
-        e = hpt_launch_clear(C, 0, s);
-        if (e) break;
         if (c->packets) {
-            /* overflowing packets' rays (none at the shipped configs), then fresh cursors again */
-            e = hpt_launch_trace_overflow(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_SHADOW(0), cur,
+            /* overflowing packets' rays (none at the shipped configs), their own cursor set */
+            e = hpt_launch_trace_overflow(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_SHADOW(0), curOverflow,
                                           std::min<uint64_t>(w.nPaths, 1u << 16), s);
-            if (e == hipSuccess) e = hpt_launch_clear(C, 0, s);
             if (e) break;
         }
         e = timed(1, [&] {
@@ -1169,8 +1211,9 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             });
             if (e1) return e1;
             e1 = timed(-1, [&] {
-                return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(p), C + HPT_C_SHADOW(p), cur, dst,
-                                        2ull * grid, s, c->P.bucketQ ? C + HPT_C_BUCKET(p, 0) : nullptr);
+                return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(p), C + HPT_C_SHADOW(p),
+                                        C + HPT_CURSOR_SET(p), dst, 2ull * grid, s,
+                                        c->P.bucketQ ? C + HPT_C_BUCKET(p, 0) : nullptr, C, q);
             });
             if (e1) return e1;
             reportLaunch("bounce");
@@ -1180,8 +1223,6 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                 (void) hipEventElapsedTime(&ms, evTrace.back().first, evTrace.back().second);
                 std::fprintf(stderr, "[bounce %d] shade %llu -> trace %.3f ms\n", b, (unsigned long long) grid, ms);
             }
-            e1 = hpt_launch_clear(C, p, s);
-            if (e1) return e1;
             return timed(3, [&] {
                 return hpt_launch_post(sc, c->P, c->qTrace, C + HPT_C_TRACE(p), c->qShade[q], C + HPT_C_SHADE(q), C, grid, s);
             });
@@ -1246,6 +1287,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                 evOther[i].resize(evMarkOther[i]);
             }
             if (counted) HIPCHK(c, hipMemcpyAsync(c->dstats, c->dstats + 24, 24 * 8, hipMemcpyDeviceToDevice, s));
+            HIPCHK(c, hipMemcpyAsync(c->dBlockCost, c->dBlockCost + c->ownCap, localBlocks * 4, hipMemcpyDeviceToDevice, s));
             j0 -= (int) nSpp;
             continue;
         }
@@ -1452,6 +1494,41 @@ int hpt_render_multi(hpt_context *const *ctxs, int n, const hpt_render_params *p
     }
     HIPCHK(c0, hipMemcpyAsync(film, c0->mfilm, pixels * 16, hipMemcpyDeviceToHost, c0->stream));
     HIPCHK(c0, hipStreamSynchronize(c0->stream));
+    return HPT_OK;
+}
+
+int hpt_block_deal(int width, int height, int n_shards, const double *weights, int32_t *shard_of_block) {
+    if (width <= 0 || height <= 0 || n_shards <= 0 || !shard_of_block) return HPT_EINVAL;
+    const int nbx = (width + HPT_BLOCK - 1) / HPT_BLOCK, nby = (height + HPT_BLOCK - 1) / HPT_BLOCK;
+    std::vector<double> w;
+    if (weights) w.assign(weights, weights + (size_t) nbx * nby);
+    const std::vector<int> s = dealBlocks(nbx, nby, n_shards, w);
+    for (size_t i = 0; i < s.size(); ++i) shard_of_block[i] = s[i];
+    return HPT_OK;
+}
+
+int hpt_set_block_weights(hpt_context *c, const double *weights, int n_blocks) {
+    if (!c || n_blocks < 0 || (n_blocks > 0 && !weights)) return HPT_EINVAL;
+    for (int i = 0; i < n_blocks; ++i)
+        if (!(weights[i] >= 0.0) || !std::isfinite(weights[i]))
+            return setErr(c, HPT_EINVAL, "block weights must be finite and >= 0");
+    c->blockWeights.assign(weights, weights + n_blocks);
+    c->weightsVersion++;
+    c->schedules.clear(); /* a shard's waves change with the deal: their bounce schedules do too */
+    return HPT_OK;
+}
+
+int hpt_get_block_costs(hpt_context *c, uint64_t *costs, int n_blocks) {
+    if (!c || !costs || n_blocks < 0) return HPT_EINVAL;
+    std::memset(costs, 0, (size_t) n_blocks * sizeof(uint64_t));
+    if (c->device == HPT_HOST_ONLY || !c->dBlockCost || c->ownBlocks.empty()) return HPT_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    std::vector<uint32_t> local(c->ownBlocks.size());
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipMemcpy(local.data(), c->dBlockCost, local.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemset(c->dBlockCost, 0, local.size() * 4));
+    for (size_t k = 0; k < local.size(); ++k)
+        if ((int) c->ownBlocks[k] < n_blocks) costs[c->ownBlocks[k]] = local[k];
     return HPT_OK;
 }
 

@@ -9,8 +9,8 @@
 #include "../hpt_device.h"
 
 /* Counter block (uint32 words).  Bounce b uses the slots of parity
-   p = b & 1 (the camera pass is bounce 0); k_clear zeroes the other parity's
-   slots once bounce b's trace launch has run. */
+   p = b & 1 (the camera pass is bounce 0); bounce b's trace launch zeroes the other parity's
+   slots (clearNextParity). */
 #define HPT_C_TRACE(p) (0 + (p))  /* closest-hit rays of bounce b (traceQ[p]) */
 #define HPT_C_SHADOW(p) (2 + (p)) /* shadow rays of bounce b (shadowQ[p]) */
 #define HPT_C_SHADE(p) (4 + (p))  /* paths bounce b shades (shadeQ[p]: survivors of the previous post) */
@@ -38,7 +38,12 @@
 #define HPT_CURSORS 64
 #define HPT_CURSOR_STRIDE 32
 #define HPT_CURSOR_OFFSET 64
-#define HPT_COUNTER_WORDS (HPT_CURSOR_OFFSET + HPT_CURSORS * HPT_CURSOR_STRIDE)
+/* cursor sets: 0 / 1 the bounce trace launches of parity 0 / 1 (k_trace of parity p zeroes set
+   p ^ 1 and the counts of parity p ^ 1 for the next bounce: no clearing launch), 2 the camera
+   packets, 3 their overflow launch; all four start at zero with the wave's counter block */
+#define HPT_CURSOR_SETS 4
+#define HPT_CURSOR_SET(s) (HPT_CURSOR_OFFSET + (s) * HPT_CURSORS * HPT_CURSOR_STRIDE)
+#define HPT_COUNTER_WORDS (HPT_CURSOR_OFFSET + HPT_CURSOR_SETS * HPT_CURSORS * HPT_CURSOR_STRIDE)
 
 /* One wave of paths: every pixel of this shard's 32x32 blocks x samples
    [sppBegin, sppBegin + nSpp).  Path id = slot * nSpp + (j - sppBegin),
@@ -93,6 +98,11 @@ struct HptPaths {
        each a trace-queue position, or a shadow-queue position | HPT_BUCKET_SHADOW */
     uint32_t *bucketQ;
     uint32_t bucketCap;
+    /* per owned 32x32 block: path-bounces shaded (k_shade, k_tail), the measured work the cost-
+       balanced shard deal reads back (hpt_get_block_costs); nullptr: not counted.  costSpp is
+       the wave's nSpp (path id -> block: id / nSpp >> 10) */
+    uint32_t *blockCost;
+    uint32_t costSpp;
     float4 *bw;        /* bsdf weight rgb, bsdf pdf                  */
     float4 *sdir;      /* shadow ray direction xyz, maxt             */
     float4 *scontrib;  /* NEE contribution rgb (added if unoccluded) */
@@ -108,10 +118,13 @@ struct HptPaths {
 hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPaths &P, uint32_t *traceQ,
                              uint32_t *nTrace, hipStream_t s);
 /* one persistent traversal launch: closest-hit rays traceQ[0, *nTrace), shadow rays shadowQ[0, *nShadow) */
-/* nBucket (nullptr: queue order): the launch's HPT_BUCKETS claim-order bucket lengths (P.bucketQ) */
+/* nBucket (nullptr: queue order): the launch's HPT_BUCKETS claim-order bucket lengths (P.bucketQ).
+   counters (nullptr: none): a bounce launch of parity p = nextParity ^ 1 also zeroes the counts and
+   cursor set of parity nextParity, which the next bounce appends to / claims from */
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
-                            uint64_t maxItems, hipStream_t s, const uint32_t *nBucket = nullptr);
+                            uint64_t maxItems, hipStream_t s, const uint32_t *nBucket = nullptr,
+                            uint32_t *counters = nullptr, uint32_t nextParity = 0);
 hipError_t hpt_launch_env_filtered_batch(const HptScene &sc, int n, const float *d, const float *rx, const float *ry,
                                         float *out, hipStream_t s);
 /* closest-hit rays as 64-ray packets (coherent rays: the camera pass); the rays of a packet whose
@@ -137,7 +150,6 @@ hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t
 #define HPT_ITEMS_ON_DEVICE (~0ull)
 hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
                            uint32_t *counters, uint64_t items, uint32_t tailFrom, hipStream_t s);
-hipError_t hpt_launch_clear(uint32_t *counters, uint32_t parity, hipStream_t s);
 /* dst[i] += src[i] over n RGBW pixels (hpt_render_multi's film combine) */
 hipError_t hpt_launch_film_add(float4 *dst, const float4 *src, size_t n, hipStream_t s);
 /* k_splat + k_gather; partial = (nPaths / nSpp) * 9 float4 of scratch */

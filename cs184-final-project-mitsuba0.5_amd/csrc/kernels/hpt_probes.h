@@ -82,6 +82,7 @@ struct TailProbe {
     unsigned long long begin = __builtin_amdgcn_s_memrealtime();
     __device__ void onItem(bool counted) { items += counted ? 1u : 0u; }
     __device__ void onRound() { ++rounds; }
+    __device__ void onDrainRound(uint64_t) { ++rounds; }
     /* phase 0: the iteration starts (shade), 1: trace starts, 2: post starts, 3: the iteration ends */
     __device__ void phase(int k) {
         const unsigned long long t = __builtin_amdgcn_s_memrealtime();
@@ -120,6 +121,7 @@ struct TailProbe {
 #else
     __device__ void onItem(bool) {}
     __device__ void onRound() {}
+    __device__ void onDrainRound(uint64_t) {}
     __device__ void phase(int) {}
     __device__ void finish() {}
 #endif

@@ -647,45 +647,32 @@ HD uint32_t selectBit(uint64_t m, uint32_t k) {
    traced) and finish(key, r).  Every wave exits once all shards are exhausted and its
    lanes have drained, so the grid always completes. */
 #include "hpt_probes.h"
-template <int STACK, bool STATS, bool SPLIT = (!STATS && HPT_DRAIN_SPLIT), class IO>
-__device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint32_t *cursors, uint2 *stk,
-                                                uint32_t *stats) {
-    TraceProbe probe;
-    const uint32_t lane = __lane_id();
-    TraceRay r;
-    TraceCounters tc;
-    uint32_t nC = 0, nS = 0, nU = 0;
-    uint32_t maxRounds = 0, maxRestarts = 0, restartRays = 0, restarts = 0; /* STATS: per-ray tails */
-    auto rayDone = [&](uint32_t leaves, uint32_t rs) {
-        if (STATS) {
-            maxRounds = max(maxRounds, leaves);
-            maxRestarts = max(maxRestarts, rs);
-            restartRays += rs > 0 ? 1u : 0u;
-            restarts += rs;
-        }
-    };
-    bool active = false, exhausted = false;
-    uint32_t shard = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % HPT_CURSORS;
-    int tried = 0;
-    /* drain splitting (HPT_DRAIN_SPLIT; never in the counted kernels, whose counts price the
-       unsplit traversal): lanes of split rays, and those of them that have finished their
-       interval while the ray's answer is still open (wave-uniform masks) */
-    static_assert(!(SPLIT && STATS), "the counted traversal is not split");
+/* Drain splitting (HPT_DRAIN_SPLIT).  Once a persistent wave's claims find the queue empty, an
+   idle lane takes over part of a running ray of its wave (see above); the members of a split
+   ray (same LDS key, same kind) each trace their interval and decide() gives the ray its
+   answer once it is decided.  Wave-uniform state: the lanes of split rays, and those of them
+   that have finished their interval while the ray's answer is still open.  Used by the drain of
+   tracePersistent and by k_tail, whose few live rays leave most lanes of a wave idle. */
+template <int STACK>
+struct RaySplitter {
+    uint2 *stk;
+    int stride;
     uint64_t splitM = 0, waitM = 0;
-    const int stride = (int) blockDim.x;
-    /* the j-th of n pieces of [a, b] starts here (the same expression on the donor and the helper) */
-    auto pieceStart = [](float a, float b, uint32_t j, uint32_t n) {
-        return j >= n ? b : a + (b - a) * ((float) j / (float) n);
-    };
     uint32_t rot = 0; /* rotates which running rays get helpers first */
+    /* the j-th of n pieces of [a, b] starts here (the same expression on the donor and the helper) */
+    static __device__ __forceinline__ float pieceStart(float a, float b, uint32_t j, uint32_t n) {
+        return j >= n ? b : a + (b - a) * ((float) j / (float) n);
+    }
     /* the lane index, recomputed where it is needed (kept live from the top it costs the
        traversal a register) */
-    auto laneNow = []() {
+    static __device__ __forceinline__ uint32_t laneNow() {
         uint32_t l;
         asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
         return l;
-    };
-    auto splitStep = [&](TraceRay &r, bool &active) {
+    }
+    /* whether this lane's ray is a member of a split ray (its answer is decide()'s) */
+    __device__ __forceinline__ bool member() const { return ((splitM >> laneNow()) & 1u) != 0; }
+    __device__ __forceinline__ void step(TraceRay &r, bool &active) {
         const uint32_t lane = laneNow();
         const uint64_t actM = __ballot(active), idleM = ~(actM | waitM);
         const float end = __uint_as_float(stk[(STACK + HPT_ROW_MM) * stride].y);
@@ -765,9 +752,11 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
         splitM |= __ballot(give) | __ballot(take);
         rot += nS;
         asm volatile("" ::: "memory"); /* traceRound re-reads the rows (see stashRay) */
-    };
+    }
     /* newW: split lanes that finished their interval this round */
-    auto decideSplit = [&](TraceRay &r, bool &active, uint64_t newW) {
+    template <class IO>
+    __device__ __forceinline__ uint32_t decide(const HptScene &sc, IO &io, TraceRay &r, bool &active, uint64_t newW) {
+        uint32_t nU = 0;
         const uint32_t lane = laneNow();
         waitM |= newW;
         const uint2 kr = stk[(STACK + 1) * stride], mm = stk[(STACK + HPT_ROW_MM) * stride];
@@ -808,7 +797,51 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             }
             newW &= ~memM;
         }
+        return nU;
+    }
+    /* trace every active lane's ray to its answer, idle lanes helping (IO::finish writes it);
+       returns the unoccluded shadow rays finished */
+    template <bool LAT, class IO, class Probe>
+    __device__ __forceinline__ uint32_t drain(const HptScene &sc, IO &io, TraceRay &r, bool &active, TraceCounters &tc,
+                                              Probe &probe) {
+        uint32_t nU = 0;
+        while (true) {
+            step(r, active);
+            if (__ballot(active) == 0) break;
+            probe.onDrainRound(__ballot(active));
+            bool fin = false;
+            if (active && traceRound<STACK, false, LAT>(sc, r, stk, stride, tc)) {
+                fin = true;
+                if (!member()) nU += io.finish(sc, rayKey<STACK>(stk, stride), r);
+                active = false;
+            }
+            if (splitM) nU += decide(sc, io, r, active, __ballot(fin) & splitM);
+        }
+        return nU;
+    }
+};
+
+template <int STACK, bool STATS, bool SPLIT = (!STATS && HPT_DRAIN_SPLIT), class IO>
+__device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint32_t *cursors, uint2 *stk,
+                                                uint32_t *stats) {
+    TraceProbe probe;
+    const uint32_t lane = __lane_id();
+    TraceRay r;
+    TraceCounters tc;
+    uint32_t nC = 0, nS = 0, nU = 0;
+    uint32_t maxRounds = 0, maxRestarts = 0, restartRays = 0, restarts = 0; /* STATS: per-ray tails */
+    auto rayDone = [&](uint32_t leaves, uint32_t rs) {
+        if (STATS) {
+            maxRounds = max(maxRounds, leaves);
+            maxRestarts = max(maxRestarts, rs);
+            restartRays += rs > 0 ? 1u : 0u;
+            restarts += rs;
+        }
     };
+    bool active = false, exhausted = false;
+    uint32_t shard = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % HPT_CURSORS;
+    int tried = 0;
+    static_assert(!(SPLIT && STATS), "the counted traversal is not split");
     while (true) {
         const uint64_t idle = __ballot(!active);
         if (!exhausted && __popcll(idle) >= HPT_REFILL) {
@@ -869,18 +902,8 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
     }
     if (SPLIT) {
         probe.onDrainStart();
-        while (true) {
-            splitStep(r, active);
-            if (__ballot(active) == 0) break;
-            probe.onDrainRound(__ballot(active));
-            bool fin = false;
-            if (active && traceRound<STACK, STATS>(sc, r, stk, (int) blockDim.x, tc)) {
-                fin = true;
-                if (!((splitM >> laneNow()) & 1u)) nU += io.finish(sc, rayKey<STACK>(stk, (int) blockDim.x), r);
-                active = false;
-            }
-            if (splitM) decideSplit(r, active, __ballot(fin) & splitM);
-        }
+        RaySplitter<STACK> split{stk, (int) blockDim.x};
+        nU += split.template drain<false>(sc, io, r, active, tc, probe);
     }
     probe.finish();
     if (STATS) {
@@ -2200,6 +2223,21 @@ __device__ __forceinline__ void qpushBucket(bool pred, uint32_t b, uint32_t valu
     __syncthreads();
 }
 
+/* one shaded path-bounce of path `id` per lane where pred, added to its block's cost: lanes
+   of the same block share one atomic (a wave's paths are mostly of one or two blocks) */
+__device__ __forceinline__ void countBlockCost(const HptPaths &P, bool pred, uint32_t id) {
+    if (!P.blockCost) return;
+    const uint32_t blk = pred ? (id / P.costSpp) >> 10 : 0xffffffffu;
+    uint64_t todo = __ballot(pred);
+    while (todo) { /* wave-uniform */
+        const int L = __ffsll((unsigned long long) todo) - 1;
+        const uint32_t b = (uint32_t) __builtin_amdgcn_readlane((int) blk, L);
+        const uint64_t m = __ballot(pred && blk == b);
+        if (__lane_id() == (uint32_t) L) atomicAdd(&P.blockCost[b], (uint32_t) __popcll(m));
+        todo &= ~m;
+    }
+}
+
 /* a ray's claim-order bucket: the length of its interval inside the scene box against the box
    diagonal (rays that leave the hair's box soon are short; the thresholds are the quartiles of
    the headline frame's bounce rays, tools/ray_order_probe.py) */
@@ -2424,11 +2462,25 @@ HD BouncePathIO bouncePathIO(const HptPaths &P, const uint32_t *traceQ, const ui
     }
     return io;
 }
+/* the next bounce's counts and cursor set start at zero (what a separate clearing launch did):
+   nothing of this launch reads them, and the next bounce's first kernel runs after it */
+__device__ __forceinline__ void clearNextParity(uint32_t *counters, uint32_t q) {
+    if (!counters || blockIdx.x != 0) return;
+    uint32_t *cur = counters + HPT_CURSOR_SET(q);
+    for (uint32_t i = threadIdx.x; i < HPT_CURSORS; i += blockDim.x) cur[i * HPT_CURSOR_STRIDE] = 0;
+    if (threadIdx.x == 0) {
+        counters[HPT_C_TRACE(q)] = 0;
+        counters[HPT_C_SHADOW(q)] = 0;
+        counters[HPT_C_SHADE(q)] = 0;
+        for (int b = 0; b < HPT_BUCKETS; ++b) counters[HPT_C_BUCKET(q, b)] = 0;
+    }
+}
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
     const uint32_t *__restrict__ nTrace, const uint32_t *__restrict__ nShadow, uint32_t *__restrict__ cursors,
-    const uint32_t *__restrict__ nBucket) {
+    const uint32_t *__restrict__ nBucket, uint32_t *counters, uint32_t nextParity) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
+    clearNextParity(counters, nextParity);
     BouncePathIO io = bouncePathIO(P, traceQ, shadowQ, nTrace, nShadow, nBucket);
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
@@ -2439,8 +2491,10 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
                                                                               const uint32_t *__restrict__ nShadow,
                                                                               uint32_t *__restrict__ cursors,
                                                                               const uint32_t *__restrict__ nBucket,
+                                                                              uint32_t *counters, uint32_t nextParity,
                                                                               uint32_t *stats) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
+    clearNextParity(counters, nextParity);
     BouncePathIO io = bouncePathIO(P, traceQ, shadowQ, nTrace, nShadow, nBucket);
     tracePersistent<HPT_STACK, true>(sc, io, cursors, stk + threadIdx.x, stats);
 }
@@ -2667,6 +2721,7 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
     bool cont = false, shadow = false;
     uint32_t id = 0;
     float4 in[3], cOut[4], sOut[3];
+    countBlockCost(P, tid < n, tid < n ? shadeQ[tid] : 0u);
     if (tid < n) {
         id = shadeQ[tid];
 #pragma unroll
@@ -2813,6 +2868,9 @@ struct HptTail {
     uint32_t pairs;    /* lane pairs per wave that take paths (1..32); 0: from the queue length, on the device */
     uint32_t tailFrom; /* the launch takes the queue only when it is shorter than this (device-side bounce control) */
 };
+#ifndef HPT_TAIL_SPLIT
+#define HPT_TAIL_SPLIT 1 /* k_tail's idle lanes help trace its rays (RaySplitter); 0: one lane per ray, latency mode */
+#endif
 template <bool MULTI>
 __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const HptTail &T,
                                           uint32_t *__restrict__ counters, uint2 *stk) {
@@ -2879,6 +2937,7 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
         }
         probe.phase(0);
         bool cont = false, shadow = false;
+        countBlockCost(P, live && !odd, id);
         if (live && !odd) {
             ++nb;
             shadePath<MULTI>(sc, P, id, hitRec, counters, cont, shadow, nullptr, nullptr, nullptr);
@@ -2890,7 +2949,25 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
         probe.phase(1);
         /* one call site: the shadow ray (even lane) and the continuation ray (odd
            lane) are traced at the same time, not one after the other */
-        if (live && (odd ? cont : shadow)) trace(!odd);
+        if (HPT_TAIL_SPLIT) {
+            /* ... and the wave's idle lanes help: every pending subtree of a long ray can go to
+               an idle lane (RaySplitter, the drain of k_trace), so a bounce waits for the
+               wave's longest ray cut into pieces instead of whole */
+            TraceRay r;
+            bool act = false;
+            if (live && (odd ? cont : shadow)) {
+                const bool shadowRay = !odd;
+                const float4 ro = P.ro[id], rd = shadowRay ? P.sdir[id] : P.rd[id];
+                act = beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(rd.x, rd.y, rd.z), shadowRay ? kEpsilon : ro.w, rd.w,
+                               shadowRay);
+                stashRay<HPT_STACK>(stk, (int) blockDim.x, r, id);
+                if (!act) io.finish(sc, id, r);
+            }
+            RaySplitter<HPT_STACK> split{stk, (int) blockDim.x};
+            split.template drain<false>(sc, io, r, act, tc, probe);
+        } else if (live && (odd ? cont : shadow)) {
+            trace(!odd);
+        }
         __threadfence_block(); /* the hit record is in HBM for the even lane */
         probe.phase(2);
         bool alive = false;
@@ -3164,20 +3241,6 @@ extern "C" __global__ void k_env_filtered_batch(HptScene sc, int n, const float 
     out[3 * i + 2] = v.z;
 }
 
-/* after bounce b's trace launch (parity p): zero the counts bounce b + 1
-   appends to (parity p ^ 1, consumed by bounce b - 1) and reset the trace
-   cursors */
-extern "C" __global__ void k_clear(uint32_t *counters, uint32_t p) {
-    uint32_t *cur = counters + HPT_CURSOR_OFFSET;
-    for (uint32_t i = threadIdx.x; i < HPT_CURSORS; i += blockDim.x) cur[i * HPT_CURSOR_STRIDE] = 0;
-    if (threadIdx.x == 0) {
-        const uint32_t q = p ^ 1u;
-        counters[HPT_C_TRACE(q)] = 0;
-        counters[HPT_C_SHADOW(q)] = 0;
-        counters[HPT_C_SHADE(q)] = 0;
-        for (int b = 0; b < HPT_BUCKETS; ++b) counters[HPT_C_BUCKET(q, b)] = 0;
-    }
-}
 
 /* ------------------------------------------------------------------ */
 /* host-side launch wrappers (declared in hpt_kernels.h)               */
@@ -3226,15 +3289,17 @@ static unsigned persistentBlocks(const void *kernel, uint64_t items, int block =
 
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
-                            uint64_t maxItems, hipStream_t s, const uint32_t *nBucket) {
+                            uint64_t maxItems, hipStream_t s, const uint32_t *nBucket, uint32_t *counters,
+                            uint32_t nextParity) {
     if (maxItems == 0) return hipSuccess;
     hptProbeBeforeTraceLaunch(s);
     if (stats)
         hipLaunchKernelGGL(k_trace_counted, dim3(persistentBlocks((const void *) k_trace_counted, maxItems)),
-                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, nBucket, stats);
+                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, nBucket,
+                           counters, nextParity, stats);
     else
         hipLaunchKernelGGL(k_trace, dim3(persistentBlocks((const void *) k_trace, maxItems)), dim3(HPT_TRACE_BLOCK), 0, s,
-                           sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, nBucket);
+                           sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, nBucket, counters, nextParity);
     return hipGetLastError();
 }
 hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
@@ -3253,7 +3318,9 @@ hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const 
 hipError_t hpt_launch_trace_overflow(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *overflowQ,
                                      const uint32_t *nOverflow, uint32_t *cursors, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_trace_overflow, dim3(persistentBlocks((const void *) k_trace_overflow, maxItems)),
+    /* overflowing packets are rare (none at the shipped configs): a small persistent grid that
+       claims whatever the packet pass left, instead of a chip-filling launch that finds nothing */
+    hipLaunchKernelGGL(k_trace_overflow, dim3(std::min(persistentBlocks((const void *) k_trace_overflow, maxItems), 32u)),
                        dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, overflowQ, nOverflow, cursors);
     return hipGetLastError();
 }
@@ -3317,10 +3384,6 @@ extern "C" __global__ __launch_bounds__(256) void k_film_add(float4 *__restrict_
 hipError_t hpt_launch_film_add(float4 *dst, const float4 *src, size_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_film_add, dim3(blocksFor(n, 256)), dim3(256), 0, s, dst, src, (uint64_t) n);
-    return hipGetLastError();
-}
-hipError_t hpt_launch_clear(uint32_t *counters, uint32_t parity, hipStream_t s) {
-    hipLaunchKernelGGL(k_clear, dim3(1), dim3(128), 0, s, counters, parity);
     return hipGetLastError();
 }
 hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *partial, float4 *film,

@@ -52,6 +52,39 @@ def block_owner(nbx: int, nby: int, world: int) -> list[int]:
     return owner
 
 
+def block_owner_weighted(nbx: int, nby: int, world: int, weights) -> list[int]:
+    """The work-balanced deal (hpt_capi.cpp dealBlocks, hpt_set_block_weights): blocks by
+    descending weight (ties in Hilbert order), each to the rank with the least weight so far
+    (ties to the lowest rank).  weights[b] is block b's measured work."""
+    order = block_order(nbx, nby)
+    pos = sorted(range(len(order)), key=lambda i: -float(weights[order[i]]))  # stable: Hilbert ties
+    load = [0.0] * world
+    owner = [0] * (nbx * nby)
+    for i in pos:
+        r = min(range(world), key=lambda k: (load[k], k))
+        owner[order[i]] = r
+        load[r] += float(weights[order[i]])
+    return owner
+
+
+def balance_blocks(renderer, n_blocks: int, world: int, dist=None, device=None):
+    """After a frame: every rank reads the path-bounces its blocks shaded
+    (hpt_get_block_costs), the counts are summed over ranks, and every rank sets the same
+    weights (hpt_set_block_weights), so the next frames use the same work-balanced deal.
+    Returns the weights."""
+    import numpy as np
+    import torch
+    costs = renderer.block_costs(n_blocks).astype(np.float64)
+    if world > 1:
+        if dist is None:
+            import torch.distributed as dist
+        t = torch.tensor(costs, dtype=torch.float64, device=device)
+        dist.all_reduce(t)
+        costs = t.cpu().numpy()
+    renderer.set_block_weights(costs)
+    return costs
+
+
 def render_frame(render_shard, film, rank: int, world: int, dist=None):
     """render_shard(shard, n_shards, film) accumulates this rank's blocks into
     `film` (a torch tensor; device for RCCL, CPU for gloo); the films are then

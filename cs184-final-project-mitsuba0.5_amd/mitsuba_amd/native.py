@@ -81,6 +81,9 @@ SIGNATURES = {
     "hpt_set_traversal_bounds": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
     "hpt_set_packet_stack": (C.c_int, [C.c_void_p, C.c_uint32]),
     "hpt_clear_schedules": (C.c_int, [C.c_void_p]),
+    "hpt_get_block_costs": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.c_int]),
+    "hpt_set_block_weights": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int]),
+    "hpt_block_deal": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
     "hpt_debug_sfmt": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
     "hpt_set_integrator": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
     "hpt_set_hair_file": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_float, _f]),
@@ -156,6 +159,19 @@ class HairPTError(RuntimeError):
         self.code = code
 
 
+def block_deal(width: int, height: int, n_shards: int, weights=None) -> np.ndarray:
+    """shard of every 32x32 image block (hpt_block_deal): Hilbert-cyclic, or work-balanced"""
+    lib = load_library()
+    nb = ((width + 31) // 32) * ((height + 31) // 32)
+    out = np.zeros(nb, dtype=np.int32)
+    w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float64)
+    rc = lib.hpt_block_deal(width, height, n_shards, None if w is None else w.ctypes.data_as(C.POINTER(C.c_double)),
+                            out.ctypes.data_as(C.POINTER(C.c_int32)))
+    if rc != 0:
+        raise HairPTError("hpt_block_deal failed (%d)" % rc, rc)
+    return out
+
+
 class Renderer:
     """One HIP context on one MI355X (the drop-in for a Mitsuba render job)."""
 
@@ -227,6 +243,20 @@ class Renderer:
     def set_packet_stack(self, entries=0):
         """test hook: limit the camera packets' stack (0 = the build's depth) to force the overflow path"""
         self._check(self.lib.hpt_set_packet_stack(self.h, entries))
+
+    def block_costs(self, n_blocks: int) -> np.ndarray:
+        """path-bounces shaded per image block since the last call (blocks this context owns)"""
+        out = np.zeros(n_blocks, dtype=np.uint64)
+        self._check(self.lib.hpt_get_block_costs(self.h, out.ctypes.data_as(C.POINTER(C.c_uint64)), n_blocks))
+        return out
+
+    def set_block_weights(self, weights=None):
+        """work-balanced shard deal from per-block weights (None: the Hilbert-cyclic deal)"""
+        if weights is None:
+            self._check(self.lib.hpt_set_block_weights(self.h, None, 0))
+            return
+        w = np.ascontiguousarray(weights, dtype=np.float64)
+        self._check(self.lib.hpt_set_block_weights(self.h, w.ctypes.data_as(C.POINTER(C.c_double)), len(w)))
 
     def clear_schedules(self):
         """forget the recorded bounce schedules: the next render of each wave reads every bounce back"""

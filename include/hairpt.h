@@ -178,6 +178,17 @@ int hpt_render_device(hpt_context *ctx, const hpt_render_params *params, void *d
 int hpt_context_share_scene(hpt_context *src, int device, hpt_context **out);
 int hpt_render_multi(hpt_context *const *ctxs, int n, const hpt_render_params *params, float *film_rgbw);
 
+/* Work-balanced shard deal (no reference counterpart; the reference's scheduler hands out blocks
+   on demand, src/librender/renderproc.cpp:68-85).  Every render counts, per 32x32 image block it
+   owns, the path-bounces it shaded; hpt_get_block_costs copies those counts (by image block
+   index by * ceil(W/32) + bx, zero for blocks other shards own) and resets them.  Ranks that add
+   their counts up and pass the same totals to hpt_set_block_weights get the same deal: blocks by
+   descending weight, each to the shard with the least weight so far (hpt_block_deal, which
+   computes it without a context).  No weights (n_blocks 0): the Hilbert-cyclic deal. */
+int hpt_get_block_costs(hpt_context *ctx, uint64_t *costs, int n_blocks);
+int hpt_set_block_weights(hpt_context *ctx, const double *weights, int n_blocks);
+int hpt_block_deal(int width, int height, int n_shards, const double *weights, int32_t *shard_of_block);
+
 typedef struct hpt_stats {
     double ms_total;               /* host wall time of the render call */
     double ms_camera, ms_trace, ms_primary, ms_shade, ms_post, ms_gather; /* HIP event sums */

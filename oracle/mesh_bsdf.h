@@ -40,11 +40,12 @@ struct SmoothPlastic {
     Spec diffuse{0.5f}, specular{1.0f};
     float fdrInt = 0, fdrExt = 0, specularSamplingWeight = 0, invEta2 = 0;
 
-    void configure() { /* :186-217 */
+    bool ensureEnergyConservation = true; /* BSDF::BSDF, bsdf.cpp:30-31 */
+    void configure() { /* :186-217; BSDF::ensureEnergyConservation, bsdf.cpp:88-113 */
         float mx = specular.max();
-        if (mx > 1.0f) specular *= 0.99f * (1.0f / mx);
+        if (ensureEnergyConservation && mx > 1.0f) specular *= 0.99f * (1.0f / mx);
         mx = diffuse.max();
-        if (mx > 1.0f) diffuse *= 0.99f * (1.0f / mx);
+        if (ensureEnergyConservation && mx > 1.0f) diffuse *= 0.99f * (1.0f / mx);
         fdrInt = fresnelDiffuseReflectance(1 / eta);
         fdrExt = fresnelDiffuseReflectance(eta);
         const float dAvg = diffuse.getLuminance(), sAvg = specular.getLuminance();

@@ -3034,12 +3034,14 @@ int orc_set_diffuse_checkerboard(orc_scene *s, const float color0[3], const floa
     return 0;
 }
 
-int orc_set_plastic(orc_scene *s, float eta, int nonlinear, const float diffuse[3], const float specular[3]) {
+int orc_set_plastic(orc_scene *s, float eta, int nonlinear, const float diffuse[3], const float specular[3],
+                    int ensure_energy_conservation) {
     BsdfInst &b = lastBsdf(s);
     b.kind = 6;
     b.pl = SmoothPlastic();
     b.pl.eta = eta;
     b.pl.nonlinear = nonlinear != 0;
+    b.pl.ensureEnergyConservation = ensure_energy_conservation != 0;
     b.pl.diffuse = Spec(diffuse[0], diffuse[1], diffuse[2]);
     b.pl.specular = Spec(specular[0], specular[1], specular[2]);
     b.pl.configure();

@@ -94,7 +94,8 @@ int orc_new_bsdf(orc_scene *s);
 int orc_set_diffuse_checkerboard(orc_scene *s, const float color0[3], const float color1[3], float uoffset,
                                  float voffset, float uscale, float vscale);
 /* plastic.cpp (SmoothPlastic, constant reflectances): eta = intIOR/extIOR */
-int orc_set_plastic(orc_scene *s, float eta, int nonlinear, const float diffuse[3], const float specular[3]);
+int orc_set_plastic(orc_scene *s, float eta, int nonlinear, const float diffuse[3], const float specular[3],
+                    int ensure_energy_conservation);
 int orc_set_twosided(orc_scene *s, int nested0, int nested1);
 /* obj.cpp WavefrontOBJ (to_world row-major, may be NULL) / rectangle.cpp */
 int orc_add_obj(orc_scene *s, const char *path, const float *to_world, int face_normals, int flip_normals,

@@ -73,7 +73,7 @@ _SIG = {
     # C1 mesh scene (oracle/mesh_bsdf.h, mesh_geom.h)
     "orc_new_bsdf": (C.c_int, [C.c_void_p]),
     "orc_set_diffuse_checkerboard": (C.c_int, [C.c_void_p, _f, _f, C.c_float, C.c_float, C.c_float, C.c_float]),
-    "orc_set_plastic": (C.c_int, [C.c_void_p, C.c_float, C.c_int, _f, _f]),
+    "orc_set_plastic": (C.c_int, [C.c_void_p, C.c_float, C.c_int, _f, _f, C.c_int]),
     "orc_set_twosided": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "orc_add_obj": (C.c_int, [C.c_void_p, C.c_char_p, _f, C.c_int, C.c_int, C.c_int, C.c_int]),
     "orc_add_rectangle": (C.c_int, [C.c_void_p, _f, C.c_int, C.c_int]),
@@ -361,7 +361,8 @@ class MeshOracle(Oracle):
             self.check(self.lib.orc_set_twosided(self.s, nested[0], nested[1] if len(nested) > 1 else -1))
         elif kind == "plastic":
             self.check(self.lib.orc_set_plastic(self.s, b["intIOR"] / b["extIOR"], int(b["nonlinear"]),
-                                                p(f32(b["diffuse"]), _f), p(f32(b["specular"]), _f)))
+                                                p(f32(b["diffuse"]), _f), p(f32(b["specular"]), _f),
+                                                int(b.get("ensureEnergyConservation", True))))
         elif kind == "diffuse":
             t = b.get("reflectanceTexture")
             if t:

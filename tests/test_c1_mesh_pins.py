@@ -55,10 +55,10 @@ def _dirs(rng, n, upper=True):
     return v.astype(np.float32)
 
 
-def _plastic_oracle(eta=1.5, nonlinear=True, diffuse=(0.9, 0.9, 0.9), specular=(1, 1, 1)):
+def _plastic_oracle(eta=1.5, nonlinear=True, diffuse=(0.9, 0.9, 0.9), specular=(1, 1, 1), ensure=True):
     o = oracle_lib.MeshOracle()
     o.new_bsdf({"type": "plastic", "intIOR": eta, "extIOR": 1.0, "nonlinear": nonlinear, "diffuse": diffuse,
-                "specular": specular})
+                "specular": specular, "ensureEnergyConservation": ensure})
     return o
 
 
@@ -88,6 +88,20 @@ def test_plastic_eval_pdf(nonlinear):
     o = _plastic_oracle(1.5, nonlinear, diffuse, specular)
     rgb, pdf = o.bsdf_eval(wi, wo)
     e_rgb, e_pdf = _plastic64(wi, wo, np.float32(1.5), nonlinear, diffuse, specular)
+    np.testing.assert_allclose(rgb, e_rgb, rtol=2e-5, atol=1e-7)
+    np.testing.assert_allclose(pdf, e_pdf, rtol=2e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("ensure", [True, False])
+def test_plastic_energy_conservation(ensure):
+    """BSDF::ensureEnergyConservation (bsdf.cpp:88-113): a reflectance above 1 is scaled by
+    0.99 / max -- unless the BSDF sets ensureEnergyConservation=false"""
+    rng = np.random.default_rng(9)
+    wi, wo = _dirs(rng, 200), _dirs(rng, 200)
+    diffuse, specular = (1.2, 0.6, 0.3), (1.0, 1.0, 1.0)
+    rgb, pdf = _plastic_oracle(1.5, False, diffuse, specular, ensure).bsdf_eval(wi, wo)
+    d_eff = np.array(diffuse) * (0.99 / 1.2 if ensure else 1.0)
+    e_rgb, e_pdf = _plastic64(wi, wo, np.float32(1.5), False, tuple(d_eff), specular)
     np.testing.assert_allclose(rgb, e_rgb, rtol=2e-5, atol=1e-7)
     np.testing.assert_allclose(pdf, e_pdf, rtol=2e-5, atol=1e-7)
 
@@ -280,3 +294,26 @@ def test_rectangle(tmp_path):
     # normal = normalize(M^-T (0,0,1)) = -y here; uv = 0.5 (local + 1)
     np.testing.assert_allclose(nrm[:2], [[0, -1, 0]] * 2, atol=1e-6)
     np.testing.assert_allclose(uv[0], [0.5 * (0.5 + 1), 0.5 * (1.5 / 3 + 1)], atol=1e-6)
+
+
+@pytest.mark.parametrize("rho", [0.25, 0.5, 0.8])
+def test_integrator_diffuse_plane_under_constant_sky(rho):
+    """End-to-end closed form for the C1 CPU path's integrator (path.cpp:119-294 with NEE + BSDF
+    sampling under MIS, envmap sampling envmap.cpp:516-543, rectangle.cpp, diffuse.cpp): a
+    diffuse plane of albedo rho that fills the view, alone under a constant unit sky, reflects
+    exactly rho -- it sees nothing but the sky, so every path ends after one bounce and the
+    estimator's expectation is rho * L.  The 16x16 @ 64 spp mean is within 1.5 %."""
+    W = H = 16
+    cam = [-1, 0, 0, 0, 0, 1, 0, 0, 0, 0, -1, 5, 0, 0, 0, 1]  # at z = 5, looking down -z
+    js = {"sensor": {"toWorld": cam, "xfov": 30.0, "nearClip": 0.01, "farClip": 100.0},
+          "integrator": {"maxDepth": 65, "rrDepth": 5, "strictNormals": True, "hideEmitters": False},
+          "bsdfs": [{"type": "diffuse", "diffuse": [rho] * 3}],
+          "meshes": [{"type": "rectangle", "toWorld": [4, 0, 0, 0, 0, 4, 0, 0, 0, 0, 4, 0, 0, 0, 0, 1],
+                      "flipNormals": False, "bsdf": 0}],
+          "emitter": {"toWorld": [1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1], "scale": 1.0}}
+    o = oracle_lib.MeshOracle()
+    o.setup_scene(js, np.ones((16, 32, 3), np.float32), W, H, 64)
+    film, _ = o.render(0, 64, threads=4, width=W, height=H)
+    img = film[..., :3] / film[..., 3:4]
+    assert np.all(np.isfinite(img))
+    np.testing.assert_allclose(img.mean(axis=(0, 1)), [rho] * 3, rtol=0.015)

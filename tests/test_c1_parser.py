@@ -37,6 +37,7 @@ def test_defaults(tmp_path):
     # plastic.cpp:145-166: polypropylene / air (ior.h: 1.49 / 1.000277), specular 1, diffuse 0.5, linear
     assert pl["type"] == "plastic" and abs(pl["intIOR"] - 1.49) < 1e-6 and abs(pl["extIOR"] - 1.000277) < 1e-6
     assert pl["specular"] == [1, 1, 1] and pl["diffuse"] == [0.5, 0.5, 0.5] and pl["nonlinear"] is False
+    assert pl["ensureEnergyConservation"] is True  # bsdf.cpp:30-31 default
     tex = js["bsdfs"][rect["bsdf"]]["reflectanceTexture"]
     # checkerboard.cpp:49-51 colours, texture.cpp:82-91 uvscale -> uscale / vscale
     assert tex["color0"] == pytest.approx([0.4] * 3) and tex["color1"] == pytest.approx([0.2] * 3)

@@ -17,7 +17,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import scene_util
-from mitsuba_amd import distributed
+from mitsuba_amd import distributed, native
 
 W, H, SPP, N = 72, 40, 2, 600  # 3 x 2 blocks of 32x32 (ragged right/bottom edges)
 
@@ -115,3 +115,59 @@ def test_bench_timed_steps_takes_max_over_ranks(tmp_path):
     assert d0[1] == d1[1] == 3  # exactly K timed steps, each followed by the stats callback
     assert d0[0] == d1[0]       # every rank holds the MAX over ranks
     assert d0[0] >= 3 * 0.04    # ... which is the slower rank's (rank 1 sleeps 40 ms per step)
+
+
+@pytest.mark.parametrize("w,h,world", [(512, 512, 8), (1024, 1024, 8), (200, 130, 3), (512, 512, 2)])
+def test_weighted_deal_matches_mirror(w, h, world):
+    """hpt_block_deal (the renderer's work-balanced deal) equals distributed.block_owner_weighted,
+    every block is owned once, the ranks' loads are balanced to within one block's weight, and
+    without weights it is the Hilbert-cyclic deal."""
+    nbx, nby = (w + 31) // 32, (h + 31) // 32
+    rng = np.random.default_rng(7)
+    weights = rng.gamma(2.0, 1000.0, nbx * nby)
+    weights[rng.random(nbx * nby) < 0.2] = 0.0  # empty blocks (no hair)
+    got = native.block_deal(w, h, world, weights)
+    assert list(got) == distributed.block_owner_weighted(nbx, nby, world, weights)
+    loads = np.bincount(got, weights=weights, minlength=world)
+    assert loads.max() - loads.min() <= weights.max() + 1e-9
+    assert list(native.block_deal(w, h, world)) == distributed.block_owner(nbx, nby, world)
+
+
+class _FakeCosts:
+    """stands in for a Renderer: the blocks this rank owns report their (made-up) work"""
+
+    def __init__(self, costs):
+        self.costs, self.weights = costs, None
+
+    def block_costs(self, n):
+        return self.costs[:n].copy()
+
+    def set_block_weights(self, w):
+        self.weights = np.array(w)
+
+
+def _balance_worker(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        nbx = nby = 4
+        owner = np.array(distributed.block_owner(nbx, nby, world))
+        full = np.arange(1, nbx * nby + 1, dtype=np.uint64) * 10
+        mine = np.where(owner == rank, full, 0).astype(np.uint64)
+        fake = _FakeCosts(mine)
+        w = distributed.balance_blocks(fake, nbx * nby, world, dist, "cpu")
+        np.save(os.path.join(out_dir, "w%d.npy" % rank), fake.weights)
+        assert (w == fake.weights).all()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_balance_blocks_sums_costs_over_ranks(tmp_path):
+    """bench.py --balance: the ranks' per-block counts (each rank only its own blocks) are summed
+    with an all-reduce, and every rank sets the same full weight vector (so the same deal)."""
+    world = 2
+    mp.spawn(_balance_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    w0, w1 = np.load(tmp_path / "w0.npy"), np.load(tmp_path / "w1.npy")
+    np.testing.assert_array_equal(w0, w1)
+    np.testing.assert_array_equal(w0, np.arange(1, 17) * 10.0)
