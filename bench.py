@@ -337,7 +337,7 @@ def main():
                                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved_pk / HBM_PEAK_GBS, 4),
                                 "traffic": traffic_pk,
                                 "achieved_hbm": round(traffic_pk / (ms_packet / max(1, p_launches)) * 1e-6, 1)
-                                if traffic_pk else None,
+                                if traffic_pk and ms_packet > 0 else None,
                                 "algorithmic_model": "SURVEY.md 8(d) per packet step: 8 B per binary-node step, "
                                                      "4+52 B per leaf-record step (wave-uniform), 52 B ray I/O per lane",
                                 "algorithmic_bytes_per_launch": int(bytes_pk // max(1, p_launches)),

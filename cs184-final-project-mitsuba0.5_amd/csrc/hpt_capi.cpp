@@ -1034,13 +1034,14 @@ static int ensureOwnership(hpt_context *c, int W, int H, int nbx, int nby, int s
         c->ownCap = 0;
         HIPCHK(c, hipMalloc((void **) &c->dBlockOf, n * sizeof(uint32_t)));
         HIPCHK(c, hipMalloc((void **) &c->dLocalOf, n * sizeof(int32_t)));
-        HIPCHK(c, hipMalloc((void **) &c->dBlockCost, 2 * n * sizeof(uint32_t))); /* + a snapshot per wave */
+        /* HPT_COST_STRIPES stripes of n counters, + a snapshot of them per wave */
+        HIPCHK(c, hipMalloc((void **) &c->dBlockCost, 2 * HPT_COST_STRIPES * n * sizeof(uint32_t)));
         c->ownCap = n;
     }
     if (!blockOf.empty())
         HIPCHK(c, hipMemcpy(c->dBlockOf, blockOf.data(), blockOf.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     HIPCHK(c, hipMemcpy(c->dLocalOf, localOf.data(), localOf.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    HIPCHK(c, hipMemset(c->dBlockCost, 0, n * sizeof(uint32_t))); /* costs are per ownership */
+    HIPCHK(c, hipMemset(c->dBlockCost, 0, HPT_COST_STRIPES * c->ownCap * sizeof(uint32_t))); /* costs are per ownership */
     c->ownW = W, c->ownH = H, c->ownShard = shard, c->ownShards = nShards, c->ownLocal = (int) blockOf.size();
     c->ownWeights = c->weightsVersion;
     c->ownBlocks.assign(blockOf.begin(), blockOf.end());
@@ -1079,6 +1080,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     hipStream_t s = c->stream;
     c->P.bucketQ = c->claimBuckets ? c->bucketBuf : nullptr;
     c->P.blockCost = c->dBlockCost;
+    c->P.costStride = (uint32_t) c->ownCap;
+    const size_t costWords = (size_t) HPT_COST_STRIPES * c->ownCap;
     c->P.bucketCap = (uint32_t) std::min<uint64_t>(2 * c->capacity, 0xffffffffull);
     if (!c->scDev) HIPCHK(c, hipMalloc((void **) &c->scDev, sizeof(HptScene)));
     if (c->scShadow.size() != sizeof(HptScene) || std::memcmp(c->scShadow.data(), &c->sc, sizeof(HptScene)) != 0) {
@@ -1159,7 +1162,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         size_t evMarkOther[7];
         for (int i = 0; i < 7; ++i) evMarkOther[i] = evOther[i].size();
         if (counted) HIPCHK(c, hipMemcpyAsync(c->dstats + 24, c->dstats, 24 * 8, hipMemcpyDeviceToDevice, s));
-        HIPCHK(c, hipMemcpyAsync(c->dBlockCost + c->ownCap, c->dBlockCost, localBlocks * 4, hipMemcpyDeviceToDevice, s));
+        HIPCHK(c, hipMemcpyAsync(c->dBlockCost + costWords, c->dBlockCost, costWords * 4, hipMemcpyDeviceToDevice, s));
         HIPCHK(c, hipMemsetAsync(c->counters, 0, HPT_COUNTER_WORDS * 4, s));
         uint32_t *C = c->counters, *dst = counted ? (uint32_t *) c->dstats : nullptr;
         uint32_t *curPacket = C + HPT_CURSOR_SET(2), *curOverflow = C + HPT_CURSOR_SET(3);
@@ -1287,7 +1290,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                 evOther[i].resize(evMarkOther[i]);
             }
             if (counted) HIPCHK(c, hipMemcpyAsync(c->dstats, c->dstats + 24, 24 * 8, hipMemcpyDeviceToDevice, s));
-            HIPCHK(c, hipMemcpyAsync(c->dBlockCost, c->dBlockCost + c->ownCap, localBlocks * 4, hipMemcpyDeviceToDevice, s));
+            HIPCHK(c, hipMemcpyAsync(c->dBlockCost, c->dBlockCost + costWords, costWords * 4, hipMemcpyDeviceToDevice, s));
             j0 -= (int) nSpp;
             continue;
         }
@@ -1523,12 +1526,16 @@ int hpt_get_block_costs(hpt_context *c, uint64_t *costs, int n_blocks) {
     std::memset(costs, 0, (size_t) n_blocks * sizeof(uint64_t));
     if (c->device == HPT_HOST_ONLY || !c->dBlockCost || c->ownBlocks.empty()) return HPT_OK;
     HIPCHK(c, hipSetDevice(c->device));
-    std::vector<uint32_t> local(c->ownBlocks.size());
+    const size_t words = (size_t) HPT_COST_STRIPES * c->ownCap;
+    std::vector<uint32_t> local(words);
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    HIPCHK(c, hipMemcpy(local.data(), c->dBlockCost, local.size() * 4, hipMemcpyDeviceToHost));
-    HIPCHK(c, hipMemset(c->dBlockCost, 0, local.size() * 4));
-    for (size_t k = 0; k < local.size(); ++k)
-        if ((int) c->ownBlocks[k] < n_blocks) costs[c->ownBlocks[k]] = local[k];
+    HIPCHK(c, hipMemcpy(local.data(), c->dBlockCost, words * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemset(c->dBlockCost, 0, words * 4));
+    for (size_t k = 0; k < c->ownBlocks.size(); ++k) {
+        uint64_t sum = 0; /* the stripes of block k */
+        for (int st = 0; st < HPT_COST_STRIPES; ++st) sum += local[(size_t) st * c->ownCap + k];
+        if ((int) c->ownBlocks[k] < n_blocks) costs[c->ownBlocks[k]] = sum;
+    }
     return HPT_OK;
 }
 

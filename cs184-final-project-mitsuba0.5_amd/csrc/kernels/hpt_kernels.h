@@ -100,15 +100,19 @@ struct HptPaths {
     uint32_t bucketCap;
     /* per owned 32x32 block: path-bounces shaded (k_shade, k_tail), the measured work the cost-
        balanced shard deal reads back (hpt_get_block_costs); nullptr: not counted.  costSpp is
-       the wave's nSpp (path id -> block: id / nSpp >> 10) */
+       the wave's nSpp (path id -> block: id / nSpp >> 10).  The counts are striped: wave w adds
+   to stripe w % HPT_COST_STRIPES at blockCost[stripe * costStride + block] (a bounce's queue
+   is in block order, so every resident wave counts into the same block at once: one counter
+   per block serialised ~70 k atomics per launch and cost k_shade 4 ms per frame) */
     uint32_t *blockCost;
-    uint32_t costSpp;
+    uint32_t costSpp, costStride;
     float4 *bw;        /* bsdf weight rgb, bsdf pdf                  */
     float4 *sdir;      /* shadow ray direction xyz, maxt             */
     float4 *scontrib;  /* NEE contribution rgb (added if unoccluded) */
 };
 
 
+#define HPT_COST_STRIPES 64
 #define HPT_BUCKET_SHADOW 0x80000000u
 /* hit record of a miss (a segment id never has all 31 bits set) */
 #define HPT_MISS 0xffffffffu

@@ -2224,16 +2224,19 @@ __device__ __forceinline__ void qpushBucket(bool pred, uint32_t b, uint32_t valu
 }
 
 /* one shaded path-bounce of path `id` per lane where pred, added to its block's cost: lanes
-   of the same block share one atomic (a wave's paths are mostly of one or two blocks) */
+   of the same block share one atomic (a wave's paths are mostly of one or two blocks), into
+   the wave's stripe of the counters (HptPaths::blockCost) */
 __device__ __forceinline__ void countBlockCost(const HptPaths &P, bool pred, uint32_t id) {
     if (!P.blockCost) return;
     const uint32_t blk = pred ? (id / P.costSpp) >> 10 : 0xffffffffu;
+    uint32_t *const stripe =
+        P.blockCost + ((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % HPT_COST_STRIPES) * P.costStride;
     uint64_t todo = __ballot(pred);
     while (todo) { /* wave-uniform */
         const int L = __ffsll((unsigned long long) todo) - 1;
         const uint32_t b = (uint32_t) __builtin_amdgcn_readlane((int) blk, L);
         const uint64_t m = __ballot(pred && blk == b);
-        if (__lane_id() == (uint32_t) L) atomicAdd(&P.blockCost[b], (uint32_t) __popcll(m));
+        if (__lane_id() == (uint32_t) L) atomicAdd(&stripe[b], (uint32_t) __popcll(m));
         todo &= ~m;
     }
 }
