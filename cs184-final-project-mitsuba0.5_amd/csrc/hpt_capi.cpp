@@ -65,7 +65,7 @@ static bool defaultBounceAhead() {
 /* launch cut (HptPaths::carryRec): HPT_CUT=0 lets every bounce launch drain its last rays */
 static bool defaultCut() {
     const char *v = std::getenv("HPT_CUT");
-    return v ? std::atoi(v) != 0 : true;
+    return v ? std::atoi(v) != 0 : false; /* off until measured on the GPU */
 }
 /* a bounce launch cuts only with at least this many rays per lane (HPT_CUT_MIN; 0: always, a test hook) */
 static int defaultCutMin() {

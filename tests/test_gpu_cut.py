@@ -45,7 +45,7 @@ def _renders(name, n, radii, monkeypatch, cut, cut_min, tail, ahead="1", times=3
 def test_cut_bit_identical(name, n, radii, tail, monkeypatch):
     (ref, s0), = _renders(name, n, radii, monkeypatch, "0", "4", tail, ahead="0", times=1)
     assert s0.cut_rays == 0 and s0.carry_flushes == 0
-    runs = _renders(name, n, radii, monkeypatch, "1", "0", tail)
+    runs = _renders(name, n, radii, monkeypatch, "1", "0", tail)  # HPT_CUT=1 explicitly (the default is off until measured)
     for k, (film, s) in enumerate(runs):
         np.testing.assert_array_equal(film, ref, err_msg=f"render {k}")
         # the same path-bounces are shaded, whichever launch traced their rays
