@@ -1270,6 +1270,20 @@ HD float longitudinalM(float v, float sinThetaI, float sinThetaO, float cosTheta
     if (v < 0.1f) return expf(-b + logI0(a) - 1.0f / v + 0.6931f + logf(1.0f / (2.0f * v)));
     return expf(-b) * I0(a) / (2.0f * v * sinhf(1.0f / v));
 }
+/* the same with the lobe's constants 1 / v and log(1 / (2 v)) (v < 0.1) or 2 v sinh(1 / v) computed
+   once per bounce (MarschnerWi): identical values, identical result */
+struct LobeConst {
+    float invV, k; /* k: logf(1 / (2 v)) when v < 0.1, else 2 v sinh(1 / v) */
+};
+HD LobeConst lobeConst(float v) {
+    return {1.0f / v, v < 0.1f ? logf(1.0f / (2.0f * v)) : 2.0f * v * sinhf(1.0f / v)};
+}
+HD float longitudinalMc(float v, LobeConst c, float sinThetaI, float sinThetaO, float cosThetaI, float cosThetaO) {
+    float a = cosThetaI * cosThetaO / v;
+    float b = sinThetaI * sinThetaO / v;
+    if (v < 0.1f) return expf(-b + logI0(a) - c.invV + 0.6931f + c.k);
+    return expf(-b) * I0(a) / c.k;
+}
 
 /* Azimuthal::eval (:80-94) */
 HD V3 azEval(const HptF4 *__restrict__ tab, float phi, float cosThetaD) {
@@ -1338,30 +1352,86 @@ HD float roughTransSlice(const float *__restrict__ trans, int transSize, float c
 }
 HD float roughTrans(const HptMarschner &m, float cosTheta) { return roughTransSlice(m.trans, m.transSize, cosTheta); }
 
+/* The terms of MarschnerDiffuse::eval / ::sample that depend on wi only: a bounce evaluates
+   the BSDF for its NEE direction, samples it and evaluates it again for the sampled direction,
+   all with one wi, so k_shade computes them once (the same expressions: bit-identical) */
+struct MarschnerWi {
+    float thetaI;
+    float sR, cR, sTT, cTT, sTRT, cTRT; /* sin / cos of thetaI shifted per lobe (:391-393) */
+    float T12;                          /* roughTrans(wi.z) */
+    LobeConst kR, kTT, kTRT;            /* longitudinalM's per-lobe constants */
+};
+HD MarschnerWi marschnerWi(const HptMarschner &m, V3 wi) {
+    MarschnerWi w;
+    w.thetaI = asinf(clampf(wi.y, -1.0f, 1.0f));
+    const float thetaIR = w.thetaI - 2.0f * m.scaleAngleRad;
+    const float thetaITT = w.thetaI + m.scaleAngleRad;
+    const float thetaITRT = w.thetaI + 4.0f * m.scaleAngleRad;
+    w.sR = sinf(thetaIR), w.cR = cosf(thetaIR);
+    w.sTT = sinf(thetaITT), w.cTT = cosf(thetaITT);
+    w.sTRT = sinf(thetaITRT), w.cTRT = cosf(thetaITRT);
+    w.T12 = roughTrans(m, wi.z);
+    w.kR = lobeConst(m.vR);
+    w.kTT = lobeConst(m.vTT);
+    w.kTRT = lobeConst(m.vTRT);
+    return w;
+}
 /* MarschnerDiffuse::eval (:377-482), hasDiffuse = true */
-HD V3 marschnerEval(const HptMarschner &m, V3 wi, V3 wo) {
-    float sinThetaI = wi.y, sinThetaO = wo.y;
+HD V3 marschnerEvalW(const HptMarschner &m, const MarschnerWi &w, V3 wo) {
+    float sinThetaO = wo.y;
     float cosThetaO = trigInverse(sinThetaO);
-    float thetaI = asinf(clampf(sinThetaI, -1.0f, 1.0f));
     float thetaO = asinf(clampf(sinThetaO, -1.0f, 1.0f));
-    float thetaD = (thetaO - thetaI) * 0.5f;
+    float thetaD = (thetaO - w.thetaI) * 0.5f;
     float cosThetaD = cosf(thetaD);
     float phi = atan2f(wo.x, wo.z);
     if (phi < 0.0f) phi += kPi * 2.0f;
-    float thetaIR = thetaI - 2.0f * m.scaleAngleRad;
-    float thetaITT = thetaI + m.scaleAngleRad;
-    float thetaITRT = thetaI + 4.0f * m.scaleAngleRad;
-    float MR = longitudinalM(m.vR, sinf(thetaIR), sinThetaO, cosf(thetaIR), cosThetaO);
-    float MTT = longitudinalM(m.vTT, sinf(thetaITT), sinThetaO, cosf(thetaITT), cosThetaO);
-    float MTRT = longitudinalM(m.vTRT, sinf(thetaITRT), sinThetaO, cosf(thetaITRT), cosThetaO);
+    float MR = longitudinalMc(m.vR, w.kR, w.sR, sinThetaO, w.cR, cosThetaO);
+    float MTT = longitudinalMc(m.vTT, w.kTT, w.sTT, sinThetaO, w.cTT, cosThetaO);
+    float MTRT = longitudinalMc(m.vTRT, w.kTRT, w.sTRT, sinThetaO, w.cTRT, cosThetaO);
     V3 result = (0.15f * MR) * azEval(m.table[0], phi, cosThetaD) + MTT * azEval(m.table[1], phi, cosThetaD) +
                 MTRT * azEval(m.table[2], phi, cosThetaD);
     V3 diff = v3(m.diffuse[0], m.diffuse[1], m.diffuse[2]);
-    float T12 = roughTrans(m, wi.z);
     float T21 = roughTrans(m, wo.z);
     diff = divs(diff, 1 - m.fdr);
-    result = result + diff * (kInvPi * wo.z * T12 * T21 * m.invEta2);
+    result = result + diff * (kInvPi * wo.z * w.T12 * T21 * m.invEta2);
     return result;
+}
+HD V3 marschnerEval(const HptMarschner &m, V3 wi, V3 wo) { return marschnerEvalW(m, marschnerWi(m, wi), wo); }
+/* k_shade keeps a bounce's MarschnerWi in LDS between its NEE evaluation and its BSDF sample
+   (nine more registers live across NEE would cost k_shade a wave per SIMD); row k of thread t at
+   l[k * stride] */
+#define HPT_WI_ROWS 14
+HD void stashWi(float *l, int stride, const MarschnerWi &w) {
+    l[8 * stride] = w.kR.invV;
+    l[9 * stride] = w.kR.k;
+    l[10 * stride] = w.kTT.invV;
+    l[11 * stride] = w.kTT.k;
+    l[12 * stride] = w.kTRT.invV;
+    l[13 * stride] = w.kTRT.k;
+    l[0] = w.thetaI;
+    l[stride] = w.sR;
+    l[2 * stride] = w.cR;
+    l[3 * stride] = w.sTT;
+    l[4 * stride] = w.cTT;
+    l[5 * stride] = w.sTRT;
+    l[6 * stride] = w.cTRT;
+    l[7 * stride] = w.T12;
+    asm volatile("" ::: "memory"); /* re-read where used, not forwarded (forwarding keeps the registers) */
+}
+HD MarschnerWi loadWi(const float *l, int stride) {
+    MarschnerWi w;
+    w.thetaI = l[0];
+    w.sR = l[stride];
+    w.cR = l[2 * stride];
+    w.sTT = l[3 * stride];
+    w.cTT = l[4 * stride];
+    w.sTRT = l[5 * stride];
+    w.cTRT = l[6 * stride];
+    w.T12 = l[7 * stride];
+    w.kR = {l[8 * stride], l[9 * stride]};
+    w.kTT = {l[10 * stride], l[11 * stride]};
+    w.kTRT = {l[12 * stride], l[13 * stride]};
+    return w;
 }
 
 /* sampleM (:582-592) */
@@ -1383,36 +1453,33 @@ struct GlobalTabs {
 
 /* MarschnerDiffuse::sample (:594-744); pdf() == 1 (:517-520) */
 template <class Tabs>
-HD V3 marschnerSample(const HptMarschner &m, const Tabs &tabs, V3 wi, float sx, float sy, V3 &wo, uint32_t &type) {
+HD V3 marschnerSampleW(const HptMarschner &m, const MarschnerWi &w, const Tabs &tabs, V3 wi, float sx, float sy, V3 &wo,
+                       uint32_t &type) {
     float sinThetaI = wi.y;
     float cosThetaI = trigInverse(sinThetaI);
-    float thetaI = asinf(clampf(sinThetaI, -1.0f, 1.0f));
-    float thetaIR = thetaI - 2.0f * m.scaleAngleRad;
-    float thetaITT = thetaI + m.scaleAngleRad;
-    float thetaITRT = thetaI + 4.0f * m.scaleAngleRad;
     float weightR = azWeight(tabs.sums(0), cosThetaI);
     float weightTT = azWeight(tabs.sums(1), cosThetaI);
     float weightTRT = azWeight(tabs.sums(2), cosThetaI);
     int lobe;
-    float v, theta;
+    float v, sinTheta, cosTheta; /* of the chosen lobe's shifted thetaI (:624-641) */
     float target = sx * (weightR + weightTT + weightTRT);
     if (target < weightR) {
-        lobe = 0; v = m.vR; theta = thetaIR;
+        lobe = 0; v = m.vR; sinTheta = w.sR; cosTheta = w.cR;
     } else if (target < weightR + weightTT) {
-        lobe = 1; v = m.vTT; theta = thetaITT;
+        lobe = 1; v = m.vTT; sinTheta = w.sTT; cosTheta = w.cTT;
     } else {
-        lobe = 2; v = m.vTRT; theta = thetaITRT;
+        lobe = 2; v = m.vTRT; sinTheta = w.sTRT; cosTheta = w.cTRT;
     }
-    float sinThetaO = sampleM(v, sinf(theta), cosf(theta), sx, sy);
+    float sinThetaO = sampleM(v, sinTheta, cosTheta, sx, sy);
     float cosThetaO = trigInverse(sinThetaO);
     float thetaO = asinf(clampf(sinThetaO, -1.0f, 1.0f));
-    float thetaD = (thetaO - thetaI) * 0.5f;
+    float thetaD = (thetaO - w.thetaI) * 0.5f;
     float cosThetaD = cosf(thetaD);
     float phi = azSample(tabs.cdf(lobe), cosThetaD, sy);
     float sinPhi = sinf(phi), cosPhi = cosf(phi);
-    float probSpecular = 1 - roughTrans(m, wi.z);
-    float w = m.specularSamplingWeight;
-    probSpecular = (probSpecular * w) / (probSpecular * w + (1 - probSpecular) * (1 - w));
+    float probSpecular = 1 - w.T12;
+    const float sw = m.specularSamplingWeight;
+    probSpecular = (probSpecular * sw) / (probSpecular * sw + (1 - probSpecular) * (1 - sw));
     if (sy < probSpecular) {
         wo = v3(sinPhi * cosThetaO, sinThetaO, cosPhi * cosThetaO);
         type = HPT_EDELTA_REFLECTION;
@@ -1420,8 +1487,12 @@ HD V3 marschnerSample(const HptMarschner &m, const Tabs &tabs, V3 wi, float sx, 
         type = HPT_EDIFFUSE_REFLECTION;
         wo = squareToCosineHemisphere(sx, sy);
     }
-    V3 e = marschnerEval(m, wi, wo);
+    V3 e = marschnerEvalW(m, w, wo);
     return divs(e, 1.0f);
+}
+template <class Tabs>
+HD V3 marschnerSample(const HptMarschner &m, const Tabs &tabs, V3 wi, float sx, float sy, V3 &wo, uint32_t &type) {
+    return marschnerSampleW(m, marschnerWi(m, wi), tabs, wi, sx, sy, wo, type);
 }
 
 /* ------------------------------------------------------------------ */
@@ -2683,7 +2754,7 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
    everything by path */
 template <bool MULTI, bool REC = false>
 HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec, uint32_t *__restrict__ counters,
-                  bool &cont, bool &shadow, const float4 *in, float4 *cOut, float4 *sOut) {
+                  bool &cont, bool &shadow, const float4 *in, float4 *cOut, float4 *sOut, float *wiL) {
     {
         uint32_t st = REC ? __float_as_uint(in[2].w) : P.state[id];
         uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st);
@@ -2709,6 +2780,9 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
             const uint64_t sidx = REC ? ((uint64_t) __float_as_uint(rd.w) << 32) | __float_as_uint(ro.w) : P.sobol[id];
             const float4 thr = REC ? in[2] : P.thr[id];
             V3 T = v3(thr.x, thr.y, thr.z);
+            /* Marschner: the wi terms of the bounce's NEE evaluation and BSDF sample, once */
+            const bool mar = B.kind == HPT_BSDF_MARSCHNER;
+            if (mar) stashWi(wiL, (int) blockDim.x, marschnerWi(B.mar, wi));
             /* ---- direct illumination (path.cpp:175, scene.cpp:828-852, envmap.cpp:516-543) ---- */
             if (B.smooth) {
                 float nx = sobolSampleUniform(sc, sidx, dim), ny = sobolSampleUniform(sc, sidx, dim + 1);
@@ -2722,7 +2796,7 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
                       farT <= 0)) {
                     V3 val = divs(value, pdf);
                     V3 wo = sh.toLocal(dW);
-                    V3 bsdfVal = bsdfEval(B, wi, wo);
+                    V3 bsdfVal = mar ? marschnerEvalW(B.mar, loadWi(wiL, (int) blockDim.x), wo) : bsdfEval(B, wi, wo);
                     if (!isZero(bsdfVal) && (!sc.strictNormals || dot(geo.n, dW) * wo.z > 0)) {
                         float bp = bsdfPdf(B, wi, wo);
                         float weight = miWeight(pdf, bp);
@@ -2748,7 +2822,12 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
             float bpdf = 0.0f;
             uint32_t type = 0;
             V3 w;
-            w = bsdfSample(B, wi, bx, by, woL, bpdf, type);
+            if (mar) {
+                bpdf = 1.0f;
+                w = marschnerSampleW(B.mar, loadWi(wiL, (int) blockDim.x), GlobalTabs{B.mar}, wi, bx, by, woL, type);
+            } else {
+                w = bsdfSample(B, wi, bx, by, woL, bpdf, type);
+            }
             if (!isZero(w)) {
                 V3 wo = sh.toWorld(woL);
                 float woDotGeoN = dot(geo.n, wo);
@@ -2793,6 +2872,8 @@ template <bool MULTI>
 __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
                                             uint32_t *__restrict__ traceQ, uint32_t *__restrict__ shadowQ,
                                             const HptShadeIO &q) {
+    __shared__ float wiLds[HPT_WI_ROWS * HPT_SHADE_BLOCK];
+    float *const wiL = wiLds + threadIdx.x;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n0 = *q.nShade;
     const uint32_t n = n0 < q.tailFrom ? 0u : n0; /* a short queue is the tail launch's bounce */
@@ -2812,7 +2893,7 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
         id = shadeQ[tid];
 #pragma unroll
         for (int i = 0; i < 3; ++i) in[i] = P.shadeRec[3 * tid + i];
-        shadePath<MULTI, true>(sc, P, id, P.hitS[tid], q.counters, cont, shadow, in, cOut, sOut);
+        shadePath<MULTI, true>(sc, P, id, P.hitS[tid], q.counters, cont, shadow, in, cOut, sOut, wiL);
     }
     /* the hit record starts pending: a trace launch that cuts may leave the ray unfinished */
     const uint32_t cpos = qpushBlockRec<HPT_SHADE_BLOCK, 4>(cont, id, traceQ, q.nTrace, P.postRec, cOut, P.hitQ, HPT_PENDING);
@@ -2996,6 +3077,8 @@ struct HptTail {
 template <bool MULTI>
 __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const HptTail &T,
                                           uint32_t *__restrict__ counters, uint2 *stk) {
+    __shared__ float wiLds[HPT_WI_ROWS * HPT_TRACE_BLOCK];
+    float *const wiL = wiLds + threadIdx.x;
     const uint32_t lane = __lane_id(), partner = lane & ~1u;
     const bool odd = (lane & 1u) != 0;
     const uint32_t n0 = *T.nShade;
@@ -3062,7 +3145,7 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
         countBlockCost(P, live && !odd, id);
         if (live && !odd) {
             ++nb;
-            shadePath<MULTI>(sc, P, id, hitRec, counters, cont, shadow, nullptr, nullptr, nullptr);
+            shadePath<MULTI>(sc, P, id, hitRec, counters, cont, shadow, nullptr, nullptr, nullptr, wiL);
         }
         __threadfence_block(); /* the continuation ray is in HBM for the odd lane */
         const int f = __shfl((cont ? 1 : 0) | (shadow ? 2 : 0), (int) partner);
