@@ -70,7 +70,12 @@ static bool defaultCut() {
 /* a bounce launch cuts only with at least this many rays per lane (HPT_CUT_MIN; 0: always, a test hook) */
 static int defaultCutMin() {
     const char *v = std::getenv("HPT_CUT_MIN");
-    return v ? std::max(0, std::atoi(v)) : 4;
+    return v ? std::min(254, std::max(0, std::atoi(v))) : 4;
+}
+/* a wave drains this many microseconds after its dry point before it may cut (HPT_CUT_AFTER_US) */
+static int defaultCutAfterUs() {
+    const char *v = std::getenv("HPT_CUT_AFTER_US");
+    return v ? std::min(100000, std::max(0, std::atoi(v))) : 0;
 }
 static bool defaultClaimBuckets() {
     const char *v = std::getenv("HPT_CLAIM_BUCKETS");
@@ -134,7 +139,7 @@ struct hpt_context {
     uint32_t *bucketBuf = nullptr;
     bool claimBuckets = defaultClaimBuckets();
     bool cut = defaultCut();
-    int cutMin = defaultCutMin();
+    int cutMin = defaultCutMin(), cutAfterUs = defaultCutAfterUs();
     uint32_t *counters = nullptr;
     uint64_t *dstats = nullptr;
     float4 *partial = nullptr;     /* film splat partials: slots x 9 (k_splat -> k_gather) */
@@ -1238,7 +1243,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                 return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(p), C + HPT_C_SHADOW(p),
                                         C + HPT_CURSOR_SET(p), dst, 2ull * grid + carryIn, s,
                                         c->P.bucketQ ? C + HPT_C_BUCKET(p, 0) : nullptr, C, q,
-                                        cut && c->cut ? 1 + c->cutMin : 0);
+                                        cut && c->cut ? (c->cutAfterUs << 8) | (1 + c->cutMin) : 0);
             });
             if (e1) return e1;
             reportLaunch("bounce");

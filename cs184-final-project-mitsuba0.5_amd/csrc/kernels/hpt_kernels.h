@@ -148,7 +148,8 @@ hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPath
    cursor set of parity nextParity, which the next bounce appends to / claims from */
 /* counters given: the launch also traces carry set p = nextParity ^ 1 (HPT_C_CARRY(p) rays), and with
    cut = 1 + K it may leave the closest rays still running at its dry point unfinished (k_post carries
-   their paths to carry set nextParity) when it has at least K rays per lane */
+   their paths to carry set nextParity) when it has at least K rays per lane; cut | (us << 8): a wave
+   first drains for us microseconds after its dry point */
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
                             uint64_t maxItems, hipStream_t s, const uint32_t *nBucket = nullptr,

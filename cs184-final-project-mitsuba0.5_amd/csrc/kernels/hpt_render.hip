@@ -805,7 +805,9 @@ struct RaySplitter {
     __device__ __forceinline__ uint32_t drain(const HptScene &sc, IO &io, TraceRay &r, bool &active, TraceCounters &tc,
                                               Probe &probe) {
         uint32_t nU = 0;
+        const uint32_t t0 = (uint32_t) __builtin_amdgcn_s_memrealtime();
         while (true) {
+            if (io.abandonLate(active, r.shadow, t0)) break; /* launch cut after a partial drain */
             step(r, active);
             if (__ballot(active) == 0) break;
             probe.onDrainRound(__ballot(active));
@@ -2230,7 +2232,8 @@ __device__ __forceinline__ void qpushBlock2(bool pred, uint32_t value, uint32_t 
 template <int BLOCK, int NR>
 __device__ __forceinline__ uint32_t qpushBlockRec(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter,
                                                   float4 *recs, const float4 *rec, uint32_t *array2 = nullptr,
-                                                  uint32_t value2 = 0u) {
+                                                  uint32_t value2 = 0u, uint32_t cap = ~0u) {
+    /* entries at positions >= cap are not written (the caller checks the returned position) */
     constexpr int NW = BLOCK / 64;
     __shared__ uint32_t waveCount[NW];
     __shared__ uint32_t blockBase;
@@ -2249,7 +2252,7 @@ __device__ __forceinline__ uint32_t qpushBlockRec(bool pred, uint32_t value, uin
     }
     __syncthreads();
     const uint32_t pos = blockBase + waveCount[wave] + (uint32_t) __popcll(mask & ((1ull << lane) - 1ull));
-    if (pred) {
+    if (pred && pos < cap) {
         queue[pos] = value;
 #pragma unroll
         for (int i = 0; i < NR; ++i) recs[NR * pos + i] = rec[i];
@@ -2425,6 +2428,7 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
 struct HptCarryCtl {
     float4 *in;
     uint32_t n, cut;
+    uint32_t after; /* s_memrealtime ticks (10 ns) a wave drains after its dry point before it may cut */
 };
 __shared__ HptCarryCtl gCarry;
 
@@ -2538,7 +2542,13 @@ struct PathIOT {
        HPT_PENDING, as k_shade / k_post wrote them, and k_post carries their paths to the next
        bounce's launch).  A wave still tracing a shadow ray drains as before */
     HD bool abandon(bool active, bool shadow) const {
-        if (!BUCKETS || !gCarry.cut) return false;
+        if (!BUCKETS || !gCarry.cut || gCarry.after) return false;
+        return __ballot(active && shadow) == 0;
+    }
+    /* the same, in the drain, once the wave has drained `after` ticks since t0 (its dry point) */
+    HD bool abandonLate(bool active, bool shadow, uint32_t t0) const {
+        if (!BUCKETS || !gCarry.cut || !gCarry.after) return false;
+        if ((uint32_t) __builtin_amdgcn_s_memrealtime() - t0 < gCarry.after) return false;
         return __ballot(active && shadow) == 0;
     }
 };
@@ -2593,7 +2603,8 @@ HD BouncePathIO bouncePathIO(const HptPaths &P, const uint32_t *traceQ, const ui
            dry at their first claim) */
         const uint64_t lanes = (uint64_t) gridDim.x * blockDim.x;
         const uint64_t items = (uint64_t) *nTrace + *nShadow + gCarry.n;
-        gCarry.cut = carry && cut && items >= (uint64_t) (cut - 1u) * lanes ? 1u : 0u;
+        gCarry.cut = carry && cut && items >= (uint64_t) ((cut - 1u) & 0xffu) * lanes ? 1u : 0u;
+        gCarry.after = (cut >> 8) * 100u; /* cut >> 8: microseconds */
     }
     __syncthreads();
     return io;
@@ -3027,26 +3038,18 @@ extern "C" __global__ __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc,
         else alive = postPath<true>(sc, P, id, seg != HPT_MISS, counters, rec, sOut);
     }
     /* launch cut: the paths whose rays were left unfinished go to carry set carrySet ^ 1, for the
-       next bounce's trace launch (it traces them first) and k_post */
-    const uint64_t cm = __ballot(carry);
-    if (cm) {
-        const uint32_t lane = __lane_id(), leader = (uint32_t) (__ffsll((unsigned long long) cm) - 1);
+       next bounce's trace launch (it traces them first) and k_post; one atomic per block (the
+       pending paths are spread over the whole queue: one per wave serialised ~70 k atomics on
+       the count per launch) */
+    if (carrySet <= 1u) {
         const uint32_t out = carrySet ^ 1u;
-        uint32_t base = 0;
-        if (lane == leader) {
-            base = atomicAdd(&counters[HPT_C_CARRY(out)], (uint32_t) __popcll(cm));
-            atomicAdd(&counters[HPT_C_CUT_RAYS], (uint32_t) __popcll(cm));
-        }
-        base = __shfl(base, (int) leader);
-        const uint32_t j = base + (uint32_t) __popcll(cm & ((1ull << lane) - 1ull));
-        if (carry && j >= P.carryCap) atomicOr(sc.fault, HPT_FAULT_CARRY); /* more than a launch's lanes: a bug */
-        if (carry && j < P.carryCap) {
-            float4 *co = out ? P.carry[1] : P.carry[0];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) co[4 * j + i] = rec[i];
-            hptCarryIds(co, P.carryCap)[j] = id;
-            hptCarryHits(co, P.carryCap)[j] = HPT_PENDING;
-        }
+        float4 *co = out ? P.carry[1] : P.carry[0];
+        const uint32_t pos = qpushBlockRec<HPT_POST_BLOCK, 4>(carry, id, hptCarryIds(co, P.carryCap),
+                                                              &counters[HPT_C_CARRY(out)], co, rec,
+                                                              hptCarryHits(co, P.carryCap), HPT_PENDING, P.carryCap);
+        if (carry && pos >= P.carryCap) atomicOr(sc.fault, HPT_FAULT_CARRY); /* more than a launch's lanes: a bug */
+        const uint32_t nb = (uint32_t) __syncthreads_count(carry);
+        if (threadIdx.x == 0 && nb) atomicAdd(&counters[HPT_C_CUT_RAYS], nb);
     }
     /* the survivors' shade records and hit records travel with the shade queue, in its order */
     qpushBlockRec<HPT_POST_BLOCK, 3>(alive, id, shadeQ, nShade, P.shadeRec, sOut, P.hitS, seg);
@@ -3361,6 +3364,7 @@ struct BatchIO {
         return 0;
     }
     HD bool abandon(bool, bool) const { return false; } /* every ray of a batch finishes in its launch */
+    HD bool abandonLate(bool, bool, uint32_t) const { return false; }
 };
 
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptScene sc, int n, const float *o,
