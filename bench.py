@@ -223,7 +223,7 @@ def main():
                  node_slots=c.node_slots, prim_slots=c.prim_slots,
                  p_rays=c.packet_rays, p_nodes=c.packet_nodes, p_prims=c.packet_prims, p_exact=c.packet_exact,
                  p_node_slots=c.packet_node_slots, p_prim_slots=c.packet_prim_slots, p_fallbacks=c.packet_fallbacks)
-    acc = {"ms_trace": 0.0, "ms_packet": 0.0, "launches": 0, "p_launches": 0, "kernels": {}, "cut": 0}
+    acc = {"ms_trace": 0.0, "ms_packet": 0.0, "launches": 0, "p_launches": 0, "kernels": {}}
 
     def collect():
         s = r.stats()  # HIP events around every kernel (on the library's stream), no counters
@@ -231,7 +231,6 @@ def main():
         acc["launches"] += s.trace_launches
         acc["ms_packet"] += s.ms_trace_packet
         acc["p_launches"] += s.packet_launches
-        acc["cut"] += s.cut_rays
         for k in ("camera", "trace_packet", "trace", "primary", "shade", "post", "tail", "gather"):
             acc["kernels"][k] = acc["kernels"].get(k, 0.0) + getattr(s, "ms_" + k)
 
@@ -372,9 +371,6 @@ def main():
                       "camera_packet_util_nodes": round(tot["p_nodes"] / max(1, tot["p_node_slots"]), 3),
                       "camera_packet_util_prims": round(tot["p_prims"] / max(1, tot["p_prim_slots"]), 3),
                       "camera_packet_fallbacks": int(frame["p_fallbacks"]),
-                      # launch cut: closest rays per timed frame left unfinished at a
-                      # bounce launch's dry point and traced again by the next launch (rank 0)
-                      "cut_rays_per_frame": int(acc["cut"] // max(1, args.steps)),
                       "image_mean": float(img.mean()),
                       # exact-arithmetic fingerprint of the frame (sum of the RGBW film in fp64):
                       # identical for every traversal variant, since hits are bit-exact

@@ -62,21 +62,6 @@ static bool defaultBounceAhead() {
 
 /* claim-order buckets (hpt_kernels.h HPT_BUCKETS): bounce rays claimed longest first;
    HPT_CLAIM_BUCKETS=0/1 overrides the default */
-/* launch cut (HptPaths::carryRec): HPT_CUT=0 lets every bounce launch drain its last rays */
-static bool defaultCut() {
-    const char *v = std::getenv("HPT_CUT");
-    return v ? std::atoi(v) != 0 : false; /* off until measured on the GPU */
-}
-/* a bounce launch cuts only with at least this many rays per lane (HPT_CUT_MIN; 0: always, a test hook) */
-static int defaultCutMin() {
-    const char *v = std::getenv("HPT_CUT_MIN");
-    return v ? std::min(254, std::max(0, std::atoi(v))) : 4;
-}
-/* a wave drains this many microseconds after its dry point before it may cut (HPT_CUT_AFTER_US) */
-static int defaultCutAfterUs() {
-    const char *v = std::getenv("HPT_CUT_AFTER_US");
-    return v ? std::min(100000, std::max(0, std::atoi(v))) : 0;
-}
 static bool defaultClaimBuckets() {
     const char *v = std::getenv("HPT_CLAIM_BUCKETS");
     return v ? std::atoi(v) != 0 : false;
@@ -138,8 +123,6 @@ struct hpt_context {
     uint32_t *qTrace = nullptr, *qShadow = nullptr, *qShade[2] = {nullptr, nullptr};
     uint32_t *bucketBuf = nullptr;
     bool claimBuckets = defaultClaimBuckets();
-    bool cut = defaultCut();
-    int cutMin = defaultCutMin(), cutAfterUs = defaultCutAfterUs();
     uint32_t *counters = nullptr;
     uint64_t *dstats = nullptr;
     float4 *partial = nullptr;     /* film splat partials: slots x 9 (k_splat -> k_gather) */
@@ -267,10 +250,6 @@ int ensureWave(hpt_context *c, uint64_t n) {
     r |= alloc(n * 4, (void **) &c->qShade[0]);
     r |= alloc(n * 4, (void **) &c->qShade[1]);
     r |= alloc((size_t) HPT_BUCKETS * 2 * n * 4, (void **) &c->bucketBuf); /* claim-order buckets: all rays of a bounce fit one */
-    /* the two carry sets of the launch cut: as many rays as a k_trace launch holds lanes */
-    const uint32_t cap = hpt_trace_resident_lanes();
-    for (int k = 0; k < 2; ++k) r |= alloc((size_t) cap * (64 + 4 + 4), (void **) &c->P.carry[k]);
-    c->P.carryCap = cap;
     r |= alloc(HPT_COUNTER_WORDS * 4, (void **) &c->counters);
     r |= alloc(2 * 24 * 8, (void **) &c->dstats); /* the counters, and a snapshot at the start of a wave */
     if (r) return HPT_EDEVICE;
@@ -292,7 +271,6 @@ int checkFault(hpt_context *c) {
         return setErr(c, HPT_ETRAVERSAL, "kd-tree traversal exceeded 2^18 leaf rounds for a ray (malformed tree?)");
     if (f & HPT_FAULT_RESTARTS)
         return setErr(c, HPT_ETRAVERSAL, "kd-tree traversal exceeded its kd-restart bound for a ray");
-    if (f & HPT_FAULT_CARRY) return setErr(c, HPT_EDEVICE, "internal error: a launch cut overflowed its carry set");
     return HPT_OK;
 }
 
@@ -1228,22 +1206,17 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         bool learn = c->bounceAhead && !ahead, extended = false;
         BounceSchedule seen;
         int b = 1, bounce = 0;
-        /* launch cut: a bounce's trace launch may leave up to carryCap closest rays to the next one,
-           whose trace and post launches take them on top of their own queues (grids sized for it) */
-        const uint64_t carryIn = c->P.carryCap;
-        auto wavefrontBounce = [&](uint32_t p, uint64_t grid, bool cut) -> hipError_t {
+        auto wavefrontBounce = [&](uint32_t p, uint64_t grid, uint32_t tailFrom) -> hipError_t {
             const uint32_t q = p ^ 1u;
             hipError_t e1 = timed(2, [&] {
                 return hpt_launch_shade(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), c->qTrace, C + HPT_C_TRACE(p),
-                                        c->qShadow, C + HPT_C_SHADOW(p), C, grid, 0u, s, C + HPT_C_BUCKET(p, 0),
-                                        C + HPT_C_CARRY(q));
+                                        c->qShadow, C + HPT_C_SHADOW(p), C, grid, tailFrom, s, C + HPT_C_BUCKET(p, 0));
             });
             if (e1) return e1;
             e1 = timed(-1, [&] {
                 return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(p), C + HPT_C_SHADOW(p),
-                                        C + HPT_CURSOR_SET(p), dst, 2ull * grid + carryIn, s,
-                                        c->P.bucketQ ? C + HPT_C_BUCKET(p, 0) : nullptr, C, q,
-                                        cut && c->cut ? (c->cutAfterUs << 8) | (1 + c->cutMin) : 0);
+                                        C + HPT_CURSOR_SET(p), dst, 2ull * grid, s,
+                                        c->P.bucketQ ? C + HPT_C_BUCKET(p, 0) : nullptr, C, q);
             });
             if (e1) return e1;
             reportLaunch("bounce");
@@ -1254,18 +1227,13 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                 std::fprintf(stderr, "[bounce %d] shade %llu -> trace %.3f ms\n", b, (unsigned long long) grid, ms);
             }
             return timed(3, [&] {
-                return hpt_launch_post(sc, c->P, c->qTrace, C + HPT_C_TRACE(p), c->qShade[q], C + HPT_C_SHADE(q), C,
-                                       grid + carryIn, s, p);
+                return hpt_launch_post(sc, c->P, c->qTrace, C + HPT_C_TRACE(p), c->qShade[q], C + HPT_C_SHADE(q), C, grid, s);
             });
         };
         if (ahead) {
-            /* which paths a bounce holds depends on which rays the launches before it cut (a
-               matter of timing): the grids get carryCap of headroom, and the schedule's last
-               wavefront bounce does not cut (its tail, or the host, takes what follows) */
             const BounceSchedule &k = known->second;
-            const uint64_t margin = c->cut ? carryIn : 0;
             for (size_t i = 0; i < k.shade.size() && e == hipSuccess; ++i, ++b)
-                e = wavefrontBounce((uint32_t) b & 1u, k.shade[i] + margin, i + 1 < k.shade.size());
+                e = wavefrontBounce((uint32_t) b & 1u, k.shade[i], 0u);
             if (e == hipSuccess && k.tail)
                 e = timed(5, [&] {
                     const uint32_t p = (uint32_t) b & 1u;
@@ -1280,8 +1248,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e) break;
             const uint32_t n = hostCnt[HPT_C_SHADE(p)];
-            const uint32_t carry = std::min(hostCnt[HPT_C_CARRY(p)], c->P.carryCap); /* rays the last launch cut */
-            if ((n == 0 && carry == 0) || hostCnt[HPT_C_TAIL_PATHS] != 0) break; /* no live path, or k_tail took the rest */
+            if (n == 0 || hostCnt[HPT_C_TAIL_PATHS] != 0) break; /* no live path, or k_tail took the rest */
             if (ahead && fits) {
                 /* the schedule did not cover the wave (its tail declined, or bounces ran past it):
                    re-record it as the part launched ahead plus the bounces read back from here */
@@ -1291,27 +1258,6 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                 fits = false;
                 learn = extended = true;
                 c->stats.schedule_extensions++;
-            }
-            if (carry && (n == 0 || n < c->tailPaths)) {
-                /* the last bounce cut rays and no wavefront bounce follows: trace them (and nothing
-                   else: this bounce's queues are empty) and post their paths into this bounce's shade
-                   queue, then look again */
-                e = timed(-1, [&] {
-                    return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(p), C + HPT_C_SHADOW(p),
-                                            C + HPT_CURSOR_SET(p), dst, carry, s, nullptr, C, p ^ 1u, 0);
-                });
-                if (e == hipSuccess)
-                    e = timed(3, [&] {
-                        return hpt_launch_post(sc, c->P, c->qTrace, C + HPT_C_TRACE(p), c->qShade[p], C + HPT_C_SHADE(p),
-                                               C, carry, s, p);
-                    });
-                /* the carry set and cursors of parity p are used up: a wavefront bounce may follow */
-                if (e == hipSuccess) e = hipMemsetAsync(C + HPT_C_CARRY(p), 0, 4, s);
-                if (e == hipSuccess) e = hipMemsetAsync(C + HPT_CURSOR_SET(p), 0, HPT_CURSORS * HPT_CURSOR_STRIDE * 4, s);
-                if (e) break;
-                c->stats.carry_flushes++;
-                --b;
-                continue;
             }
             if (n < c->tailPaths) {
                 /* few live paths: finish them all in one launch (k_tail) */
@@ -1323,7 +1269,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                 break;
             }
             seen.shade.push_back(n);
-            e = wavefrontBounce(p, n, true);
+            e = wavefrontBounce(p, n, 0u);
         }
         if (e) break;
         if (hostCnt[HPT_C_OVERFLOW] && !ahead) {
@@ -1362,7 +1308,6 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             uint64_t shaded = 0;
             std::memcpy(&shaded, hostCnt + HPT_C_BOUNCES, 8);
             bounces += shaded + hostCnt[HPT_C_TAIL_BOUNCES]; /* k_tail counts its first bounce too */
-            c->stats.cut_rays += hostCnt[HPT_C_CUT_RAYS];
             c->stats.tail_paths += hostCnt[HPT_C_TAIL_PATHS];
             bounce = (int) hostCnt[HPT_C_LAUNCHES];
         }

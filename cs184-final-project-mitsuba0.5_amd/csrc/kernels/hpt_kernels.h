@@ -18,15 +18,10 @@
 #define HPT_C_LAUNCHES 8     /* bounces that shaded live paths (k_shade or k_tail launches with work) */
 #define HPT_C_TAIL_PATHS 9   /* paths k_tail took over */
 #define HPT_C_OVERFLOW 10    /* a k_shade grid (sized from a schedule) was shorter than its queue */
-/* rays in carry set p (HptPaths::carryRec[p]): closest rays the bounce launch of parity p ^ 1 cut
-   at its dry point, for the next launch (parity p) to trace from their start; may exceed
-   HptPaths::carryCap (the rays past it were not cut).  Words 11 and 15 */
-#define HPT_C_CARRY(p) (11 + 4 * (p))
 #define HPT_C_ERROR 12       /* set when a path runs out of Sobol dimensions */
 #define HPT_C_TAIL_BOUNCES 13 /* path-bounces shaded inside k_tail */
 #define HPT_C_TAIL_CURSOR 14  /* k_tail's work claims */
-#define HPT_C_CUT_RAYS 24     /* rays the wave's launches cut (HPT_C_CARRY counts, summed before they are zeroed) */
-#define HPT_Q_COUNT 32        /* the words the host reads back */
+#define HPT_Q_COUNT 16
 /* claim-order buckets of a bounce's trace launch (parity p): rays appended by k_shade to
    HptPaths::bucketQ by the length of their interval inside the scene box, and claimed by
    k_trace longest first, so that the rays still running when its queue runs dry are short */
@@ -36,7 +31,6 @@
    with whatever hit it had; the render / batch call fails instead) */
 #define HPT_FAULT_LEAVES 1u   /* more than HptScene::maxLeafRounds (2^18) leaf rounds for one ray */
 #define HPT_FAULT_RESTARTS 2u /* more than HptScene::maxRestarts (1024) kd-restarts for one ray */
-#define HPT_FAULT_CARRY 4u    /* a launch cut left more rays than a trace launch holds lanes (internal error) */
 #define HPT_MAX_LEAF_ROUNDS (1u << 18)
 #define HPT_MAX_RESTARTS 1024u
 /* k_trace work cursors (persistent waves claim rays from them), one per
@@ -112,13 +106,6 @@ struct HptPaths {
    per block serialised ~70 k atomics per launch and cost k_shade 4 ms per frame) */
     uint32_t *blockCost;
     uint32_t costSpp, costStride;
-    /* Launch cut: a bounce launch whose queues run dry stops tracing its closest
-       rays still in flight instead of waiting ~0.5 ms for them (the drain).  Each such ray's post
-       record (64 B, = postRec), path id and, once traced again, hit go to carry set p ^ 1 (p: the
-       launch's parity), whose rays the next bounce launch claims first and whose paths the next
-       k_post posts.  carryCap: k_trace's resident lanes, the most rays one launch can hold */
-    float4 *carry[2]; /* set k: carryCap post records (4 float4), then carryCap path ids, then carryCap hits */
-    uint32_t carryCap;
     float4 *bw;        /* bsdf weight rgb, bsdf pdf                  */
     float4 *sdir;      /* shadow ray direction xyz, maxt             */
     float4 *scontrib;  /* NEE contribution rgb (added if unoccluded) */
@@ -126,14 +113,6 @@ struct HptPaths {
 
 
 #define HPT_COST_STRIPES 64
-/* hit record of a closest ray cut at its launch's dry point (k_post leaves the path to the next
-   bounce's k_post, which reads the carried ray's hit) */
-#define HPT_PENDING 0xfffffffeu
-/* the parts of a carry set (HptPaths::carry) */
-__host__ __device__ inline uint32_t *hptCarryIds(float4 *set, uint32_t cap) { return reinterpret_cast<uint32_t *>(set + 4ull * cap); }
-__host__ __device__ inline uint32_t *hptCarryHits(float4 *set, uint32_t cap) { return hptCarryIds(set, cap) + cap; }
-/* trace key of a carried ray (its index in the carry set | this bit) */
-#define HPT_CARRY_BIT 0x80000000u
 #define HPT_BUCKET_SHADOW 0x80000000u
 /* hit record of a miss (a segment id never has all 31 bits set) */
 #define HPT_MISS 0xffffffffu
@@ -146,19 +125,13 @@ hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPath
 /* nBucket (nullptr: queue order): the launch's HPT_BUCKETS claim-order bucket lengths (P.bucketQ).
    counters (nullptr: none): a bounce launch of parity p = nextParity ^ 1 also zeroes the counts and
    cursor set of parity nextParity, which the next bounce appends to / claims from */
-/* counters given: the launch also traces carry set p = nextParity ^ 1 (HPT_C_CARRY(p) rays), and with
-   cut = 1 + K it may leave the closest rays still running at its dry point unfinished (k_post carries
-   their paths to carry set nextParity) when it has at least K rays per lane; cut | (us << 8): a wave
-   first drains for us microseconds after its dry point */
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
                             uint64_t maxItems, hipStream_t s, const uint32_t *nBucket = nullptr,
-                            uint32_t *counters = nullptr, uint32_t nextParity = 0, int cut = 0);
+                            uint32_t *counters = nullptr, uint32_t nextParity = 0);
 /* the camera pass's rays one per lane (HPT_PACKETS=0): traceQ[0, *nTrace), hits to P.hitQ by position */
 hipError_t hpt_launch_trace_camera(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
                                    uint32_t *cursors, uint32_t *stats, uint64_t maxItems, hipStream_t s);
-/* the most lanes a k_trace launch holds on the current device (HptPaths::carryCap) */
-uint32_t hpt_trace_resident_lanes();
 hipError_t hpt_launch_env_filtered_batch(const HptScene &sc, int n, const float *d, const float *rx, const float *ry,
                                         float *out, hipStream_t s);
 /* closest-hit rays as 64-ray packets (coherent rays: the camera pass); the rays of a packet whose
@@ -173,15 +146,11 @@ hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint3
                               uint32_t *shadeQ, uint32_t *nShade, uint64_t maxItems, hipStream_t s);
 /* tailFrom: the launch leaves a queue shorter than this to the tail launch of the same
    bounce (0: always shade); a queue longer than the grid (maxItems) sets HPT_C_OVERFLOW */
-/* carryClear: the carry count the bounce's trace launch cuts into (zeroed before it runs) */
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
                             uint32_t *traceQ, uint32_t *nTrace, uint32_t *shadowQ, uint32_t *nShadow, uint32_t *counters,
-                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s, uint32_t *nBucket = nullptr,
-                            uint32_t *carryClear = nullptr);
-/* carrySet 0 / 1: the paths of that carry set are posted too (after traceQ's); ~0u: none */
+                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s, uint32_t *nBucket = nullptr);
 hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
-                           uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s,
-                           uint32_t carrySet = ~0u);
+                           uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s);
 /* the rest of every live path (the shade queue) to termination in one launch, when the queue
    is shorter than tailFrom (~0u: always); items = HPT_ITEMS_ON_DEVICE when the host has not
    read the queue length (the launch then sizes its work from it on the device) */

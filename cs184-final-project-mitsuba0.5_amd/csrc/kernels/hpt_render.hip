@@ -805,9 +805,7 @@ struct RaySplitter {
     __device__ __forceinline__ uint32_t drain(const HptScene &sc, IO &io, TraceRay &r, bool &active, TraceCounters &tc,
                                               Probe &probe) {
         uint32_t nU = 0;
-        const uint32_t t0 = (uint32_t) __builtin_amdgcn_s_memrealtime();
         while (true) {
-            if (io.abandonLate(active, r.shadow, t0)) break; /* launch cut after a partial drain */
             step(r, active);
             if (__ballot(active) == 0) break;
             probe.onDrainRound(__ballot(active));
@@ -902,7 +900,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             active = false;
         }
     }
-    if (SPLIT && !io.abandon(active, r.shadow)) {
+    if (SPLIT) {
         probe.onDrainStart();
         RaySplitter<STACK> split{stk, (int) blockDim.x};
         nU += split.template drain<false>(sc, io, r, active, tc, probe);
@@ -2232,8 +2230,7 @@ __device__ __forceinline__ void qpushBlock2(bool pred, uint32_t value, uint32_t 
 template <int BLOCK, int NR>
 __device__ __forceinline__ uint32_t qpushBlockRec(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter,
                                                   float4 *recs, const float4 *rec, uint32_t *array2 = nullptr,
-                                                  uint32_t value2 = 0u, uint32_t cap = ~0u) {
-    /* entries at positions >= cap are not written (the caller checks the returned position) */
+                                                  uint32_t value2 = 0u) {
     constexpr int NW = BLOCK / 64;
     __shared__ uint32_t waveCount[NW];
     __shared__ uint32_t blockBase;
@@ -2252,7 +2249,7 @@ __device__ __forceinline__ uint32_t qpushBlockRec(bool pred, uint32_t value, uin
     }
     __syncthreads();
     const uint32_t pos = blockBase + waveCount[wave] + (uint32_t) __popcll(mask & ((1ull << lane) - 1ull));
-    if (pred && pos < cap) {
+    if (pred) {
         queue[pos] = value;
 #pragma unroll
         for (int i = 0; i < NR; ++i) recs[NR * pos + i] = rec[i];
@@ -2421,17 +2418,6 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
    claimed together, so a launch's record writes fill whole lines in L2
    instead of a 32-byte sector per lone path-indexed 16-byte store.
    posQ (k_trace_overflow): the queue positions of the rays to trace. */
-/* A bounce launch's carry control (launch cut, HptPaths::carry): the carried rays of the previous
-   bounce (n of carry set `in`) and whether the launch may leave rays unfinished, for the whole
-   block in LDS -- k_trace has no scalar registers to spare for them (they are read at claims and
-   at the dry point only) */
-struct HptCarryCtl {
-    float4 *in;
-    uint32_t n, cut;
-    uint32_t after; /* s_memrealtime ticks (10 ns) a wave drains after its dry point before it may cut */
-};
-__shared__ HptCarryCtl gCarry;
-
 template <bool BUCKETS>
 struct PathIOT {
     HptPaths P;
@@ -2443,35 +2429,19 @@ struct PathIOT {
     bool recs; /* bounce launches: rays from the queue-ordered records, keys are queue positions */
     const uint32_t *bq; /* claim-order buckets (P.bucketQ), longest rays first; nullptr: queue order */
     uint32_t nb[BUCKETS ? HPT_BUCKETS : 1];
-    /* bounce launches (BUCKETS): the previous launch's carried rays, claimed after this one's
-       (gCarry) */
-    HD uint32_t nCarry() const { return BUCKETS ? gCarry.n : 0u; }
-    HD uint32_t count() const { return nTrace + nShadow + nCarry(); }
+    HD uint32_t count() const { return nTrace + nShadow; }
     /* cursor shard s of HPT_CURSORS: its length, and its j-th work item (a work index k: closest
-       rays [0, nTrace), shadow rays [nTrace, nTrace + nShadow), carried rays after them).
-       A bounce launch's shard holds the s-th part of the carried rays, then of the shadow rays,
-       then of the closest rays, in that claim order: the rays still running when the queues run
-       dry are closest rays, which the launch can cut.  With buckets a shard walks the s-th part
-       of every bucket after its carried rays, longest bucket first, so every shard claims long
-       rays before short ones */
+       rays [0, nTrace), then shadow rays).  With buckets a shard walks the s-th part of every
+       bucket, longest bucket first, so every shard claims long rays before short ones */
     HD uint32_t shardSize(uint32_t s) const {
-        if (!BUCKETS) return shardLo(count(), s + 1) - shardLo(count(), s);
-        const uint32_t nC = nCarry();
-        uint32_t n = shardLo(nC, s + 1) - shardLo(nC, s);
-        if (!bq) return n + shardLo(nShadow, s + 1) - shardLo(nShadow, s) + shardLo(nTrace, s + 1) - shardLo(nTrace, s);
+        if (!BUCKETS || !bq) return shardLo(count(), s + 1) - shardLo(count(), s);
+        uint32_t n = 0;
 #pragma unroll
         for (int b = 0; b < HPT_BUCKETS; ++b) n += shardLo(nb[b], s + 1) - shardLo(nb[b], s);
         return n;
     }
     HD uint32_t item(uint32_t s, uint32_t j) const {
-        if (!BUCKETS) return shardLo(count(), s) + j;
-        const uint32_t nC = nCarry(), c0 = shardLo(nC, s), cS = shardLo(nC, s + 1) - c0;
-        if (j < cS) return nTrace + nShadow + c0 + j;
-        j -= cS;
-        if (!bq) {
-            const uint32_t s0 = shardLo(nShadow, s), sS = shardLo(nShadow, s + 1) - s0;
-            return j < sS ? nTrace + s0 + j : shardLo(nTrace, s) + (j - sS);
-        }
+        if (!BUCKETS || !bq) return shardLo(count(), s) + j;
 #pragma unroll
         for (int b = HPT_BUCKETS - 1; b >= 0; --b) {
             const uint32_t lo = shardLo(nb[b], s), sz = shardLo(nb[b], s + 1) - lo;
@@ -2490,17 +2460,9 @@ struct PathIOT {
                 const float4 o = P.postRec[4 * k], d = P.postRec[4 * k + 1];
                 return beginRay(sc, r, v3(o.x, o.y, o.z), v3(d.x, d.y, d.z), kEpsilon, finf(), false);
             }
-            if (!BUCKETS || k < nTrace + nShadow) {
-                id = k - nTrace;
-                const float4 o = P.shadowRec[3 * id], d = P.shadowRec[3 * id + 1];
-                return beginRay(sc, r, v3(o.x, o.y, o.z), v3(d.x, d.y, d.z), kEpsilon, d.w, true);
-            }
-            /* a carried ray: the previous launch cut it, it is traced again from its start */
-            const uint32_t ci = k - nTrace - nShadow;
-            id = ci | HPT_CARRY_BIT;
-            const float4 *in = gCarry.in;
-            const float4 o = in[4 * ci], d = in[4 * ci + 1];
-            return beginRay(sc, r, v3(o.x, o.y, o.z), v3(d.x, d.y, d.z), kEpsilon, finf(), false);
+            id = k - nTrace;
+            const float4 o = P.shadowRec[3 * id], d = P.shadowRec[3 * id + 1];
+            return beginRay(sc, r, v3(o.x, o.y, o.z), v3(d.x, d.y, d.z), kEpsilon, d.w, true);
         }
         if (k < nTrace) {
             const uint32_t q = posQ ? posQ[k] : k;
@@ -2517,18 +2479,13 @@ struct PathIOT {
     /* id: the record's queue position / path (closest), the path (shadow ray);
        returns 1 for an unoccluded shadow ray */
     HD uint32_t finish(const HptScene &sc, uint32_t id, const TraceRay &r) {
-        const bool carried = BUCKETS && !r.shadow && (id & HPT_CARRY_BIT);
         if (HPT_PROBE_WANTS_PATH) {
-            const uint32_t path = r.shadow ? (recs ? shadowQ[id] : id)
-                                           : (carried ? hptCarryIds(gCarry.in, P.carryCap)[id & ~HPT_CARRY_BIT]
-                                                      : (byQueue && traceQ && !posQ ? traceQ[id] : HPT_MISS));
+            const uint32_t path = r.shadow ? (recs ? shadowQ[id] : id) : (byQueue && traceQ && !posQ ? traceQ[id] : HPT_MISS);
             probeRayFinished(r, path, r.shadow ? nTrace + id : id, recs);
         }
         if (!r.shadow) {
             /* the shading kernel re-derives the point from the segment and the accepted root */
-            const uint32_t rec = r.found ? r.segHit : HPT_MISS;
-            if (carried) hptCarryHits(gCarry.in, P.carryCap)[id & ~HPT_CARRY_BIT] = rec;
-            else (byQueue ? P.hitQ : P.hit)[id] = rec;
+            (byQueue ? P.hitQ : P.hit)[id] = r.found ? r.segHit : HPT_MISS;
             return 0;
         }
         if (r.found) return 0;
@@ -2536,20 +2493,6 @@ struct PathIOT {
         const float4 c = recs ? P.shadowRec[3 * id + 2] : P.scontrib[id], l = P.li[path];
         P.li[path] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
         return 1;
-    }
-    /* Launch cut, at a wave's dry point (wave-uniform): true when the wave may leave its running
-       rays unfinished -- the launch cuts and they are all closest rays (their hit records stay
-       HPT_PENDING, as k_shade / k_post wrote them, and k_post carries their paths to the next
-       bounce's launch).  A wave still tracing a shadow ray drains as before */
-    HD bool abandon(bool active, bool shadow) const {
-        if (!BUCKETS || !gCarry.cut || gCarry.after) return false;
-        return __ballot(active && shadow) == 0;
-    }
-    /* the same, in the drain, once the wave has drained `after` ticks since t0 (its dry point) */
-    HD bool abandonLate(bool active, bool shadow, uint32_t t0) const {
-        if (!BUCKETS || !gCarry.cut || !gCarry.after) return false;
-        if ((uint32_t) __builtin_amdgcn_s_memrealtime() - t0 < gCarry.after) return false;
-        return __ballot(active && shadow) == 0;
     }
 };
 
@@ -2584,29 +2527,13 @@ using BouncePathIO = PathIOT<true>;  /* queue order or claim-order buckets (k_tr
    the host knows them) */
 /* a bounce launch's work: its queue lengths and, with claim-order buckets, their lengths */
 HD BouncePathIO bouncePathIO(const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ, const uint32_t *nTrace,
-                             const uint32_t *nShadow, const uint32_t *nBucket, uint32_t *counters, uint32_t nextParity,
-                             uint32_t cut) {
+                             const uint32_t *nShadow, const uint32_t *nBucket) {
     BouncePathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0, true, nullptr, true};
     if (nBucket && P.bucketQ) {
         io.bq = P.bucketQ;
 #pragma unroll
         for (int b = 0; b < HPT_BUCKETS; ++b) io.nb[b] = nBucket[b];
     }
-    /* carry set p (this launch's parity) in, set nextParity out; every thread writes the same values */
-    const bool carry = counters && P.carryCap;
-    const uint32_t p = nextParity ^ 1u;
-    if (threadIdx.x == 0) {
-        gCarry.n = carry ? min(counters[HPT_C_CARRY(p)], P.carryCap) : 0u;
-        gCarry.in = p ? P.carry[1] : P.carry[0];
-        /* cut = 1 + K: only a launch with at least K rays per lane cuts (the rays still running
-           at its dry point are then at most 1 / K of its work; a smaller launch's lanes would be
-           dry at their first claim) */
-        const uint64_t lanes = (uint64_t) gridDim.x * blockDim.x;
-        const uint64_t items = (uint64_t) *nTrace + *nShadow + gCarry.n;
-        gCarry.cut = carry && cut && items >= (uint64_t) ((cut - 1u) & 0xffu) * lanes ? 1u : 0u;
-        gCarry.after = (cut >> 8) * 100u; /* cut >> 8: microseconds */
-    }
-    __syncthreads();
     return io;
 }
 /* the next bounce's counts and cursor set start at zero (what a separate clearing launch did):
@@ -2625,10 +2552,10 @@ __device__ __forceinline__ void clearNextParity(uint32_t *counters, uint32_t q) 
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
     const uint32_t *__restrict__ nTrace, const uint32_t *__restrict__ nShadow, uint32_t *__restrict__ cursors,
-    const uint32_t *__restrict__ nBucket, uint32_t *counters, uint32_t nextParity, uint32_t cut) {
+    const uint32_t *__restrict__ nBucket, uint32_t *counters, uint32_t nextParity) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    BouncePathIO io = bouncePathIO(P, traceQ, shadowQ, nTrace, nShadow, nBucket, counters, nextParity, cut);
     clearNextParity(counters, nextParity);
+    BouncePathIO io = bouncePathIO(P, traceQ, shadowQ, nTrace, nShadow, nBucket);
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(HptScene sc, HptPaths P,
@@ -2641,11 +2568,13 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
                                                                               uint32_t *counters, uint32_t nextParity,
                                                                               uint32_t *stats) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    BouncePathIO io = bouncePathIO(P, traceQ, shadowQ, nTrace, nShadow, nBucket, counters, nextParity, 0u);
     clearNextParity(counters, nextParity);
+    BouncePathIO io = bouncePathIO(P, traceQ, shadowQ, nTrace, nShadow, nBucket);
     tracePersistent<HPT_STACK, true>(sc, io, cursors, stk + threadIdx.x, stats);
 }
-/* the camera pass's rays one per lane (HPT_PACKETS=0): camera-queue positions are the keys */
+
+/* the camera pass's rays one per lane (HPT_PACKETS=0): camera-queue positions are the keys and
+   the hits go to P.hitQ by position, as the packet kernel writes them */
 template <bool STATS>
 __device__ __forceinline__ void traceCamera(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ,
                                             const uint32_t *nTrace, uint32_t *cursors, uint32_t *stats, uint2 *stk) {
@@ -2877,7 +2806,6 @@ struct HptShadeIO {
     uint32_t *nTrace, *nShadow, *counters;
     uint32_t tailFrom; /* a queue shorter than this is k_tail's (device-side bounce control); 0: always shade */
     uint32_t *nBucket; /* the next trace launch's claim-order bucket lengths (nullptr: no buckets) */
-    uint32_t *carryClear; /* the carry count the bounce's trace launch cuts into (nullptr: none) */
 };
 template <bool MULTI>
 __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
@@ -2888,7 +2816,6 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n0 = *q.nShade;
     const uint32_t n = n0 < q.tailFrom ? 0u : n0; /* a short queue is the tail launch's bounce */
-    if (blockIdx.x == 0 && threadIdx.x == 0 && q.carryClear) *q.carryClear = 0u; /* read back only after this bounce */
     if (blockIdx.x == 0 && threadIdx.x == 0 && n != 0) {
         atomicAdd((unsigned long long *) (q.counters + HPT_C_BOUNCES), (unsigned long long) n);
         atomicAdd(&q.counters[HPT_C_LAUNCHES], 1u);
@@ -2906,8 +2833,7 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
         for (int i = 0; i < 3; ++i) in[i] = P.shadeRec[3 * tid + i];
         shadePath<MULTI, true>(sc, P, id, P.hitS[tid], q.counters, cont, shadow, in, cOut, sOut, wiL);
     }
-    /* the hit record starts pending: a trace launch that cuts may leave the ray unfinished */
-    const uint32_t cpos = qpushBlockRec<HPT_SHADE_BLOCK, 4>(cont, id, traceQ, q.nTrace, P.postRec, cOut, P.hitQ, HPT_PENDING);
+    const uint32_t cpos = qpushBlockRec<HPT_SHADE_BLOCK, 4>(cont, id, traceQ, q.nTrace, P.postRec, cOut);
     const uint32_t spos = qpushBlockRec<HPT_SHADE_BLOCK, 3>(shadow, id, shadowQ, q.nShadow, P.shadowRec, sOut);
     if (q.nBucket) { /* uniform: the launch's claim-order buckets */
         const uint32_t bc = cont ? claimBucket(sc, v3(cOut[0].x, cOut[0].y, cOut[0].z), v3(cOut[1].x, cOut[1].y, cOut[1].z), finf()) : 0u;
@@ -3010,13 +2936,10 @@ extern "C" __global__ __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc,
                                                           const uint32_t *__restrict__ traceQ,
                                                           const uint32_t *__restrict__ nTrace,
                                                           uint32_t *__restrict__ shadeQ, uint32_t *__restrict__ nShade,
-                                                          uint32_t *__restrict__ counters, uint32_t carrySet) {
+                                                          uint32_t *__restrict__ counters) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = *nTrace; /* <= the bounce's shade queue, which k_shade checked against the grid */
-    /* then the paths the previous bounce carried (carry set carrySet: their closest rays were
-       traced again by this bounce's launch) */
-    const uint32_t nC = carrySet <= 1u ? min(counters[HPT_C_CARRY(carrySet)], P.carryCap) : 0u;
-    bool alive = false, carry = false;
+    bool alive = false;
     uint32_t id = 0;
     uint32_t seg = HPT_MISS;
     float4 rec[4], sOut[3];
@@ -3025,31 +2948,7 @@ extern "C" __global__ __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc,
         seg = P.hitQ[tid];
 #pragma unroll
         for (int i = 0; i < 4; ++i) rec[i] = P.postRec[4 * tid + i];
-    } else if (tid - n < nC) {
-        const uint32_t ci = tid - n;
-        float4 *cr = carrySet ? P.carry[1] : P.carry[0];
-        id = hptCarryIds(cr, P.carryCap)[ci];
-        seg = hptCarryHits(cr, P.carryCap)[ci];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) rec[i] = cr[4 * ci + i];
-    }
-    if (tid < n + nC) {
-        if (seg == HPT_PENDING) carry = true; /* the launch cut the ray: the path waits a bounce */
-        else alive = postPath<true>(sc, P, id, seg != HPT_MISS, counters, rec, sOut);
-    }
-    /* launch cut: the paths whose rays were left unfinished go to carry set carrySet ^ 1, for the
-       next bounce's trace launch (it traces them first) and k_post; one atomic per block (the
-       pending paths are spread over the whole queue: one per wave serialised ~70 k atomics on
-       the count per launch) */
-    if (carrySet <= 1u) {
-        const uint32_t out = carrySet ^ 1u;
-        float4 *co = out ? P.carry[1] : P.carry[0];
-        const uint32_t pos = qpushBlockRec<HPT_POST_BLOCK, 4>(carry, id, hptCarryIds(co, P.carryCap),
-                                                              &counters[HPT_C_CARRY(out)], co, rec,
-                                                              hptCarryHits(co, P.carryCap), HPT_PENDING, P.carryCap);
-        if (carry && pos >= P.carryCap) atomicOr(sc.fault, HPT_FAULT_CARRY); /* more than a launch's lanes: a bug */
-        const uint32_t nb = (uint32_t) __syncthreads_count(carry);
-        if (threadIdx.x == 0 && nb) atomicAdd(&counters[HPT_C_CUT_RAYS], nb);
+        alive = postPath<true>(sc, P, id, seg != HPT_MISS, counters, rec, sOut);
     }
     /* the survivors' shade records and hit records travel with the shade queue, in its order */
     qpushBlockRec<HPT_POST_BLOCK, 3>(alive, id, shadeQ, nShade, P.shadeRec, sOut, P.hitS, seg);
@@ -3363,8 +3262,6 @@ struct BatchIO {
         outP[3 * i + 2] = p.z;
         return 0;
     }
-    HD bool abandon(bool, bool) const { return false; } /* every ray of a batch finishes in its launch */
-    HD bool abandonLate(bool, bool, uint32_t) const { return false; }
 };
 
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptScene sc, int n, const float *o,
@@ -3500,7 +3397,7 @@ static unsigned persistentBlocks(const void *kernel, uint64_t items, int block =
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
                             uint64_t maxItems, hipStream_t s, const uint32_t *nBucket, uint32_t *counters,
-                            uint32_t nextParity, int cut) {
+                            uint32_t nextParity) {
     if (maxItems == 0) return hipSuccess;
     hptProbeBeforeTraceLaunch(s);
     if (stats)
@@ -3509,8 +3406,7 @@ hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_
                            counters, nextParity, stats);
     else
         hipLaunchKernelGGL(k_trace, dim3(persistentBlocks((const void *) k_trace, maxItems)), dim3(HPT_TRACE_BLOCK), 0, s,
-                           sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, nBucket, counters, nextParity,
-                           counters && cut > 0 ? (uint32_t) cut : 0u);
+                           sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, nBucket, counters, nextParity);
     return hipGetLastError();
 }
 hipError_t hpt_launch_trace_camera(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
@@ -3524,7 +3420,6 @@ hipError_t hpt_launch_trace_camera(const HptScene &sc, const HptPaths &P, const 
                            dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, nTrace, cursors);
     return hipGetLastError();
 }
-uint32_t hpt_trace_resident_lanes() { return persistentBlocks((const void *) k_trace, ~0ull >> 8) * HPT_TRACE_BLOCK; }
 hipError_t hpt_launch_trace_packet(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
                                    uint32_t *cursors, uint32_t *stats, uint64_t maxItems, uint32_t *overflowQ,
                                    uint32_t *nOverflow, hipStream_t s) {
@@ -3556,10 +3451,9 @@ hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint3
 }
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
                             uint32_t *traceQ, uint32_t *nTrace, uint32_t *shadowQ, uint32_t *nShadow, uint32_t *counters,
-                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s, uint32_t *nBucket,
-                            uint32_t *carryClear) {
+                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s, uint32_t *nBucket) {
     if (maxItems == 0) return hipSuccess;
-    const HptShadeIO q{nShade, nTrace, nShadow, counters, tailFrom, P.bucketQ ? nBucket : nullptr, carryClear};
+    const HptShadeIO q{nShade, nTrace, nShadow, counters, tailFrom, P.bucketQ ? nBucket : nullptr};
     if (sc.nShapes > 1)
         hipLaunchKernelGGL(k_shade_multi, dim3(blocksFor(maxItems, HPT_SHADE_BLOCK)), dim3(HPT_SHADE_BLOCK), 0, s, sc, P, shadeQ,
                            traceQ, shadowQ, q);
@@ -3569,11 +3463,10 @@ hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_
     return hipGetLastError();
 }
 hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
-                           uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s,
-                           uint32_t carrySet) {
+                           uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
     hipLaunchKernelGGL(k_post, dim3(blocksFor(maxItems, HPT_POST_BLOCK)), dim3(HPT_POST_BLOCK), 0, s, sc, P, traceQ, nTrace,
-                       shadeQ, nShade, counters, carrySet);
+                       shadeQ, nShade, counters);
     return hipGetLastError();
 }
 hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,

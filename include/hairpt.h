@@ -223,10 +223,6 @@ typedef struct hpt_stats {
     /* waves whose schedule was launched ahead but did not cover them (the tail declined, or
        bounces ran past it): finished bounce by bounce and their schedule re-recorded */
     uint64_t schedule_extensions;
-    /* launch cut (HPT_CUT=0: off): closest rays cut at their bounce launch's dry point and traced
-       again by the next launch, and the extra launches that traced such rays when no wavefront
-       bounce followed */
-    uint64_t cut_rays, carry_flushes;
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 
