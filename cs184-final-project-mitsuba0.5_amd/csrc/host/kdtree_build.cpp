@@ -641,6 +641,15 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
     if (S == 0) {
         t.nodes.push_back({0x80000000u, 0});
         t.leaves = 1;
+        /* the two-level form too (every traversal kernel reads it): one empty leaf behind a
+           split that sends every ray to it, like buildNode4's single-leaf tree; the empty
+           box above does not stop rays (its slabs are [-inf, inf]) */
+        HptNode4 nd{};
+        const float inf = std::numeric_limits<float>::infinity();
+        std::memcpy(&nd.w[0], &inf, 4);
+        nd.w[4] = nd.w[5] = nd.w[6] = nd.w[7] = 0x80000000u;
+        t.nodes4.push_back(nd);
+        t.leafTable.push_back(0), t.leafTable.push_back(0);
         return t;
     }
     int lg = 0;
