@@ -211,7 +211,7 @@ def main():
         # the warm-up frame's per-block path-bounces, summed over the ranks, deal the blocks
         # longest-first (the same deal on every rank); one more frame records its schedules
         distributed.balance_blocks(r, ((W + 31) // 32) * ((H + 31) // 32), world, dist,
-                                   "cuda:%d" % local if backend == "nccl" else "cpu")
+                                   "cuda:%d" % local if backend == "nccl" else "cpu", spp=spp, width=W, height=H)
         step(1)
         balanced = True
     # one untimed counted frame: traversal counters for the byte model (the

@@ -67,11 +67,28 @@ def block_owner_weighted(nbx: int, nby: int, world: int, weights) -> list[int]:
     return owner
 
 
-def balance_blocks(renderer, n_blocks: int, world: int, dist=None, device=None):
+# A block's camera pass in path-bounce units: the headline frame's camera pass (packets, 29.5 ms
+# for 67 M camera rays) against its bounces (trace + shade + post + tail, 113 ms for 113 M
+# path-bounces): 0.44 of a path-bounce per camera ray.  Sky blocks shade no bounce, but each
+# of their pixels still costs its camera rays.
+CAMERA_RAY_WEIGHT = 0.44
+
+
+def block_weights(costs, spp: int, width: int, height: int, block: int = 32):
+    """Per-block work for the deal: the path-bounces a block shaded (hpt_get_block_costs)
+    plus its camera rays (its pixels x spp) weighted by CAMERA_RAY_WEIGHT."""
+    import numpy as np
+    nbx, nby = (width + block - 1) // block, (height + block - 1) // block
+    bx, by = np.meshgrid(np.arange(nbx), np.arange(nby))
+    pixels = (np.minimum(block, width - bx * block) * np.minimum(block, height - by * block)).ravel()
+    return np.asarray(costs, np.float64) + CAMERA_RAY_WEIGHT * spp * pixels.astype(np.float64)
+
+
+def balance_blocks(renderer, n_blocks: int, world: int, dist=None, device=None, spp=None, width=None, height=None):
     """After a frame: every rank reads the path-bounces its blocks shaded
     (hpt_get_block_costs), the counts are summed over ranks, and every rank sets the same
-    weights (hpt_set_block_weights), so the next frames use the same work-balanced deal.
-    Returns the weights."""
+    weights (hpt_set_block_weights; with spp / width / height the camera rays are added, see
+    block_weights), so the next frames use the same work-balanced deal.  Returns the weights."""
     import numpy as np
     import torch
     costs = renderer.block_costs(n_blocks).astype(np.float64)
@@ -81,6 +98,8 @@ def balance_blocks(renderer, n_blocks: int, world: int, dist=None, device=None):
         t = torch.tensor(costs, dtype=torch.float64, device=device)
         dist.all_reduce(t)
         costs = t.cpu().numpy()
+    if spp is not None:
+        costs = block_weights(costs, spp, width, height)
     renderer.set_block_weights(costs)
     return costs
 

@@ -171,3 +171,15 @@ def test_balance_blocks_sums_costs_over_ranks(tmp_path):
     w0, w1 = np.load(tmp_path / "w0.npy"), np.load(tmp_path / "w1.npy")
     np.testing.assert_array_equal(w0, w1)
     np.testing.assert_array_equal(w0, np.arange(1, 17) * 10.0)
+
+
+def test_block_weights_add_camera_rays():
+    """bench.py's deal weighs a block by its path-bounces plus its camera rays (pixels x spp x
+    CAMERA_RAY_WEIGHT): a sky block (no bounce) is not free, an edge block has fewer pixels."""
+    import numpy as np
+    W, H, spp = 80, 40, 16  # 3 x 2 blocks; the last column is 16 pixels wide, the last row 8 high
+    costs = np.array([100, 0, 5, 7, 0, 0], np.uint64)
+    w = distributed.block_weights(costs, spp, W, H)
+    px = np.array([32 * 32, 32 * 32, 16 * 32, 32 * 8, 32 * 8, 16 * 8], np.float64)
+    np.testing.assert_allclose(w, costs.astype(np.float64) + distributed.CAMERA_RAY_WEIGHT * spp * px)
+    assert w[1] > 0 and w[4] < w[1]

@@ -30,8 +30,9 @@ def main():
     ap.add_argument("--ns", default="2,4,8", help="shard counts to time (besides N=1)")
     ap.add_argument("--split", choices=["blocks", "spp"], default="blocks",
                     help="rank r of N: its Hilbert-cyclic blocks (bench.py) or spp range [r*spp/N, (r+1)*spp/N) of every pixel")
-    ap.add_argument("--balance", action="store_true",
-                    help="deal the blocks by the path-bounces each shaded in a first frame (hpt_set_block_weights)")
+    ap.add_argument("--balance", nargs="?", const="camera", choices=["bounces", "camera"],
+                    help="deal the blocks by the work each did in a first frame (hpt_set_block_weights): its "
+                         "path-bounces, or those plus its camera rays (bench.py's deal, the default)")
     ap.add_argument("--stats-level", type=int, default=1, help="hpt_render_params.collect_stats of the timed renders")
     a = ap.parse_args()
     cfg = scenes.CONFIGS[a.config]
@@ -59,7 +60,10 @@ def main():
     r.render_device(film.data_ptr(), 0, spp)  # warm-up
     if a.balance:  # every block's measured work, as bench.py's ranks sum it
         nb = ((cfg["width"] + 31) // 32) * ((cfg["height"] + 31) // 32)
-        r.set_block_weights(r.block_costs(nb).astype("float64"))
+        from mitsuba_amd import distributed
+        costs = r.block_costs(nb).astype("float64")
+        r.set_block_weights(costs if a.balance == "bounces" else
+                            distributed.block_weights(costs, spp, cfg["width"], cfg["height"]))
     t1, _ = timed(0, 1)
     out = {"config": a.config, "N1_ms": round(t1 * 1e3, 3), "shards": {}}
     for n in [int(x) for x in a.ns.split(",")]:
