@@ -1155,6 +1155,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         w.blockOf = c->dBlockOf;
         c->P.costSpp = w.nSpp;
         w.localOf = c->dLocalOf;
+        w.doneIf = nullptr;
+        w.doneParity = 0;
         c->stats.waves++;
         /* a wave rendered again after its schedule overflowed must not count twice: the timing
            events and traversal counters of the discarded attempt are rolled back to here */
@@ -1203,6 +1205,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         auto known = c->schedules.find(key);
         const bool ahead = c->bounceAhead && !perLaunch && !bounceReport && known != c->schedules.end();
         bool fits = true; /* the schedule launched ahead was the whole wave */
+        bool gatheredAhead = false, firstRead = true, doneAtFirstRead = false;
         bool learn = c->bounceAhead && !ahead, extended = false;
         BounceSchedule seen;
         int b = 1, bounce = 0;
@@ -1241,6 +1244,17 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                                            c->tailPaths, s);
                 });
             if (e) break;
+            /* the gather right behind the schedule, guarded on the device (the wave is done: no
+               live path in this bounce's shade queue, or the tail took it; no overflow), so the
+               host's counter read-back no longer stands between the last bounce and it */
+            if (!perLaunch) {
+                HptWave wg = w;
+                wg.doneIf = C;
+                wg.doneParity = (uint32_t) b & 1u;
+                e = timed(4, [&] { return hpt_launch_gather(sc, wg, c->P, c->partial, dFilm, s); });
+                if (e) break;
+                gatheredAhead = true;
+            }
         }
         for (; e == hipSuccess; ++b) {
             const uint32_t p = (uint32_t) b & 1u;
@@ -1248,6 +1262,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e) break;
             const uint32_t n = hostCnt[HPT_C_SHADE(p)];
+            if (firstRead) doneAtFirstRead = hptWaveDone(hostCnt, p); /* what the early gather's guard saw */
+            firstRead = false;
             if (n == 0 || hostCnt[HPT_C_TAIL_PATHS] != 0) break; /* no live path, or k_tail took the rest */
             if (ahead && fits) {
                 /* the schedule did not cover the wave (its tail declined, or bounces ran past it):
@@ -1318,7 +1334,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             return setErr(c, HPT_EINVAL, "Lookup dimension exceeds the direction number table size! You may have "
                                          "to reduce the 'maxDepth' parameter of your integrator.");
         }
-        e = timed(4, [&] { return hpt_launch_gather(sc, w, c->P, c->partial, dFilm, s); });
+        if (!(gatheredAhead && doneAtFirstRead)) /* (else the guarded gather launched ahead took the wave) */
+            e = timed(4, [&] { return hpt_launch_gather(sc, w, c->P, c->partial, dFilm, s); });
         c->stats.paths += w.nPaths;
     }
     hipError_t e2 = hipStreamSynchronize(s);

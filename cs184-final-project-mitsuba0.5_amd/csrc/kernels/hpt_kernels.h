@@ -55,7 +55,15 @@ struct HptWave {
     int shard, nShards;
     const uint32_t *blockOf; /* this shard's k-th 32x32 block -> image block index (by * nbx + bx) */
     const int32_t *localOf;  /* image block index -> k, or -1 when another shard owns it */
+    /* k_splat / k_gather launched before the host has read the wave's counters back (bounces
+       launched ahead): they run only if the wave is done -- no live path left in shade queue
+       doneParity, or k_tail took the rest; no overflow, no error.  nullptr: always */
+    const uint32_t *doneIf;
+    uint32_t doneParity;
 };
+__host__ __device__ inline bool hptWaveDone(const uint32_t *c, uint32_t p) {
+    return (c[HPT_C_SHADE(p)] == 0u || c[HPT_C_TAIL_PATHS] != 0u) && c[HPT_C_OVERFLOW] == 0u && c[HPT_C_ERROR] == 0u;
+}
 
 /* HptPaths::state packing.  dim < 2048 (the Sobol table has 1024 dimensions
    and a path stops before it runs out); depth < 8192, far beyond any path the

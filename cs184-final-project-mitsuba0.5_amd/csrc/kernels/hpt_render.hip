@@ -3117,6 +3117,7 @@ k_tail_multi(HptScene sc, HptPaths P, HptTail T, uint32_t *__restrict__ counters
    with a fixed xor tree -> partial[slot][9] (RGB, weight). */
 extern "C" __global__ __launch_bounds__(256) void k_splat(HptScene sc, HptWave w, HptPaths P,
                                                            float4 *__restrict__ partial) {
+    if (w.doneIf && !hptWaveDone(w.doneIf, w.doneParity)) return; /* uniform: the host gathers later */
     const uint32_t slot = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t nSlots = w.nPaths / w.nSpp;
@@ -3172,6 +3173,7 @@ extern "C" __global__ __launch_bounds__(256) void k_splat(HptScene sc, HptWave w
    its 3x3 neighbours (owned by this shard) addressed to it. */
 extern "C" __global__ __launch_bounds__(256) void k_gather(HptScene sc, HptWave w, const float4 *__restrict__ partial,
                                                             float4 *film) {
+    if (w.doneIf && !hptWaveDone(w.doneIf, w.doneParity)) return; /* uniform: the host gathers later */
     const uint32_t pix = blockIdx.x * blockDim.x + threadIdx.x;
     if (pix >= (uint32_t) (w.width * w.height)) return;
     const int x = (int) (pix % (uint32_t) w.width), y = (int) (pix / (uint32_t) w.width);
