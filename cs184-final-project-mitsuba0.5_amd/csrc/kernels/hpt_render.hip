@@ -1043,11 +1043,14 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
             const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
             const float ra = axis == 0 ? rcp.x : (axis == 1 ? rcp.y : rcp.z);
             const float ts = (split - oa) * ra;
-            const bool below = (oa < split) | ((oa == split) & (da <= 0.0f));
-            const bool nearOnly = !(ts <= r.tmax) | (ts <= 0.0f);
-            const bool farOnly = !nearOnly & (ts < r.tmin);
-            const bool both = !(nearOnly | farOnly);
-            const uint64_t mBelow = __ballot(me & below);
+            /* every lane's decisions as wave masks: one compare each, the logic on scalar masks
+               (the same predicates as traceRound's: below, near only, far only, both) */
+            const uint64_t mBelowAll = __builtin_amdgcn_ballot_w64(oa < split) |
+                                       (__builtin_amdgcn_ballot_w64(oa == split) & __builtin_amdgcn_ballot_w64(da <= 0.0f));
+            const uint64_t mNearAll = ~__builtin_amdgcn_ballot_w64(ts <= r.tmax) | __builtin_amdgcn_ballot_w64(ts <= 0.0f);
+            const uint64_t mFarAll = ~mNearAll & __builtin_amdgcn_ballot_w64(ts < r.tmin);
+            const uint64_t mBothAll = ~(mNearAll | mFarAll);
+            const uint64_t mBelow = mBelowAll & act;
             if (mBelow != 0 && mBelow != act) {
                 /* the lanes disagree on the front-to-back order: the others revisit this node later */
                 if (sp == spMax) return false;
@@ -1055,10 +1058,9 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
                 ++sp;
                 act = mBelow;
             }
-            const bool in = laneIn(act);
             const uint32_t belowG = (act & mBelow) != 0 ? 1u : 0u;
             const uint32_t first = left + (belowG ? 0u : 1u), second = left + (belowG ? 1u : 0u);
-            const uint64_t mFirst = __ballot(in & !farOnly), mBoth = __ballot(in & both), mFar = __ballot(in & farOnly);
+            const uint64_t mFirst = act & ~mFarAll, mBoth = act & mBothAll, mFar = act & mFarAll;
             if (mFirst == 0) { /* nobody needs the first child (so no lane is "both") */
                 node = second;
                 act = mFar;
@@ -1067,10 +1069,11 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
             }
             if ((mBoth | mFar) != 0) {
                 if (sp == spMax) return false;
-                if (in & both) L.saved[sp][lane] = r.tmax;
+                const bool bothMe = laneIn(mBoth);
+                if (bothMe) L.saved[sp][lane] = r.tmax;
                 if (lane == 0) L.ent[sp] = PacketEntry{second, 0u, mBoth, mFar};
                 ++sp;
-                if (in & both) r.tmax = ts;
+                if (bothMe) r.tmax = ts;
             }
             node = first;
             act = mFirst;
