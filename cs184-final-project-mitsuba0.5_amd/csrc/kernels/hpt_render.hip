@@ -2199,6 +2199,49 @@ __device__ __forceinline__ void qpushBlock(bool pred, uint32_t value, uint32_t *
     __syncthreads(); /* waveCount / blockBase may be reused by a second push */
 }
 
+/* The camera queue's push: qpushBlock, but a pixel's samples are laid out by
+   the quadrant of the pixel their film position falls in (then in sample
+   order), so a 64-ray packet of k_trace_packet covers a quarter of the pixel
+   instead of all of it when a wave holds 256 of its samples.  A segment is
+   the wps consecutive waves holding one pixel's samples (wps = 1: no
+   reordering); queue order is (segment, quadrant, wave, lane).  The per-(wave,
+   quadrant) counts, 64 for a 1024-thread block, are scanned by wave 0 and the
+   block takes one atomicAdd.  Only the queue order changes: every path's ray,
+   hit and film contribution are its own. */
+template <int BLOCK>
+__device__ __forceinline__ void qpushCamera(bool pred, uint32_t quad, uint32_t wps, uint32_t value, uint32_t *queue,
+                                            uint32_t *counter) {
+    constexpr int NW = BLOCK / 64, NE = NW * 4;
+    static_assert(NE <= 64, "one wave scans the (wave, quadrant) counts");
+    __shared__ uint32_t cnt[NE];
+    const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
+    const uint32_t wIn = wave % wps;
+    const uint32_t fBase = (wave - wIn) * 4 + wIn; /* + quadrant * wps */
+    uint64_t mine = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64(pred && quad == q);
+        if (lane == q) cnt[fBase + q * wps] = (uint32_t) __popcll(m);
+        if (quad == q) mine = m;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const uint32_t c = lane < (uint32_t) NE ? cnt[lane] : 0u;
+        uint32_t incl = c;
+#pragma unroll
+        for (int s = 1; s < 64; s <<= 1) {
+            const uint32_t u = __shfl_up(incl, s);
+            if (lane >= (uint32_t) s) incl += u;
+        }
+        uint32_t base = 0;
+        if (lane == 63) base = incl ? atomicAdd(counter, incl) : 0u;
+        base = __shfl(base, 63);
+        if (lane < (uint32_t) NE) cnt[lane] = base + incl - c;
+    }
+    __syncthreads();
+    if (pred) queue[cnt[fBase + quad * wps] + (uint32_t) __popcll(mine & ((1ull << lane) - 1ull))] = value;
+}
+
 /* qpushBlock that also stores value2 at the same position of a parallel array */
 template <int BLOCK>
 __device__ __forceinline__ void qpushBlock2(bool pred, uint32_t value, uint32_t *queue, uint32_t value2,
@@ -2380,8 +2423,10 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
     uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     bool valid = id < w.nPaths;
     int px = 0, py = 0;
-    uint32_t j = 0;
+    uint32_t j = 0, quad = 0;
     if (valid) valid = decodePath(w, id, px, py, j);
+    /* a pixel's samples as whole waves of the block: sort them by quadrant (qpushCamera) */
+    const uint32_t wps = (w.nSpp % 64u == 0 && w.nSpp >= 128u && HPT_QBLOCK % w.nSpp == 0) ? w.nSpp / 64u : 1u;
     if (valid) {
         const HptCamera &c = sc.cam;
         uint64_t sidx = (c.logRes > 1) ? sobolLookUp(sc, c.logRes, j, (uint32_t) px, (uint32_t) py) : (uint64_t) j;
@@ -2394,6 +2439,7 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
             oy = sobolSample(sc, sidx, 1);
         }
         float posx = px + ox, posy = py + oy;
+        if (wps > 1) quad = (posx - px >= 0.5f ? 1u : 0u) | (posy - py >= 0.5f ? 2u : 0u);
         V3 o, dw;
         float mint, maxt;
         cameraRay(c, posx, posy, o, dw, mint, maxt);
@@ -2408,7 +2454,7 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
         P.state[id] = 0xffffffffu; /* outside the image */
         P.li[id] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
-    qpushBlock<HPT_QBLOCK>(valid, id, traceQ, nTrace);
+    qpushCamera<HPT_QBLOCK>(valid, quad, wps, id, traceQ, nTrace);
 }
 
 /* k_trace: the wave's closest-hit rays (traceQ[0, nTrace)) then its any-hit

@@ -67,11 +67,11 @@ def block_owner_weighted(nbx: int, nby: int, world: int, weights) -> list[int]:
     return owner
 
 
-# A block's camera pass in path-bounce units: the headline frame's camera pass (packets, 29.5 ms
-# for 67 M camera rays) against its bounces (trace + shade + post + tail, 113 ms for 113 M
-# path-bounces): 0.44 of a path-bounce per camera ray.  Sky blocks shade no bounce, but each
+# A block's camera pass in path-bounce units: the headline frame's camera pass (quadrant packets,
+# 23.4 ms for 67 M camera rays) against its bounces (trace + shade + post + tail, 110.8 ms for
+# 113 M path-bounces): 0.36 of a path-bounce per camera ray (0.44 before the quadrant packets).  Sky blocks shade no bounce, but each
 # of their pixels still costs its camera rays.
-CAMERA_RAY_WEIGHT = 0.44
+CAMERA_RAY_WEIGHT = 0.36
 
 
 def block_weights(costs, spp: int, width: int, height: int, block: int = 32):

@@ -509,6 +509,34 @@ def test_tail_kernel_bit_identical(name, n, radii, monkeypatch):
     np.testing.assert_array_equal(films[0], films[2])
 
 
+@pytest.mark.parametrize("spp", [128, 256, 512])
+def test_camera_quadrant_packets(spp, monkeypatch):
+    """A wave holding 128 / 256 / 512 samples of a pixel queues them by the
+    quadrant of the pixel they fall in (k_camera's qpushCamera), so a 64-ray
+    packet covers part of the pixel.  Only the queue order changes: the film
+    equals the one-ray-per-lane camera pass (HPT_PACKETS=0) bit for bit, and
+    the same frame in waves of 64 samples (no reordering) up to summation order;
+    at 256 spp it also matches the oracle at the reference-flags floor."""
+    films = []
+    for packets in ("1", "0"):
+        monkeypatch.setenv("HPT_PACKETS", packets)
+        _, r, o = scene_util.make("furball_marschner", 3000, 48, 32, spp, device=0)
+        films.append(r.render(0, spp, collect_stats=True))
+        if packets == "1":
+            assert r.stats().packet_launches >= 1
+            small = r.render(0, spp, max_wave_paths=2 * 1024 * 64)  # two 32x32 blocks of slots
+    np.testing.assert_array_equal(films[0], films[1])
+    np.testing.assert_allclose(small, films[0], rtol=1e-5, atol=1e-6)
+    if spp == 256:
+        ofilm, _ = o.render(0, spp, threads=16, width=48, height=32)
+        np.testing.assert_allclose(films[0][..., 3], ofilm[..., 3], rtol=1e-5)
+        a, b = native.develop(films[0]), native.develop(ofilm)
+        m = scene_util.l2_metrics(b, a)
+        same = np.all(np.abs(a - b) <= 1e-5 * np.abs(b) + 1e-7, axis=-1)
+        floor, floor_same = scene_util.reference_flags_floor("furball_marschner", 3000, r, 48, 32, spp)
+        scene_util.assert_at_floor(m, floor, same.mean(), floor_same, factor=2.0)
+
+
 def test_full_size_headline_frame():
     """BASELINE.json configs[2] at its full size (furball, 40,000 strands,
     512x512 @ 256 spp, maxDepth 65): deterministic, shard- and spp-split
