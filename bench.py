@@ -204,14 +204,18 @@ def main():
             distributed.render_frame(shard_to_host, host_film, rank, world, dist)
             film.copy_(host_film)
 
-    for _ in range(args.warmup):
+    n_blocks = ((W + 31) // 32) * ((H + 31) // 32)
+    balance = world > 1 and args.balance == "on"
+    for i in range(args.warmup):
+        if balance and i == args.warmup - 1:
+            r.block_costs(n_blocks)  # read and reset: the counts balance_blocks reads cover one frame
         step(1)
     balanced = False
-    if world > 1 and args.balance == "on":
-        # the warm-up frame's per-block path-bounces, summed over the ranks, deal the blocks
+    if balance:
+        # the last warm-up frame's per-block path-bounces, summed over the ranks, deal the blocks
         # longest-first (the same deal on every rank); one more frame records its schedules
-        distributed.balance_blocks(r, ((W + 31) // 32) * ((H + 31) // 32), world, dist,
-                                   "cuda:%d" % local if backend == "nccl" else "cpu", spp=spp, width=W, height=H)
+        distributed.balance_blocks(r, n_blocks, world, dist, "cuda:%d" % local if backend == "nccl" else "cpu",
+                                   spp=spp, width=W, height=H, frames=1)
         step(1)
         balanced = True
     # one untimed counted frame: traversal counters for the byte model (the

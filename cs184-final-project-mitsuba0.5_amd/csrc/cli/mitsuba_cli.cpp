@@ -157,7 +157,14 @@ int main(int argc, char **argv) {
         if (devs.empty())
             for (int g = 0; g < o.gpus; ++g) devs.push_back(o.device + g);
         const int G = (int) devs.size();
-        std::vector<hpt_context *> ctx(G, nullptr);
+        /* every context of this scene is destroyed on every way out of the iteration */
+        struct Contexts {
+            std::vector<hpt_context *> v;
+            ~Contexts() {
+                for (hpt_context *c : v) hpt_context_destroy(c);
+            }
+        } owned{std::vector<hpt_context *>(G, nullptr)};
+        std::vector<hpt_context *> &ctx = owned.v;
         int W = 0, H = 0, spp = 0;
         /* the scene once: parse, hair, kd-tree, tables on the first device's context ... */
         const auto tLoad = std::chrono::steady_clock::now();
@@ -194,10 +201,17 @@ int main(int argc, char **argv) {
             const auto tShare = std::chrono::steady_clock::now();
             std::vector<int> rcs(G, 0);
             std::vector<std::thread> th;
-            for (int g = 1; g < G; ++g) th.emplace_back([&, g] { rcs[g] = hpt_context_share_scene(ctx[0], devs[g], &ctx[g]); });
-            for (auto &t : th) t.join();
+            std::vector<std::string> shareErr(G);
             for (int g = 1; g < G; ++g)
-                if (rcs[g]) { std::fprintf(stderr, "device %d: %s\n", devs[g], hpt_last_error(ctx[0])); return 3; }
+                th.emplace_back([&, g] {
+                    rcs[g] = hpt_context_share_scene(ctx[0], devs[g], &ctx[g]);
+                    if (rcs[g]) shareErr[g] = hpt_last_error(nullptr); /* this thread's message */
+                });
+            for (auto &t : th) t.join();
+            /* a failed share reports on the failing thread (hpt_last_error(NULL)), never on the shared
+               source context, which every worker reads at once */
+            for (int g = 1; g < G; ++g)
+                if (rcs[g]) { std::fprintf(stderr, "device %d: %s\n", devs[g], shareErr[g].c_str()); return 3; }
             if (!o.quiet)
                 std::printf("Scene loaded once (%.2f s) and shared with %d more device context%s (%.2f s)\n", loadSec,
                             G - 1, G > 2 ? "s" : "",
@@ -255,7 +269,6 @@ int main(int argc, char **argv) {
                             (unsigned long long) s.bounces, s.max_bounces);
             }
         }
-        for (auto c : ctx) hpt_context_destroy(c);
     }
     return 0;
 }

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -60,12 +61,6 @@ static bool defaultBounceAhead() {
     return v ? std::atoi(v) != 0 : true;
 }
 
-/* claim-order buckets (hpt_kernels.h HPT_BUCKETS): bounce rays claimed longest first;
-   HPT_CLAIM_BUCKETS=0/1 overrides the default */
-static bool defaultClaimBuckets() {
-    const char *v = std::getenv("HPT_CLAIM_BUCKETS");
-    return v ? std::atoi(v) != 0 : false;
-}
 /* the bounce schedule of a wave of paths: the shade-queue length of each wavefront bounce,
    and whether a k_tail launch took the rest */
 struct BounceSchedule {
@@ -121,8 +116,6 @@ struct hpt_context {
     HptPaths P;
     /* rays of the bounce; paths to shade by bounce parity (shadeQ[p] is post's output for p ^ 1) */
     uint32_t *qTrace = nullptr, *qShadow = nullptr, *qShade[2] = {nullptr, nullptr};
-    uint32_t *bucketBuf = nullptr;
-    bool claimBuckets = defaultClaimBuckets();
     uint32_t *counters = nullptr;
     uint64_t *dstats = nullptr;
     float4 *partial = nullptr;     /* film splat partials: slots x 9 (k_splat -> k_gather) */
@@ -136,12 +129,18 @@ struct hpt_context {
     uint32_t *dBlockCost = nullptr;     /* path-bounces shaded per owned block (HptPaths::blockCost) */
     std::vector<double> blockWeights;   /* hpt_set_block_weights (empty: Hilbert-cyclic deal) */
     uint64_t weightsVersion = 0;
+    /* the prepared scene this context renders: a process-unique number given by each successful
+       hpt_prepare and copied by hpt_context_share_scene, so hpt_render_multi can refuse contexts
+       that would render different scenes into one film (0: not prepared) */
+    uint64_t sceneId = 0;
     hpt_stats stats;
     std::vector<hipEvent_t> evPool;
     /* hpt_render_multi: this context's shard film, and (on the receiving context) the staging
        buffer the other devices' films are copied into */
     float4 *mfilm = nullptr, *mstage = nullptr;
     size_t mfilmPixels = 0, mstagePixels = 0;
+    std::vector<hipStream_t> peerStreams; /* one copy stream (and its done event) per peer film */
+    std::vector<hipEvent_t> peerEvents;
 };
 
 namespace {
@@ -163,8 +162,13 @@ BsdfDesc &singleBsdf(SceneDesc &d, const char *type) {
     return d.bsdfs[0];
 }
 
+/* errors of calls that have no context of their own to report on (hpt_context_create,
+   hpt_context_share_scene): per calling thread, read with hpt_last_error(NULL) */
+thread_local std::string tlsErr;
+
 int setErr(hpt_context *c, int code, const std::string &m) {
     if (c) c->err = m;
+    else tlsErr = m;
     return code;
 }
 
@@ -249,7 +253,6 @@ int ensureWave(hpt_context *c, uint64_t n) {
     r |= alloc(n * 4, (void **) &c->qShadow);
     r |= alloc(n * 4, (void **) &c->qShade[0]);
     r |= alloc(n * 4, (void **) &c->qShade[1]);
-    r |= alloc((size_t) HPT_BUCKETS * 2 * n * 4, (void **) &c->bucketBuf); /* claim-order buckets: all rays of a bounce fit one */
     r |= alloc(HPT_COUNTER_WORDS * 4, (void **) &c->counters);
     r |= alloc(2 * 24 * 8, (void **) &c->dstats); /* the counters, and a snapshot at the start of a wave */
     if (r) return HPT_EDEVICE;
@@ -340,12 +343,17 @@ void hpt_context_destroy(hpt_context *c) {
     if (c->mfilm) (void) hipFree(c->mfilm);
     if (c->mstage) (void) hipFree(c->mstage);
     for (auto e : c->evPool) (void) hipEventDestroy(e);
+    for (auto e : c->peerEvents) (void) hipEventDestroy(e);
+    for (auto ps : c->peerStreams) (void) hipStreamDestroy(ps);
     (void) hipHostFree(c->hostCnt);
     (void) hipStreamDestroy(c->stream);
     delete c;
 }
 
-const char *hpt_last_error(const hpt_context *c) { return c ? c->err.c_str() : "null context"; }
+const char *hpt_last_error(const hpt_context *c) {
+    if (c) return c->err.c_str();
+    return tlsErr.empty() ? "null context" : tlsErr.c_str();
+}
 
 int hpt_set_data_dir(hpt_context *c, const char *dir) {
     if (!c || !dir) return HPT_EINVAL;
@@ -704,7 +712,13 @@ int hpt_prepare(hpt_context *c) {
     } catch (const std::exception &e) {
         return setErr(c, HPT_EIO, e.what());
     }
-    return uploadScene(c);
+    c->sceneId = 0;
+    const int rc = uploadScene(c);
+    if (rc == HPT_OK) {
+        static std::atomic<uint64_t> counter{0};
+        c->sceneId = ++counter;
+    }
+    return rc;
 }
 
 /* the device half of hpt_prepare: the host-built scene (kd-tree, tables, envmap) to this
@@ -1014,6 +1028,9 @@ static int ensureOwnership(hpt_context *c, int W, int H, int nbx, int nby, int s
     if (c->ownW == W && c->ownH == H && c->ownShard == shard && c->ownShards == nShards &&
         c->ownWeights == c->weightsVersion)
         return HPT_OK;
+    if (!c->blockWeights.empty() && c->blockWeights.size() != (size_t) nbx * nby)
+        return setErr(c, HPT_EINVAL, "hpt_set_block_weights gave " + std::to_string(c->blockWeights.size()) +
+                                         " block weights for a frame of " + std::to_string(nbx * nby) + " blocks");
     const std::vector<uint32_t> order = blockOrder(nbx, nby);
     const std::vector<int> shardOf = dealBlocks(nbx, nby, nShards, c->blockWeights);
     std::vector<uint32_t> blockOf;
@@ -1078,11 +1095,9 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         c->partialSlots = slots;
     }
     hipStream_t s = c->stream;
-    c->P.bucketQ = c->claimBuckets ? c->bucketBuf : nullptr;
     c->P.blockCost = c->dBlockCost;
     c->P.costStride = (uint32_t) c->ownCap;
     const size_t costWords = (size_t) HPT_COST_STRIPES * c->ownCap;
-    c->P.bucketCap = (uint32_t) std::min<uint64_t>(2 * c->capacity, 0xffffffffull);
     if (!c->scDev) HIPCHK(c, hipMalloc((void **) &c->scDev, sizeof(HptScene)));
     if (c->scShadow.size() != sizeof(HptScene) || std::memcmp(c->scShadow.data(), &c->sc, sizeof(HptScene)) != 0) {
         HIPCHK(c, hipMemcpy(c->scDev, &c->sc, sizeof(HptScene), hipMemcpyHostToDevice));
@@ -1213,13 +1228,12 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             const uint32_t q = p ^ 1u;
             hipError_t e1 = timed(2, [&] {
                 return hpt_launch_shade(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), c->qTrace, C + HPT_C_TRACE(p),
-                                        c->qShadow, C + HPT_C_SHADOW(p), C, grid, tailFrom, s, C + HPT_C_BUCKET(p, 0));
+                                        c->qShadow, C + HPT_C_SHADOW(p), C, grid, tailFrom, s);
             });
             if (e1) return e1;
             e1 = timed(-1, [&] {
                 return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(p), C + HPT_C_SHADOW(p),
-                                        C + HPT_CURSOR_SET(p), dst, 2ull * grid, s,
-                                        c->P.bucketQ ? C + HPT_C_BUCKET(p, 0) : nullptr, C, q);
+                                        C + HPT_CURSOR_SET(p), dst, 2ull * grid, s, C, q);
             });
             if (e1) return e1;
             reportLaunch("bounce");
@@ -1418,12 +1432,14 @@ int hpt_render(hpt_context *c, const hpt_render_params *prm, float *film) {
 int hpt_context_share_scene(hpt_context *src, int device, hpt_context **out) {
     if (!src || !out) return HPT_EINVAL;
     *out = nullptr;
-    if (!src->prepared) return setErr(src, HPT_ESTATE, "hpt_context_share_scene: the source context is not prepared");
+    /* src is only read here (several threads may share one source at once): failures are
+       reported to the calling thread, hpt_last_error(NULL), never written to src */
+    if (!src->prepared) return setErr(nullptr, HPT_ESTATE, "hpt_context_share_scene: the source context is not prepared");
     hpt_context *c = nullptr;
     int rc = hpt_context_create(device, &c);
-    if (rc) return setErr(src, rc, "hpt_context_share_scene: no gfx950 context on device " + std::to_string(device));
-    /* the host-built scene, as hpt_prepare left it on src (read-only there: several threads may
-       share one source at once) */
+    if (rc)
+        return setErr(nullptr, rc, "hpt_context_share_scene: no gfx950 context on device " + std::to_string(device));
+    /* the host-built scene, as hpt_prepare left it on src */
     c->dataDir = src->dataDir;
     c->desc = src->desc;
     c->haveCamera = src->haveCamera, c->haveHair = src->haveHair, c->haveBSDF = src->haveBSDF;
@@ -1439,13 +1455,17 @@ int hpt_context_share_scene(hpt_context *src, int device, hpt_context **out) {
     c->vdcInv = src->vdcInv;
     c->maxLeafRounds = src->maxLeafRounds, c->maxRestarts = src->maxRestarts, c->packetStack = src->packetStack;
     c->tailPaths = src->tailPaths, c->bounceAhead = src->bounceAhead, c->packets = src->packets;
-    c->claimBuckets = src->claimBuckets;
+    /* the shard deal: hpt_render_multi gives shard g to context g, and every context must deal
+       the blocks the same way or some blocks are rendered twice and others never */
+    c->blockWeights = src->blockWeights;
+    c->weightsVersion = src->weightsVersion + 1;
     rc = uploadScene(c);
     if (rc) {
-        setErr(src, rc, c->err);
+        setErr(nullptr, rc, c->err);
         hpt_context_destroy(c);
         return rc;
     }
+    c->sceneId = src->sceneId;
     *out = c;
     return HPT_OK;
 }
@@ -1453,12 +1473,26 @@ int hpt_context_share_scene(hpt_context *src, int device, hpt_context **out) {
 int hpt_render_multi(hpt_context *const *ctxs, int n, const hpt_render_params *prm, float *film) {
     if (!ctxs || n <= 0 || !prm || !film) return HPT_EINVAL;
     hpt_context *c0 = ctxs[0];
+    if (!c0) return HPT_EINVAL;
     for (int g = 0; g < n; ++g) {
-        if (!ctxs[g]) return HPT_EINVAL;
-        if (ctxs[g]->device == HPT_HOST_ONLY) return setErr(c0, HPT_EDEVICE, "host-only context cannot render");
-        if (!ctxs[g]->prepared) return setErr(c0, HPT_ESTATE, "hpt_render_multi: a context is not prepared");
-        if (ctxs[g]->sc.cam.width != c0->sc.cam.width || ctxs[g]->sc.cam.height != c0->sc.cam.height)
-            return setErr(c0, HPT_EINVAL, "hpt_render_multi: contexts render different film sizes");
+        const hpt_context *c = ctxs[g];
+        if (!c) return HPT_EINVAL;
+        if (c->device == HPT_HOST_ONLY) return setErr(c0, HPT_EDEVICE, "host-only context cannot render");
+        if (!c->prepared) return setErr(c0, HPT_ESTATE, "hpt_render_multi: a context is not prepared");
+        /* one film from one scene: every context must be a share of the same prepared scene
+           (re-preparing or re-configuring a context gives it a scene of its own), with the same
+           camera and integrator settings and the same shard deal */
+        if (c->sceneId != c0->sceneId)
+            return setErr(c0, HPT_EINVAL, "hpt_render_multi: context " + std::to_string(g) +
+                                              " renders a different prepared scene (share one with hpt_context_share_scene)");
+        if (std::memcmp(&c->sc.cam, &c0->sc.cam, sizeof(HptCamera)) != 0 || c->sc.maxDepth != c0->sc.maxDepth ||
+            c->sc.rrDepth != c0->sc.rrDepth || c->sc.strictNormals != c0->sc.strictNormals ||
+            c->sc.hideEmitters != c0->sc.hideEmitters || c->sc.scramble != c0->sc.scramble || c->desc.spp != c0->desc.spp)
+            return setErr(c0, HPT_EINVAL, "hpt_render_multi: context " + std::to_string(g) +
+                                              " has a different camera, sampler or integrator setting");
+        if (c->blockWeights != c0->blockWeights)
+            return setErr(c0, HPT_EINVAL, "hpt_render_multi: context " + std::to_string(g) +
+                                              " deals the blocks with different weights (hpt_set_block_weights on every context)");
     }
     const size_t pixels = (size_t) c0->sc.cam.width * c0->sc.cam.height;
     /* every context renders its shard into its own device film; the receiving context's film
@@ -1483,6 +1517,8 @@ int hpt_render_multi(hpt_context *const *ctxs, int n, const hpt_render_params *p
         p.shard = g;
         p.n_shards = n;
         rcs[g] = renderImpl(c, &p, c->mfilm);
+        /* the film is complete on this context's stream before the receiving device reads it */
+        if (rcs[g] == HPT_OK && g > 0 && (e = hipStreamSynchronize(c->stream)) != hipSuccess) fail(e);
     };
     {
         std::vector<std::thread> th;
@@ -1495,22 +1531,52 @@ int hpt_render_multi(hpt_context *const *ctxs, int n, const hpt_render_params *p
             if (g) setErr(c0, rcs[g], "device " + std::to_string(ctxs[g]->device) + ": " + ctxs[g]->err);
             return rcs[g];
         }
-    /* the film combine (renderproc.cpp:142-145) on the receiving device: each other film over
-       xGMI (peer copy) into a staging buffer, added in shard order, so the sum is the host sum
-       f0 + f1 + ... of the same films */
+    /* the film combine (renderproc.cpp:142-145) on the receiving device: every other film is
+       pulled at once over xGMI (peer copies, one stream and staging buffer per peer), then
+       added in shard order, so the sum is the host sum f0 + f1 + ... of the same films */
     HIPCHK(c0, hipSetDevice(c0->device));
-    if (n > 1 && c0->mstagePixels < pixels) {
-        if (c0->mstage) (void) hipFree(c0->mstage);
-        c0->mstage = nullptr;
-        c0->mstagePixels = 0;
-        HIPCHK(c0, hipMalloc((void **) &c0->mstage, pixels * 16));
-        c0->mstagePixels = pixels;
-    }
-    for (int g = 1; g < n; ++g) {
-        if (ctxs[g]->device != c0->device) (void) hipDeviceEnablePeerAccess(ctxs[g]->device, 0); /* once; later calls report it done */
-        (void) hipGetLastError();
-        HIPCHK(c0, hipMemcpyPeerAsync(c0->mstage, c0->device, ctxs[g]->mfilm, ctxs[g]->device, pixels * 16, c0->stream));
-        HIPCHK(c0, hpt_launch_film_add(c0->mfilm, c0->mstage, pixels, c0->stream));
+    if (n > 1) {
+        const size_t need = (size_t) (n - 1) * pixels;
+        if (c0->mstagePixels < need) {
+            if (c0->mstage) (void) hipFree(c0->mstage);
+            c0->mstage = nullptr;
+            c0->mstagePixels = 0;
+            HIPCHK(c0, hipMalloc((void **) &c0->mstage, need * 16));
+            c0->mstagePixels = need;
+        }
+        while ((int) c0->peerStreams.size() < n - 1) {
+            hipStream_t ps;
+            hipEvent_t pe;
+            HIPCHK(c0, hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
+            if (hipEventCreateWithFlags(&pe, hipEventDisableTiming) != hipSuccess) {
+                (void) hipStreamDestroy(ps);
+                return setErr(c0, HPT_EDEVICE, "hpt_render_multi: cannot create a copy event");
+            }
+            c0->peerStreams.push_back(ps);
+            c0->peerEvents.push_back(pe);
+        }
+        for (int g = 1; g < n; ++g) {
+            const int dg = ctxs[g]->device;
+            if (dg != c0->device) {
+                int can = 0;
+                HIPCHK(c0, hipDeviceCanAccessPeer(&can, c0->device, dg));
+                if (!can)
+                    return setErr(c0, HPT_EDEVICE, "hpt_render_multi: device " + std::to_string(c0->device) +
+                                                       " cannot access device " + std::to_string(dg) + " (no peer path)");
+                const hipError_t pe = hipDeviceEnablePeerAccess(dg, 0);
+                if (pe == hipErrorPeerAccessAlreadyEnabled) (void) hipGetLastError(); /* enabled by an earlier call */
+                else if (pe != hipSuccess)
+                    return setErr(c0, HPT_EDEVICE, "hipDeviceEnablePeerAccess(" + std::to_string(dg) +
+                                                       "): " + hipGetErrorString(pe));
+            }
+            float4 *stage = c0->mstage + (size_t) (g - 1) * pixels;
+            HIPCHK(c0, hipMemcpyPeerAsync(stage, c0->device, ctxs[g]->mfilm, dg, pixels * 16, c0->peerStreams[g - 1]));
+            HIPCHK(c0, hipEventRecord(c0->peerEvents[g - 1], c0->peerStreams[g - 1]));
+        }
+        for (int g = 1; g < n; ++g) {
+            HIPCHK(c0, hipStreamWaitEvent(c0->stream, c0->peerEvents[g - 1], 0));
+            HIPCHK(c0, hpt_launch_film_add(c0->mfilm, c0->mstage + (size_t) (g - 1) * pixels, pixels, c0->stream));
+        }
     }
     HIPCHK(c0, hipMemcpyAsync(film, c0->mfilm, pixels * 16, hipMemcpyDeviceToHost, c0->stream));
     HIPCHK(c0, hipStreamSynchronize(c0->stream));
@@ -1522,6 +1588,10 @@ int hpt_block_deal(int width, int height, int n_shards, const double *weights, i
     const int nbx = (width + HPT_BLOCK - 1) / HPT_BLOCK, nby = (height + HPT_BLOCK - 1) / HPT_BLOCK;
     std::vector<double> w;
     if (weights) w.assign(weights, weights + (size_t) nbx * nby);
+    /* the deal's sort needs a strict weak order: no NaN (and, as hpt_set_block_weights, no negative
+       or infinite weight) */
+    for (double x : w)
+        if (!(x >= 0.0) || !std::isfinite(x)) return HPT_EINVAL;
     const std::vector<int> s = dealBlocks(nbx, nby, n_shards, w);
     for (size_t i = 0; i < s.size(); ++i) shard_of_block[i] = s[i];
     return HPT_OK;

@@ -22,11 +22,6 @@
 #define HPT_C_TAIL_BOUNCES 13 /* path-bounces shaded inside k_tail */
 #define HPT_C_TAIL_CURSOR 14  /* k_tail's work claims */
 #define HPT_Q_COUNT 16
-/* claim-order buckets of a bounce's trace launch (parity p): rays appended by k_shade to
-   HptPaths::bucketQ by the length of their interval inside the scene box, and claimed by
-   k_trace longest first, so that the rays still running when its queue runs dry are short */
-#define HPT_BUCKETS 4
-#define HPT_C_BUCKET(p, b) (16 + HPT_BUCKETS * (p) + (b))
 /* HptScene::fault bits: a traversal bound fired (the ray would otherwise end
    with whatever hit it had; the render / batch call fails instead) */
 #define HPT_FAULT_LEAVES 1u   /* more than HptScene::maxLeafRounds (2^18) leaf rounds for one ray */
@@ -102,10 +97,6 @@ struct HptPaths {
        The by-path arrays above (ro, rd, thr, state, bw, sdir, scontrib) are k_camera's and
        k_tail's. */
     float4 *postRec, *shadowRec, *shadeRec;
-    /* claim-order buckets (nullptr: off): bucket b holds bucketCap entries from b * bucketCap,
-       each a trace-queue position, or a shadow-queue position | HPT_BUCKET_SHADOW */
-    uint32_t *bucketQ;
-    uint32_t bucketCap;
     /* per owned 32x32 block: path-bounces shaded (k_shade, k_tail), the measured work the cost-
        balanced shard deal reads back (hpt_get_block_costs); nullptr: not counted.  costSpp is
        the wave's nSpp (path id -> block: id / nSpp >> 10).  The counts are striped: wave w adds
@@ -121,7 +112,6 @@ struct HptPaths {
 
 
 #define HPT_COST_STRIPES 64
-#define HPT_BUCKET_SHADOW 0x80000000u
 /* hit record of a miss (a segment id never has all 31 bits set) */
 #define HPT_MISS 0xffffffffu
 
@@ -130,13 +120,11 @@ struct HptPaths {
 hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPaths &P, uint32_t *traceQ,
                              uint32_t *nTrace, hipStream_t s);
 /* one persistent traversal launch: closest-hit rays traceQ[0, *nTrace), shadow rays shadowQ[0, *nShadow) */
-/* nBucket (nullptr: queue order): the launch's HPT_BUCKETS claim-order bucket lengths (P.bucketQ).
-   counters (nullptr: none): a bounce launch of parity p = nextParity ^ 1 also zeroes the counts and
+/* counters (nullptr: none): a bounce launch of parity p = nextParity ^ 1 also zeroes the counts and
    cursor set of parity nextParity, which the next bounce appends to / claims from */
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
-                            uint64_t maxItems, hipStream_t s, const uint32_t *nBucket = nullptr,
-                            uint32_t *counters = nullptr, uint32_t nextParity = 0);
+                            uint64_t maxItems, hipStream_t s, uint32_t *counters = nullptr, uint32_t nextParity = 0);
 /* the camera pass's rays one per lane (HPT_PACKETS=0): traceQ[0, *nTrace), hits to P.hitQ by position */
 hipError_t hpt_launch_trace_camera(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
                                    uint32_t *cursors, uint32_t *stats, uint64_t maxItems, hipStream_t s);
@@ -156,7 +144,7 @@ hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint3
    bounce (0: always shade); a queue longer than the grid (maxItems) sets HPT_C_OVERFLOW */
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
                             uint32_t *traceQ, uint32_t *nTrace, uint32_t *shadowQ, uint32_t *nShadow, uint32_t *counters,
-                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s, uint32_t *nBucket = nullptr);
+                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s);
 hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
                            uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s);
 /* the rest of every live path (the shade queue) to termination in one launch, when the queue

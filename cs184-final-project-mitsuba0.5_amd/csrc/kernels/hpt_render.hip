@@ -848,14 +848,13 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
             const uint32_t n = (uint32_t) __popcll(idle);
             uint32_t start = 0, got = 0;
             while (true) { /* wave-uniform */
-                const uint32_t lo = IO::kContiguous ? shardLo(io.count(), shard) : 0u;
-                const uint32_t size = IO::kContiguous ? shardLo(io.count(), shard + 1) - lo : io.shardSize(shard);
+                const uint32_t lo = shardLo(io.count(), shard);
+                const uint32_t size = shardLo(io.count(), shard + 1) - lo;
                 uint32_t base = 0;
                 if (lane == 0) base = atomicAdd(&cursors[shard * HPT_CURSOR_STRIDE], n);
                 base = __shfl(base, 0);
                 if (base < size) {
-                    /* contiguous shards: the first item claimed; buckets: the offset in the shard */
-                    start = lo + base;
+                    start = lo + base; /* the first item claimed */
                     got = min(n, size - base);
                     break;
                 }
@@ -872,7 +871,7 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
                 const uint32_t rank =
                     __builtin_amdgcn_mbcnt_hi((uint32_t) (idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) idle, 0u));
                 if (rank < got) {
-                    active = io.begin(sc, IO::kContiguous ? start + rank : io.item(shard, start + rank), r);
+                    active = io.begin(sc, start + rank, r);
                     if (STATS) {
                         nC += r.shadow ? 0u : 1u;
                         nS += r.shadow ? 1u : 0u;
@@ -2305,41 +2304,6 @@ __device__ __forceinline__ uint32_t qpushBlockRec(bool pred, uint32_t value, uin
     return pos; /* the entry's queue position (meaningful where pred) */
 }
 
-/* Claim-order buckets (hpt_kernels.h HPT_BUCKETS): append value to bucket b (0 = shortest
-   rays) of P.bucketQ, one atomic per non-empty bucket per block.  Every thread of the block
-   must call it. */
-template <int BLOCK>
-__device__ __forceinline__ void qpushBucket(bool pred, uint32_t b, uint32_t value, uint32_t *bucketQ, uint32_t cap,
-                                            uint32_t *counts) {
-    constexpr int NW = BLOCK / 64;
-    __shared__ uint32_t waveCount[HPT_BUCKETS][NW];
-    __shared__ uint32_t blockBase[HPT_BUCKETS];
-    const uint32_t lane = __lane_id(), wave = threadIdx.x >> 6;
-    uint64_t mine = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < HPT_BUCKETS; ++k) {
-        const uint64_t m = __ballot(pred && b == k);
-        if (lane == 0) waveCount[k][wave] = (uint32_t) __popcll(m);
-        if (b == k) mine = m;
-    }
-    __syncthreads();
-    if (threadIdx.x < HPT_BUCKETS) {
-        const uint32_t k = threadIdx.x;
-        uint32_t tot = 0;
-        for (int w = 0; w < NW; ++w) {
-            const uint32_t c = waveCount[k][w];
-            waveCount[k][w] = tot;
-            tot += c;
-        }
-        blockBase[k] = tot ? atomicAdd(&counts[k], tot) : 0u;
-    }
-    __syncthreads();
-    if (pred)
-        bucketQ[(size_t) b * cap + blockBase[b] + waveCount[b][wave] + (uint32_t) __popcll(mine & ((1ull << lane) - 1ull))] =
-            value;
-    __syncthreads();
-}
-
 /* one shaded path-bounce of path `id` per lane where pred, added to its block's cost: lanes
    of the same block share one atomic (a wave's paths are mostly of one or two blocks), into
    the wave's stripe of the counters (HptPaths::blockCost) */
@@ -2356,19 +2320,6 @@ __device__ __forceinline__ void countBlockCost(const HptPaths &P, bool pred, uin
         if (__lane_id() == (uint32_t) L) atomicAdd(&stripe[b], (uint32_t) __popcll(m));
         todo &= ~m;
     }
-}
-
-/* a ray's claim-order bucket: the length of its interval inside the scene box against the box
-   diagonal (rays that leave the hair's box soon are short; the thresholds are the quartiles of
-   the headline frame's bounce rays, tools/ray_order_probe.py) */
-HD uint32_t claimBucket(const HptScene &sc, V3 o, V3 d, float maxt) {
-    float nearT, farT;
-    const V3 rcp = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    if (!aabbIntersect(sc, o, d, rcp, nearT, farT)) return 0u;
-    const float len = fminr(farT, maxt) - fmaxr(nearT, 0.0f);
-    const float ex = sc.aabbMax[0] - sc.aabbMin[0], ey = sc.aabbMax[1] - sc.aabbMin[1], ez = sc.aabbMax[2] - sc.aabbMin[2];
-    const float rel2 = len * len / (ex * ex + ey * ey + ez * ez);
-    return (rel2 > 0.24f * 0.24f ? 1u : 0u) + (rel2 > 0.33f * 0.33f ? 1u : 0u) + (rel2 > 0.45f * 0.45f ? 1u : 0u);
 }
 
 /* append to a queue: one atomic per wave (wave64 ballot + mbcnt) */
@@ -2467,41 +2418,15 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
    claimed together, so a launch's record writes fill whole lines in L2
    instead of a 32-byte sector per lone path-indexed 16-byte store.
    posQ (k_trace_overflow): the queue positions of the rays to trace. */
-template <bool BUCKETS>
-struct PathIOT {
+struct PathIO {
     HptPaths P;
     const uint32_t *traceQ, *shadowQ;
     uint32_t nTrace, nShadow, id;
     bool byQueue;
     const uint32_t *posQ;
-    static constexpr bool kContiguous = !BUCKETS; /* a shard's items are consecutive work indices */
     bool recs; /* bounce launches: rays from the queue-ordered records, keys are queue positions */
-    const uint32_t *bq; /* claim-order buckets (P.bucketQ), longest rays first; nullptr: queue order */
-    uint32_t nb[BUCKETS ? HPT_BUCKETS : 1];
+    /* work indices: closest rays [0, nTrace), then shadow rays */
     HD uint32_t count() const { return nTrace + nShadow; }
-    /* cursor shard s of HPT_CURSORS: its length, and its j-th work item (a work index k: closest
-       rays [0, nTrace), then shadow rays).  With buckets a shard walks the s-th part of every
-       bucket, longest bucket first, so every shard claims long rays before short ones */
-    HD uint32_t shardSize(uint32_t s) const {
-        if (!BUCKETS || !bq) return shardLo(count(), s + 1) - shardLo(count(), s);
-        uint32_t n = 0;
-#pragma unroll
-        for (int b = 0; b < HPT_BUCKETS; ++b) n += shardLo(nb[b], s + 1) - shardLo(nb[b], s);
-        return n;
-    }
-    HD uint32_t item(uint32_t s, uint32_t j) const {
-        if (!BUCKETS || !bq) return shardLo(count(), s) + j;
-#pragma unroll
-        for (int b = HPT_BUCKETS - 1; b >= 0; --b) {
-            const uint32_t lo = shardLo(nb[b], s), sz = shardLo(nb[b], s + 1) - lo;
-            if (j < sz || b == 0) {
-                const uint32_t e = bq[(size_t) b * P.bucketCap + lo + j];
-                return (e & HPT_BUCKET_SHADOW) ? nTrace + (e & ~HPT_BUCKET_SHADOW) : e;
-            }
-            j -= sz;
-        }
-        return 0;
-    }
     HD bool begin(const HptScene &sc, uint32_t k, TraceRay &r) {
         if (recs) { /* a bounce ray leaves the hit point at kEpsilon (path.cpp:213, scene.cpp:838) */
             if (k < nTrace) {
@@ -2545,8 +2470,6 @@ struct PathIOT {
     }
 };
 
-using PathIO = PathIOT<false>;       /* queue order */
-using BouncePathIO = PathIOT<true>;  /* queue order or claim-order buckets (k_trace) */
 
 /* k_trace launch shape (measured on MI355X, furball 512^2 @ 256 spp):
    persistent 256-thread blocks (64 and 128 are within 1.5%); an 8-entry ring
@@ -2574,16 +2497,10 @@ using BouncePathIO = PathIOT<true>;  /* queue order or claim-order buckets (k_tr
 
 /* the queue lengths come from device memory (the launch is enqueued before
    the host knows them) */
-/* a bounce launch's work: its queue lengths and, with claim-order buckets, their lengths */
-HD BouncePathIO bouncePathIO(const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ, const uint32_t *nTrace,
-                             const uint32_t *nShadow, const uint32_t *nBucket) {
-    BouncePathIO io{P, traceQ, shadowQ, *nTrace, *nShadow, 0, true, nullptr, true};
-    if (nBucket && P.bucketQ) {
-        io.bq = P.bucketQ;
-#pragma unroll
-        for (int b = 0; b < HPT_BUCKETS; ++b) io.nb[b] = nBucket[b];
-    }
-    return io;
+/* a bounce launch's work: its queue lengths */
+HD PathIO bouncePathIO(const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ, const uint32_t *nTrace,
+                       const uint32_t *nShadow) {
+    return PathIO{P, traceQ, shadowQ, *nTrace, *nShadow, 0, true, nullptr, true};
 }
 /* the next bounce's counts and cursor set start at zero (what a separate clearing launch did):
    nothing of this launch reads them, and the next bounce's first kernel runs after it */
@@ -2595,16 +2512,15 @@ __device__ __forceinline__ void clearNextParity(uint32_t *counters, uint32_t q) 
         counters[HPT_C_TRACE(q)] = 0;
         counters[HPT_C_SHADOW(q)] = 0;
         counters[HPT_C_SHADE(q)] = 0;
-        for (int b = 0; b < HPT_BUCKETS; ++b) counters[HPT_C_BUCKET(q, b)] = 0;
     }
 }
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
     const uint32_t *__restrict__ nTrace, const uint32_t *__restrict__ nShadow, uint32_t *__restrict__ cursors,
-    const uint32_t *__restrict__ nBucket, uint32_t *counters, uint32_t nextParity) {
+    uint32_t *counters, uint32_t nextParity) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     clearNextParity(counters, nextParity);
-    BouncePathIO io = bouncePathIO(P, traceQ, shadowQ, nTrace, nShadow, nBucket);
+    PathIO io = bouncePathIO(P, traceQ, shadowQ, nTrace, nShadow);
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(HptScene sc, HptPaths P,
@@ -2613,12 +2529,11 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
                                                                               const uint32_t *__restrict__ nTrace,
                                                                               const uint32_t *__restrict__ nShadow,
                                                                               uint32_t *__restrict__ cursors,
-                                                                              const uint32_t *__restrict__ nBucket,
                                                                               uint32_t *counters, uint32_t nextParity,
                                                                               uint32_t *stats) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     clearNextParity(counters, nextParity);
-    BouncePathIO io = bouncePathIO(P, traceQ, shadowQ, nTrace, nShadow, nBucket);
+    PathIO io = bouncePathIO(P, traceQ, shadowQ, nTrace, nShadow);
     tracePersistent<HPT_STACK, true>(sc, io, cursors, stk + threadIdx.x, stats);
 }
 
@@ -2854,7 +2769,6 @@ struct HptShadeIO {
     const uint32_t *nShade;
     uint32_t *nTrace, *nShadow, *counters;
     uint32_t tailFrom; /* a queue shorter than this is k_tail's (device-side bounce control); 0: always shade */
-    uint32_t *nBucket; /* the next trace launch's claim-order bucket lengths (nullptr: no buckets) */
 };
 template <bool MULTI>
 __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
@@ -2882,14 +2796,8 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
         for (int i = 0; i < 3; ++i) in[i] = P.shadeRec[3 * tid + i];
         shadePath<MULTI, true>(sc, P, id, P.hitS[tid], q.counters, cont, shadow, in, cOut, sOut, wiL);
     }
-    const uint32_t cpos = qpushBlockRec<HPT_SHADE_BLOCK, 4>(cont, id, traceQ, q.nTrace, P.postRec, cOut);
-    const uint32_t spos = qpushBlockRec<HPT_SHADE_BLOCK, 3>(shadow, id, shadowQ, q.nShadow, P.shadowRec, sOut);
-    if (q.nBucket) { /* uniform: the launch's claim-order buckets */
-        const uint32_t bc = cont ? claimBucket(sc, v3(cOut[0].x, cOut[0].y, cOut[0].z), v3(cOut[1].x, cOut[1].y, cOut[1].z), finf()) : 0u;
-        qpushBucket<HPT_SHADE_BLOCK>(cont, bc, cpos, P.bucketQ, P.bucketCap, q.nBucket);
-        const uint32_t bs = shadow ? claimBucket(sc, v3(sOut[0].x, sOut[0].y, sOut[0].z), v3(sOut[1].x, sOut[1].y, sOut[1].z), sOut[1].w) : 0u;
-        qpushBucket<HPT_SHADE_BLOCK>(shadow, bs, spos | HPT_BUCKET_SHADOW, P.bucketQ, P.bucketCap, q.nBucket);
-    }
+    qpushBlockRec<HPT_SHADE_BLOCK, 4>(cont, id, traceQ, q.nTrace, P.postRec, cOut);
+    qpushBlockRec<HPT_SHADE_BLOCK, 3>(shadow, id, shadowQ, q.nShadow, P.shadowRec, sOut);
 }
 #ifndef HPT_SHADE_WAVES
 #define HPT_SHADE_WAVES 0 /* 0: natural allocation (100 VGPRs = 5 waves/SIMD) */
@@ -3290,10 +3198,7 @@ struct BatchIO {
     uint32_t n;
     bool shadow;
     uint32_t cur;
-    static constexpr bool kContiguous = true;
     HD uint32_t count() const { return n; }
-    HD uint32_t shardSize(uint32_t s) const { return shardLo(n, s + 1) - shardLo(n, s); }
-    HD uint32_t item(uint32_t s, uint32_t j) const { return shardLo(n, s) + j; }
     HD uint32_t key() const { return cur; }
     HD bool begin(const HptScene &sc, uint32_t i, TraceRay &r) {
         cur = i;
@@ -3447,17 +3352,16 @@ static unsigned persistentBlocks(const void *kernel, uint64_t items, int block =
 
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
-                            uint64_t maxItems, hipStream_t s, const uint32_t *nBucket, uint32_t *counters,
-                            uint32_t nextParity) {
+                            uint64_t maxItems, hipStream_t s, uint32_t *counters, uint32_t nextParity) {
     if (maxItems == 0) return hipSuccess;
     hptProbeBeforeTraceLaunch(s);
     if (stats)
         hipLaunchKernelGGL(k_trace_counted, dim3(persistentBlocks((const void *) k_trace_counted, maxItems)),
-                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, nBucket,
+                           dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, nTrace, nShadow, cursors,
                            counters, nextParity, stats);
     else
         hipLaunchKernelGGL(k_trace, dim3(persistentBlocks((const void *) k_trace, maxItems)), dim3(HPT_TRACE_BLOCK), 0, s,
-                           sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, nBucket, counters, nextParity);
+                           sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, counters, nextParity);
     return hipGetLastError();
 }
 hipError_t hpt_launch_trace_camera(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
@@ -3502,9 +3406,9 @@ hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint3
 }
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
                             uint32_t *traceQ, uint32_t *nTrace, uint32_t *shadowQ, uint32_t *nShadow, uint32_t *counters,
-                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s, uint32_t *nBucket) {
+                            uint64_t maxItems, uint32_t tailFrom, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
-    const HptShadeIO q{nShade, nTrace, nShadow, counters, tailFrom, P.bucketQ ? nBucket : nullptr};
+    const HptShadeIO q{nShade, nTrace, nShadow, counters, tailFrom};
     if (sc.nShapes > 1)
         hipLaunchKernelGGL(k_shade_multi, dim3(blocksFor(maxItems, HPT_SHADE_BLOCK)), dim3(HPT_SHADE_BLOCK), 0, s, sc, P, shadeQ,
                            traceQ, shadowQ, q);

@@ -84,14 +84,20 @@ def block_weights(costs, spp: int, width: int, height: int, block: int = 32):
     return np.asarray(costs, np.float64) + CAMERA_RAY_WEIGHT * spp * pixels.astype(np.float64)
 
 
-def balance_blocks(renderer, n_blocks: int, world: int, dist=None, device=None, spp=None, width=None, height=None):
+def balance_blocks(renderer, n_blocks: int, world: int, dist=None, device=None, spp=None, width=None, height=None,
+                   frames: int = 1):
     """After a frame: every rank reads the path-bounces its blocks shaded
     (hpt_get_block_costs), the counts are summed over ranks, and every rank sets the same
     weights (hpt_set_block_weights; with spp / width / height the camera rays are added, see
-    block_weights), so the next frames use the same work-balanced deal.  Returns the weights."""
+    block_weights), so the next frames use the same work-balanced deal.  The device counts
+    add up over every render since the last read: `frames` is how many frames of spp samples
+    they cover (they are divided by it, so the per-frame camera-ray term of block_weights
+    keeps its weight).  Returns the weights."""
     import numpy as np
     import torch
-    costs = renderer.block_costs(n_blocks).astype(np.float64)
+    if frames < 1:
+        raise ValueError("balance_blocks: the costs must cover at least one frame")
+    costs = renderer.block_costs(n_blocks).astype(np.float64) / float(frames)
     if world > 1:
         if dist is None:
             import torch.distributed as dist

@@ -191,7 +191,9 @@ class Renderer:
         """a context on `device` rendering this prepared context's scene (parsed, loaded and built
         once, uploaded again: hpt_context_share_scene)"""
         h = C.c_void_p()
-        self._check(self.lib.hpt_context_share_scene(self.h, device, C.byref(h)))
+        rc = self.lib.hpt_context_share_scene(self.h, device, C.byref(h))
+        if rc != 0:  # reported to this thread, not on the (shared, read-only) source context
+            raise HairPTError("hairpt error %d: %s" % (rc, self.lib.hpt_last_error(None).decode()), rc)
         return Renderer(device, _handle=h)
 
     def close(self):

@@ -15,7 +15,12 @@
  *   - all buffers are caller-owned; host pointers unless the name says
  *     "device";
  *   - a context drives one HIP device; calls on one context are not
- *     thread-safe (one context per rank / GPU).
+ *     thread-safe (one context per rank / GPU), except that several threads
+ *     may call hpt_context_share_scene on one prepared source at once (it only
+ *     reads the source);
+ *   - calls that fail before they have a context of their own to report on
+ *     (hpt_context_create, hpt_context_share_scene) leave the message for the
+ *     calling thread: hpt_last_error(NULL).
  */
 #ifndef HAIRPT_H
 #define HAIRPT_H
@@ -174,7 +179,11 @@ int hpt_render_device(hpt_context *ctx, const hpt_render_params *params, void *d
    kd-tree not built again, only uploaded -- and hpt_render_multi renders shard g of n on
    ctxs[g] (on their own threads), combines the films on ctxs[0]'s device (peer copies over
    xGMI, added in shard order: the same sum as adding the n host films) and ACCUMULATES the
-   result into film_rgbw.  params->shard / n_shards are ignored. */
+   result into film_rgbw.  params->shard / n_shards are ignored.  The contexts must render one
+   scene: shares of the same prepared context (a context prepared again renders a scene of its
+   own), with equal camera / sampler / integrator settings and equal block weights (the shard
+   deal; share_scene copies the source's) -- otherwise HPT_EINVAL before anything renders.  A
+   share failure is reported to the calling thread (hpt_last_error(NULL)), never on src. */
 int hpt_context_share_scene(hpt_context *src, int device, hpt_context **out);
 int hpt_render_multi(hpt_context *const *ctxs, int n, const hpt_render_params *params, float *film_rgbw);
 
@@ -184,7 +193,9 @@ int hpt_render_multi(hpt_context *const *ctxs, int n, const hpt_render_params *p
    index by * ceil(W/32) + bx, zero for blocks other shards own) and resets them.  Ranks that add
    their counts up and pass the same totals to hpt_set_block_weights get the same deal: blocks by
    descending weight, each to the shard with the least weight so far (hpt_block_deal, which
-   computes it without a context).  No weights (n_blocks 0): the Hilbert-cyclic deal. */
+   computes it without a context).  No weights (n_blocks 0): the Hilbert-cyclic deal.  Weights
+   must be finite and >= 0 (HPT_EINVAL), and a render whose frame has a different number of
+   blocks than the weights fails with HPT_EINVAL. */
 int hpt_get_block_costs(hpt_context *ctx, uint64_t *costs, int n_blocks);
 int hpt_set_block_weights(hpt_context *ctx, const double *weights, int n_blocks);
 int hpt_block_deal(int width, int height, int n_shards, const double *weights, int32_t *shard_of_block);

@@ -46,9 +46,19 @@ def test_share_scene_needs_a_prepared_source(tmp_path):
     xml = scene_util.scenes.make_scene("furball_marschner", str(tmp_path), n_strands=100)
     r = native.Renderer(device=native.HOST_ONLY)
     r.load_scene_xml(xml, {})
-    with pytest.raises(native.HairPTError):
+    with pytest.raises(native.HairPTError, match="not prepared"):
         r.share_scene(native.HOST_ONLY)
+    # the message went to the calling thread (hpt_last_error(NULL)), not to the source context
+    assert r.lib.hpt_last_error(r.h).decode() == ""
     r.close()
+
+
+def test_block_weights_are_checked():
+    # the deal's sort needs a strict weak order: NaN, negative or infinite weights are refused
+    for bad in (np.nan, -1.0, np.inf):
+        with pytest.raises(native.HairPTError):
+            native.block_deal(64, 64, 2, [1.0, bad, 2.0, 3.0])
+    assert list(native.block_deal(64, 64, 2, [4.0, 1.0, 2.0, 3.0])) == [0, 0, 1, 1]  # 4 | 3, 2 | 1
 
 
 @pytest.mark.gpu
@@ -72,6 +82,43 @@ def test_render_multi_two_contexts_one_device(tmp_path):
     np.testing.assert_allclose(acc, single, rtol=1e-5, atol=1e-5)
     r1.close()
     r0.close()
+
+
+@pytest.mark.gpu
+def test_render_multi_weighted_deal_and_mismatches(tmp_path):
+    """weights set before the share travel with it (every block rendered exactly once); contexts
+    that would render different deals or scenes into one film are refused before rendering"""
+    xml = scene_util.scenes.make_scene("furball_marschner", str(tmp_path), n_strands=1500)
+    defs = {"spp": 4, "width": 96, "height": 64}
+    r0 = native.Renderer(device=0)
+    r0.load_scene_xml(xml, defs)
+    r0.prepare()
+    single = r0.render(0, 4)
+    w = np.array([5.0, 1.0, 1.0, 1.0, 1.0, 9.0])
+    r0.set_block_weights(w)
+    r1 = r0.share_scene(0)
+    multi = native.Renderer.render_multi([r0, r1], 0, 4)
+    np.testing.assert_allclose(multi, single, rtol=1e-5, atol=1e-5)
+    np.testing.assert_array_equal(multi[..., 3], single[..., 3])  # every pixel's samples once
+    # a context whose weights differ from ctxs[0]'s
+    r1.set_block_weights(w[::-1].copy())
+    with pytest.raises(native.HairPTError, match="weights"):
+        native.Renderer.render_multi([r0, r1], 0, 4)
+    r1.set_block_weights(w)
+    np.testing.assert_array_equal(native.Renderer.render_multi([r0, r1], 0, 4), multi)
+    # a context prepared again renders a scene of its own
+    r1.prepare()
+    with pytest.raises(native.HairPTError, match="different prepared scene"):
+        native.Renderer.render_multi([r0, r1], 0, 4)
+    # weights for another frame size fail the render loudly
+    r2 = native.Renderer(device=0)
+    r2.load_scene_xml(xml, defs)
+    r2.prepare()
+    r2.set_block_weights(np.ones(4))
+    with pytest.raises(native.HairPTError, match="block weights"):
+        r2.render(0, 4)
+    for r in (r2, r1, r0):
+        r.close()
 
 
 @pytest.mark.gpu
