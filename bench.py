@@ -226,19 +226,25 @@ def main():
                  unocc=c.shadow_unoccluded, bounces=c.bounces, launches=c.trace_launches,
                  node_slots=c.node_slots, prim_slots=c.prim_slots,
                  p_rays=c.packet_rays, p_nodes=c.packet_nodes, p_prims=c.packet_prims, p_exact=c.packet_exact,
-                 p_node_slots=c.packet_node_slots, p_prim_slots=c.packet_prim_slots, p_fallbacks=c.packet_fallbacks)
+                 p_node_slots=c.packet_node_slots, p_prim_slots=c.packet_prim_slots, p_fallbacks=c.packet_fallbacks,
+                 cut=c.cut_rays)
     acc = {"ms_trace": 0.0, "ms_packet": 0.0, "launches": 0, "p_launches": 0, "kernels": {}}
 
     def collect():
-        s = r.stats()  # HIP events around every kernel (on the library's stream), no counters
+        # HIP events (on the library's stream) around the traversal launches only (collect_stats 3):
+        # an event around every kernel costs the frame ~4 us per event between launches
+        s = r.stats()
         acc["ms_trace"] += s.ms_trace
         acc["launches"] += s.trace_launches
         acc["ms_packet"] += s.ms_trace_packet
         acc["p_launches"] += s.packet_launches
-        for k in ("camera", "trace_packet", "trace", "primary", "shade", "post", "tail", "gather"):
-            acc["kernels"][k] = acc["kernels"].get(k, 0.0) + getattr(s, "ms_" + k)
 
-    dt = timed_steps(lambda: step(1), args.steps, world, dist, torch.cuda.synchronize, "cuda:%d" % local, collect)
+    dt = timed_steps(lambda: step(3), args.steps, world, dist, torch.cuda.synchronize, "cuda:%d" % local, collect)
+    # the per-kernel split of one more (untimed) frame, with an event around every kernel
+    step(1)
+    s1 = r.stats()
+    for k in ("camera", "trace_packet", "trace", "primary", "shade", "post", "tail", "gather"):
+        acc["kernels"][k] = getattr(s1, "ms_" + k)
     # the same frame once more with no recorded bounce schedule (what a render of a new spp range
     # or the CLI's first pass does: every bounce's queue length read back); not
     # part of `value`, which times repeated frames of the same spp range
@@ -360,9 +366,14 @@ def main():
             # value times repeated frames of one spp range, whose bounces are launched ahead on the
             # schedule recorded by the first render; this is that first render (one frame)
             "first_render_ms": round(first_ms, 3),
-            "kernel_ms_per_step": {k: round(v / args.steps, 3) for k, v in ms_kernels.items()},
+            "kernel_ms_per_step": {k: round(v, 3) for k, v in ms_kernels.items()},
+            "timing": "timed steps: HIP events around the traversal launches only (collect_stats 3); "
+                      "kernel_ms_per_step: one more frame with an event around every kernel",
             "cpu_baseline": cpu,
             "stats": {"bounces_per_path": round(tot["bounces"] / max(1, paths_total / world), 4),
+                      # the resumable cut: rays the counted frame's bounce launches saved at their dry
+                      # point and the next launch resumed
+                      "cut_rays_per_step": int(frame["cut"]),
                       "nodes_per_ray": round(tot["nodes"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "binary_nodes_per_ray": round(tot["bnodes"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "prims_per_ray": round(tot["prims"] / max(1, tot["closest"] + tot["shadow"]), 2),

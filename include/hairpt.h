@@ -162,7 +162,9 @@ typedef struct hpt_render_params {
                                       Hilbert curve over the block grid (multi-GPU; hpt_capi.cpp blockOrder) */
     uint64_t max_wave_paths;       /* 0 = automatic (HBM-sized waves) */
     int collect_stats;             /* 0 none, 1 per-kernel HIP event timing,
-                                      2 timing + traversal counters (slower k_trace variant) */
+                                      2 timing + traversal counters (slower k_trace variant),
+                                      3 HIP event timing of the traversal launches only
+                                        (k_trace, k_trace_packet: the roofline's kernels) */
 } hpt_render_params;
 
 /* SamplingIntegrator::render/renderBlock + MIPathTracer::Li + ImageBlock::put
@@ -234,6 +236,9 @@ typedef struct hpt_stats {
     /* waves whose schedule was launched ahead but did not cover them (the tail declined, or
        bounces ran past it): finished bounce by bounce and their schedule re-recorded */
     uint64_t schedule_extensions;
+    /* the resumable cut: rays the bounce trace launches saved at their dry point and the next
+       launch resumed (instead of draining them), over the render call */
+    uint64_t cut_rays;
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 

@@ -33,7 +33,9 @@ def main():
     ap.add_argument("--balance", nargs="?", const="camera", choices=["bounces", "camera"],
                     help="deal the blocks by the work each did in a first frame (hpt_set_block_weights): its "
                          "path-bounces, or those plus its camera rays (bench.py's deal, the default)")
-    ap.add_argument("--stats-level", type=int, default=1, help="hpt_render_params.collect_stats of the timed renders")
+    ap.add_argument("--stats-level", type=int, default=0,
+                    help="hpt_render_params.collect_stats of the timed renders (0: no events between launches; the "
+                         "per-kernel split comes from one more render of the shard at level 1)")
     a = ap.parse_args()
     cfg = scenes.CONFIGS[a.config]
     xml = scenes.make_scene(a.config, os.path.join(tempfile.gettempdir(), "hpt_shards"), n_strands=cfg["n"])
@@ -55,6 +57,12 @@ def main():
                 r.render_device(film.data_ptr(), 0, spp, shard=shard, n_shards=n, collect_stats=a.stats_level)
             torch.cuda.synchronize()
             best = min(best, time.perf_counter() - t0)
+        if a.stats_level == 0:  # the per-kernel split, from one more (untimed) render with events
+            if a.split == "spp":
+                r.render_device(film.data_ptr(), shard * spp // n, (shard + 1) * spp // n, collect_stats=1)
+            else:
+                r.render_device(film.data_ptr(), 0, spp, shard=shard, n_shards=n, collect_stats=1)
+            torch.cuda.synchronize()
         return best, r.stats()
 
     r.render_device(film.data_ptr(), 0, spp)  # warm-up
