@@ -69,6 +69,13 @@ static uint32_t defaultCutMin() {
     const char *v = std::getenv("HPT_CUT_MIN");
     return v ? (uint32_t) std::strtoul(v, nullptr, 10) : 0u;
 }
+/* with the cut on, k_tail takes a bounce's queue below this many paths (HPT_CUT_TAIL): the paths the
+   last cutting bounce held back run one bounce behind the rest, and the tail, not one more
+   wavefront bounce, finishes them */
+static uint32_t defaultCutTail() {
+    const char *v = std::getenv("HPT_CUT_TAIL");
+    return v ? (uint32_t) std::strtoul(v, nullptr, 10) : (1u << 19);
+}
 /* the bounce schedule of a wave of paths: the shade-queue length of each wavefront bounce,
    and whether a k_tail launch took the rest */
 struct BounceSchedule {
@@ -90,6 +97,7 @@ struct hpt_context {
     int device = 0;
     uint32_t tailPaths = defaultTailPaths();
     uint32_t cutMin = defaultCutMin();
+    uint32_t cutTail = defaultCutTail();
     uint32_t cutEpoch = 0;         /* per trace launch that may cut (HptPaths::cutMark) */
     std::vector<DevBuf> carryBufs; /* carryRay / carryPath / cutMark, allocated with the first cut */
     uint64_t carryPaths = 0;       /* paths cutMark covers */
@@ -1137,7 +1145,9 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     if ((r = ensureCarry(c, waveCap))) return r;
     /* the resumable cut: never below the tail threshold (the launch before k_tail drains) */
     const bool cutOn = c->cutMin != 0 && c->P.cutMark != nullptr;
-    const uint32_t cutMin = std::max(c->cutMin, c->tailPaths);
+    /* the tail threshold, raised with the cut (defaultCutTail) */
+    const uint32_t tailPaths = cutOn ? std::max(c->tailPaths, c->cutTail) : c->tailPaths;
+    const uint32_t cutMin = std::max(c->cutMin, tailPaths);
     const uint64_t carrySlack = cutOn ? c->P.carryCap : 0; /* the most rays / paths a bounce can hold back */
     if (slots > c->partialSlots) {
         if (c->partial) (void) hipFree(c->partial);
@@ -1281,9 +1291,16 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         int b = 1, bounce = 0;
         /* grid: the shade launch's; traceExtra / postExtra: room for the rays / paths the previous
            bounce held back (read back: their counts; launched ahead: the schedule's slack) */
+        /* Bounce b's k_post starts Russian roulette at b >= rrDepth (path.cpp:276, depth b): from
+           there on most paths end each bounce, and paths held back there would trail the rest
+           by a bounce through bounces that otherwise would not run.  So the cut stops one bounce
+           earlier: the paths the last cutting launch holds back are posted with the others at
+           the bounce before roulette, and k_tail (cutTail) finishes what trails */
+        const int rrDepth = c->sc.rrDepth;
         auto wavefrontBounce = [&](uint32_t p, uint64_t grid, uint32_t tailFrom, uint64_t traceExtra,
                                    uint64_t postExtra) -> hipError_t {
             const uint32_t q = p ^ 1u;
+            const bool cutHere = cutOn && (rrDepth <= 0 || b < rrDepth);
             const uint32_t epoch = cutOn ? ++c->cutEpoch : 0u;
             if (cutOn && epoch == 0) return hipErrorUnknown; /* 2^32 cut launches: never in practice */
             hipError_t e1 = timed(2, [&] {
@@ -1293,7 +1310,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             if (e1) return e1;
             e1 = timed(-1, [&] {
                 return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(p), C + HPT_C_SHADOW(p),
-                                        C + HPT_CURSOR_SET(p), dst, 2ull * grid + traceExtra, s, C, q, cutOn ? cutMin : 0u,
+                                        C + HPT_CURSOR_SET(p), dst, 2ull * grid + traceExtra, s, C, q, cutHere ? cutMin : 0u,
                                         epoch);
             });
             if (e1) return e1;
@@ -1320,7 +1337,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                 e = timed(5, [&] {
                     const uint32_t p = (uint32_t) b & 1u;
                     return hpt_launch_tail(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), C, HPT_ITEMS_ON_DEVICE,
-                                           c->tailPaths, s);
+                                           tailPaths, s);
                 });
             if (e) break;
             /* the gather right behind the schedule, guarded on the device (the wave is done: no
@@ -1357,7 +1374,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                 learn = extended = true;
                 c->stats.schedule_extensions++;
             }
-            if (n < c->tailPaths && noCarry) {
+            if (n < tailPaths && noCarry) {
                 /* few live paths: finish them all in one launch (k_tail) */
                 seen.tail = true;
                 e = timed(5, [&] { return hpt_launch_tail(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), C, n, ~0u, s); });
@@ -1526,6 +1543,7 @@ int hpt_context_share_scene(hpt_context *src, int device, hpt_context **out) {
     c->vdcInv = src->vdcInv;
     c->maxLeafRounds = src->maxLeafRounds, c->maxRestarts = src->maxRestarts, c->packetStack = src->packetStack;
     c->tailPaths = src->tailPaths, c->bounceAhead = src->bounceAhead, c->packets = src->packets;
+    c->cutMin = src->cutMin, c->cutTail = src->cutTail;
     /* the shard deal: hpt_render_multi gives shard g to context g, and every context must deal
        the blocks the same way or some blocks are rendered twice and others never */
     c->blockWeights = src->blockWeights;

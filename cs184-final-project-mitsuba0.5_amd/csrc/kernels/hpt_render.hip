@@ -2501,7 +2501,9 @@ struct BounceIO {
     uint32_t nCarry, nTrace, nShadow, id;
     const float4 *carryIn; /* carryRay[p ^ 1]: the rays the previous launch cut */
     float4 *carryOut;      /* carryRay[p] */
-    uint32_t *nCarryOut, *nCutStat;
+    uint32_t *counters;    /* the counter block (one pointer and the parity, not three pointers: k_trace's
+                              SGPRs are spent) */
+    uint32_t par;          /* the launch's parity p */
     uint32_t epoch;
     bool cut;
     static constexpr bool kCut = true;
@@ -2588,8 +2590,8 @@ struct BounceIO {
         if (m == 0) return;
         uint32_t base = 0;
         if (__lane_id() == 0) {
-            base = atomicAdd(nCarryOut, (uint32_t) __popcll(m));
-            atomicAdd(nCutStat, (uint32_t) __popcll(m));
+            base = atomicAdd(counters + HPT_C_CARRY_RAYS(par), (uint32_t) __popcll(m));
+            atomicAdd(counters + HPT_C_CUT_RAYS, (uint32_t) __popcll(m));
         }
         base = (uint32_t) __builtin_amdgcn_readfirstlane((int) base);
         if (!active) return;
@@ -2669,13 +2671,11 @@ struct BounceIO {
 HD BounceIO bounceIO(const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ, const uint32_t *nTrace,
                      const uint32_t *nShadow, uint32_t *counters, uint32_t nextParity, uint32_t cutMin, uint32_t epoch) {
     const uint32_t p = nextParity ^ 1u;
-    BounceIO io{P, traceQ, shadowQ, 0, *nTrace, *nShadow, 0, nullptr, nullptr, nullptr, nullptr, epoch, false};
+    BounceIO io{P, traceQ, shadowQ, 0, *nTrace, *nShadow, 0, nullptr, nullptr, counters, p, epoch, false};
     if (counters) {
         io.nCarry = counters[HPT_C_CARRY_RAYS(nextParity)];
         io.carryIn = P.carryRay[nextParity];
         io.carryOut = P.carryRay[p];
-        io.nCarryOut = counters + HPT_C_CARRY_RAYS(p);
-        io.nCutStat = counters + HPT_C_CUT_RAYS;
         io.cut = cutMin != 0 && io.nTrace >= cutMin && P.carryRay[p] != nullptr;
     }
     return io;

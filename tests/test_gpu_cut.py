@@ -6,7 +6,8 @@ next launch resumes it first, and the bounce's k_post holds the ray's path back 
 its rays are done.  Each ray therefore tests the same segments in the same order with the
 same intervals, and each path adds its NEE term before its emitter term (path.cpp:119-294):
 the film must be bit-identical to the drained render, with the rays cut and resumed any
-number of times (HPT_CUT_MIN low: small launches cut at once, resumed rays are cut again),
+number of times (HPT_CUT_MIN low: small launches cut at once, resumed rays are cut again;
+the cut stops at the bounce where Russian roulette starts),
 in the read-back loop and with the bounces launched ahead, with and without k_tail, for one
 and several hair shapes, and over several waves of paths.
 """
@@ -23,6 +24,7 @@ HAIRCURL_RADII = (0.0025, 0.0025)
 def _render(name, n, radii, monkeypatch, cut_min, tail, ahead, times=1, w=64, h=48, spp=16, max_wave=0):
     monkeypatch.setenv("HPT_CUT_MIN", str(cut_min))
     monkeypatch.setenv("HPT_TAIL_PATHS", tail)
+    monkeypatch.setenv("HPT_CUT_TAIL", tail)  # (the shipped one, 2^19, would take these small frames whole)
     monkeypatch.setenv("HPT_BOUNCE_AHEAD", ahead)
     _, r, _ = scene_util.make(name, n, w, h, spp, device=0, radii=radii)
     out = []
@@ -61,8 +63,8 @@ def test_cut_several_waves(monkeypatch):
 
 
 def test_cut_default_threshold_large_frame(monkeypatch):
-    """at the shipped threshold (2^18 closest rays) a 256x256 @ 64 frame of 4 M paths cuts its
-    first bounces' launches on its own; the film equals the drained one bit for bit"""
+    """at 2^18 closest rays and the 2^17 tail a 256x256 @ 64 frame of 4 M paths cuts its first
+    bounces' launches on its own; the film equals the drained one bit for bit"""
     [(ref, s0)] = _render("furball_marschner", 8000, None, monkeypatch, 0, str(1 << 17), "1", w=256, h=256, spp=64)
     (f1, s1), (f2, s2) = _render("furball_marschner", 8000, None, monkeypatch, 1 << 18, str(1 << 17), "1", times=2,
                                  w=256, h=256, spp=64)
