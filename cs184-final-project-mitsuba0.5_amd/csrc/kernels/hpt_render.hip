@@ -2768,7 +2768,11 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY voi
     const uint32_t *__restrict__ nOverflow, uint32_t *__restrict__ cursors) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     /* overflowQ holds camera-queue positions (the packet kernel's keys) */
-    PathIO io{P, traceQ, nullptr, *nOverflow, 0, 0, true, overflowQ, false};
+    const uint32_t n = *nOverflow;
+    /* none at the shipped configs: leave at once (the claim walk over every cursor shard took the
+       empty launch 30 us per frame) */
+    if (n == 0) return;
+    PathIO io{P, traceQ, nullptr, n, 0, 0, true, overflowQ, false};
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
 
