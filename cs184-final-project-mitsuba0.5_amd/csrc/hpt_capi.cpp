@@ -822,6 +822,12 @@ static int uploadScene(hpt_context *c) {
             rec.mar.vTT = m.vTT;
             rec.mar.vTRT = m.vTRT;
             rec.mar.scaleAngleRad = m.scaleAngleRad;
+            const float lobeV[3] = {m.vR, m.vTT, m.vTRT};
+            for (int l = 0; l < 3; ++l) {
+                const float v = lobeV[l];
+                rec.mar.lobeInvV[l] = 1.0f / v;
+                rec.mar.lobeK[l] = v < 0.1f ? logf(1.0f / (2.0f * v)) : 2.0f * v * sinhf(1.0f / v);
+            }
             for (int k = 0; k < 3; ++k) rec.mar.diffuse[k] = m.diffuse[k];
         } else if (rec.kind == HPT_BSDF_ROUGHPLASTIC) {
             r |= upload(c, c->rp[i].trans.data(), c->rp[i].trans.size() * 4, (const void **) &rec.rp.trans);

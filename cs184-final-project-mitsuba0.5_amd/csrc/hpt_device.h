@@ -95,6 +95,9 @@ struct HptMarschner {
     float fdr, invEta2, specularSamplingWeight;
     float vR, vTT, vTRT, scaleAngleRad;
     float diffuse[3];
+    /* longitudinalM's per-lobe constants (marschner_diffuse.cpp:364-374), R, TT, TRT: 1 / v, and
+       log(1 / (2 v)) when v < 0.1, else 2 v sinh(1 / v) */
+    float lobeInvV[3], lobeK[3];
 };
 
 struct HptKajiyaKay {

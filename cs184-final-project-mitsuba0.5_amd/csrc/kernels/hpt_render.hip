@@ -1280,19 +1280,14 @@ HD float longitudinalM(float v, float sinThetaI, float sinThetaO, float cosTheta
     if (v < 0.1f) return expf(-b + logI0(a) - 1.0f / v + 0.6931f + logf(1.0f / (2.0f * v)));
     return expf(-b) * I0(a) / (2.0f * v * sinhf(1.0f / v));
 }
-/* the same with the lobe's constants 1 / v and log(1 / (2 v)) (v < 0.1) or 2 v sinh(1 / v) computed
-   once per bounce (MarschnerWi): identical values, identical result */
-struct LobeConst {
-    float invV, k; /* k: logf(1 / (2 v)) when v < 0.1, else 2 v sinh(1 / v) */
-};
-HD LobeConst lobeConst(float v) {
-    return {1.0f / v, v < 0.1f ? logf(1.0f / (2.0f * v)) : 2.0f * v * sinhf(1.0f / v)};
-}
-HD float longitudinalMc(float v, LobeConst c, float sinThetaI, float sinThetaO, float cosThetaI, float cosThetaO) {
+/* the same with the lobe's constants 1 / v and log(1 / (2 v)) (v < 0.1) or 2 v sinh(1 / v), which
+   depend on the BSDF only: the host computes them once at upload (HptMarschner::lobeInvV, lobeK) */
+HD float longitudinalMc(float v, float invV, float k, float sinThetaI, float sinThetaO, float cosThetaI,
+                        float cosThetaO) {
     float a = cosThetaI * cosThetaO / v;
     float b = sinThetaI * sinThetaO / v;
-    if (v < 0.1f) return expf(-b + logI0(a) - c.invV + 0.6931f + c.k);
-    return expf(-b) * I0(a) / c.k;
+    if (v < 0.1f) return expf(-b + logI0(a) - invV + 0.6931f + k);
+    return expf(-b) * I0(a) / k;
 }
 
 /* Azimuthal::eval (:80-94) */
@@ -1369,7 +1364,6 @@ struct MarschnerWi {
     float thetaI;
     float sR, cR, sTT, cTT, sTRT, cTRT; /* sin / cos of thetaI shifted per lobe (:391-393) */
     float T12;                          /* roughTrans(wi.z) */
-    LobeConst kR, kTT, kTRT;            /* longitudinalM's per-lobe constants */
 };
 HD MarschnerWi marschnerWi(const HptMarschner &m, V3 wi) {
     MarschnerWi w;
@@ -1381,13 +1375,11 @@ HD MarschnerWi marschnerWi(const HptMarschner &m, V3 wi) {
     w.sTT = sinf(thetaITT), w.cTT = cosf(thetaITT);
     w.sTRT = sinf(thetaITRT), w.cTRT = cosf(thetaITRT);
     w.T12 = roughTrans(m, wi.z);
-    w.kR = lobeConst(m.vR);
-    w.kTT = lobeConst(m.vTT);
-    w.kTRT = lobeConst(m.vTRT);
     return w;
 }
 /* MarschnerDiffuse::eval (:377-482), hasDiffuse = true */
 HD V3 marschnerEvalW(const HptMarschner &m, const MarschnerWi &w, V3 wo) {
+    float T21 = roughTrans(m, wo.z); /* first: fewer values live across its powf */
     float sinThetaO = wo.y;
     float cosThetaO = trigInverse(sinThetaO);
     float thetaO = asinf(clampf(sinThetaO, -1.0f, 1.0f));
@@ -1395,13 +1387,12 @@ HD V3 marschnerEvalW(const HptMarschner &m, const MarschnerWi &w, V3 wo) {
     float cosThetaD = cosf(thetaD);
     float phi = atan2f(wo.x, wo.z);
     if (phi < 0.0f) phi += kPi * 2.0f;
-    float MR = longitudinalMc(m.vR, w.kR, w.sR, sinThetaO, w.cR, cosThetaO);
-    float MTT = longitudinalMc(m.vTT, w.kTT, w.sTT, sinThetaO, w.cTT, cosThetaO);
-    float MTRT = longitudinalMc(m.vTRT, w.kTRT, w.sTRT, sinThetaO, w.cTRT, cosThetaO);
+    float MR = longitudinalMc(m.vR, m.lobeInvV[0], m.lobeK[0], w.sR, sinThetaO, w.cR, cosThetaO);
+    float MTT = longitudinalMc(m.vTT, m.lobeInvV[1], m.lobeK[1], w.sTT, sinThetaO, w.cTT, cosThetaO);
+    float MTRT = longitudinalMc(m.vTRT, m.lobeInvV[2], m.lobeK[2], w.sTRT, sinThetaO, w.cTRT, cosThetaO);
     V3 result = (0.15f * MR) * azEval(m.table[0], phi, cosThetaD) + MTT * azEval(m.table[1], phi, cosThetaD) +
                 MTRT * azEval(m.table[2], phi, cosThetaD);
     V3 diff = v3(m.diffuse[0], m.diffuse[1], m.diffuse[2]);
-    float T21 = roughTrans(m, wo.z);
     diff = divs(diff, 1 - m.fdr);
     result = result + diff * (kInvPi * wo.z * w.T12 * T21 * m.invEta2);
     return result;
@@ -1410,14 +1401,8 @@ HD V3 marschnerEval(const HptMarschner &m, V3 wi, V3 wo) { return marschnerEvalW
 /* k_shade keeps a bounce's MarschnerWi in LDS between its NEE evaluation and its BSDF sample
    (nine more registers live across NEE would cost k_shade a wave per SIMD); row k of thread t at
    l[k * stride] */
-#define HPT_WI_ROWS 14
+#define HPT_WI_ROWS 8
 HD void stashWi(float *l, int stride, const MarschnerWi &w) {
-    l[8 * stride] = w.kR.invV;
-    l[9 * stride] = w.kR.k;
-    l[10 * stride] = w.kTT.invV;
-    l[11 * stride] = w.kTT.k;
-    l[12 * stride] = w.kTRT.invV;
-    l[13 * stride] = w.kTRT.k;
     l[0] = w.thetaI;
     l[stride] = w.sR;
     l[2 * stride] = w.cR;
@@ -1438,10 +1423,30 @@ HD MarschnerWi loadWi(const float *l, int stride) {
     w.sTRT = l[5 * stride];
     w.cTRT = l[6 * stride];
     w.T12 = l[7 * stride];
-    w.kR = {l[8 * stride], l[9 * stride]};
-    w.kTT = {l[10 * stride], l[11 * stride]};
-    w.kTRT = {l[12 * stride], l[13 * stride]};
     return w;
+}
+
+/* k_shade also keeps the shading point's position, normal and shading tangent, wi and the shadow
+   record in LDS, from the intersection record to the queue appends (stride HPT_SHADE_BLOCK): the
+   registers they would hold across both BSDF evaluations keep k_shade at 6 waves per SIMD.
+   Marschner reads only wi.y after marschnerWi (kRowWiY); the other BSDFs keep wi in rows 0-2. */
+enum : int {
+    kRowWiY = HPT_WI_ROWS,
+    kRowP = kRowWiY + 1,
+    kRowGeoN = kRowP + 3,
+    kRowShS = kRowGeoN + 3,
+    kRowSd = kRowShS + 3, /* shadow ray direction, max t */
+    kRowSc = kRowSd + 4,  /* NEE contribution */
+    kShadeRows = kRowSc + 3
+};
+HD void stashV3(float *l, int stride, int row, V3 v) {
+    l[row * stride] = v.x;
+    l[(row + 1) * stride] = v.y;
+    l[(row + 2) * stride] = v.z;
+}
+HD V3 loadV3(const float *l, int stride, int row) {
+    asm volatile("" ::: "memory"); /* read where used, not hoisted to the stash */
+    return v3(l[row * stride], l[(row + 1) * stride], l[(row + 2) * stride]);
 }
 
 /* sampleM (:582-592) */
@@ -2846,6 +2851,7 @@ template <bool MULTI, bool REC = false>
 HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec, uint32_t *__restrict__ counters,
                   bool &cont, bool &shadow, const float4 *in, float4 *cOut, float4 *sOut, float *wiL) {
     {
+        const int stride = REC ? HPT_SHADE_BLOCK : (int) blockDim.x; /* REC: k_shade's block, immediate LDS offsets */
         uint32_t st = REC ? __float_as_uint(in[2].w) : P.state[id];
         uint32_t dim = HPT_ST_DIM(st), depth = HPT_ST_DEPTH(st);
         const float4 ro = REC ? in[0] : P.ro[id], rd = REC ? in[1] : P.rd[id];
@@ -2863,6 +2869,24 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
             atomicOr(&counters[HPT_C_ERROR], 1u);
             stop = true;
         }
+        /* REC: p and the frame go to LDS rows and every later use reads them back (sh.n == geo.n,
+           sh.t == cross(sh.n, sh.s) as fillIts computes it) */
+        if (REC) {
+            stashV3(wiL, stride, kRowP, p);
+            stashV3(wiL, stride, kRowGeoN, geo.n);
+            stashV3(wiL, stride, kRowShS, sh.s);
+            asm volatile("" ::: "memory");
+        }
+        auto ldP = [&]() { return REC ? loadV3(wiL, stride, kRowP) : p; };
+        auto ldGeoN = [&]() { return REC ? loadV3(wiL, stride, kRowGeoN) : geo.n; };
+        auto ldSh = [&]() {
+            if (!REC) return sh;
+            Frame f;
+            f.n = loadV3(wiL, stride, kRowGeoN);
+            f.s = loadV3(wiL, stride, kRowShS);
+            f.t = cross(f.n, f.s);
+            return f;
+        };
         /* one inlined copy per BSDF source: the scene's own (kernel
            argument, scalar loads) or, with several hair shapes, the hit
            shape's entry of sc.bsdfs */
@@ -2872,7 +2896,20 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
             V3 T = v3(thr.x, thr.y, thr.z);
             /* Marschner: the wi terms of the bounce's NEE evaluation and BSDF sample, once */
             const bool mar = B.kind == HPT_BSDF_MARSCHNER;
-            if (mar) stashWi(wiL, (int) blockDim.x, marschnerWi(B.mar, wi));
+            if (REC) {
+                if (mar) wiL[kRowWiY * stride] = wi.y;
+                else stashV3(wiL, stride, 0, wi);
+            }
+            if (mar) stashWi(wiL, stride, marschnerWi(B.mar, wi));
+            else if (REC) asm volatile("" ::: "memory");
+            auto ldWi = [&]() {
+                if (!REC) return wi;
+                if (mar) {
+                    asm volatile("" ::: "memory");
+                    return v3(0.0f, wiL[kRowWiY * stride], 0.0f);
+                }
+                return loadV3(wiL, stride, 0);
+            };
             /* ---- direct illumination (path.cpp:175, scene.cpp:828-852, envmap.cpp:516-543) ---- */
             if (B.smooth) {
                 float nx = sobolSampleUniform(sc, sidx, dim), ny = sobolSampleUniform(sc, sidx, dim + 1);
@@ -2882,21 +2919,22 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
                 envSampleDir(sc.env, nx, ny, dl, value, pdf);
                 V3 dW = envToWorld(sc.env, dl);
                 float nearT, farT;
-                if (!(isZero(value) || pdf == 0 || !bsphereIntersect(sc.env, p, dW, nearT, farT) || nearT >= 0 ||
+                if (!(isZero(value) || pdf == 0 || !bsphereIntersect(sc.env, ldP(), dW, nearT, farT) || nearT >= 0 ||
                       farT <= 0)) {
                     V3 val = divs(value, pdf);
-                    V3 wo = sh.toLocal(dW);
-                    V3 bsdfVal = mar ? marschnerEvalW(B.mar, loadWi(wiL, (int) blockDim.x), wo) : bsdfEval(B, wi, wo);
-                    if (!isZero(bsdfVal) && (!sc.strictNormals || dot(geo.n, dW) * wo.z > 0)) {
-                        float bp = bsdfPdf(B, wi, wo);
+                    V3 wo = ldSh().toLocal(dW);
+                    V3 bsdfVal = mar ? marschnerEvalW(B.mar, loadWi(wiL, stride), wo) : bsdfEval(B, ldWi(), wo);
+                    if (!isZero(bsdfVal) && (!sc.strictNormals || dot(ldGeoN(), dW) * wo.z > 0)) {
+                        float bp = bsdfPdf(B, ldWi(), wo);
                         float weight = miWeight(pdf, bp);
                         V3 c = mul(mul(T, val), bsdfVal) * weight;
                         const float4 sd = make_float4(dW.x, dW.y, dW.z, farT * (1 - kShadowEpsilon));
                         const float4 sc4 = make_float4(c.x, c.y, c.z, 0.0f);
                         if (REC) {
-                            sOut[0] = make_float4(p.x, p.y, p.z, 0.0f);
-                            sOut[1] = sd;
-                            sOut[2] = sc4;
+                            stashV3(wiL, stride, kRowSd, dW);
+                            wiL[(kRowSd + 3) * stride] = sd.w;
+                            stashV3(wiL, stride, kRowSc, c);
+                            asm volatile("" ::: "memory");
                         } else {
                             P.sdir[id] = sd;
                             P.scontrib[id] = sc4;
@@ -2914,16 +2952,17 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
             V3 w;
             if (mar) {
                 bpdf = 1.0f;
-                w = marschnerSampleW(B.mar, loadWi(wiL, (int) blockDim.x), GlobalTabs{B.mar}, wi, bx, by, woL, type);
+                w = marschnerSampleW(B.mar, loadWi(wiL, stride), GlobalTabs{B.mar}, ldWi(), bx, by, woL, type);
             } else {
-                w = bsdfSample(B, wi, bx, by, woL, bpdf, type);
+                w = bsdfSample(B, ldWi(), bx, by, woL, bpdf, type);
             }
             if (!isZero(w)) {
-                V3 wo = sh.toWorld(woL);
-                float woDotGeoN = dot(geo.n, wo);
+                V3 wo = ldSh().toWorld(woL);
+                float woDotGeoN = dot(ldGeoN(), wo);
                 if (!(sc.strictNormals && woDotGeoN * woL.z <= 0)) {
                     const float4 bw = make_float4(w.x, w.y, w.z, bpdf);
                     if (REC) {
+                        const V3 p = ldP();
                         cOut[0] = make_float4(p.x, p.y, p.z, ro.w); /* the Sobol index travels in .w */
                         cOut[1] = make_float4(wo.x, wo.y, wo.z, rd.w);
                         cOut[2] = bw;
@@ -2961,7 +3000,7 @@ template <bool MULTI>
 __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
                                             uint32_t *__restrict__ traceQ, uint32_t *__restrict__ shadowQ,
                                             const HptShadeIO &q) {
-    __shared__ float wiLds[HPT_WI_ROWS * HPT_SHADE_BLOCK];
+    __shared__ float wiLds[kShadeRows * HPT_SHADE_BLOCK];
     float *const wiL = wiLds + threadIdx.x;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n0 = *q.nShade;
@@ -2986,10 +3025,20 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
         shadePath<MULTI, true>(sc, P, id, P.hitS[tid], q.counters, cont, shadow, in, cOut, sOut, wiL);
     }
     qpushBlockRec<HPT_SHADE_BLOCK, 4>(cont, id, traceQ, q.nTrace, P.postRec, cOut);
+    if (shadow) { /* the shadow record from its LDS rows */
+        const V3 p = loadV3(wiL, HPT_SHADE_BLOCK, kRowP), d = loadV3(wiL, HPT_SHADE_BLOCK, kRowSd);
+        const V3 c = loadV3(wiL, HPT_SHADE_BLOCK, kRowSc);
+        sOut[0] = make_float4(p.x, p.y, p.z, 0.0f);
+        sOut[1] = make_float4(d.x, d.y, d.z, wiL[(kRowSd + 3) * HPT_SHADE_BLOCK]);
+        sOut[2] = make_float4(c.x, c.y, c.z, 0.0f);
+    }
     qpushBlockRec<HPT_SHADE_BLOCK, 3>(shadow, id, shadowQ, q.nShadow, P.shadowRec, sOut);
 }
 #ifndef HPT_SHADE_WAVES
-#define HPT_SHADE_WAVES 0 /* 0: natural allocation (100 VGPRs = 5 waves/SIMD) */
+/* 6: 72 VGPRs with the shading frame, wi and the shadow record in LDS (25 rows, 25.6 KB per block:
+   six blocks fill the CU's LDS); 0: natural allocation (87 VGPRs = 5 waves/SIMD).
+   Measured: k_shade 15.55 -> 15.14 ms per frame (C3) */
+#define HPT_SHADE_WAVES 6
 #endif
 #if HPT_SHADE_WAVES > 0
 #define HPT_SHADE_OCCUPANCY __attribute__((amdgpu_waves_per_eu(HPT_SHADE_WAVES)))
