@@ -335,7 +335,9 @@ def main():
                          "frac_hbm": round(traffic / (ms_trace / max(1, launches)) * 1e-6 / HBM_PEAK_GBS, 4)
                          if traffic else None,
                          "algorithmic_model": "SURVEY.md 8(d): 8 B per binary kd-node visit, 4+52 B per primitive "
-                                              "test, ray I/O 52 (closest) / 36 (+48 unoccluded) B",
+                                              "test, ray I/O 52 (closest) / 36 (+48 unoccluded) B; the closest "
+                                              "ray's hit record is priced at 8(d)'s 16 B (segment, t, root), "
+                                              "while the product writes a 4-B hit word",
                          "algorithmic_bytes_per_launch": int(bytes_alg // max(1, launches)),
                          "achieved_layout": round(achieved_lay, 1),
                          "layout_bytes_per_launch": int(bytes_lay // max(1, launches)),
