@@ -25,6 +25,8 @@ for spec in "$@"; do
       --title "r05 $cfg: rocprofv3 summary of bench.py --config $cfg --steps $steps --warmup 1" \
       --json "$ROOT/profiles/traffic_${cfg}.json" --workload "$WL" > /dev/null || exit 1
   cp "$ROOT/profiles/traffic_${cfg}.json" "$ROOT/gpurun_out/r05cfg/traffic_${cfg}.json" || exit 1
+  # the databases stay on the box (gpurun merges at most 64 MiB back): the summary has what is kept
+  rm -rf "$OUT/trace" "$OUT/fetch" "$OUT/write" "$ROOT/gpurun_out/pmc_r05_$cfg"
   echo "== $cfg bench with cpu_baseline"
   timeout -k 10 600 python3 -u "$ROOT/bench.py" --config $cfg --steps $steps --warmup 1 --cpu-spp $cspp \
       > "$ROOT/gpurun_out/r05cfg/r05_bench_${cfg}.json" 2> "$ROOT/gpurun_out/r05cfg/r05_bench_${cfg}.err" || exit 1

@@ -38,6 +38,10 @@ def pmc_summary(d):
         for kn, ctr, val in db.execute("select kernel_name, counter_name, sum(value) from counters_collection "
                                        "group by kernel_name, counter_name"):
             sums.setdefault(kn, {})[ctr] = val
+        # the kernel's summed launch durations (ns) in the pass that counted SQ_INSTS_SALU
+        for kn, dur in db.execute("select kernel_name, sum(duration) from counters_collection "
+                                  "where counter_name='SQ_INSTS_SALU' group by kernel_name"):
+            sums.setdefault(kn, {})["_salu_pass_ns"] = dur
     out = {}
     for kn, c in sums.items():
         cyc = c.get("SQ_WAVE_CYCLES")
@@ -54,6 +58,12 @@ def pmc_summary(d):
         if waves:
             r["vmem_per_wave"] = c.get("SQ_INSTS_VMEM_RD", 0) / waves
             r["lds_per_wave"] = c.get("SQ_INSTS_LDS", 0) / waves
+            r["salu_per_wave"] = c.get("SQ_INSTS_SALU", 0) / waves
+            r["valu_per_wave"] = c.get("SQ_INSTS_VALU", 0) / waves
+        if c.get("_salu_pass_ns"):
+            # the CU's one scalar unit issues at most one instruction per cycle (MI355X_MICROARCH.md:
+            # 4 SIMDs, 1 scalar unit per CU): SALU instructions per CU-cycle at 2.4 GHz over 256 CUs
+            r["salu_issue"] = c.get("SQ_INSTS_SALU", 0) / (c["_salu_pass_ns"] * 2.4 * 256)
         r["counters"] = c
         out[kn] = r
     return out
@@ -109,16 +119,19 @@ def main():
                   "SQ_WAVE_CYCLES (wave-cycles parked on a dependency, mostly memory), valu = "
                   "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES, inst-wait = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES, "
                   "L2 hit = TCC_HIT / (TCC_HIT + TCC_MISS), L1 miss to L2 = TCP_TCC_READ_REQ / "
-                  "TCP_TOTAL_CACHE_ACCESSES.", "",
-                  "| kernel | wait | inst-wait | valu | L2 hit | L1->L2 reads | VMEM rd / wave | LDS inst / wave |",
-                  "|---|---:|---:|---:|---:|---:|---:|---:|"]
+                  "TCP_TOTAL_CACHE_ACCESSES, SALU issue = SQ_INSTS_SALU per CU-cycle (2.4 GHz, 256 CUs; the "
+                  "CU's one scalar unit issues at most one per cycle).", "",
+                  "| kernel | wait | inst-wait | valu | L2 hit | L1->L2 reads | VMEM rd / wave | LDS inst / wave "
+                  "| SALU inst / wave | VALU inst / wave | SALU issue |",
+                  "|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|---:|"]
         for kn in ("k_trace", "k_trace_packet", "k_shade", "k_post", "k_tail", "k_camera", "k_primary"):
             v = pmc.get(kn)
             if not v:
                 continue
-            lines.append("| %s | %s | %s | %s | %s | %s | %s | %s |" % (
+            lines.append("| %s | %s | %s | %s | %s | %s | %s | %s | %s | %s | %s |" % (
                 kn, fmt(v.get("wait")), fmt(v.get("inst_wait")), fmt(v.get("valu")), fmt(v.get("l2_hit")),
-                fmt(v.get("l1_miss")), fmt(v.get("vmem_per_wave"), 0), fmt(v.get("lds_per_wave"), 0)))
+                fmt(v.get("l1_miss")), fmt(v.get("vmem_per_wave"), 0), fmt(v.get("lds_per_wave"), 0),
+                fmt(v.get("salu_per_wave"), 0), fmt(v.get("valu_per_wave"), 0), fmt(v.get("salu_issue"))))
     open(a.out, "w").write("\n".join(lines) + "\n")
     if a.json:
         import json
