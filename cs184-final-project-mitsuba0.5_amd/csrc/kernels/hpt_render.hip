@@ -1013,14 +1013,17 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
 #ifdef __HIP_DEVICE_COMPILE__
     /* the tree is read-only for the launch and every fetch address is wave-uniform:
        constant-address-space reads let the compiler issue scalar loads */
-    typedef const __attribute__((address_space(4))) uint32_t *CU32;
-    typedef const __attribute__((address_space(4))) float *CF32;
-    const CU32 nodeW = (CU32) sc.nodes;
-    const CF32 leafW = (CF32) sc.leafF;
-    auto nodes = [&](uint32_t i) { return HptNode{nodeW[2 * i], nodeW[2 * i + 1]}; };
-    auto leaf = [&](uint32_t i) {
-        return make_float4(leafW[4 * i], leafW[4 * i + 1], leafW[4 * i + 2], leafW[4 * i + 3]);
+    typedef const __attribute__((address_space(4))) char *CB;
+    typedef const __attribute__((address_space(4))) uint2 *CU2;
+    typedef const __attribute__((address_space(4))) float4 *CF4;
+    const CB nodeB = (CB) sc.nodes, leafB = (CB) sc.leafF;
+    /* 32-bit byte offsets (the tree's arrays are far below 4 GB): the scalar loads take them
+       as an SGPR offset instead of a 64-bit address add per fetch */
+    auto nodes = [&](uint32_t i) {
+        const uint2 v = *(CU2) (nodeB + (uint64_t) (i << 3));
+        return HptNode{v.x, v.y};
     };
+    auto leaf = [&](uint32_t i) { return *(CF4) (leafB + (uint64_t) (i << 4)); };
 #else
     const HptNode *__restrict__ nodeP = sc.nodes;
     const float4 *__restrict__ leafP = reinterpret_cast<const float4 *>(sc.leafF);
@@ -1035,10 +1038,14 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
     uint32_t node = 0;
     int sp = 0;
     uint32_t steps = 0;
+    /* the lane's "found" as a 0/1 word in a vector register: a bool carried around the loop is a
+       lane mask the compiler re-merges with exec on every iteration (three scalar instructions) */
+    uint32_t found = r.found ? 1u : 0u;
     while (true) {
-        /* ---- descend to a leaf ---- */
-        HptNode nd = nodes(node);
-        while (!(nd.w0 & 0x80000000u)) {
+        /* one node per iteration (a flat loop: the node fetch is the loop's only one) */
+        const HptNode nd = nodes(node);
+        if (!(nd.w0 & 0x80000000u)) {
+            /* ---- an inner node: descend ---- */
             const bool me = laneIn(act);
             if (STATS) {
                 tc.nodes += me ? 1u : 0u;
@@ -1052,11 +1059,11 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
             const float ts = (split - oa) * ra;
             /* every lane's decisions as wave masks: one compare each, the logic on scalar masks
                (the same predicates as traceRound's: below, near only, far only, both) */
-            const uint64_t mBelowAll = __builtin_amdgcn_ballot_w64(oa < split) |
-                                       (__builtin_amdgcn_ballot_w64(oa == split) & __builtin_amdgcn_ballot_w64(da <= 0.0f));
             const uint64_t mNearAll = ~__builtin_amdgcn_ballot_w64(ts <= r.tmax) | __builtin_amdgcn_ballot_w64(ts <= 0.0f);
             const uint64_t mFarAll = ~mNearAll & __builtin_amdgcn_ballot_w64(ts < r.tmin);
             const uint64_t mBothAll = ~(mNearAll | mFarAll);
+            const uint64_t mBelowAll = __builtin_amdgcn_ballot_w64(oa < split) |
+                                       (__builtin_amdgcn_ballot_w64(oa == split) & __builtin_amdgcn_ballot_w64(da <= 0.0f));
             const uint64_t mBelow = mBelowAll & act;
             if (mBelow != 0 && mBelow != act) {
                 /* the lanes disagree on the front-to-back order: the others revisit this node later */
@@ -1065,26 +1072,33 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
                 ++sp;
                 act = mBelow;
             }
-            const uint32_t belowG = (act & mBelow) != 0 ? 1u : 0u;
-            const uint32_t first = left + (belowG ? 0u : 1u), second = left + (belowG ? 1u : 0u);
+            /* below (all of act, or none): the first child is the left one; as integer
+               arithmetic on the mask, not a boolean (which the compiler routes through a VGPR) */
+            const uint64_t anyBelow = act & mBelow;
+#ifdef __HIP_DEVICE_COMPILE__
+            uint32_t notBelow;
+            asm("s_cmp_eq_u64 %1, 0\n\ts_cselect_b32 %0, 1, 0" : "=s"(notBelow) : "s"(anyBelow) : "scc");
+#else
+            const uint32_t notBelow = anyBelow == 0 ? 1u : 0u;
+#endif
+            const uint32_t first = left + notBelow, second = left + (notBelow ^ 1u);
             const uint64_t mFirst = act & ~mFarAll, mBoth = act & mBothAll, mFar = act & mFarAll;
             if (mFirst == 0) { /* nobody needs the first child (so no lane is "both") */
                 node = second;
                 act = mFar;
-                nd = nodes(node);
                 continue;
             }
             if ((mBoth | mFar) != 0) {
                 if (sp == spMax) return false;
                 const bool bothMe = laneIn(mBoth);
-                if (bothMe) L.saved[sp][lane] = r.tmax;
+                L.saved[sp][lane] = r.tmax; /* every lane: only the "both" lanes read it back */
                 if (lane == 0) L.ent[sp] = PacketEntry{second, 0u, mBoth, mFar};
                 ++sp;
-                if (bothMe) r.tmax = ts;
+                r.tmax = bothMe ? ts : r.tmax;
             }
             node = first;
             act = mFirst;
-            nd = nodes(node);
+            continue;
         }
         /* ---- leaf: the member lanes test its segments (pre-test, then exact) ---- */
         const bool me = laneIn(act);
@@ -1114,32 +1128,38 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
                         tc.prims += me ? 1u : 0u;
                         if (lane == 0) tc.primSlots += 64;
                     }
-                    if (me && segMayHit(ra[k], rb[k], o, d, sc.maxRadius)) mask |= 1u << k;
+                    /* every lane runs the pre-test (VALU is idle here) and the result is masked:
+                       no exec-mask branch around it */
+                    const bool may = segMayHit(ra[k], rb[k], o, d, sc.maxRadius);
+                    mask |= (me && may) ? 1u << k : 0u;
                 }
             }
-            while (mask) {
-                const uint32_t k = (uint32_t) (__ffs(mask) - 1);
-                mask &= mask - 1;
-                uint32_t sg = __float_as_uint(rb[0].z);
+            /* the exact tests in record order, one predicated block per record */
 #pragma unroll
-                for (uint32_t q = 1; q < HPT_PACKET_LEAF_BATCH; ++q) sg = k == q ? __float_as_uint(rb[q].z) : sg;
-                const float rad = segRadius(sc, sg);
-                const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
-                if (STATS) ++tc.exact;
-                float t;
-                uint32_t far;
-                if (segIntersect(sc.segs, sg, o, d, r2, r.mint, r.tHit, t, far)) {
-                    r.found = true;
-                    r.tHit = t;
-                    r.segHit = sg | (far << 31);
+            for (uint32_t k = 0; k < HPT_PACKET_LEAF_BATCH; ++k) {
+                if (mask & (1u << k)) {
+                    const uint32_t sg = __float_as_uint(rb[k].z);
+                    const float rad = segRadius(sc, sg);
+                    const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
+                    if (STATS) ++tc.exact;
+                    float t;
+                    uint32_t far;
+                    if (segIntersect(sc.segs, sg, o, d, r2, r.mint, r.tHit, t, far)) {
+                        found = 1u;
+                        r.tHit = t;
+                        r.segHit = sg | (far << 31);
+                    }
                 }
             }
         }
-        done |= __ballot(me && r.found && r.tHit <= r.tmax);
+        done |= __ballot(me && found != 0u && r.tHit <= r.tmax);
         if (++steps > (1u << 20)) return false; /* malformed tree: let the lanes finish alone */
         /* ---- pop the next subtree some unfinished lane needs ---- */
         while (true) {
-            if (sp == 0) return true;
+            if (sp == 0) {
+                r.found = found != 0u;
+                return true;
+            }
             --sp;
             const PacketEntry en = L.ent[sp];
             const uint64_t enBoth = uniform64(en.mBoth), enFar = uniform64(en.mFar);
@@ -1148,10 +1168,10 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
                 act = enBoth & ~done;
             } else {
                 const bool inB = laneIn(enBoth & ~done);
-                if (inB) {
-                    r.tmin = r.tmax;
-                    r.tmax = L.saved[sp][lane];
-                }
+                /* every lane reads its saved row; the "both" lanes take it (selects, no exec branch) */
+                const float sv = L.saved[sp][lane];
+                r.tmin = inB ? r.tmax : r.tmin;
+                r.tmax = inB ? sv : r.tmax;
                 done |= __ballot(inB && r.tmin > r.tHit);
                 act = (enBoth | enFar) & ~done;
             }
