@@ -972,53 +972,62 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
    Havran traversal (sahkdtree3.h:178-308) would enter.  At a split every
    member lane computes its own t and near/far/both decision exactly as
    traceRound does; the packet enters the first child if any lane needs it
-   and stacks the second child with the masks of the lanes that need it
-   ("both" lanes also stack their own tmax).  Lanes that disagree on the
-   front-to-back order split the packet (the second group revisits the node
-   later).  A lane therefore tests the same leaves in the same order with
-   the same intervals as its own traversal, and its result is bit-identical.
-   A packet whose stack would overflow finishes lane by lane (traceRound). */
+   and stacks the second child for the lanes that need it ("both" lanes also
+   stack their own tmax).  Lanes that disagree on the front-to-back order
+   split the packet (the second group revisits the node later).  A lane
+   therefore tests the same leaves in the same order with the same intervals
+   as its own traversal, and its result is bit-identical.  A packet whose
+   stack would overflow finishes lane by lane (traceRound). */
 #ifndef HPT_PACKET_LEAF_BATCH
 #define HPT_PACKET_LEAF_BATCH 2 /* leaf records per round trip in the packet traversal: 1 / 2 / 4 / 6 gave 30.98 / 29.53 / 30.54 / 30.55 ms per headline frame */
 #endif
 #ifndef HPT_PACKET_STACK
-#define HPT_PACKET_STACK 23 /* 6.4 KB of LDS per wave: 6 waves/SIMD fit the 160 KB (24 entries did not) */
+#define HPT_PACKET_STACK 22 /* 5.5 KB of LDS per wave: 7 waves/SIMD fit the 160 KB (no packet overflowed at the headline) */
 #endif
-struct PacketEntry {
-    uint32_t node, revisit;
-    uint64_t mBoth, mFar; /* lanes that stacked their tmax / that skipped the first child */
-};
 struct PacketLds {
-    PacketEntry ent[HPT_PACKET_STACK];
-    float saved[HPT_PACKET_STACK][64];
+    float saved[HPT_PACKET_STACK][64]; /* entry e: one word per lane (tracePacket) */
 };
-static_assert(sizeof(PacketLds) >= sizeof(uint2) * (8 + HPT_RAY_ROWS) * 64,
-              "the fallback ring stack reuses the packet stack's LDS");
+/* the batch entry point's per-lane fallback (tracePackets INLINE) puts an 8-entry ring stack and
+   the ray rows in the packet's LDS: there it is declared with room for them */
+union PacketLdsInline {
+    PacketLds p;
+    uint2 ring[(8 + HPT_RAY_ROWS) * 64];
+};
 
-/* a wave-uniform 64-bit value into scalar registers (readfirstlane returns a
-   signed int: widen through uint32_t, or lane 31's bit would smear upwards) */
-HD uint64_t uniform64(uint64_t v) {
-    return (uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) v) |
-           ((uint64_t) (uint32_t) __builtin_amdgcn_readfirstlane((uint32_t) (v >> 32)) << 32);
+/* The per-lane state lives in vector registers: a lane's "active", "done" and "found" are 0/1
+   words, not lane masks, so their logic runs on the SIMDs' VALUs and not on the CU's one scalar
+   unit (with wave masks the packet pass saturated it: SALU issue 0.85 at 24 waves per CU,
+   profiles/r05_furball_marschner_kernels.md); a wave-uniform decision is one ballot of a word,
+   compared with zero.  The stack keeps each entry's node in one lane of a vector register
+   (lane e = entry e, bit 31 = revisit) and one LDS word per lane: the lane's saved tmax when it
+   was "both" (any bit pattern below HPT_PK_FAR), HPT_PK_FAR when it skipped the first child,
+   HPT_PK_OUT when it is not in the entry, and for a revisit entry HPT_PK_IN / HPT_PK_OUT. */
+#define HPT_PK_FAR 0xFFFFFFFDu
+#define HPT_PK_IN 0xFFFFFFFEu
+#define HPT_PK_OUT 0xFFFFFFFFu
+HD uint32_t pkWord(uint32_t x) { /* keep a 0/1 word a word (not folded back into a lane mask) */
+#ifdef __HIP_DEVICE_COMPILE__
+    asm("" : "+v"(x));
+#endif
+    return x;
 }
+HD uint32_t pkFlag(bool b) { return pkWord(b ? 1u : 0u); }
+HD bool pkAny(uint32_t x) { return __builtin_amdgcn_ballot_w64(x != 0u) != 0; }
 
-/* this lane's bit of a wave-uniform lane mask: v_cndmask on the mask itself
-   (no lane index or 64-bit shift kept in vector registers) */
-HD bool laneIn(uint64_t mask) { return __builtin_amdgcn_inverse_ballot_w64(mask); }
-
-/* returns false when the packet stack overflowed (the caller then traces each lane alone) */
+#define PK_OVERFLOW \
+    status = 2;     \
+    continue
+#define PK_DONE \
+    status = 1; \
+    break
 template <bool STATS>
 HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, TraceCounters &tc) {
     const uint32_t lane = __lane_id();
 #ifdef __HIP_DEVICE_COMPILE__
-    /* the tree is read-only for the launch and every fetch address is wave-uniform:
-       constant-address-space reads let the compiler issue scalar loads */
     typedef const __attribute__((address_space(4))) char *CB;
     typedef const __attribute__((address_space(4))) uint2 *CU2;
     typedef const __attribute__((address_space(4))) float4 *CF4;
     const CB nodeB = (CB) sc.nodes, leafB = (CB) sc.leafF;
-    /* 32-bit byte offsets (the tree's arrays are far below 4 GB): the scalar loads take them
-       as an SGPR offset instead of a 64-bit address add per fetch */
     auto nodes = [&](uint32_t i) {
         const uint2 v = *(CU2) (nodeB + (uint64_t) (i << 3));
         return HptNode{v.x, v.y};
@@ -1030,25 +1039,24 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
     auto nodes = [&](uint32_t i) { return nodeP[i]; };
     auto leaf = [&](uint32_t i) { return leafP[i]; };
 #endif
+    uint32_t *const row = reinterpret_cast<uint32_t *>(&L.saved[0][0]) + lane; /* entry e at row[64 * e] */
     const V3 o = r.o, d = r.d, rcp = r.rcp;
     const int spMax = sc.packetStack ? min((int) sc.packetStack, HPT_PACKET_STACK) : HPT_PACKET_STACK;
-    uint64_t done = ~__ballot(valid);
-    uint64_t act = ~done;
-    if (act == 0) return true;
+    uint32_t act = pkFlag(valid), done = pkFlag(!valid);
+    if (!pkAny(act)) return true;
+    uint32_t found = pkFlag(r.found);
+    uint32_t stackNode = 0; /* lane e: entry e's node | revisit << 31 */
     uint32_t node = 0;
     int sp = 0;
     uint32_t steps = 0;
-    /* the lane's "found" as a 0/1 word in a vector register: a bool carried around the loop is a
-       lane mask the compiler re-merges with exec on every iteration (three scalar instructions) */
-    uint32_t found = r.found ? 1u : 0u;
-    while (true) {
-        /* one node per iteration (a flat loop: the node fetch is the loop's only one) */
+    int status = 0; /* 0 running, 1 every lane done, 2 stack overflow / malformed tree */
+    auto pushNode = [&](uint32_t v) { stackNode = (int) lane == sp ? v : stackNode; };
+    while (status == 0) {
         const HptNode nd = nodes(node);
         if (!(nd.w0 & 0x80000000u)) {
-            /* ---- an inner node: descend ---- */
-            const bool me = laneIn(act);
+            /* ---- an inner node ---- */
             if (STATS) {
-                tc.nodes += me ? 1u : 0u;
+                tc.nodes += act;
                 if (lane == 0) tc.nodeSlots += 64;
             }
             const uint32_t axis = nd.w0 & 3u, left = nd.w0 >> 2;
@@ -1057,60 +1065,49 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
             const float da = axis == 0 ? d.x : (axis == 1 ? d.y : d.z);
             const float ra = axis == 0 ? rcp.x : (axis == 1 ? rcp.y : rcp.z);
             const float ts = (split - oa) * ra;
-            /* every lane's decisions as wave masks: one compare each, the logic on scalar masks
-               (the same predicates as traceRound's: below, near only, far only, both) */
-            const uint64_t mNearAll = ~__builtin_amdgcn_ballot_w64(ts <= r.tmax) | __builtin_amdgcn_ballot_w64(ts <= 0.0f);
-            const uint64_t mFarAll = ~mNearAll & __builtin_amdgcn_ballot_w64(ts < r.tmin);
-            const uint64_t mBothAll = ~(mNearAll | mFarAll);
-            const uint64_t mBelowAll = __builtin_amdgcn_ballot_w64(oa < split) |
-                                       (__builtin_amdgcn_ballot_w64(oa == split) & __builtin_amdgcn_ballot_w64(da <= 0.0f));
-            const uint64_t mBelow = mBelowAll & act;
-            if (mBelow != 0 && mBelow != act) {
+            const uint32_t below = pkFlag(oa < split) | (pkFlag(oa == split) & pkFlag(da <= 0.0f));
+            const uint32_t nearOnly = pkFlag(!(ts <= r.tmax)) | pkFlag(ts <= 0.0f);
+            const uint32_t farOnly = (nearOnly ^ 1u) & pkFlag(ts < r.tmin);
+            const uint32_t both = (nearOnly | farOnly) ^ 1u;
+            const bool belowG = pkAny(act & below);
+            if (belowG && pkAny(act & (below ^ 1u))) {
                 /* the lanes disagree on the front-to-back order: the others revisit this node later */
-                if (sp == spMax) return false;
-                if (lane == 0) L.ent[sp] = PacketEntry{node, 1u, act & ~mBelow, 0ull};
+                if (sp == spMax) {
+                    PK_OVERFLOW;
+                }
+                row[64 * sp] = (act & (below ^ 1u)) ? HPT_PK_IN : HPT_PK_OUT;
+                pushNode(node | 0x80000000u);
                 ++sp;
-                act = mBelow;
+                act &= below;
             }
-            /* below (all of act, or none): the first child is the left one; as integer
-               arithmetic on the mask, not a boolean (which the compiler routes through a VGPR) */
-            const uint64_t anyBelow = act & mBelow;
-#ifdef __HIP_DEVICE_COMPILE__
-            uint32_t notBelow;
-            asm("s_cmp_eq_u64 %1, 0\n\ts_cselect_b32 %0, 1, 0" : "=s"(notBelow) : "s"(anyBelow) : "scc");
-#else
-            const uint32_t notBelow = anyBelow == 0 ? 1u : 0u;
-#endif
-            const uint32_t first = left + notBelow, second = left + (notBelow ^ 1u);
-            const uint64_t mFirst = act & ~mFarAll, mBoth = act & mBothAll, mFar = act & mFarAll;
-            if (mFirst == 0) { /* nobody needs the first child (so no lane is "both") */
+            const uint32_t first = left + (belowG ? 0u : 1u), second = left + (belowG ? 1u : 0u);
+            const uint32_t needFirst = act & (farOnly ^ 1u);
+            if (!pkAny(needFirst)) { /* nobody needs the first child (so no lane is "both") */
                 node = second;
-                act = mFar;
+                act &= farOnly;
                 continue;
             }
-            if ((mBoth | mFar) != 0) {
-                if (sp == spMax) return false;
-                const bool bothMe = laneIn(mBoth);
-                L.saved[sp][lane] = r.tmax; /* every lane: only the "both" lanes read it back */
-                if (lane == 0) L.ent[sp] = PacketEntry{second, 0u, mBoth, mFar};
+            if (pkAny(act & (farOnly | both))) {
+                if (sp == spMax) {
+                    PK_OVERFLOW;
+                }
+                const uint32_t bMe = act & both;
+                row[64 * sp] = bMe ? __float_as_uint(r.tmax) : ((act & farOnly) ? HPT_PK_FAR : HPT_PK_OUT);
+                pushNode(second);
                 ++sp;
-                r.tmax = bothMe ? ts : r.tmax;
+                r.tmax = bMe ? ts : r.tmax;
             }
             node = first;
-            act = mFirst;
+            act = needFirst;
             continue;
         }
         /* ---- leaf: the member lanes test its segments (pre-test, then exact) ---- */
-        const bool me = laneIn(act);
+        const bool me = act != 0u;
         if (STATS) {
-            tc.nodes += me ? 1u : 0u;
+            tc.nodes += act;
             if (lane == 0) tc.nodeSlots += 64;
         }
         const uint32_t lf = nd.w0 & 0x7fffffffu, ll = nd.w1;
-        /* HPT_PACKET_LEAF_BATCH records per round trip (wave-uniform scalar loads issued
-           together), pre-test into a candidate mask, then the exact tests in record order:
-           the same tests in the same order as one record at a time (the pre-test does not
-           read tHit), so the hits are identical */
         for (uint32_t c0 = lf; c0 < ll; c0 += HPT_PACKET_LEAF_BATCH) {
             const uint32_t n = min(ll - c0, (uint32_t) HPT_PACKET_LEAF_BATCH);
             float4 ra[HPT_PACKET_LEAF_BATCH], rb[HPT_PACKET_LEAF_BATCH];
@@ -1125,16 +1122,13 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
             for (uint32_t k = 0; k < HPT_PACKET_LEAF_BATCH; ++k) {
                 if (k < n) {
                     if (STATS) {
-                        tc.prims += me ? 1u : 0u;
+                        tc.prims += act;
                         if (lane == 0) tc.primSlots += 64;
                     }
-                    /* every lane runs the pre-test (VALU is idle here) and the result is masked:
-                       no exec-mask branch around it */
                     const bool may = segMayHit(ra[k], rb[k], o, d, sc.maxRadius);
                     mask |= (me && may) ? 1u << k : 0u;
                 }
             }
-            /* the exact tests in record order, one predicated block per record */
 #pragma unroll
             for (uint32_t k = 0; k < HPT_PACKET_LEAF_BATCH; ++k) {
                 if (mask & (1u << k)) {
@@ -1152,35 +1146,36 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
                 }
             }
         }
-        done |= __ballot(me && found != 0u && r.tHit <= r.tmax);
-        if (++steps > (1u << 20)) return false; /* malformed tree: let the lanes finish alone */
+        done |= act & found & pkFlag(r.tHit <= r.tmax);
+        if (++steps > (1u << 20)) { /* malformed tree: let the lanes finish alone */
+            PK_OVERFLOW;
+        }
         /* ---- pop the next subtree some unfinished lane needs ---- */
         while (true) {
             if (sp == 0) {
-                r.found = found != 0u;
-                return true;
+                PK_DONE;
             }
             --sp;
-            const PacketEntry en = L.ent[sp];
-            const uint64_t enBoth = uniform64(en.mBoth), enFar = uniform64(en.mFar);
-            const uint32_t enNode = (uint32_t) __builtin_amdgcn_readfirstlane(en.node);
-            if (__builtin_amdgcn_readfirstlane(en.revisit)) {
-                act = enBoth & ~done;
+            const uint32_t en = (uint32_t) __builtin_amdgcn_readlane((int) stackNode, sp);
+            const uint32_t w = row[64 * sp];
+            const uint32_t live = done ^ 1u;
+            if (en & 0x80000000u) {
+                act = pkFlag(w == HPT_PK_IN) & live;
             } else {
-                const bool inB = laneIn(enBoth & ~done);
-                /* every lane reads its saved row; the "both" lanes take it (selects, no exec branch) */
-                const float sv = L.saved[sp][lane];
+                const uint32_t inB = pkFlag(w < HPT_PK_FAR) & live;
                 r.tmin = inB ? r.tmax : r.tmin;
-                r.tmax = inB ? sv : r.tmax;
-                done |= __ballot(inB && r.tmin > r.tHit);
-                act = (enBoth | enFar) & ~done;
+                r.tmax = inB ? __uint_as_float(w) : r.tmax;
+                done |= inB & pkFlag(r.tmin > r.tHit);
+                act = pkFlag(w <= HPT_PK_FAR) & (done ^ 1u);
             }
-            if (act != 0) {
-                node = enNode;
+            if (pkAny(act)) {
+                node = en & 0x7fffffffu;
                 break;
             }
         }
     }
+    r.found = found != 0u;
+    return status == 1;
 }
 
 /* Persistent packet tracer: each wave claims 64 consecutive closest-hit rays
@@ -2767,7 +2762,7 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_camera_cou
 
 /* k_trace_packet: the camera pass's closest-hit rays as 64-ray packets */
 #ifndef HPT_PACKET_WAVES
-#define HPT_PACKET_WAVES 6 /* 34.6 -> 32.9 ms per frame vs 5 (spills only in the per-packet prologue) */
+#define HPT_PACKET_WAVES 7 /* 72 VGPRs (3 spilled outside the node loop): 19.7 -> 18.7 ms per frame vs 6 */
 #endif
 #ifndef HPT_PACKET_BLOCK
 #define HPT_PACKET_BLOCK HPT_TRACE_BLOCK
@@ -3521,10 +3516,10 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptS
                                                                             float *outP, uint8_t *outHit,
                                                                             uint32_t *cursor) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    __shared__ PacketLds lds[HPT_TRACE_BLOCK / 64];
+    __shared__ PacketLdsInline lds[HPT_TRACE_BLOCK / 64];
     BatchIO io{o, d, mint, maxt, outT, outP, outSeg, outHit, (uint32_t) n, (flags & 1) != 0, 0u};
     if ((flags & 4) && !(flags & 1))
-        tracePackets<false, true>(sc, io, cursor, lds[threadIdx.x >> 6], nullptr);
+        tracePackets<false, true>(sc, io, cursor, lds[threadIdx.x >> 6].p, nullptr);
     else if (flags & 2)
         tracePersistent<2, false>(sc, io, cursor, stk + threadIdx.x, nullptr);
     else if (flags & 8)
