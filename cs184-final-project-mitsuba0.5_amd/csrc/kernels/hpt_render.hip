@@ -2426,8 +2426,8 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
         P.rd[id] = make_float4(dw.x, dw.y, dw.z, maxt);
         P.pos[id] = make_float2(posx, posy);
         P.sobol[id] = sidx;
-        P.state[id] = hptState(0u, 1u, 2u); /* dim = 2, depth = 1 */
-        P.thr[id] = make_float4(1.0f, 1.0f, 1.0f, 0.0f);
+        /* a camera path's throughput (1) and state (dim 2, depth 1) are the same for every path:
+           k_primary writes them into its shade record, none goes through HBM here */
         P.li[id] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     } else if (id < w.nPaths) {
         P.state[id] = 0xffffffffu; /* outside the image */
@@ -2832,12 +2832,13 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
         seg = P.hitQ[tid];
         if (seg != HPT_MISS) {
             alive = true;
-            /* the shade record (hpt_kernels.h): the camera ray, its Sobol index, throughput 1, state */
-            const float4 ro = P.ro[id], rd = P.rd[id], thr = P.thr[id];
+            /* the shade record (hpt_kernels.h): the camera ray, its Sobol index, throughput 1 and
+               the camera state (dim = 2, depth = 1) */
+            const float4 ro = P.ro[id], rd = P.rd[id];
             const uint64_t sidx = P.sobol[id];
             sOut[0] = make_float4(ro.x, ro.y, ro.z, __uint_as_float((uint32_t) sidx));
             sOut[1] = make_float4(rd.x, rd.y, rd.z, __uint_as_float((uint32_t) (sidx >> 32)));
-            sOut[2] = make_float4(thr.x, thr.y, thr.z, __uint_as_float(P.state[id]));
+            sOut[2] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(hptState(0u, 1u, 2u)));
         } else if (!sc.hideEmitters) {
             /* a camera ray keeps its differentials: EWA-filtered lookup (envmap.cpp:394-406) */
             const float4 rd = P.rd[id];
