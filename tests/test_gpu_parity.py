@@ -200,6 +200,26 @@ def test_packet_trace_bit_exact(fixture, request):
         np.testing.assert_array_equal(gp, op)
 
 
+def test_packet_trace_inline_fallback_bit_exact(furball):
+    """The batch entry point finishes an overflowing packet lane by lane inside the kernel
+    (tracePackets INLINE: the ring stack and ray rows in the packet's LDS, declared with room
+    for them, PacketLdsInline).  With the packet stack limited to 1 and 3 entries most packets
+    overflow; every lane's hit must still equal the oracle's Havran traversal."""
+    _, r, o = furball
+    orig, dirs, mint, maxt = _packet_rays(r, 600, 14, 3e-3)
+    ot, oiv, op = o.trace(orig, dirs, mint, maxt)
+    assert (oiv >= 0).sum() > 500
+    try:
+        for entries in (1, 3):
+            r.set_packet_stack(entries)
+            gt, giv, gp = r.trace(orig, dirs, mint, maxt, packet=True)
+            np.testing.assert_array_equal(giv, oiv)
+            np.testing.assert_array_equal(gt, ot)
+            np.testing.assert_array_equal(gp, op)
+    finally:
+        r.set_packet_stack(0)
+
+
 @pytest.fixture(scope="module")
 def haircurl():
     """models/hair-curl: four hair shapes with their own roughplastic BSDFs
