@@ -979,10 +979,14 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
    as its own traversal, and its result is bit-identical.  A packet whose
    stack would overflow finishes lane by lane (traceRound). */
 #ifndef HPT_PACKET_LEAF_BATCH
-#define HPT_PACKET_LEAF_BATCH 2 /* leaf records per round trip in the packet traversal: 1 / 2 / 4 / 6 gave 30.98 / 29.53 / 30.54 / 30.55 ms per headline frame */
+/* leaf records per round trip in the packet traversal.  Round 3 (mask kernel): 1 / 2 / 4 / 6 gave
+   30.98 / 29.53 / 30.54 / 30.55 ms per headline frame; round 5 (lane words): 1 / 2 / 3 / 4 gave
+   17.71 / 18.65 / 18.54 / 18.86 ms at 7 waves, and one record per trip needs 63 VGPRs, which lets
+   the kernel run 8 waves/SIMD (17.08 ms) */
+#define HPT_PACKET_LEAF_BATCH 1
 #endif
 #ifndef HPT_PACKET_STACK
-#define HPT_PACKET_STACK 22 /* 5.5 KB of LDS per wave: 7 waves/SIMD fit the 160 KB (no packet overflowed at the headline) */
+#define HPT_PACKET_STACK 20 /* 5 KB of LDS per wave: 8 waves/SIMD fit the 160 KB (no packet overflowed at the headline) */
 #endif
 struct PacketLds {
     float saved[HPT_PACKET_STACK][64]; /* entry e: one word per lane (tracePacket) */
@@ -2762,7 +2766,7 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_camera_cou
 
 /* k_trace_packet: the camera pass's closest-hit rays as 64-ray packets */
 #ifndef HPT_PACKET_WAVES
-#define HPT_PACKET_WAVES 7 /* 72 VGPRs (3 spilled outside the node loop): 19.7 -> 18.7 ms per frame vs 6 */
+#define HPT_PACKET_WAVES 8 /* 63 VGPRs, no spills (one leaf record per trip): 17.1 ms per frame (7 waves: 17.7) */
 #endif
 #ifndef HPT_PACKET_BLOCK
 #define HPT_PACKET_BLOCK HPT_TRACE_BLOCK
