@@ -1181,6 +1181,8 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
     r.found = found != 0u;
     return status == 1;
 }
+#undef PK_OVERFLOW
+#undef PK_DONE
 
 /* Persistent packet tracer: each wave claims 64 consecutive closest-hit rays
    (the camera queue keeps a pixel's samples together), traces them as one
