@@ -178,6 +178,8 @@ struct KDTreeHost {
     std::vector<uint32_t> prims;          /* segment index per leaf entry */
     std::vector<HptSegment> segs;         /* per segment (index = segment id) */
     std::vector<HptSegF> leafF;           /* fp32 pre-test records in leaf (prims) order */
+    std::vector<HptSegQ> leafQ;           /* the same as 16-byte records (quantised axis) */
+    float preRadius = 0.0f;               /* pre-test radius bound for leafQ (HptSegQ) */
     std::vector<HptNode4> nodes4;         /* two-level nodes for the device traversal */
     std::vector<uint32_t> leafTable;      /* (start, end) of leaves too large for an inline ref */
     std::vector<uint32_t> segFirstVertex; /* segment id -> first vertex index */

@@ -570,6 +570,55 @@ void buildNode4(const BNode *root, KDTreeHost &t) {
     if (t.leafTable.empty()) t.leafTable.push_back(0), t.leafTable.push_back(0);
 }
 
+/* HptSegQ's axis: oct encoding (16:16) of the fp64 axis, and its decode with the device's fp32
+   operations (axisOctDecode in hpt_render.hip) */
+uint32_t axisOctEncode(const double a[3]) {
+    const double l1 = std::fabs(a[0]) + std::fabs(a[1]) + std::fabs(a[2]);
+    double u = a[0] / l1, v = a[1] / l1;
+    if (a[2] < 0.0) {
+        const double fu = (1.0 - std::fabs(v)) * (u >= 0.0 ? 1.0 : -1.0);
+        const double fv = (1.0 - std::fabs(u)) * (v >= 0.0 ? 1.0 : -1.0);
+        u = fu, v = fv;
+    }
+    auto q = [](double x) {
+        return (uint32_t) std::min(65535.0, std::max(0.0, std::nearbyint((x * 0.5 + 0.5) * 65535.0)));
+    };
+    return q(u) | (q(v) << 16);
+}
+void axisOctDecode(uint32_t q, float &x, float &y, float &z) {
+    const float u = (float) (q & 0xffffu) * (2.0f / 65535.0f) - 1.0f;
+    const float v = (float) (q >> 16) * (2.0f / 65535.0f) - 1.0f;
+    z = 1.0f - std::fabs(u) - std::fabs(v);
+    x = u;
+    y = v;
+    if (z < 0.0f) {
+        x = (1.0f - std::fabs(v)) * (u >= 0.0f ? 1.0f : -1.0f);
+        y = (1.0f - std::fabs(u)) * (v >= 0.0f ? 1.0f : -1.0f);
+    }
+}
+
+/* the radius bound that keeps the quantised-axis pre-test conservative: a point the exact test
+   accepts lies within r of the axis line at an axial offset s from v1, s in [-r tan(phi1),
+   len + r tan(phi2)] (phi = the angle between the axis and a miter plane's normal, hair.cpp:
+   537-541), so it lies within r + |s| sin(theta) of the quantised line through v1 (theta = the
+   angle between the two axes).  Returns r + max|s| sin(theta) for one segment. */
+double quantisedReach(const HptSegment &g, double r, float ax, float ay, float az) {
+    const double q[3] = {ax, ay, az};
+    const double ql = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
+    const double c[3] = {g.axis[1] * q[2] - g.axis[2] * q[1], g.axis[2] * q[0] - g.axis[0] * q[2],
+                         g.axis[0] * q[1] - g.axis[1] * q[0]};
+    const double sinTheta = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]) / ql;
+    auto tanOf = [](const double n[3], const double a[3]) {
+        const double cs = std::fabs(n[0] * a[0] + n[1] * a[1] + n[2] * a[2]);
+        if (cs < 1e-9) return std::numeric_limits<double>::infinity();
+        return std::sqrt(std::max(0.0, 1.0 - cs * cs)) / cs;
+    };
+    const double len = std::sqrt((g.v2[0] - g.v1[0]) * (g.v2[0] - g.v1[0]) + (g.v2[1] - g.v1[1]) * (g.v2[1] - g.v1[1]) +
+                                 (g.v2[2] - g.v1[2]) * (g.v2[2] - g.v1[2]));
+    const double reach = std::max(r * tanOf(g.n1, g.axis), len + r * tanOf(g.n2, g.axis));
+    return r + reach * sinTheta;
+}
+
 } // namespace
 
 KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
@@ -678,6 +727,26 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
         }
         f.seg = s;
         f.radius = hair.radiusOf(segIv[s]);
+    }
+    /* the 16-byte records and their radius bound (a 1e-5 relative slack covers the fp32 rounding of
+       the bound itself and of the device's decode) */
+    t.leafQ.resize(t.prims.size());
+    {
+        std::vector<double> reach(S, -1.0);
+        double preR = 0.0;
+        for (size_t e = 0; e < t.prims.size(); ++e) {
+            const uint32_t s = t.prims[e];
+            HptSegQ &q = t.leafQ[e];
+            for (int k = 0; k < 3; ++k) q.v1[k] = t.leafF[e].v1[k];
+            q.axisOct = axisOctEncode(t.segs[s].axis);
+            if (reach[s] < 0.0) {
+                float x, y, z;
+                axisOctDecode(q.axisOct, x, y, z);
+                reach[s] = quantisedReach(t.segs[s], (double) t.leafF[e].radius, x, y, z);
+                preR = std::max(preR, reach[s]);
+            }
+        }
+        t.preRadius = (float) (preR * (1.0 + 1e-5));
     }
     t.buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return t;

@@ -798,6 +798,8 @@ static int uploadScene(hpt_context *c) {
     r |= upload(c, c->tree.nodes4.data(), c->tree.nodes4.size() * sizeof(HptNode4), (const void **) &sc.nodes4);
     r |= upload(c, c->tree.leafTable.data(), c->tree.leafTable.size() * 4, (const void **) &sc.leafTable);
     r |= upload(c, c->tree.leafF.data(), c->tree.leafF.size() * sizeof(HptSegF), (const void **) &sc.leafF);
+    r |= upload(c, c->tree.leafQ.data(), c->tree.leafQ.size() * sizeof(HptSegQ), (const void **) &sc.leafQ);
+    r |= upload(c, c->tree.prims.data(), c->tree.prims.size() * 4, (const void **) &sc.leafSeg);
     r |= upload(c, c->tree.segs.data(), c->tree.segs.size() * sizeof(HptSegment), (const void **) &sc.segs);
     for (int i = 0; i < 3; ++i) {
         sc.aabbMin[i] = c->tree.aabbMin[i];
@@ -844,6 +846,7 @@ static int uploadScene(hpt_context *c) {
     sc.radius = shapes[0].radius;
     sc.maxRadius = 0.0f;
     for (const HptShape &h : shapes) sc.maxRadius = std::max(sc.maxRadius, h.radius);
+    sc.preRadius = std::max(sc.maxRadius, c->tree.preRadius);
     sc.bsdf = c->bsdfRec[shapes[0].bsdf];
     if (nShapes > 1) {
         r |= upload(c, shapes.data(), shapes.size() * sizeof(HptShape), (const void **) &sc.shapes);

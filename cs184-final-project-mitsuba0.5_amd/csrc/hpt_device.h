@@ -55,6 +55,18 @@ struct HptSegF {
     float radius;  /* its shape's radius */
 };
 
+/* 16-byte pre-test record of the per-lane traversal (k_trace), leaf order:
+ * the segment's first vertex and its axis oct-encoded in 16:16 bits (one
+ * dwordx4 per record instead of 24 of HptSegF's 32 bytes).  The quantised
+ * axis turns the pre-test line by an angle theta; HptScene::preRadius widens
+ * the radius by the segment's axial reach times sin(theta), so the test stays
+ * conservative.  Decoded by axisOctDecode (hpt_render.hip) and its host
+ * twin in kdtree_build.cpp, with the same fp32 operations. */
+struct HptSegQ {
+    float v1[3];
+    uint32_t axisOct;
+};
+
 /* kd-tree node, 8 bytes (gkdtree.h:452-583 layout with absolute child index):
  *   inner: w0 = (left << 2) | axis, w1 = float bits of split; right = left + 1
  *   leaf : w0 = 0x80000000 | primStart, w1 = primEnd (indices into prim list) */
@@ -193,10 +205,13 @@ struct HptScene {
     const HptNode4 *nodes4;
     const uint32_t *leafTable;
     const HptSegF *leafF;       /* leaf primitive list (fp32 pre-test records) */
+    const HptSegQ *leafQ;       /* the same list as 16-byte records (k_trace's leaf pass) */
+    const uint32_t *leafSeg;    /* segment id per leaf entry */
     const HptSegment *segs;
     float aabbMin[3], aabbMax[3];
     float radius;               /* shape 0's radius (every shape's when nShapes == 1) */
     float maxRadius;            /* largest shape radius: bound for the conservative fp32 pre-test */
+    float preRadius;            /* the bound for the HptSegQ pre-test (quantised axis, see HptSegQ) */
     HptBsdf bsdf;               /* shape 0's BSDF */
     /* several hair shapes (hair-curl): HptSegment::shape indexes shapes[],
        which gives the radius and the entry of bsdfs[] (both in HBM: a kernel

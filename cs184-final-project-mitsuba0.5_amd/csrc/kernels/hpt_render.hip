@@ -259,6 +259,24 @@ HD bool segMayHit(const float4 a, const float4 b, V3 o, V3 d, float r) {
     return wn <= r * __builtin_amdgcn_sqrtf(nn) * 1.000001f + 3e-6f * (r + fabsf(wx) + fabsf(wy) + fabsf(wz));
 }
 
+/* HptSegQ: the oct-decoded axis (kdtree_build.cpp's axisOctDecode does the same fp32 operations on
+   the host to bound the quantisation angle) and the pre-test on it.  The axis is not unit length
+   (|axis| in [1/sqrt(3), 1]): the test is scale-invariant in the axis except for the absolute rounding
+   margin, which a shorter axis only makes looser.  preRadius covers the quantised axis's turn. */
+HD V3 axisOctDecode(uint32_t q) {
+    const float u = (float) (q & 0xffffu) * (2.0f / 65535.0f) - 1.0f;
+    const float v = (float) (q >> 16) * (2.0f / 65535.0f) - 1.0f;
+    const float z = 1.0f - fabsf(u) - fabsf(v);
+    const float fx = (1.0f - fabsf(v)) * (u >= 0.0f ? 1.0f : -1.0f);
+    const float fy = (1.0f - fabsf(u)) * (v >= 0.0f ? 1.0f : -1.0f);
+    return v3(z < 0.0f ? fx : u, z < 0.0f ? fy : v, z);
+}
+HD bool segMayHitQ(const uint4 q, V3 o, V3 d, float preRadius) {
+    const V3 a = axisOctDecode(q.w);
+    return segMayHit(make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), a.x),
+                     make_float4(a.y, a.z, 0.0f, 0.0f), o, d, preRadius);
+}
+
 /* adaptive ray epsilon: skdtree.cpp:126-129 (closest) / :213-216 (shadow) */
 HD float adaptiveMint(V3 o, float mint, bool shadow) {
     if (mint != kEpsilon) return mint;
@@ -360,6 +378,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     static_assert((STACK & (STACK - 1)) == 0, "the ring stack index is masked");
     static_assert(!(LAT && STATS), "the latency-mode leaf pass keeps no traversal counters");
     const float4 *__restrict__ leafF = reinterpret_cast<const float4 *>(sc.leafF);
+    const uint4 *__restrict__ leafQ = reinterpret_cast<const uint4 *>(sc.leafQ);
     /* the ray as plain values: selecting among struct members by axis would be
        folded into a dynamically addressed load and push the state to scratch */
     const uint2 cr0 = stk[STACK * stride], cr1 = stk[(STACK + 1) * stride];
@@ -472,7 +491,9 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
        (32 records per chunk; the next record is fetched while the current one
        is tested), then the exact fp64 test runs on the marked ones -- the
        prefetched records are dead by then, so the fp64 test's registers do
-       not stack on top of them */
+       not stack on top of them.  Outside latency mode the pre-test reads the
+       16-byte HptSegQ records (one dwordx4 per record: the kernel's vector
+       memory path is busy ~3/4 of its cycles) */
     const uint32_t first = leafFirst, last = leafLast;
     if (LAT) {
         /* latency mode (k_tail: few waves, registers to spare): every record of a
@@ -522,24 +543,21 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
     for (uint32_t c0 = first; c0 < last; c0 += 32) {
         const uint32_t c1 = min(last, c0 + 32);
         uint32_t mask = 0;
-        float4 na = leafF[2 * c0], nb = leafF[2 * c0 + 1];
+        uint4 nq = leafQ[c0];
         for (uint32_t e = c0; e < c1; ++e) {
-            const float4 fa = na, fb = nb;
-            if (e + 1 < c1) {
-                na = leafF[2 * e + 2];
-                nb = leafF[2 * e + 3];
-            }
+            const uint4 fq = nq;
+            if (e + 1 < c1) nq = leafQ[e + 1];
             if (STATS) {
                 ++tc.prims;
                 tc.shadowPrims += r.shadow ? 1u : 0u;
                 if (waveLeader()) tc.primSlots += 64;
             }
-            if (segMayHit(fa, fb, o, d, sc.maxRadius)) mask |= 1u << (e - c0);
+            if (segMayHitQ(fq, o, d, sc.preRadius)) mask |= 1u << (e - c0);
         }
         while (mask) {
             const uint32_t e = c0 + (uint32_t) (__ffs(mask) - 1);
             mask &= mask - 1;
-            const uint32_t s = __float_as_uint(leafF[2 * e + 1].z);
+            const uint32_t s = sc.leafSeg[e];
             const float rad = segRadius(sc, s);
             const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
             if (STATS) ++tc.exact;

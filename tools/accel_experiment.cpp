@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <random>
 #include <vector>
 
@@ -59,10 +60,15 @@ struct Ray {
 
 struct Counts {
     double nodes = 0, prims = 0, boxes = 0, leaves = 0;
+    /* node fetches if the binary tree were stored as G-level groups (group roots at depth % G == 0):
+       eager[G] = the node4 scheme (a far side's splits evaluated at push time, so pops land on group
+       roots), local3 = 3-level groups whose stack entries may point inside a group (a pop refetches) */
+    double eager[5] = {0, 0, 0, 0, 0}, local3 = 0, maxStack = 0;
     uint64_t rays = 0;
 };
 
 /* ---------------- kd-tree (binary HptNode, front-to-back) ---------------- */
+static std::vector<uint8_t> g_depth; /* binary depth of every kd node */
 static bool traceKD(const KDTreeHost &kd, float radius, const Ray &r, double &tHit, uint32_t &seg, Counts &c) {
     float tmin = r.mint, tmax = r.maxt;
     /* scene AABB clip */
@@ -84,10 +90,15 @@ static bool traceKD(const KDTreeHost &kd, float radius, const Ray &r, double &tH
     double best = r.maxt;
     bool found = false;
     D3 o = d3(r.o[0], r.o[1], r.o[2]), d = d3(r.d[0], r.d[1], r.d[2]);
+    bool popped = false;
     while (true) {
         const HptNode &n = kd.nodes[node];
         c.nodes++;
         if (!(n.w0 & 0x80000000u)) {
+            const int dep = g_depth[node];
+            for (int G = 1; G <= 4; ++G) c.eager[G] += (dep % G == 0) ? 1 : 0;
+            c.local3 += (dep % 3 == 0 || popped) ? 1 : 0;
+            popped = false;
             int ax = n.w0 & 3;
             uint32_t left = n.w0 >> 2;
             float split;
@@ -124,12 +135,120 @@ static bool traceKD(const KDTreeHost &kd, float radius, const Ray &r, double &tH
         if (found && best <= tmax) break;
         if (sp == 0) break;
         --sp;
+        popped = true;
         node = st[sp].n;
         tmin = st[sp].tmin;
         tmax = st[sp].tmax;
         if (found && tmin > best) break;
     }
     tHit = best;
+    return found;
+}
+
+/* The same traversal with G-level grouped nodes whose far sides are expanded at push time (the
+   node4 scheme for G = 2): a pushed node inside a group is split on its interval right away and its
+   children pushed instead (recursively, down to the next group root or a leaf).  Counts group
+   fetches, the peak stack depth and how many rays would overflow an 8-entry ring stack. */
+struct EagerCounts {
+    double fetches = 0, peak = 0, over8 = 0, pushes = 0;
+    uint64_t rays = 0, mism = 0;
+};
+static bool traceKDEager(const KDTreeHost &kd, int G, float radius, const Ray &r, double &tHit, uint32_t &seg,
+                         EagerCounts &c) {
+    float tmin = r.mint, tmax = r.maxt;
+    for (int a = 0; a < 3; ++a) {
+        float inv = 1.0f / r.d[a];
+        float t0 = (kd.aabbMin[a] - r.o[a]) * inv, t1 = (kd.aabbMax[a] - r.o[a]) * inv;
+        if (t0 > t1) std::swap(t0, t1);
+        tmin = std::max(tmin, t0);
+        tmax = std::min(tmax, t1);
+    }
+    c.rays++;
+    if (!(tmax > tmin)) return false;
+    struct E {
+        uint32_t n;
+        float tmin, tmax;
+    } st[512];
+    int sp = 0, peak = 0;
+    auto split = [&](uint32_t node, float a, float b, uint32_t &first, uint32_t &second, float &ts, int &kind) {
+        const HptNode &n = kd.nodes[node];
+        int ax = n.w0 & 3;
+        uint32_t left = n.w0 >> 2;
+        float spl;
+        std::memcpy(&spl, &n.w1, 4);
+        ts = (spl - r.o[ax]) / r.d[ax];
+        bool below = r.o[ax] < spl || (r.o[ax] == spl && r.d[ax] <= 0);
+        first = below ? left : left + 1, second = below ? left + 1 : left;
+        kind = (ts > b || ts <= 0) ? 0 : (ts < a ? 1 : 2); /* near only, far only, both */
+    };
+    /* push node X over [a, b], expanding it while it is an inner node inside a group */
+    std::function<void(uint32_t, float, float)> push = [&](uint32_t x, float a, float b) {
+        const HptNode &n = kd.nodes[x];
+        if ((n.w0 & 0x80000000u) || g_depth[x] % G == 0) {
+            st[sp++] = {x, a, b};
+            c.pushes++;
+            peak = std::max(peak, sp);
+            return;
+        }
+        uint32_t f, s2;
+        float ts;
+        int kind;
+        split(x, a, b, f, s2, ts, kind);
+        if (kind == 0) push(f, a, b);
+        else if (kind == 1) push(s2, a, b);
+        else {
+            push(s2, ts, b);
+            push(f, a, ts);
+        }
+    };
+    uint32_t node = 0;
+    double best = r.maxt;
+    bool found = false;
+    D3 o = d3(r.o[0], r.o[1], r.o[2]), d = d3(r.d[0], r.d[1], r.d[2]);
+    bool fetched = false; /* the current group is in registers */
+    while (true) {
+        const HptNode &n = kd.nodes[node];
+        if (!(n.w0 & 0x80000000u)) {
+            if (g_depth[node] % G == 0) c.fetches++;
+            uint32_t f, s2;
+            float ts;
+            int kind;
+            split(node, tmin, tmax, f, s2, ts, kind);
+            if (kind == 0) node = f;
+            else if (kind == 1) node = s2;
+            else {
+                push(s2, ts, tmax);
+                node = f;
+                tmax = ts;
+            }
+            continue;
+        }
+        for (uint32_t e = n.w0 & 0x7fffffffu; e < n.w1; ++e) {
+            double t;
+            uint32_t s = kd.prims[e];
+            if (segHit(kd.segs[s], radius, o, d, r.mint, best, t)) {
+                found = true;
+                if (r.shadow) {
+                    tHit = t;
+                    goto done;
+                }
+                best = t;
+                seg = s;
+            }
+        }
+        if (found && best <= tmax) break;
+        if (sp == 0) break;
+        --sp;
+        node = st[sp].n;
+        tmin = st[sp].tmin;
+        tmax = st[sp].tmax;
+        if (found && tmin > best) break;
+    }
+    tHit = best;
+done:
+    c.peak += peak;
+    c.over8 += peak > 8 ? 1 : 0;
+    (void) fetched;
     return found;
 }
 
@@ -456,10 +575,19 @@ int main(int argc, char **argv) {
         appendHair(hair, one);
     }
     KDTreeHost kd = buildHairKDTree(hair, d.kd);
+    g_depth.assign(kd.nodes.size(), 0);
+    for (size_t i = 0; i < kd.nodes.size(); ++i)
+        if (!(kd.nodes[i].w0 & 0x80000000u)) {
+            const uint32_t left = kd.nodes[i].w0 >> 2;
+            g_depth[left] = g_depth[left + 1] = (uint8_t) (g_depth[i] + 1);
+        }
     const size_t nseg = kd.segs.size();
     float radius = hair.radius;
     printf("segments %zu, kd nodes %zu, kd refs %zu (%.2f per segment), build %.2f s\n", nseg, kd.nodes.size(),
            kd.prims.size(), (double) kd.prims.size() / nseg, kd.buildSeconds);
+    printf("radius %.6g, 16-byte pre-test radius bound %.6g (x%.5f)\n", hair.radius, kd.preRadius,
+           kd.preRadius / hair.radius);
+    if (argc > 5) return 0;
 
     /* segment solids: axis segment extended by the miter overhang, radius + slack */
     std::vector<SegInfo> S(nseg);
@@ -566,6 +694,32 @@ int main(int argc, char **argv) {
                    ck[k].leaves / n, ck[k].prims / n, (unsigned long long) cb[k].rays);
         }
         printf("W=%d wide nodes %zu, mismatches %zu\n", W, wn.size(), mism);
+        if (W == 2)
+            for (int G = 1; G <= 4; ++G) {
+                const std::vector<Ray> *sets[3] = {&camRays, &sec0, &sh0};
+                for (int k = 0; k < 3; ++k) {
+                    EagerCounts ec;
+                    for (auto &r : *sets[k]) {
+                        double t1 = 0, t2 = 0;
+                        uint32_t s1 = 0, s2 = 0;
+                        Counts dummy;
+                        bool h1 = traceKD(kd, radius, r, t1, s1, dummy);
+                        bool h2 = traceKDEager(kd, G, radius, r, t2, s2, ec);
+                        if (h1 != h2 || (h1 && !r.shadow && (s1 != s2 || t1 != t2))) ec.mism++;
+                    }
+                    double n = (double) std::max<uint64_t>(1, ec.rays);
+                    printf("eager G=%d %-12s fetches %.2f  pushes %.2f  mean peak stack %.2f  rays over 8 entries "
+                           "%.3f%%  mismatches %llu\n", G, nm[k], ec.fetches / n, ec.pushes / n, ec.peak / n,
+                           100.0 * ec.over8 / n, (unsigned long long) ec.mism);
+                }
+            }
+        if (W == 2)
+            for (int k = 0; k < 3; ++k) {
+                double n = (double) std::max<uint64_t>(1, ck[k].rays);
+                printf("kd %-12s inner-node fetches: binary %.2f, eager 2-level %.2f, 3-level %.2f, 4-level %.2f; "
+                       "3-level with in-group stack entries %.2f\n", nm[k], ck[k].eager[1] / n, ck[k].eager[2] / n,
+                       ck[k].eager[3] / n, ck[k].eager[4] / n, ck[k].local3 / n);
+            }
     }
     return 0;
 }
