@@ -42,9 +42,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 BYTES_CLOSEST, BYTES_SHADOW, BYTES_UNOCC = 52, 36, 48
 B8D_NODE, B8D_REF, B8D_PRIM = 8, 4, 52
 # the layout-specific figure (what this build's records actually are): 32 B per two-level HptNode4
-# fetch, 32 B leaf-ordered fp32 pre-test record per primitive test, 128 B segment record per exact
-# fp64 test; the packet pass reads 8-byte binary HptNodes
-BYTES_NODE4, BYTES_PRIM, BYTES_EXACT, BYTES_NODE2 = 32, 32, 128, 8
+# fetch, 16 B leaf-ordered fp32 pre-test record (HptSegQ) per primitive test, 128 B segment record
+# per exact fp64 test; the packet pass reads 8-byte binary HptNodes and 32-byte HptSegF records
+BYTES_NODE4, BYTES_PRIM, BYTES_EXACT, BYTES_NODE2, BYTES_PRIM_PACKET = 32, 16, 128, 8, 32
 
 
 def parse():
@@ -271,7 +271,7 @@ def main():
     pk_node_steps, pk_prim_steps = tot["p_node_slots"] / 64.0, tot["p_prim_slots"] / 64.0
     bytes_pk = io_pk + B8D_NODE * pk_node_steps + (B8D_REF + B8D_PRIM) * pk_prim_steps
     bytes_pk_lane = io_pk + B8D_NODE * tot["p_nodes"] + (B8D_REF + B8D_PRIM) * tot["p_prims"]
-    bytes_pk_lay = io_pk + BYTES_NODE2 * pk_node_steps + BYTES_PRIM * pk_prim_steps + BYTES_EXACT * tot["p_exact"]
+    bytes_pk_lay = io_pk + BYTES_NODE2 * pk_node_steps + BYTES_PRIM_PACKET * pk_prim_steps + BYTES_EXACT * tot["p_exact"]
     achieved_pk, achieved_pk_lay = gbs(bytes_pk, ms_packet), gbs(bytes_pk_lay, ms_packet)
     # the whole frame on SURVEY.md 8(d)'s B_path: camera ray + state 40 B per path; per path-bounce
     # the state queue read + write 2 x 80, the hit record 40, the BSDF's table reads (Marschner
