@@ -746,7 +746,10 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
                 preR = std::max(preR, reach[s]);
             }
         }
-        t.preRadius = (float) (preR * (1.0 + 1e-5));
+        /* a miter plane parallel to the axis (a strand folding back on itself) makes the reach
+           unbounded: the bound then passes every record (still conservative); kept finite so the
+           device's products with it never form inf * 0 */
+        t.preRadius = (float) std::min(preR * (1.0 + 1e-5), 1e30);
     }
     t.buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return t;
