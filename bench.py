@@ -10,12 +10,15 @@ With N GPUs the frame's 32x32 blocks are dealt cyclically along a Hilbert curve 
 the RGBW films are summed on rank 0 with one RCCL reduce (strong scaling).
 
 Launch:  python bench.py [--gpus 1 --steps 3 --warmup 1]
+         python bench.py --gpus N ...   (starts the N ranks itself: a child torch.distributed.run)
          python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
-Prints ONE JSON line on rank 0.
+Prints ONE JSON line on rank 0.  --gpus must equal WORLD_SIZE when a launcher set it.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import tempfile
 import time
@@ -150,10 +153,43 @@ def timed_steps(step, steps, world, dist_mod, sync, device, after_step=None):
     return float(t.item())
 
 
+def launch_ranks(n_ranks, argv):
+    """`bench.py --gpus N` without a launcher: run the N ranks as a CHILD torch.distributed.run
+    (one process per GPU; this parent has made no HIP call, and it does not exec: it waits for
+    the child and returns its exit code).  The ranks inherit stdout, so rank 0's one JSON line
+    is this command's output.  One command drives every worker, as mitsuba.cpp:281-329 does."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n_ranks),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def check_world(gpus, env):
+    """The rank count the launcher gave (WORLD_SIZE) must be the --gpus asked for: a line that says
+    n_gpus N must have run N ranks.  Returns the world size; raises SystemExit on a mismatch."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None:
+        if gpus != 1:
+            raise SystemExit("bench.py: --gpus %d needs %d ranks; run it without a launcher (it starts them) or under "
+                             "torch.distributed.run --nproc-per-node %d" % (gpus, gpus, gpus))
+        return 1
+    if int(ws) != gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%s ranks" % (gpus, ws))
+    return int(ws)
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = check_world(args.gpus, os.environ)
     rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     # HPT_BENCH_BACKEND=gloo only rehearses N > 1 on a one-GPU box (RCCL refuses two
     # ranks on one device): the film is reduced from a host copy.  Never the bench.
     backend = os.environ.get("HPT_BENCH_BACKEND", "nccl")
@@ -164,8 +200,20 @@ def main():
     elif local >= n_dev:
         raise SystemExit("LOCAL_RANK %d but only %d visible GPU(s): one rank per GPU (HIP_VISIBLE_DEVICES too narrow?)"
                          % (local, n_dev))
+    pg = {"dist_backend": None, "world_size": 1, "rccl_version": None}
     if world > 1:
         dist.init_process_group(backend)  # "nccl" = RCCL over xGMI on ROCm
+        # what the process group itself reports (not the launcher's environment)
+        pg["dist_backend"] = str(dist.get_backend())
+        pg["world_size"] = dist.get_world_size()
+        if pg["world_size"] != world:
+            raise SystemExit("bench.py: the process group has %d ranks, WORLD_SIZE says %d" % (pg["world_size"], world))
+        if pg["dist_backend"] == "nccl":
+            try:
+                import torch.cuda.nccl as tnccl
+                pg["rccl_version"] = ".".join(str(v) for v in tnccl.version())
+            except Exception as ex:  # noqa: BLE001 -- a version we cannot read is recorded as such
+                pg["rccl_version"] = "unknown (%s)" % type(ex).__name__
     torch.cuda.set_device(local)
     cfg = scenes.CONFIGS[args.config]
     n = args.strands or cfg["n"]
@@ -226,8 +274,7 @@ def main():
                  unocc=c.shadow_unoccluded, bounces=c.bounces, launches=c.trace_launches,
                  node_slots=c.node_slots, prim_slots=c.prim_slots,
                  p_rays=c.packet_rays, p_nodes=c.packet_nodes, p_prims=c.packet_prims, p_exact=c.packet_exact,
-                 p_node_slots=c.packet_node_slots, p_prim_slots=c.packet_prim_slots, p_fallbacks=c.packet_fallbacks,
-                 cut=c.cut_rays)
+                 p_node_slots=c.packet_node_slots, p_prim_slots=c.packet_prim_slots, p_fallbacks=c.packet_fallbacks)
     acc = {"ms_trace": 0.0, "ms_packet": 0.0, "launches": 0, "p_launches": 0, "kernels": {}}
 
     def collect():
@@ -317,6 +364,7 @@ def main():
             "data": "synthetic hair (seeded, BINARY_HAIR; reference hair blobs absent) lit by the scene's sunsky (Hosek-Wilkie sky + Preetham sun rasterised like sunsky.cpp)",
             "config": {"workload": workload,
                        "paths_per_step": W * H * spp, "parallelism": "tiles%d" % world,
+                       "gpus_arg": args.gpus, **pg,
                        "deal": "work-balanced (warm-up frame's path-bounces per block)" if balanced
                        else "Hilbert-cyclic 32x32 blocks",
                        **({"rehearsal": "HPT_BENCH_BACKEND=gloo: ranks share GPUs, host-copy reduce"}
@@ -373,9 +421,6 @@ def main():
                       "kernel_ms_per_step: one more frame with an event around every kernel",
             "cpu_baseline": cpu,
             "stats": {"bounces_per_path": round(tot["bounces"] / max(1, paths_total / world), 4),
-                      # the resumable cut: rays the counted frame's bounce launches saved at their dry
-                      # point and the next launch resumed
-                      "cut_rays_per_step": int(frame["cut"]),
                       "nodes_per_ray": round(tot["nodes"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "binary_nodes_per_ray": round(tot["bnodes"] / max(1, tot["closest"] + tot["shadow"]), 2),
                       "prims_per_ray": round(tot["prims"] / max(1, tot["closest"] + tot["shadow"]), 2),

@@ -61,27 +61,11 @@ static bool defaultBounceAhead() {
     return v ? std::atoi(v) != 0 : true;
 }
 
-/* the resumable cut (hpt_kernels.h HPT_C_CARRY_*): a bounce's trace launch with at least this many
-   closest rays saves the rays still running at its dry point for the next launch instead of
-   draining them (HPT_CUT_MIN; 0, the default, turns the cut off).  Never below the tail threshold:
-   the launch before the tail must drain (k_tail takes no cut work) */
-static uint32_t defaultCutMin() {
-    const char *v = std::getenv("HPT_CUT_MIN");
-    return v ? (uint32_t) std::strtoul(v, nullptr, 10) : 0u;
-}
-/* with the cut on, k_tail takes a bounce's queue below this many paths (HPT_CUT_TAIL): the paths the
-   last cutting bounce held back run one bounce behind the rest, and the tail, not one more
-   wavefront bounce, finishes them */
-static uint32_t defaultCutTail() {
-    const char *v = std::getenv("HPT_CUT_TAIL");
-    return v ? (uint32_t) std::strtoul(v, nullptr, 10) : (1u << 19);
-}
 /* the bounce schedule of a wave of paths: the shade-queue length of each wavefront bounce,
    and whether a k_tail launch took the rest */
 struct BounceSchedule {
     std::vector<uint32_t> shade;
     bool tail = false;
-    uint32_t held = 0; /* the most rays + paths a bounce held back for the next (the resumable cut) */
 };
 
 /* test hook: HPT_SCHEDULE_TEST=1 records schedules with half the queue lengths (the bounces
@@ -96,11 +80,6 @@ static int scheduleTestHook() {
 struct hpt_context {
     int device = 0;
     uint32_t tailPaths = defaultTailPaths();
-    uint32_t cutMin = defaultCutMin();
-    uint32_t cutTail = defaultCutTail();
-    uint32_t cutEpoch = 0;         /* per trace launch that may cut (HptPaths::cutMark) */
-    std::vector<DevBuf> carryBufs; /* carryRay / carryPath / cutMark, allocated with the first cut */
-    uint64_t carryPaths = 0;       /* paths cutMark covers */
     bool bounceAhead = defaultBounceAhead();
     int scheduleTest = scheduleTestHook();
     /* schedules of the waves rendered since the last prepare, by (spp begin, spp count,
@@ -275,43 +254,9 @@ int ensureWave(hpt_context *c, uint64_t n) {
     r |= alloc(n * 4, (void **) &c->qShade[0]);
     r |= alloc(n * 4, (void **) &c->qShade[1]);
     r |= alloc(HPT_COUNTER_WORDS * 4, (void **) &c->counters);
-    c->P.carryRay[0] = c->P.carryRay[1] = c->P.carryPath[0] = c->P.carryPath[1] = nullptr;
-    c->P.cutMark = nullptr;
-    c->P.carryCap = 0;
-    freeBufs(c->carryBufs);
-    c->carryPaths = 0;
     r |= alloc(2 * 24 * 8, (void **) &c->dstats); /* the counters, and a snapshot at the start of a wave */
     if (r) return HPT_EDEVICE;
     c->capacity = n;
-    return HPT_OK;
-}
-
-/* the resumable cut's buffers (only when it is on): two parities of saved rays and held-back paths,
-   each for every resident lane of k_trace, and the per-path cut marks (zero: no epoch) */
-int ensureCarry(hpt_context *c, uint64_t n) {
-    if (c->cutMin == 0 || (c->P.cutMark && c->carryPaths >= n)) return HPT_OK;
-    freeBufs(c->carryBufs);
-    c->P.cutMark = nullptr;
-    const uint64_t cap = hpt_trace_resident_lanes();
-    auto alloc = [&](size_t bytes, void **p) -> int {
-        DevBuf b;
-        b.bytes = bytes;
-        HIPCHK(c, hipMalloc(&b.p, bytes));
-        c->carryBufs.push_back(b);
-        *p = b.p;
-        return HPT_OK;
-    };
-    int r = 0;
-    for (int q = 0; q < 2; ++q) {
-        r |= alloc(cap * HPT_CARRY_RAY * 16, (void **) &c->P.carryRay[q]);
-        r |= alloc(cap * HPT_CARRY_PATH * 16, (void **) &c->P.carryPath[q]);
-    }
-    r |= alloc(n * 4, (void **) &c->P.cutMark);
-    if (r) return HPT_EDEVICE;
-    HIPCHK(c, hipMemset(c->P.cutMark, 0, n * 4));
-    c->P.carryCap = (uint32_t) cap;
-    c->carryPaths = n;
-    c->cutEpoch = 0;
     return HPT_OK;
 }
 
@@ -1151,13 +1096,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
     if (waveCap > 0xffffffffull) return setErr(c, HPT_EINVAL, "wave too large");
     int r = ensureWave(c, waveCap);
     if (r) return r;
-    if ((r = ensureCarry(c, waveCap))) return r;
-    /* the resumable cut: never below the tail threshold (the launch before k_tail drains) */
-    const bool cutOn = c->cutMin != 0 && c->P.cutMark != nullptr;
-    /* the tail threshold, raised with the cut (defaultCutTail) */
-    const uint32_t tailPaths = cutOn ? std::max(c->tailPaths, c->cutTail) : c->tailPaths;
-    const uint32_t cutMin = std::max(c->cutMin, tailPaths);
-    const uint64_t carrySlack = cutOn ? c->P.carryCap : 0; /* the most rays / paths a bounce can hold back */
+    const uint32_t tailPaths = c->tailPaths;
     if (slots > c->partialSlots) {
         if (c->partial) (void) hipFree(c->partial);
         c->partial = nullptr;
@@ -1298,20 +1237,9 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         bool learn = c->bounceAhead && !ahead, extended = false;
         BounceSchedule seen;
         int b = 1, bounce = 0;
-        /* grid: the shade launch's; traceExtra / postExtra: room for the rays / paths the previous
-           bounce held back (read back: their counts; launched ahead: the schedule's slack) */
-        /* Bounce b's k_post starts Russian roulette at b >= rrDepth (path.cpp:276, depth b): from
-           there on most paths end each bounce, and paths held back there would trail the rest
-           by a bounce through bounces that otherwise would not run.  So the cut stops one bounce
-           earlier: the paths the last cutting launch holds back are posted with the others at
-           the bounce before roulette, and k_tail (cutTail) finishes what trails */
-        const int rrDepth = c->sc.rrDepth;
-        auto wavefrontBounce = [&](uint32_t p, uint64_t grid, uint32_t tailFrom, uint64_t traceExtra,
-                                   uint64_t postExtra) -> hipError_t {
+        /* grid: the shade launch's (the trace launch's work is at most twice it, the post's at most it) */
+        auto wavefrontBounce = [&](uint32_t p, uint64_t grid, uint32_t tailFrom) -> hipError_t {
             const uint32_t q = p ^ 1u;
-            const bool cutHere = cutOn && (rrDepth <= 0 || b < rrDepth);
-            const uint32_t epoch = cutOn ? ++c->cutEpoch : 0u;
-            if (cutOn && epoch == 0) return hipErrorUnknown; /* 2^32 cut launches: never in practice */
             hipError_t e1 = timed(2, [&] {
                 return hpt_launch_shade(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), c->qTrace, C + HPT_C_TRACE(p),
                                         c->qShadow, C + HPT_C_SHADOW(p), C, grid, tailFrom, s);
@@ -1319,8 +1247,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             if (e1) return e1;
             e1 = timed(-1, [&] {
                 return hpt_launch_trace(sc, c->P, c->qTrace, c->qShadow, C + HPT_C_TRACE(p), C + HPT_C_SHADOW(p),
-                                        C + HPT_CURSOR_SET(p), dst, 2ull * grid + traceExtra, s, C, q, cutHere ? cutMin : 0u,
-                                        epoch);
+                                        C + HPT_CURSOR_SET(p), dst, 2ull * grid, s, C, q);
             });
             if (e1) return e1;
             reportLaunch("bounce");
@@ -1332,16 +1259,13 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             }
             return timed(3, [&] {
                 return hpt_launch_post(sc, c->P, c->qTrace, C + HPT_C_TRACE(p), c->qShade[q], C + HPT_C_SHADE(q), C,
-                                       grid + postExtra, s, p, epoch);
+                                       grid, s);
             });
         };
         if (ahead) {
             const BounceSchedule &k = known->second;
-            /* with the cut, a bounce's queue moves with the paths held back, which vary from render
-               to render: every grid gets room for twice the most the recording held back */
-            const uint64_t slack = k.held ? std::min<uint64_t>(carrySlack, 2ull * k.held + 4096) : 0;
             for (size_t i = 0; i < k.shade.size() && e == hipSuccess; ++i, ++b)
-                e = wavefrontBounce((uint32_t) b & 1u, std::min<uint64_t>(k.shade[i] + slack, w.nPaths), 0u, slack, slack);
+                e = wavefrontBounce((uint32_t) b & 1u, k.shade[i], 0u);
             if (e == hipSuccess && k.tail)
                 e = timed(5, [&] {
                     const uint32_t p = (uint32_t) b & 1u;
@@ -1367,23 +1291,20 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             if (e == hipSuccess) e = hipStreamSynchronize(s);
             if (e) break;
             const uint32_t n = hostCnt[HPT_C_SHADE(p)];
-            /* rays or paths the previous bounce held back (the cut) keep the wave going */
-            const bool noCarry = hptNoCarry(hostCnt, p ^ 1u);
             if (firstRead) doneAtFirstRead = hptWaveDone(hostCnt, p); /* what the early gather's guard saw */
             firstRead = false;
-            if ((n == 0 && noCarry) || hostCnt[HPT_C_TAIL_PATHS] != 0) break; /* no live path, or k_tail took the rest */
+            if (n == 0 || hostCnt[HPT_C_TAIL_PATHS] != 0) break; /* no live path, or k_tail took the rest */
             if (ahead && fits) {
                 /* the schedule did not cover the wave (its tail declined, or bounces ran past it):
                    re-record it as the part launched ahead plus the bounces read back from here */
                 seen.shade = known->second.shade;
                 seen.tail = false;
-                seen.held = known->second.held;
                 c->schedules.erase(key);
                 fits = false;
                 learn = extended = true;
                 c->stats.schedule_extensions++;
             }
-            if (n < tailPaths && noCarry) {
+            if (n < tailPaths) {
                 /* few live paths: finish them all in one launch (k_tail) */
                 seen.tail = true;
                 e = timed(5, [&] { return hpt_launch_tail(sc, c->P, c->qShade[p], C + HPT_C_SHADE(p), C, n, ~0u, s); });
@@ -1393,9 +1314,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                 break;
             }
             seen.shade.push_back(n);
-            const uint32_t heldRays = hostCnt[HPT_C_CARRY_RAYS(p ^ 1u)], heldPaths = hostCnt[HPT_C_CARRY_PATHS(p ^ 1u)];
-            seen.held = std::max(seen.held, heldRays + heldPaths);
-            e = wavefrontBounce(p, n, 0u, heldRays, heldPaths);
+            e = wavefrontBounce(p, n, 0u);
         }
         if (e) break;
         if (hostCnt[HPT_C_OVERFLOW] && !ahead) {
@@ -1435,7 +1354,6 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             std::memcpy(&shaded, hostCnt + HPT_C_BOUNCES, 8);
             bounces += shaded + hostCnt[HPT_C_TAIL_BOUNCES]; /* k_tail counts its first bounce too */
             c->stats.tail_paths += hostCnt[HPT_C_TAIL_PATHS];
-            c->stats.cut_rays += hostCnt[HPT_C_CUT_RAYS];
             bounce = (int) hostCnt[HPT_C_LAUNCHES];
         }
         maxB = std::max(maxB, bounce);
@@ -1552,7 +1470,6 @@ int hpt_context_share_scene(hpt_context *src, int device, hpt_context **out) {
     c->vdcInv = src->vdcInv;
     c->maxLeafRounds = src->maxLeafRounds, c->maxRestarts = src->maxRestarts, c->packetStack = src->packetStack;
     c->tailPaths = src->tailPaths, c->bounceAhead = src->bounceAhead, c->packets = src->packets;
-    c->cutMin = src->cutMin, c->cutTail = src->cutTail;
     /* the shard deal: hpt_render_multi gives shard g to context g, and every context must deal
        the blocks the same way or some blocks are rendered twice and others never */
     c->blockWeights = src->blockWeights;

@@ -21,13 +21,6 @@
 #define HPT_C_ERROR 12       /* set when a path runs out of Sobol dimensions */
 #define HPT_C_TAIL_BOUNCES 13 /* path-bounces shaded inside k_tail */
 #define HPT_C_TAIL_CURSOR 14  /* k_tail's work claims */
-/* the resumable cut (k_trace / k_post, hpt_launch_trace's cutMin): rays a bounce's trace launch
-   of parity p left unfinished at its dry point (their traversal state saved in
-   HptPaths::carryRay[p]), and paths its k_post held back because one of their rays was cut
-   (records in HptPaths::carryPath[p]) */
-#define HPT_C_CARRY_RAYS(p) (16 + (p))
-#define HPT_C_CARRY_PATHS(p) (18 + (p))
-#define HPT_C_CUT_RAYS 20     /* rays cut over the wave (statistics) */
 #define HPT_Q_COUNT 24
 /* HptScene::fault bits: a traversal bound fired (the ray would otherwise end
    with whatever hit it had; the render / batch call fails instead) */
@@ -64,12 +57,8 @@ struct HptWave {
     const uint32_t *doneIf;
     uint32_t doneParity;
 };
-/* nothing of bounce b - 1 (parity q) is held back by a cut: no ray of its trace launch, no path of its post */
-__host__ __device__ inline bool hptNoCarry(const uint32_t *c, uint32_t q) {
-    return c[HPT_C_CARRY_RAYS(q)] == 0u && c[HPT_C_CARRY_PATHS(q)] == 0u;
-}
 __host__ __device__ inline bool hptWaveDone(const uint32_t *c, uint32_t p) {
-    return ((c[HPT_C_SHADE(p)] == 0u && hptNoCarry(c, p ^ 1u)) || c[HPT_C_TAIL_PATHS] != 0u) && c[HPT_C_OVERFLOW] == 0u &&
+    return (c[HPT_C_SHADE(p)] == 0u || c[HPT_C_TAIL_PATHS] != 0u) && c[HPT_C_OVERFLOW] == 0u &&
            c[HPT_C_ERROR] == 0u;
 }
 
@@ -110,14 +99,6 @@ struct HptPaths {
        The by-path arrays above (ro, rd, thr, state, bw, sdir, scontrib) are k_camera's and
        k_tail's. */
     float4 *postRec, *shadowRec, *shadeRec;
-    /* The resumable cut: a trace launch whose queue runs dry saves the traversal state of every
-       ray still running (HPT_CARRY_RAY float4s each, carryRay[p] by cut position) and the next
-       launch resumes it; cutMark[path] = the launch's epoch when a ray of the path was cut; k_post
-       holds such a path back (carryPath[p]: its post record and hit word) until its rays are done.
-       carryCap: rays one launch can leave (every resident lane of k_trace) */
-    float4 *carryRay[2], *carryPath[2];
-    uint32_t *cutMark;
-    uint32_t carryCap;
     /* per owned 32x32 block: path-bounces shaded (k_shade, k_tail), the measured work the cost-
        balanced shard deal reads back (hpt_get_block_costs); nullptr: not counted.  costSpp is
        the wave's nSpp (path id -> block: id / nSpp >> 10).  The counts are striped: wave w adds
@@ -133,11 +114,6 @@ struct HptPaths {
 
 
 #define HPT_COST_STRIPES 64
-#define HPT_CARRY_RAY 9   /* float4s of a cut ray: o|mint, d|maxt, tmin tmax tHit segHit, node top sp|flags cnt,
-                             NEE contribution|path, the 8 stack entries */
-#define HPT_CARRY_PATH 5  /* float4s of a held-back path: its post record (4), path | hit word */
-#define HPT_HIT_PENDING 0xfffffffeu /* a closest-hit record whose ray was cut (no segment id has all 31 bits set but one) */
-#define HPT_CUT_RESUMED 0x80000000u /* trace key of a resumed ray: | its carryRay index */
 /* hit record of a miss (a segment id never has all 31 bits set) */
 #define HPT_MISS 0xffffffffu
 
@@ -148,16 +124,9 @@ hipError_t hpt_launch_camera(const HptScene &sc, const HptWave &w, const HptPath
 /* one persistent traversal launch: closest-hit rays traceQ[0, *nTrace), shadow rays shadowQ[0, *nShadow) */
 /* counters (nullptr: none): a bounce launch of parity p = nextParity ^ 1 also zeroes the counts and
    cursor set of parity nextParity, which the next bounce appends to / claims from */
-/* cutMin (0: never): with counters, the launch of parity p = nextParity ^ 1 first resumes the rays
-   the previous launch cut (carryRay[nextParity]), and, when it has at least cutMin closest rays,
-   cuts its own running rays at its dry point (carryRay[p]) instead of draining them; epoch
-   marks their paths (cutMark) for the k_post of the same bounce */
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
-                            uint64_t maxItems, hipStream_t s, uint32_t *counters = nullptr, uint32_t nextParity = 0,
-                            uint32_t cutMin = 0, uint32_t epoch = 0);
-/* k_trace's resident lanes (the most rays one launch can leave running at its dry point) */
-uint64_t hpt_trace_resident_lanes();
+                            uint64_t maxItems, hipStream_t s, uint32_t *counters = nullptr, uint32_t nextParity = 0);
 /* the camera pass's rays one per lane (HPT_PACKETS=0): traceQ[0, *nTrace), hits to P.hitQ by position */
 hipError_t hpt_launch_trace_camera(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
                                    uint32_t *cursors, uint32_t *stats, uint64_t maxItems, hipStream_t s);
@@ -178,12 +147,8 @@ hipError_t hpt_launch_primary(const HptScene &sc, const HptPaths &P, const uint3
 hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
                             uint32_t *traceQ, uint32_t *nTrace, uint32_t *shadowQ, uint32_t *nShadow, uint32_t *counters,
                             uint64_t maxItems, uint32_t tailFrom, hipStream_t s);
-/* the bounce of parity p = the parity of nTrace's counter; with epoch != 0 it also posts the paths
-   the previous bounce held back (carryPath[p ^ 1]) whose rays are done, and holds back its own
-   paths with a ray cut in the launch of that epoch (carryPath[p]) */
 hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
-                           uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s,
-                           uint32_t parity = 0, uint32_t epoch = 0);
+                           uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s);
 /* the rest of every live path (the shade queue) to termination in one launch, when the queue
    is shorter than tailFrom (~0u: always); items = HPT_ITEMS_ON_DEVICE when the host has not
    read the queue length (the launch then sizes its work from it on the device) */

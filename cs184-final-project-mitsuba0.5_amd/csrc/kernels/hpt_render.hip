@@ -897,21 +897,12 @@ __device__ __forceinline__ void tracePersistent(const HptScene &sc, IO &io, uint
                        computed (under a branch, mint / maxt stayed live across the miss
                        path and were spilled); a miss never reads them */
                     stashRay<STACK>(stk, (int) blockDim.x, r, io.key());
-                    /* a ray a previous launch cut: its stack and round count as they were */
-                    if constexpr (IO::kCut) io.template restore<STACK>(stk, (int) blockDim.x, r);
                     if (!active) {
                         nU += io.finish(sc, io.key(), r);
                         rayDone(0u, 0u);
                     }
                 }
             }
-        }
-        if (IO::kCut && exhausted && io.cut) { /* (wave-uniform) */
-            /* the resumable cut: the queue is dry, so instead of draining, every running ray's
-               traversal state goes to the carry set the next launch resumes */
-            io.template save<STACK>(stk, (int) blockDim.x, r, active);
-            active = false;
-            break;
         }
         if (SPLIT && exhausted) break; /* the drain loop below */
         if (__ballot(active) == 0) {
@@ -2477,10 +2468,6 @@ struct PathIO {
     bool byQueue;
     const uint32_t *posQ;
     bool recs; /* bounce launches: rays from the queue-ordered records, keys are queue positions */
-    static constexpr bool kCut = false; /* (BounceIO: the resumable cut) */
-    static constexpr bool cut = false;
-    template <int STACK> HD void restore(uint2 *, int, TraceRay &) const {}
-    template <int STACK> HD void save(uint2 *, int, const TraceRay &, bool) const {}
     /* work indices: closest rays [0, nTrace), then shadow rays, in HPT_CURSORS contiguous shards */
     HD uint32_t count() const { return nTrace + nShadow; }
     HD uint32_t shardSize(uint32_t s) const { return shardLo(count(), s + 1) - shardLo(count(), s); }
@@ -2528,155 +2515,41 @@ struct PathIO {
     }
 };
 
-/* The IO of a bounce's trace launch (k_trace): rays from the queue-ordered records, and the
-   resumable cut.  Work indices: the rays the previous launch cut [0, nCarry) first (their paths
-   are a bounce behind), then the closest rays [.., + nTrace), then the shadow rays.  At the
-   launch's dry point (cut set: the launch has at least cutMin closest rays) every running ray
-   is saved -- its ray, interval, best hit, node, ring stack and round count, and what its finish
-   needs (the path, the NEE contribution) -- instead of being drained; the next launch resumes
-   it where it stopped, so it tests the same segments in the same order with the same intervals
-   and its answer is bit-identical.  A cut closest ray leaves HPT_HIT_PENDING in its hit record
-   (by queue position, and by path for a resumed ray); its path is marked with the launch's
-   epoch, and k_post holds it back until both of its rays are done, so its NEE term still
-   reaches li before post's emitter term (path.cpp order). */
+/* The IO of a bounce's trace launch (k_trace): rays from the queue-ordered records.  Work
+   indices: the closest rays [0, nTrace), then the shadow rays; the key of a ray is its work
+   index (closest: its trace-queue position, where k_post reads the hit record; shadow: nTrace +
+   its shadow-queue position). */
 struct BounceIO {
     HptPaths P;
     const uint32_t *traceQ, *shadowQ;
-    uint32_t nCarry, nTrace, nShadow, id;
-    const float4 *carryIn; /* carryRay[p ^ 1]: the rays the previous launch cut */
-    float4 *carryOut;      /* carryRay[p] */
-    uint32_t *counters;    /* the counter block (one pointer and the parity, not three pointers: k_trace's
-                              SGPRs are spent) */
-    uint32_t par;          /* the launch's parity p */
-    uint32_t epoch;
-    bool cut;
-    static constexpr bool kCut = true;
-    HD uint32_t count() const { return nCarry + nTrace + nShadow; }
-    /* Shard s of HPT_CURSORS: its slice of the resumed rays, then its slice of the new ones.  The
-       resumed rays are the previous launch's longest: spread over every shard (every wave starts
-       with a few), not packed into the first shards' waves, where they would run as one more
-       drain */
-    HD uint32_t shardSize(uint32_t s) const {
-        const uint32_t nNew = nTrace + nShadow;
-        return shardLo(nCarry, s + 1) - shardLo(nCarry, s) + shardLo(nNew, s + 1) - shardLo(nNew, s);
-    }
-    HD uint32_t item(uint32_t s, uint32_t j) const {
-        const uint32_t c0 = shardLo(nCarry, s), nc = shardLo(nCarry, s + 1) - c0;
-        return j < nc ? c0 + j : nCarry + shardLo(nTrace + nShadow, s) + (j - nc);
-    }
+    uint32_t nTrace, nShadow, id;
+    HD uint32_t count() const { return nTrace + nShadow; }
+    HD uint32_t shardSize(uint32_t s) const { return shardLo(count(), s + 1) - shardLo(count(), s); }
+    HD uint32_t item(uint32_t s, uint32_t j) const { return shardLo(count(), s) + j; }
     HD uint32_t key() const { return id; }
     HD bool begin(const HptScene &sc, uint32_t k, TraceRay &r) {
-        if (k < nCarry) { /* a ray the previous launch cut */
-            id = HPT_CUT_RESUMED | k;
-            const float4 *c = carryIn + (size_t) HPT_CARRY_RAY * k;
-            const float4 a = c[0], b = c[1], t = c[2], n = c[3];
-            r.o = v3(a.x, a.y, a.z);
-            r.d = v3(b.x, b.y, b.z);
-            r.rcp = v3(1.0f / b.x, 1.0f / b.y, 1.0f / b.z); /* beginRay's */
-            r.mint = a.w;
-            r.maxt = b.w;
-            r.tmin = t.x;
-            r.tmax = t.y;
-            r.tHit = t.z;
-            r.segHit = __float_as_uint(t.w);
-            r.node = __float_as_uint(n.x);
-            r.top = __float_as_uint(n.y);
-            const uint32_t spf = __float_as_uint(n.z);
-            r.sp = (int) (spf & 0xffu);
-            r.lost = (spf & 0x100u) != 0;
-            r.found = (spf & 0x200u) != 0;
-            r.shadow = (spf & 0x400u) != 0;
-            return true;
-        }
-        k -= nCarry;
+        id = k;
         /* a bounce ray leaves the hit point at kEpsilon (path.cpp:213, scene.cpp:838) */
         if (k < nTrace) {
-            id = k;
             const float4 o = P.postRec[4 * k], d = P.postRec[4 * k + 1];
             return beginRay(sc, r, v3(o.x, o.y, o.z), v3(d.x, d.y, d.z), kEpsilon, finf(), false);
         }
-        id = k; /* nTrace + shadow-queue position */
         const uint32_t j = k - nTrace;
         const float4 o = P.shadowRec[3 * j], d = P.shadowRec[3 * j + 1];
         return beginRay(sc, r, v3(o.x, o.y, o.z), v3(d.x, d.y, d.z), kEpsilon, d.w, true);
     }
-    /* after stashRay: a resumed ray's ring stack and round count */
-    template <int STACK>
-    HD void restore(uint2 *stk, int stride, TraceRay &r) const {
-        if (!(id & HPT_CUT_RESUMED)) return;
-        const float4 *c = carryIn + (size_t) HPT_CARRY_RAY * (id & ~HPT_CUT_RESUMED);
-        r.cnt = __float_as_uint(c[3].w);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const float4 q = c[5 + e];
-            stk[(2 * e) * stride] = make_uint2(__float_as_uint(q.x), __float_as_uint(q.y));
-            stk[(2 * e + 1) * stride] = make_uint2(__float_as_uint(q.z), __float_as_uint(q.w));
-        }
-        static_assert(STACK == 8, "a cut ray carries an 8-entry ring stack");
-        asm volatile("" ::: "memory");
-    }
-    /* the path of a ray and, for a shadow ray, its NEE contribution */
-    HD uint32_t pathOf(uint32_t key, bool shadowRay, float4 *contrib) const {
-        if (key & HPT_CUT_RESUMED) {
-            const float4 c = carryIn[(size_t) HPT_CARRY_RAY * (key & ~HPT_CUT_RESUMED) + 4];
-            if (contrib) *contrib = c;
-            return __float_as_uint(c.w);
-        }
-        if (!shadowRay) return traceQ[key];
-        const uint32_t j = key - nTrace;
-        if (contrib) *contrib = P.shadowRec[3 * j + 2];
-        return shadowQ[j];
-    }
-    /* the cut: every active lane saves its ray (one reservation per wave) */
-    template <int STACK>
-    __device__ __forceinline__ void save(uint2 *stk, int stride, const TraceRay &r, bool active) const {
-        const uint64_t m = __ballot(active);
-        if (m == 0) return;
-        uint32_t base = 0;
-        if (__lane_id() == 0) {
-            base = atomicAdd(counters + HPT_C_CARRY_RAYS(par), (uint32_t) __popcll(m));
-            atomicAdd(counters + HPT_C_CUT_RAYS, (uint32_t) __popcll(m));
-        }
-        base = (uint32_t) __builtin_amdgcn_readfirstlane((int) base);
-        if (!active) return;
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t) (m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) m, 0u));
-        const uint32_t k = rayKey<STACK>(stk, stride);
-        const uint2 mm = stk[(STACK + HPT_ROW_MM) * stride];
-        float4 contrib = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        const uint32_t path = pathOf(k, r.shadow, &contrib);
-        float4 *c = carryOut + (size_t) HPT_CARRY_RAY * (base + rank);
-        c[0] = make_float4(r.o.x, r.o.y, r.o.z, __uint_as_float(mm.x));
-        c[1] = make_float4(r.d.x, r.d.y, r.d.z, __uint_as_float(mm.y));
-        c[2] = make_float4(r.tmin, r.tmax, r.tHit, __uint_as_float(r.segHit));
-        const uint32_t spf = ((uint32_t) r.sp & 0xffu) | (r.lost ? 0x100u : 0u) | (r.found ? 0x200u : 0u) | (r.shadow ? 0x400u : 0u);
-        c[3] = make_float4(__uint_as_float(r.node), __uint_as_float(r.top), __uint_as_float(spf), __uint_as_float(r.cnt));
-        c[4] = make_float4(contrib.x, contrib.y, contrib.z, __uint_as_float(path));
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const uint2 s0 = stk[(2 * e) * stride], s1 = stk[(2 * e + 1) * stride];
-            c[5 + e] = make_float4(__uint_as_float(s0.x), __uint_as_float(s0.y), __uint_as_float(s1.x), __uint_as_float(s1.y));
-        }
-        /* the path waits in k_post; a cut closest ray's record says so */
-        P.cutMark[path] = epoch;
-        if (!r.shadow) {
-            if (k & HPT_CUT_RESUMED) P.hit[path] = HPT_HIT_PENDING;
-            else P.hitQ[k] = HPT_HIT_PENDING;
-        }
-    }
     /* returns 1 for an unoccluded shadow ray */
     HD uint32_t finish(const HptScene &sc, uint32_t key, const TraceRay &r) {
-        if (HPT_PROBE_WANTS_PATH && !(key & HPT_CUT_RESUMED))
-            probeRayFinished(r, r.shadow ? shadowQ[key - nTrace] : traceQ[key], key, true);
+        if (HPT_PROBE_WANTS_PATH) probeRayFinished(r, r.shadow ? shadowQ[key - nTrace] : traceQ[key], key, true);
         if (!r.shadow) {
             /* the shading kernel re-derives the point from the segment and the accepted root */
-            const uint32_t h = r.found ? r.segHit : HPT_MISS;
-            if (key & HPT_CUT_RESUMED) P.hit[pathOf(key, false, nullptr)] = h; /* its path waits in k_post */
-            else P.hitQ[key] = h;
+            P.hitQ[key] = r.found ? r.segHit : HPT_MISS;
             return 0;
         }
         if (r.found) return 0;
-        float4 c;
-        const uint32_t path = pathOf(key, true, &c);
+        const uint32_t j = key - nTrace;
+        const float4 c = P.shadowRec[3 * j + 2];
+        const uint32_t path = shadowQ[j];
         const float4 l = P.li[path];
         P.li[path] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
         return 1;
@@ -2710,19 +2583,9 @@ struct BounceIO {
 
 /* the queue lengths come from device memory (the launch is enqueued before
    the host knows them) */
-/* a bounce launch's work: its queue lengths, and the resumable cut (counters: the launch of parity
-   p = nextParity ^ 1 resumes the rays of carryRay[nextParity] and cuts into carryRay[p]) */
 HD BounceIO bounceIO(const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ, const uint32_t *nTrace,
-                     const uint32_t *nShadow, uint32_t *counters, uint32_t nextParity, uint32_t cutMin, uint32_t epoch) {
-    const uint32_t p = nextParity ^ 1u;
-    BounceIO io{P, traceQ, shadowQ, 0, *nTrace, *nShadow, 0, nullptr, nullptr, counters, p, epoch, false};
-    if (counters) {
-        io.nCarry = counters[HPT_C_CARRY_RAYS(nextParity)];
-        io.carryIn = P.carryRay[nextParity];
-        io.carryOut = P.carryRay[p];
-        io.cut = cutMin != 0 && io.nTrace >= cutMin && P.carryRay[p] != nullptr;
-    }
-    return io;
+                     const uint32_t *nShadow) {
+    return BounceIO{P, traceQ, shadowQ, *nTrace, *nShadow, 0};
 }
 /* the next bounce's counts and cursor set start at zero (what a separate clearing launch did):
    nothing of this launch reads them, and the next bounce's first kernel runs after it */
@@ -2734,17 +2597,14 @@ __device__ __forceinline__ void clearNextParity(uint32_t *counters, uint32_t q) 
         counters[HPT_C_TRACE(q)] = 0;
         counters[HPT_C_SHADOW(q)] = 0;
         counters[HPT_C_SHADE(q)] = 0;
-        /* this bounce's k_post holds its paths back into carryPath[q ^ 1]; the previous k_post's
-           (carryPath[q]) and the previous launch's cut rays (carryRay[q], resumed here) stay */
-        counters[HPT_C_CARRY_PATHS(q ^ 1u)] = 0;
     }
 }
 extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
     const uint32_t *__restrict__ nTrace, const uint32_t *__restrict__ nShadow, uint32_t *__restrict__ cursors,
-    uint32_t *counters, uint32_t nextParity, uint32_t cutMin, uint32_t epoch) {
+    uint32_t *counters, uint32_t nextParity) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    BounceIO io = bounceIO(P, traceQ, shadowQ, nTrace, nShadow, counters, nextParity, cutMin, epoch);
+    BounceIO io = bounceIO(P, traceQ, shadowQ, nTrace, nShadow);
     clearNextParity(counters, nextParity);
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
@@ -2755,10 +2615,9 @@ extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(Hp
                                                                               const uint32_t *__restrict__ nShadow,
                                                                               uint32_t *__restrict__ cursors,
                                                                               uint32_t *counters, uint32_t nextParity,
-                                                                              uint32_t cutMin, uint32_t epoch,
                                                                               uint32_t *stats) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
-    BounceIO io = bounceIO(P, traceQ, shadowQ, nTrace, nShadow, counters, nextParity, cutMin, epoch);
+    BounceIO io = bounceIO(P, traceQ, shadowQ, nTrace, nShadow);
     clearNextParity(counters, nextParity);
     tracePersistent<HPT_STACK, true>(sc, io, cursors, stk + threadIdx.x, stats);
 }
@@ -3034,7 +2893,6 @@ struct HptShadeIO {
     const uint32_t *nShade;
     uint32_t *nTrace, *nShadow, *counters;
     uint32_t tailFrom; /* a queue shorter than this is k_tail's (device-side bounce control); 0: always shade */
-    uint32_t parity;   /* the bounce's: the previous bounce's cut (parity ^ 1) keeps the bounce a wavefront one */
 };
 template <bool MULTI>
 __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, const uint32_t *__restrict__ shadeQ,
@@ -3044,9 +2902,8 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
     float *const wiL = wiLds + threadIdx.x;
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n0 = *q.nShade;
-    /* a short queue is the tail launch's bounce -- unless the previous bounce held rays or paths back
-       (the wavefront bounce resumes and posts them; k_tail takes no cut work) */
-    const uint32_t n = (n0 < q.tailFrom && hptNoCarry(q.counters, q.parity ^ 1u)) ? 0u : n0;
+    /* a short queue is the tail launch's bounce */
+    const uint32_t n = n0 < q.tailFrom ? 0u : n0;
     if (blockIdx.x == 0 && threadIdx.x == 0 && n != 0) {
         atomicAdd((unsigned long long *) (q.counters + HPT_C_BOUNCES), (unsigned long long) n);
         atomicAdd(&q.counters[HPT_C_LAUNCHES], 1u);
@@ -3166,26 +3023,15 @@ HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, bool hit, uint32_
     }
     return alive;
 }
-/* continuation results of a bounce (the paths of its trace queue), and the resumable cut: with an
-   epoch, the paths the previous bounce held back (carryPath[parity ^ 1]: their rays were cut in
-   that bounce's launch and resumed in this one) are posted after the queue's, and a path with a
-   ray cut in this bounce's launch (cutMark == epoch) is held back instead of posted (carryPath[
-   parity]) -- its post runs once both of its rays are done, so its NEE term reaches li first */
+/* continuation results of a bounce (the paths of its trace queue) */
 extern "C" __global__ __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc, HptPaths P,
                                                           const uint32_t *__restrict__ traceQ,
                                                           const uint32_t *__restrict__ nTrace,
                                                           uint32_t *__restrict__ shadeQ, uint32_t *__restrict__ nShade,
-                                                          uint32_t *__restrict__ counters, uint32_t parity, uint32_t epoch) {
+                                                          uint32_t *__restrict__ counters) {
     const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t n = *nTrace; /* <= the bounce's shade queue, which k_shade checked against the grid */
-    const uint32_t nIn = epoch ? counters[HPT_C_CARRY_PATHS(parity ^ 1u)] : 0u;
-    if (epoch && blockIdx.x == 0 && threadIdx.x == 0) {
-        /* the previous launch's cut rays were resumed by this bounce's launch (which read their count) */
-        counters[HPT_C_CARRY_RAYS(parity ^ 1u)] = 0;
-        /* a grid sized from a schedule that has no room for the paths held back: rendered again */
-        if ((uint64_t) n + nIn > (uint64_t) gridDim.x * blockDim.x) atomicOr(&counters[HPT_C_OVERFLOW], 1u);
-    }
-    bool alive = false, hold = false;
+    bool alive = false;
     uint32_t id = 0;
     uint32_t seg = HPT_MISS;
     float4 rec[4], sOut[3];
@@ -3194,28 +3040,10 @@ extern "C" __global__ __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc,
         seg = P.hitQ[tid];
 #pragma unroll
         for (int i = 0; i < 4; ++i) rec[i] = P.postRec[4 * tid + i];
-        hold = epoch && P.cutMark[id] == epoch;
-    } else if (tid - n < nIn) {
-        const float4 *cp = P.carryPath[parity ^ 1u] + (size_t) HPT_CARRY_PATH * (tid - n);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) rec[i] = cp[i];
-        const float4 x = cp[4];
-        id = __float_as_uint(x.x);
-        seg = __float_as_uint(x.y);
-        if (seg == HPT_HIT_PENDING) seg = P.hit[id]; /* its closest ray was cut: resumed by path */
-        hold = P.cutMark[id] == epoch;
+        alive = postPath<true>(sc, P, id, seg != HPT_MISS, counters, rec, sOut);
     }
-    if (tid < n + nIn && !hold) alive = postPath<true>(sc, P, id, seg != HPT_MISS, counters, rec, sOut);
     /* the survivors' shade records and hit records travel with the shade queue, in its order */
     qpushBlockRec<HPT_POST_BLOCK, 3>(alive, id, shadeQ, nShade, P.shadeRec, sOut, P.hitS, seg);
-    if (epoch) { /* uniform */
-        float4 hr[HPT_CARRY_PATH];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) hr[i] = rec[i];
-        hr[4] = make_float4(__uint_as_float(id), __uint_as_float(seg), 0.0f, 0.0f);
-        qpushBlockRec<HPT_POST_BLOCK, HPT_CARRY_PATH>(hold, id, nullptr, counters + HPT_C_CARRY_PATHS(parity),
-                                                      P.carryPath[parity], hr);
-    }
 }
 
 /* Tail of the frame (few live paths left, after Russian roulette has
@@ -3236,7 +3064,6 @@ struct HptTail {
     const uint32_t *shadeQ, *nShade;
     uint32_t pairs;    /* lane pairs per wave that take paths (1..32); 0: from the queue length, on the device */
     uint32_t tailFrom; /* the launch takes the queue only when it is shorter than this (device-side bounce control) */
-    uint32_t parity;   /* the bounce's: nothing of the previous bounce may be held back by a cut */
 };
 #ifndef HPT_TAIL_SPLIT
 #define HPT_TAIL_SPLIT 1 /* k_tail's idle lanes help trace its rays (RaySplitter); 0: one lane per ray, latency mode */
@@ -3249,7 +3076,7 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
     const uint32_t lane = __lane_id(), partner = lane & ~1u;
     const bool odd = (lane & 1u) != 0;
     const uint32_t n0 = *T.nShade;
-    const uint32_t total = (n0 < T.tailFrom && hptNoCarry(counters, T.parity ^ 1u)) ? n0 : 0u;
+    const uint32_t total = n0 < T.tailFrom ? n0 : 0u;
     /* nothing to take (k_shade has the bounce, or no path is live): leave the claim cursor
        alone for a later tail launch of the same wave of paths */
     if (total == 0) return;
@@ -3506,10 +3333,6 @@ struct BatchIO {
     uint32_t n;
     bool shadow;
     uint32_t cur;
-    static constexpr bool kCut = false; /* (BounceIO: the resumable cut) */
-    static constexpr bool cut = false;
-    template <int STACK> HD void restore(uint2 *, int, TraceRay &) const {}
-    template <int STACK> HD void save(uint2 *, int, const TraceRay &, bool) const {}
     HD uint32_t count() const { return n; }
     HD uint32_t shardSize(uint32_t s) const { return shardLo(n, s + 1) - shardLo(n, s); }
     HD uint32_t item(uint32_t s, uint32_t j) const { return shardLo(n, s) + j; }
@@ -3666,24 +3489,17 @@ static unsigned persistentBlocks(const void *kernel, uint64_t items, int block =
 
 hipError_t hpt_launch_trace(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *shadowQ,
                             const uint32_t *nTrace, const uint32_t *nShadow, uint32_t *cursors, uint32_t *stats,
-                            uint64_t maxItems, hipStream_t s, uint32_t *counters, uint32_t nextParity, uint32_t cutMin,
-                            uint32_t epoch) {
+                            uint64_t maxItems, hipStream_t s, uint32_t *counters, uint32_t nextParity) {
     if (maxItems == 0) return hipSuccess;
     hptProbeBeforeTraceLaunch(s);
     if (stats)
         hipLaunchKernelGGL(k_trace_counted, dim3(persistentBlocks((const void *) k_trace_counted, maxItems)),
                            dim3(HPT_TRACE_BLOCK), 0, s, sc, P, traceQ, shadowQ, nTrace, nShadow, cursors,
-                           counters, nextParity, cutMin, epoch, stats);
+                           counters, nextParity, stats);
     else
         hipLaunchKernelGGL(k_trace, dim3(persistentBlocks((const void *) k_trace, maxItems)), dim3(HPT_TRACE_BLOCK), 0, s,
-                           sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, counters, nextParity, cutMin, epoch);
+                           sc, P, traceQ, shadowQ, nTrace, nShadow, cursors, counters, nextParity);
     return hipGetLastError();
-}
-uint64_t hpt_trace_resident_lanes() {
-    /* the larger of the two bounce kernels' resident grids, every lane of it */
-    const uint64_t a = persistentBlocks((const void *) k_trace, ~0ull >> 8),
-                   b = persistentBlocks((const void *) k_trace_counted, ~0ull >> 8);
-    return std::max(a, b) * HPT_TRACE_BLOCK;
 }
 hipError_t hpt_launch_trace_camera(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
                                    uint32_t *cursors, uint32_t *stats, uint64_t maxItems, hipStream_t s) {
@@ -3729,7 +3545,7 @@ hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_
                             uint32_t *traceQ, uint32_t *nTrace, uint32_t *shadowQ, uint32_t *nShadow, uint32_t *counters,
                             uint64_t maxItems, uint32_t tailFrom, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
-    const HptShadeIO q{nShade, nTrace, nShadow, counters, tailFrom, nShade == counters + HPT_C_SHADE(1) ? 1u : 0u};
+    const HptShadeIO q{nShade, nTrace, nShadow, counters, tailFrom};
     if (sc.nShapes > 1)
         hipLaunchKernelGGL(k_shade_multi, dim3(blocksFor(maxItems, HPT_SHADE_BLOCK)), dim3(HPT_SHADE_BLOCK), 0, s, sc, P, shadeQ,
                            traceQ, shadowQ, q);
@@ -3739,11 +3555,10 @@ hipError_t hpt_launch_shade(const HptScene &sc, const HptPaths &P, const uint32_
     return hipGetLastError();
 }
 hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t *traceQ, const uint32_t *nTrace,
-                           uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s,
-                           uint32_t parity, uint32_t epoch) {
+                           uint32_t *shadeQ, uint32_t *nShade, uint32_t *counters, uint64_t maxItems, hipStream_t s) {
     if (maxItems == 0) return hipSuccess;
     hipLaunchKernelGGL(k_post, dim3(blocksFor(maxItems, HPT_POST_BLOCK)), dim3(HPT_POST_BLOCK), 0, s, sc, P, traceQ, nTrace,
-                       shadeQ, nShade, counters, parity, epoch);
+                       shadeQ, nShade, counters);
     return hipGetLastError();
 }
 hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
@@ -3760,7 +3575,7 @@ hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t
     const uint32_t K = items == HPT_ITEMS_ON_DEVICE
                            ? 0u
                            : (uint32_t) std::min<uint64_t>(32, std::max<uint64_t>(1, (items + residentWaves - 1) / residentWaves));
-    const HptTail T{shadeQ, nShade, K, tailFrom, nShade == counters + HPT_C_SHADE(1) ? 1u : 0u};
+    const HptTail T{shadeQ, nShade, K, tailFrom};
     const unsigned blocks = K ? persistentBlocks(kern, (items + K - 1) / K * 64) : residentBlocks;
     if (sc.nShapes > 1)
         hipLaunchKernelGGL(k_tail_multi, dim3(blocks), dim3(HPT_TRACE_BLOCK), 0, s, sc, P, T, counters);

@@ -236,9 +236,6 @@ typedef struct hpt_stats {
     /* waves whose schedule was launched ahead but did not cover them (the tail declined, or
        bounces ran past it): finished bounce by bounce and their schedule re-recorded */
     uint64_t schedule_extensions;
-    /* the resumable cut: rays the bounce trace launches saved at their dry point and the next
-       launch resumed (instead of draining them), over the render call */
-    uint64_t cut_rays;
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 

@@ -183,3 +183,28 @@ def test_block_weights_add_camera_rays():
     px = np.array([32 * 32, 32 * 32, 16 * 32, 32 * 8, 32 * 8, 16 * 8], np.float64)
     np.testing.assert_allclose(w, costs.astype(np.float64) + distributed.CAMERA_RAY_WEIGHT * spp * px)
     assert w[1] > 0 and w[4] < w[1]
+
+
+def test_bench_world_size_must_match_gpus():
+    """bench.py --gpus N: the launcher's WORLD_SIZE must equal N (a line saying n_gpus N ran N ranks);
+    without a launcher N = 1 runs in-process and N > 1 starts the ranks itself (launch_ranks)."""
+    import bench
+    assert bench.check_world(1, {}) == 1
+    assert bench.check_world(4, {"WORLD_SIZE": "4"}) == 4
+    with pytest.raises(SystemExit, match="WORLD_SIZE=3"):
+        bench.check_world(2, {"WORLD_SIZE": "3"})
+    with pytest.raises(SystemExit, match="needs 2 ranks"):
+        bench.check_world(2, {})
+
+
+def test_bench_mismatched_launch_fails_loudly():
+    """The whole script exits non-zero, before any device work, when --gpus and WORLD_SIZE disagree."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    res = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--cpu-baseline", "off"], cwd=root, env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert res.returncode != 0
+    assert "WORLD_SIZE=3" in res.stderr
+    assert '{"metric"' not in res.stdout
