@@ -379,9 +379,10 @@ def main():
                          "traffic_calibration": "profiles/r03_fetch_calibration.json: FETCH_SIZE is 64 B per 128-B "
                                                 "line for 8/16/32-B accesses, cold or Infinity-Cache resident (x2 = "
                                                 "line bytes); WRITE_SIZE is 32 B per lone 16-B store",
-                         "achieved_hbm": round(traffic / (ms_trace / max(1, launches)) * 1e-6, 1) if traffic else None,
+                         "achieved_hbm": round(traffic / (ms_trace / max(1, launches)) * 1e-6, 1)
+                         if traffic and ms_trace > 0 else None,
                          "frac_hbm": round(traffic / (ms_trace / max(1, launches)) * 1e-6 / HBM_PEAK_GBS, 4)
-                         if traffic else None,
+                         if traffic and ms_trace > 0 else None,
                          "algorithmic_model": "SURVEY.md 8(d): 8 B per binary kd-node visit, 4+52 B per primitive "
                                               "test, ray I/O 52 (closest) / 36 (+48 unoccluded) B; the closest "
                                               "ray's hit record is priced at 8(d)'s 16 B (segment, t, root), "

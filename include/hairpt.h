@@ -236,6 +236,10 @@ typedef struct hpt_stats {
     /* waves whose schedule was launched ahead but did not cover them (the tail declined, or
        bounces ran past it): finished bounce by bounce and their schedule re-recorded */
     uint64_t schedule_extensions;
+    /* waves whose bounces ran in one persistent k_paths launch (every bounce of the wave, no
+       per-bounce drain; a wave with a recorded schedule, HPT_PATHS != 0), and its HIP event time */
+    uint64_t paths_launches;
+    double ms_paths;
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 
