@@ -1377,6 +1377,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                                  w32(HPT_MC_DONE), w32(HPT_MC_STEPS), w32(HPT_MC_SWITCHES), w64(HPT_MC_CLAIMS),
                                  w64(HPT_MC_PHASES), w64(HPT_MC_T_TRACE) / tot, w64(HPT_MC_T_SHADE) / tot,
                                  w64(HPT_MC_T_IDLE) / tot, tot * 1e-8);
+                    std::fprintf(stderr, "[paths] rounds %.4g lane use %.3f drains %.0f\n", w64(HPT_MC_ROUNDS),
+                                 w64(HPT_MC_LANES) / std::max(1.0, 64.0 * w64(HPT_MC_ROUNDS)), w64(HPT_MC_DRAINS));
                 }
             }
             if (hostCnt[HPT_C_OVERFLOW]) c->megaScale *= 2.0; /* the wave is rendered again below */

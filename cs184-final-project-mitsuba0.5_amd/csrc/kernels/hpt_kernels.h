@@ -153,7 +153,10 @@ struct HptPaths {
 #define HPT_MC_T_IDLE 14
 #define HPT_MC_CLAIMS 15
 #define HPT_MC_PHASES 16
-#define HPT_MC_WORDS 17
+#define HPT_MC_ROUNDS 17   /* statistics: traversal rounds of the trace phases (main loop), and */
+#define HPT_MC_LANES 18    /*   the active lanes summed over them (lane use = lanes / 64 rounds) */
+#define HPT_MC_DRAINS 19   /* statistics: drains (trace phases ending with running rays) */
+#define HPT_MC_WORDS 20
 #define HPT_MC_STRIDE 32
 struct HptMega {
     float4 *rec;         /* chunk fields (above) */

@@ -85,29 +85,43 @@ HD void pathsAbort(const HptMega &M, uint32_t *counters) {
     }
 }
 
-/* The wave's state, in LDS (one copy per wave; lane 0 writes, every lane reads the same word): kept
-   out of SGPRs, which the traversal's loop needs (held in registers it spilled 150 VGPRs) */
+/* A wave traces every ray of the ray chunks it claims, up to HPT_PATHS_ENTRIES chunks in flight (it
+   refills lanes from the newest while the older ones' long rays finish), so a slot's two rays finish
+   on lanes of one wave and its completion is known in LDS: no global atomic per ray (one with a
+   return value, per ray, stalled every traversal round that finished a ray on a device round trip:
+   3x the wave cycles).  The wave's state, in LDS (lane 0 writes, every lane reads the same word):
+   kept out of SGPRs, which the traversal's loop needs */
+#ifndef HPT_PATHS_ENTRIES
+#define HPT_PATHS_ENTRIES 3
+#endif
 struct PathsWave {
     uint32_t rayTicket, postTicket;
-    uint32_t chunk, taken, total; /* the ray chunk the wave refills from */
-    uint32_t contLo, contHi, shadowLo, shadowHi;
+    uint32_t cur, taken;          /* the entry the wave refills from (HPT_NO_TICKET: none), rays handed out */
     uint32_t postCur, postNext;   /* post chunks being filled */
     uint32_t fill;                /* items in them (postCur first, then postNext) */
     uint32_t shader;              /* counted in HPT_MC_SHADERS */
     uint32_t claims;              /* statistics: ray chunks claimed */
+    uint32_t drains;              /* statistics: trace phases that ended in a drain */
+    uint64_t rounds, lanes;       /* statistics: main-loop traversal rounds, active lanes over them */
+    /* entries: a claimed chunk, its rays (closest-ray lanes, shadow-ray lanes), the slots one of
+       whose two rays has finished, the unoccluded shadow rays, rays still running (0: free) */
+    uint32_t chunk[HPT_PATHS_ENTRIES], total[HPT_PATHS_ENTRIES], left[HPT_PATHS_ENTRIES];
+    uint64_t contM[HPT_PATHS_ENTRIES], shadowM[HPT_PATHS_ENTRIES], doneM[HPT_PATHS_ENTRIES],
+        unoccM[HPT_PATHS_ENTRIES];
 };
 HD uint32_t uni(uint32_t v) { return (uint32_t) __builtin_amdgcn_readfirstlane((int) v); }
+HD uint64_t uni64(uint64_t v) { return ((uint64_t) uni((uint32_t) (v >> 32)) << 32) | uni((uint32_t) v); }
 /* lane 0 writes a field of the wave's state (the wave then reads it back) */
 #define PW_SET(w, field, v)                  \
     do {                                     \
-        const uint32_t _v = (v);             \
+        const auto _v = (v);                 \
         if (__lane_id() == 0) (w)->field = _v; \
         __builtin_amdgcn_wave_barrier();     \
     } while (0)
 #define PW_GET(w, field) uni((w)->field)
 
 /* the trace side's IO (tracePersistent's interface, for traceRound / RaySplitter): a ray's key is
-   slot << 1 | shadow */
+   entry << 7 | slot lane << 1 | shadow */
 struct PathsIO {
     const HptMega *M;
     PathsWave *w;
@@ -115,7 +129,8 @@ struct PathsIO {
     HD uint32_t key() const { return id; }
     HD bool begin(const HptScene &sc, uint32_t key, TraceRay &r) {
         id = key;
-        const float4 *f = slotFields(*M, key >> 1);
+        const uint32_t slot = w->chunk[key >> 7] * 64u + ((key >> 1) & 63u);
+        const float4 *f = slotFields(*M, slot);
         const float4 o = handoffLoadF4(f);
         /* a bounce ray leaves the hit point at kEpsilon (path.cpp:213, scene.cpp:838) */
         if (!(key & 1u)) {
@@ -125,23 +140,24 @@ struct PathsIO {
         const float4 d = handoffLoadF4(f + 64 * 5);
         return beginRay(sc, r, v3(o.x, o.y, o.z), v3(d.x, d.y, d.z), kEpsilon, d.w, true);
     }
-    /* the ray's result into its slot's state word; the slot's last ray appends the slot to the
-       wave's post chunk.  Returns 1 for an unoccluded shadow ray */
+    /* a closest ray's hit word goes to its slot (the post step reads it there); a slot whose last
+       ray this is joins the wave's post chunk.  Returns 1 for an unoccluded shadow ray */
     HD uint32_t finish(const HptScene &, uint32_t key, const TraceRay &r) {
-        const uint32_t slot = key >> 1;
+        const uint32_t e = key >> 7, l = (key >> 1) & 63u;
+        const uint64_t bit = 1ull << l;
+        const uint32_t slot = w->chunk[e] * 64u + l;
         const bool shadowRay = (key & 1u) != 0;
-        const uint64_t delta = shadowRay ? (r.found ? 0ull : 0x100ull) - 1ull
-                                         : ((uint64_t) (r.found ? r.segHit : HPT_MISS) << 32) - 1ull;
-        const uint64_t old =
-            __hip_atomic_fetch_add(M->slotSt + slot, delta, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((old & 0xffu) == 1u) {
-            const uint64_t fin = old + delta;
+        if (!shadowRay) handoffStore(M->slotSt + slot, (uint64_t) (r.found ? r.segHit : HPT_MISS));
+        else if (!r.found) atomicOr((unsigned long long *) &w->unoccM[e], (unsigned long long) bit);
+        const bool both = ((w->contM[e] & w->shadowM[e]) & bit) != 0;
+        const uint64_t old = both ? atomicOr((unsigned long long *) &w->doneM[e], (unsigned long long) bit) : 0ull;
+        if (!both || (old & bit)) { /* the slot's last ray */
+            const uint32_t item = slot | ((w->unoccM[e] & bit) ? 0x80000000u : 0u);
             const uint32_t pos = atomicAdd(&w->fill, 1u); /* LDS; < 128: the wave publishes at 64 after every round */
             const uint32_t pc = pos < 64u ? w->postCur : w->postNext;
-            if (pc < M->postCap)
-                handoffStore(M->postItems + (size_t) pc * 64 + (pos & 63u),
-                             (uint64_t) (slot | ((fin & 0x100ull) ? 0x80000000u : 0u)) | (fin & 0xffffffff00000000ull));
+            if (pc < M->postCap) handoffStore(M->postItems + (size_t) pc * 64 + (pos & 63u), (uint64_t) item);
         }
+        atomicSub(&w->left[e], 1u);
         return shadowRay && !r.found ? 1u : 0u;
     }
 };
@@ -157,7 +173,7 @@ HD void postPublish(const HptMega &M, PathsWave *w, uint32_t *counters, bool flu
     uint32_t fill = PW_GET(w, fill);
     while (fill >= 64u || (flush && fill > 0u)) {
         const uint32_t n = min(fill, 64u), cur = PW_GET(w, postCur);
-        handoffDrain(); /* every item this wave stored has been written through */
+        handoffDrain(); /* every item (and hit word) this wave stored has been written through */
         if (cur < M.postCap) {
             const uint32_t pq = waveCtlAdd(M, HPT_MC_POST_TAIL, 1u);
             if (__lane_id() == 0) handoffStore(M.postQ + pq, (uint64_t) (cur + 1u) | ((uint64_t) n << 32));
@@ -176,9 +192,17 @@ HD uint32_t rayBacklog(const HptMega &M) {
 HD bool shadeWorkReady(const HptMega &M, uint32_t nInit) {
     return waveCtlLoad(M, HPT_MC_POST_TAIL) > waveCtlLoad(M, HPT_MC_POST_HEAD) || waveCtlLoad(M, HPT_MC_INIT) < nInit;
 }
-
-/* the wave's next ray chunk: its ticket's, once published; false: none ready */
-HD bool claimRayChunk(const HptMega &M, PathsWave *w) {
+/* a free entry of the wave (HPT_NO_TICKET: none): no ray running and not the one being refilled from */
+HD uint32_t freeEntry(PathsWave *w) {
+    const uint32_t cur = PW_GET(w, cur);
+#pragma unroll
+    for (uint32_t e = 0; e < HPT_PATHS_ENTRIES; ++e)
+        if (e != cur && PW_GET(w, left[e]) == 0u) return e;
+    return HPT_NO_TICKET;
+}
+/* claim the next published ray chunk into entry e, once its ticket's chunk is published; false:
+   none ready */
+HD bool claimRayChunk(const HptMega &M, PathsWave *w, uint32_t e) {
     uint32_t t = PW_GET(w, rayTicket);
     if (t == HPT_NO_TICKET) {
         if (waveCtlLoad(M, HPT_MC_RAY_TAIL) <= waveCtlLoad(M, HPT_MC_RAY_HEAD)) return false;
@@ -191,20 +215,24 @@ HD bool claimRayChunk(const HptMega &M, PathsWave *w) {
     const uint32_t c = (uint32_t) g - 1u;
     if (c >= M.chunkCap) return false; /* (never: rayQ holds chunks this launch allocated) */
     const uint64_t cm = waveHandoffLoad(M.desc + 2 * (size_t) c), sm = waveHandoffLoad(M.desc + 2 * (size_t) c + 1);
+    const uint32_t n = (uint32_t) (__popcll(cm) + __popcll(sm));
     PW_SET(w, rayTicket, HPT_NO_TICKET);
-    PW_SET(w, chunk, c);
-    PW_SET(w, contLo, (uint32_t) cm);
-    PW_SET(w, contHi, (uint32_t) (cm >> 32));
-    PW_SET(w, shadowLo, (uint32_t) sm);
-    PW_SET(w, shadowHi, (uint32_t) (sm >> 32));
+    PW_SET(w, chunk[e], c);
+    PW_SET(w, contM[e], cm);
+    PW_SET(w, shadowM[e], sm);
+    PW_SET(w, doneM[e], 0ull);
+    PW_SET(w, unoccM[e], 0ull);
+    PW_SET(w, total[e], n);
+    PW_SET(w, left[e], n);
+    PW_SET(w, cur, e);
     PW_SET(w, taken, 0u);
-    PW_SET(w, total, (uint32_t) (__popcll(cm) + __popcll(sm)));
     PW_SET(w, claims, PW_GET(w, claims) + 1u);
     return true;
 }
 
-/* Trace phase: refill idle lanes from ray chunks until none is ready (or the wave chooses to shade),
-   then drain the lanes (idle lanes help: RaySplitter).  Returns once every lane is idle. */
+/* Trace phase: refill idle lanes from the wave's ray chunks until none is ready (or the wave chooses
+   to shade), then drain the lanes (idle lanes help: RaySplitter).  Returns once every lane is idle;
+   every claimed chunk's rays have then finished. */
 __device__ __forceinline__ void pathsTrace(const HptScene &sc, const HptMega &M, PathsWave *w, uint2 *stk,
                                            uint32_t *counters, uint32_t nInit) {
     const int stride = HPT_TRACE_BLOCK;
@@ -216,41 +244,51 @@ __device__ __forceinline__ void pathsTrace(const HptScene &sc, const HptMega &M,
     while (true) {
         const uint64_t idle = __ballot(!active);
         if (!stop && __popcll(idle) >= HPT_REFILL) {
-            if (waveCtlLoad(M, HPT_MC_ABORT) != 0u) stop = true;
-            else if (PW_GET(w, shader) == 0u && rayBacklog(M) < M.low && shadeWorkReady(M, nInit)) {
-                /* the backlog runs low: leave tracing to shade, unless enough waves already do */
-                const uint32_t k = waveCtlAdd(M, HPT_MC_SHADERS, 1u);
-                if (k < M.maxShaders) {
-                    PW_SET(w, shader, 1u);
-                    stop = true;
-                    waveCtlAdd(M, HPT_MC_SWITCHES, 1u);
-                } else {
-                    waveCtlAdd(M, HPT_MC_SHADERS, ~0u);
+            uint32_t cur = PW_GET(w, cur);
+            const uint32_t e = (cur == HPT_NO_TICKET || PW_GET(w, taken) >= PW_GET(w, total[cur])) ? freeEntry(w)
+                                                                                                   : HPT_NO_TICKET;
+            if (e == HPT_NO_TICKET) {
+                /* the chunk still has rays, or every entry has rays running: no global word is read */
+                if (cur != HPT_NO_TICKET && PW_GET(w, taken) >= PW_GET(w, total[cur])) cur = HPT_NO_TICKET;
+            } else {
+                /* the current chunk is used up: the global words are read here only (once per chunk;
+                   every wave reading them at every refill made them the launch's hottest lines) */
+                if (waveCtlLoad(M, HPT_MC_ABORT) != 0u) stop = true;
+                else if (PW_GET(w, shader) == 0u && rayBacklog(M) < M.low && shadeWorkReady(M, nInit)) {
+                    /* the backlog runs low: leave tracing to shade, unless enough waves already do */
+                    const uint32_t k = waveCtlAdd(M, HPT_MC_SHADERS, 1u);
+                    if (k < M.maxShaders) {
+                        PW_SET(w, shader, 1u);
+                        stop = true;
+                        waveCtlAdd(M, HPT_MC_SWITCHES, 1u);
+                    } else {
+                        waveCtlAdd(M, HPT_MC_SHADERS, ~0u);
+                    }
+                }
+                if (!stop) {
+                    if (claimRayChunk(M, w, e)) cur = e;
+                    else stop = true; /* none ready: drain */
                 }
             }
-            if (!stop) {
-                if (PW_GET(w, taken) >= PW_GET(w, total) && !claimRayChunk(M, w)) stop = true; /* none ready: drain */
-                else {
-                    const uint32_t taken = PW_GET(w, taken);
-                    const uint32_t got = min((uint32_t) __popcll(idle), PW_GET(w, total) - taken);
-                    if (!active) {
-                        const uint32_t rank =
-                            __builtin_amdgcn_mbcnt_hi((uint32_t) (idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) idle, 0u));
-                        if (rank < got) {
-                            const uint64_t cm = ((uint64_t) w->contHi << 32) | w->contLo;
-                            const uint64_t sm = ((uint64_t) w->shadowHi << 32) | w->shadowLo;
-                            const uint32_t j = taken + rank, nC = (uint32_t) __popcll(cm);
-                            const uint32_t sl = j < nC ? selectBit(cm, j) : selectBit(sm, j - nC);
-                            const uint32_t key = ((w->chunk * 64u + sl) << 1) | (j < nC ? 0u : 1u);
-                            active = io.begin(sc, key, r);
-                            stashRay<HPT_STACK>(stk, stride, r, io.key());
-                            if (!active) io.finish(sc, io.key(), r);
-                        }
+            if (!stop && cur != HPT_NO_TICKET) {
+                const uint32_t taken = PW_GET(w, taken), total = PW_GET(w, total[cur]);
+                const uint32_t got = min((uint32_t) __popcll(idle), total - taken);
+                if (!active) {
+                    const uint32_t rank =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t) (idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t) idle, 0u));
+                    if (rank < got) {
+                        const uint64_t cm = w->contM[cur], sm = w->shadowM[cur];
+                        const uint32_t j = taken + rank, nC = (uint32_t) __popcll(cm);
+                        const uint32_t sl = j < nC ? selectBit(cm, j) : selectBit(sm, j - nC);
+                        const uint32_t key = (cur << 7) | (sl << 1) | (j < nC ? 0u : 1u);
+                        active = io.begin(sc, key, r);
+                        stashRay<HPT_STACK>(stk, stride, r, io.key());
+                        if (!active) io.finish(sc, io.key(), r);
                     }
-                    PW_SET(w, taken, taken + got);
-                    /* rays that missed the scene finished at once: their items count before the round's */
-                    postPublish(M, w, counters, false);
                 }
+                PW_SET(w, taken, taken + got);
+                /* rays that missed the scene finished at once: their items count before the round's */
+                postPublish(M, w, counters, false);
             }
         }
         if (__ballot(active) == 0) {
@@ -261,9 +299,17 @@ __device__ __forceinline__ void pathsTrace(const HptScene &sc, const HptMega &M,
         if (stop) {
             /* nothing more to claim (or the wave goes to shade): finish the running rays, idle lanes
                helping, publishing post items as they come */
+            PW_SET(w, drains, PW_GET(w, drains) + 1u);
             RaySplitter<HPT_STACK> split{stk, stride};
             split.template drain<false>(sc, io, r, active, tc, probe, [&]() { postPublish(M, w, counters, false); });
             break;
+        }
+        {
+            const uint64_t act = __ballot(active);
+            if (__lane_id() == 0) {
+                w->rounds += 1;
+                w->lanes += (uint64_t) __popcll(act);
+            }
         }
         if (active && traceRound<HPT_STACK, false>(sc, r, stk, stride, tc)) {
             io.finish(sc, rayKey<HPT_STACK>(stk, stride), r);
@@ -271,6 +317,8 @@ __device__ __forceinline__ void pathsTrace(const HptScene &sc, const HptMega &M,
         }
         postPublish(M, w, counters, false);
     }
+    /* every claimed chunk's rays have finished: no entry is being refilled from */
+    PW_SET(w, cur, HPT_NO_TICKET);
 }
 
 /* k_shade keeps a path's radiance and id in the rows MODE 2 leaves free (the shadow record's) */
@@ -337,7 +385,6 @@ __device__ __forceinline__ bool pathsShadeStep(const HptScene &sc, const HptPath
                 atomicOr(sc.fault, HPT_FAULT_PATHS);
                 slot = 0;
             }
-            hitRec = (uint32_t) (item >> 32);
             const float4 *f = slotFields(M, slot);
             const float4 f4 = handoffLoadF4(f + 64 * 4);
             li = make_float4(f4.x, f4.y, f4.z, 0.0f);
@@ -348,6 +395,7 @@ __device__ __forceinline__ bool pathsShadeStep(const HptScene &sc, const HptPath
                 li = make_float4(li.x + cn.x, li.y + cn.y, li.z + cn.z, li.w);
             }
             if (pf & 0x80000000u) {
+                hitRec = (uint32_t) handoffLoad(M.slotSt + slot); /* the closest ray's hit word */
                 float4 rec[4];
                 rec[0] = handoffLoadF4(f);
                 rec[1] = handoffLoadF4(f + 64);
@@ -393,7 +441,6 @@ __device__ __forceinline__ bool pathsShadeStep(const HptScene &sc, const HptPath
             }
             handoffStore(out + 64 * 4, make_float4(li.x, li.y, li.z,
                                                    __uint_as_float(path | (shadow ? 0x40000000u : 0u) | (cont ? 0x80000000u : 0u))));
-            handoffStore(M.slotSt + (size_t) c * 64 + lane, (uint64_t) ((cont ? 1u : 0u) + (shadow ? 1u : 0u)));
         }
     }
     const uint64_t contM = __ballot(cont), shadowM = __ballot(shadow);
@@ -406,11 +453,12 @@ __device__ __forceinline__ bool pathsShadeStep(const HptScene &sc, const HptPath
         const uint32_t rq = waveCtlAdd(M, HPT_MC_RAY_TAIL, 1u);
         if (lane == 0) handoffStore(M.rayQ + rq, (uint64_t) c + 1u);
     }
+    /* counts: atomics whose value nobody waits for (no return: the wave does not stall on them) */
     const uint32_t nFin = (uint32_t) __popcll(__ballot(finished)), nShaded = (uint32_t) __popcll(__ballot(alive));
     if (lane == 0) {
         if (nShaded) atomicAdd((unsigned long long *) (counters + HPT_C_BOUNCES), (unsigned long long) nShaded);
-        if (nFin) __hip_atomic_fetch_add(M.ctl + HPT_MC_DONE * HPT_MC_STRIDE, nFin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(M.ctl + HPT_MC_STEPS * HPT_MC_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (nFin) (void) __hip_atomic_fetch_add(M.ctl + HPT_MC_DONE * HPT_MC_STRIDE, nFin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        (void) __hip_atomic_fetch_add(M.ctl + HPT_MC_STEPS * HPT_MC_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return true;
 }
@@ -447,11 +495,14 @@ __device__ __forceinline__ void pathsKernel(uint2 *stkBase, PathsWave *waves) {
     PathsWave *const w = waves + (threadIdx.x >> 6);
     if (__lane_id() == 0) {
         w->rayTicket = w->postTicket = HPT_NO_TICKET;
-        w->chunk = w->taken = w->total = 0u;
-        w->contLo = w->contHi = w->shadowLo = w->shadowHi = 0u;
+        w->cur = HPT_NO_TICKET;
+        w->taken = 0u;
         w->fill = 0u;
         w->shader = 0u;
         w->claims = 0u;
+        w->drains = 0u;
+        w->rounds = w->lanes = 0ull;
+        for (int e = 0; e < HPT_PATHS_ENTRIES; ++e) w->left[e] = w->total[e] = 0u;
     }
     __builtin_amdgcn_wave_barrier();
     uint32_t nInit;
@@ -500,7 +551,7 @@ __device__ __forceinline__ void pathsKernel(uint2 *stkBase, PathsWave *waves) {
             waveCtlAdd(a.M, HPT_MC_SHADERS, ~0u);
             PW_SET(w, shader, 0u);
         }
-        if (worked || PW_GET(w, taken) < PW_GET(w, total)) {
+        if (worked) {
             idleSince = 0;
             continue;
         }
@@ -530,6 +581,9 @@ __device__ __forceinline__ void pathsKernel(uint2 *stkBase, PathsWave *waves) {
         add64(HPT_MC_T_IDLE, tIdle);
         add64(HPT_MC_CLAIMS, w->claims);
         add64(HPT_MC_PHASES, phases);
+        add64(HPT_MC_ROUNDS, w->rounds);
+        add64(HPT_MC_LANES, w->lanes);
+        add64(HPT_MC_DRAINS, w->drains);
     }
 }
 } // namespace

@@ -2400,12 +2400,17 @@ HD void qpush(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
    stored after the writing wave's s_waitcnt vmcnt(0) -- the "8-B agent atomics both sides" form
    of MI355X_MICROARCH.md (inter-workgroup visibility).  Plain loads and stores would leave the
    data in one XCD's L2 or read a stale line from another. */
+#ifndef HPT_HANDOFF_PLAIN_TIMING
 HD void handoffStore(void *p, uint64_t v) {
     __hip_atomic_store(reinterpret_cast<uint64_t *>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 HD uint64_t handoffLoad(const void *p) {
     return __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+#else /* timing experiment only (make variant): plain accesses, NOT coherent between CUs */
+HD void handoffStore(void *p, uint64_t v) { *reinterpret_cast<volatile uint64_t *>(p) = v; }
+HD uint64_t handoffLoad(const void *p) { return *reinterpret_cast<const volatile uint64_t *>(p); }
+#endif
 HD void handoffStore(float4 *p, float4 v) {
     uint64_t *q = reinterpret_cast<uint64_t *>(p);
     handoffStore(q, ((uint64_t) __float_as_uint(v.y) << 32) | __float_as_uint(v.x));

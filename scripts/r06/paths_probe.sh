@@ -2,7 +2,7 @@
 # k_paths phase statistics at the headline frame for backlog-control variants (HPT_PATHS_REPORT)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
-export TMPDIR=/tmp HPT_PATHS_REPORT=1
+export TMPDIR=/tmp HPT_PATHS_REPORT=1 HPT_PATHS=1
 O=gpurun_out/r06; mkdir -p $O
 run() { # name env...
   local n=$1; shift

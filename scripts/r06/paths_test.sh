@@ -10,7 +10,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_paths.py -x -v --timeout 15
 rc=$?
 tail -5 $O/paths_test.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 240 python -u bench.py --steps 5 --warmup 2 --cpu-baseline off > $O/bench_paths.json 2> $O/bench_paths.err || exit $?
+HPT_PATHS=1 timeout -k 10 240 python -u bench.py --steps 5 --warmup 2 --cpu-baseline off > $O/bench_paths.json 2> $O/bench_paths.err || exit $?
 HPT_PATHS=0 timeout -k 10 240 python -u bench.py --steps 5 --warmup 2 --cpu-baseline off > $O/bench_wave.json 2> $O/bench_wave.err || exit $?
 python - <<'PY'
 import json
