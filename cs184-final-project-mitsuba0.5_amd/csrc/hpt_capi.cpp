@@ -61,25 +61,11 @@ static bool defaultBounceAhead() {
     return v ? std::atoi(v) != 0 : true;
 }
 
-/* HPT_PATHS=1: every bounce of a wave with a known schedule in one persistent launch (k_paths)
-   instead of the wavefront loop (off by default until it is measured faster: DESIGN.md 6) */
-static bool defaultPathsKernel() {
-    const char *v = std::getenv("HPT_PATHS");
-    return v ? std::atoi(v) != 0 : false;
-}
-/* test hook: HPT_PATHS_CAP_TEST=k gives k_paths only k ray / post chunks (its launch aborts and the
-   wave is rendered again by the wavefront loop) */
-static uint32_t pathsCapTest() {
-    const char *v = std::getenv("HPT_PATHS_CAP_TEST");
-    return v ? (uint32_t) std::strtoul(v, nullptr, 10) : 0u;
-}
 /* the bounce schedule of a wave of paths: the shade-queue length of each wavefront bounce,
-   whether a k_tail launch took the rest, and the path-bounces shaded in all (k_paths sizes its
-   chunk queues from them) */
+   and whether a k_tail launch took the rest */
 struct BounceSchedule {
     std::vector<uint32_t> shade;
     bool tail = false;
-    uint64_t bounces = 0;
 };
 
 /* test hook: HPT_SCHEDULE_TEST=1 records schedules with half the queue lengths (the bounces
@@ -95,14 +81,6 @@ struct hpt_context {
     int device = 0;
     uint32_t tailPaths = defaultTailPaths();
     bool bounceAhead = defaultBounceAhead();
-    bool pathsKernel = defaultPathsKernel();
-    uint32_t pathsCap = pathsCapTest();
-    /* k_paths' buffers (HptMega), sized for megaChunks ray chunks and post chunks; megaScale grows
-       when a launch ran out of them (the wave is rendered again by the wavefront loop) */
-    std::vector<DevBuf> megaBufs;
-    HptMega M{};
-    uint64_t megaChunks = 0;
-    double megaScale = 1.0;
     int scheduleTest = scheduleTestHook();
     /* schedules of the waves rendered since the last prepare, by (spp begin, spp count,
        shard, shards): a repeated wave launches its bounces ahead on that schedule */
@@ -282,38 +260,6 @@ int ensureWave(hpt_context *c, uint64_t n) {
     return HPT_OK;
 }
 
-/* k_paths' chunk queues for a wave of paths: chunks ray chunks (7 KB of slot fields, 512 B of slot
-   states, 16 B of lane masks, an 8-byte rayQ entry each) and as many post chunks (512 B of items,
-   an 8-byte postQ entry) */
-int ensureMega(hpt_context *c, uint64_t chunks) {
-    chunks = (chunks + 1023) & ~1023ull;
-    if (chunks > 0x7fffffffull / 64) return setErr(c, HPT_EINVAL, "k_paths: wave too large for its chunk queues");
-    if (chunks <= c->megaChunks) return HPT_OK;
-    freeBufs(c->megaBufs);
-    c->megaChunks = 0;
-    auto alloc = [&](size_t bytes, void **p) -> int {
-        DevBuf b;
-        b.bytes = bytes;
-        HIPCHK(c, hipMalloc(&b.p, bytes));
-        c->megaBufs.push_back(b);
-        *p = b.p;
-        return HPT_OK;
-    };
-    HptMega &M = c->M;
-    int r = 0;
-    r |= alloc(chunks * 64 * HPT_MEGA_FIELDS * 16, (void **) &M.rec);
-    r |= alloc(chunks * 64 * 8, (void **) &M.slotSt);
-    r |= alloc(chunks * 16, (void **) &M.desc);
-    r |= alloc(chunks * 8, (void **) &M.rayQ);
-    r |= alloc(chunks * 64 * 8, (void **) &M.postItems);
-    r |= alloc(chunks * 8, (void **) &M.postQ);
-    r |= alloc(HPT_MC_WORDS * HPT_MC_STRIDE * 4, (void **) &M.ctl);
-    if (r) return HPT_EDEVICE;
-    M.chunkCap = M.postCap = (uint32_t) chunks;
-    c->megaChunks = chunks;
-    return HPT_OK;
-}
-
 /* the traversal-bound fault word (HptScene::fault): cleared before a call's
    launches, read after them; a set bit fails the call */
 int clearFault(hpt_context *c) {
@@ -328,8 +274,6 @@ int checkFault(hpt_context *c) {
         return setErr(c, HPT_ETRAVERSAL, "kd-tree traversal exceeded 2^18 leaf rounds for a ray (malformed tree?)");
     if (f & HPT_FAULT_RESTARTS)
         return setErr(c, HPT_ETRAVERSAL, "kd-tree traversal exceeded its kd-restart bound for a ray");
-    if (f & HPT_FAULT_PATHS)
-        return setErr(c, HPT_EDEVICE, "k_paths found no work for longer than its bound while paths were live");
     return HPT_OK;
 }
 
@@ -347,6 +291,7 @@ hipEvent_t takeEvent(hpt_context *c, size_t &used) {
 extern "C" {
 
 int hpt_context_create(int device, hpt_context **out) {
+    tlsErr.clear(); /* hpt_last_error(NULL) describes this call only */
     if (!out) return HPT_EINVAL;
     *out = nullptr;
     if (device == HPT_HOST_ONLY) {
@@ -391,7 +336,6 @@ void hpt_context_destroy(hpt_context *c) {
     (void) hipStreamSynchronize(c->stream);
     freeBufs(c->sceneBufs);
     freeBufs(c->waveBufs);
-    freeBufs(c->megaBufs);
     if (c->partial) (void) hipFree(c->partial);
     if (c->dBlockOf) (void) hipFree(c->dBlockOf);
     if (c->dLocalOf) (void) hipFree(c->dLocalOf);
@@ -1176,10 +1120,10 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
        packet between two launches, and a frame of 22 launches pays ~4 us per event */
     const bool traceOnly = prm->collect_stats == 3;
     if (counted) HIPCHK(c, hipMemsetAsync(c->dstats, 0, 24 * 8, s));
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> evTrace, evOther[8];
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> evTrace, evOther[7];
     size_t evUsed = 0;
     auto timed = [&](int cls, auto fn) -> hipError_t {
-        if (!st || (traceOnly && cls != -1 && cls != 6 && cls != 7)) return fn();
+        if (!st || (traceOnly && cls != -1 && cls != 6)) return fn();
         hipEvent_t a = takeEvent(c, evUsed), b = takeEvent(c, evUsed);
         (void) hipEventRecord(a, s);
         hipError_t e = fn();
@@ -1246,8 +1190,8 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         /* a wave rendered again after its schedule overflowed must not count twice: the timing
            events and traversal counters of the discarded attempt are rolled back to here */
         const size_t evMark = evTrace.size();
-        size_t evMarkOther[8];
-        for (int i = 0; i < 8; ++i) evMarkOther[i] = evOther[i].size();
+        size_t evMarkOther[7];
+        for (int i = 0; i < 7; ++i) evMarkOther[i] = evOther[i].size();
         if (counted) HIPCHK(c, hipMemcpyAsync(c->dstats + 24, c->dstats, 24 * 8, hipMemcpyDeviceToDevice, s));
         HIPCHK(c, hipMemcpyAsync(c->dBlockCost + costWords, c->dBlockCost, costWords * 4, hipMemcpyDeviceToDevice, s));
         HIPCHK(c, hipMemsetAsync(c->counters, 0, HPT_COUNTER_WORDS * 4, s));
@@ -1319,71 +1263,6 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                                        grid, s);
             });
         };
-        /* a wave with a known schedule runs every bounce in one persistent k_paths launch (not for
-           counted frames: the traversal counters are the wavefront kernels') */
-        const bool usePaths = ahead && c->pathsKernel && !counted && known->second.bounces > 0 &&
-                              !known->second.shade.empty();
-        if (usePaths) {
-            const BounceSchedule &k = known->second;
-            const uint64_t waves = hpt_paths_resident_waves(sc.nShapes > 1);
-            /* ray / post chunks: one per shade step (64 paths), with room for part-filled steps */
-            const uint64_t need =
-                (uint64_t) (((double) k.shade[0] + (double) k.bounces) * c->megaScale / 64.0) + 16 * waves + 1024;
-            if (int rm = ensureMega(c, need)) {
-                (void) hipStreamSynchronize(s);
-                return rm;
-            }
-            c->M.chunkCap = c->M.postCap = (uint32_t) (c->pathsCap ? std::min<uint64_t>(c->pathsCap, c->megaChunks)
-                                                                   : c->megaChunks);
-            /* backlog control (HPT_PATHS_LOW / _HIGH: ray chunks per resident wave; _SHADERS: the
-               most waves that stop tracing to shade, per 64 resident waves) */
-            auto envd = [](const char *k, double d) {
-                const char *v = std::getenv(k);
-                return v ? std::atof(v) : d;
-            };
-            c->M.low = (uint32_t) (envd("HPT_PATHS_LOW", 2.0) * (double) waves);
-            c->M.high = (uint32_t) (envd("HPT_PATHS_HIGH", 4.0) * (double) waves);
-            c->M.maxShaders = (uint32_t) std::max(1.0, envd("HPT_PATHS_SHADERS", 16.0) * (double) waves / 64.0);
-            e = hpt_mega_reset(c->M, s);
-            if (e == hipSuccess)
-                e = timed(7, [&] { return hpt_launch_paths(sc, c->scDev, c->P, c->M, c->qShade[1], C, s); });
-            if (e == hipSuccess && !perLaunch) {
-                HptWave wg = w;
-                wg.doneIf = C;
-                wg.doneParity = HPT_DONE_PATHS;
-                e = timed(4, [&] { return hpt_launch_gather(sc, wg, c->P, c->partial, dFilm, s); });
-                gatheredAhead = true;
-            }
-            if (e == hipSuccess) e = hipMemcpyAsync(hostCnt, C, HPT_Q_COUNT * 4, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            if (e) break;
-            doneAtFirstRead = hptWaveDone(hostCnt, HPT_DONE_PATHS);
-            if (std::getenv("HPT_PATHS_REPORT")) {
-                /* k_paths' control words and phase statistics (HPT_MC_*) on stderr */
-                std::vector<uint32_t> ctl(HPT_MC_WORDS * HPT_MC_STRIDE);
-                if (hipMemcpy(ctl.data(), c->M.ctl, ctl.size() * 4, hipMemcpyDeviceToHost) == hipSuccess) {
-                    auto w32 = [&](int i) { return (unsigned long long) ctl[(size_t) i * HPT_MC_STRIDE]; };
-                    auto w64 = [&](int i) {
-                        uint64_t v;
-                        std::memcpy(&v, &ctl[(size_t) i * HPT_MC_STRIDE], 8);
-                        return (double) v;
-                    };
-                    const double tot = std::max(1.0, w64(HPT_MC_T_TRACE) + w64(HPT_MC_T_SHADE) + w64(HPT_MC_T_IDLE));
-                    std::fprintf(stderr, "[paths] waves %llu chunks %llu ray tail %llu head %llu posts %llu post tail %llu "
-                                 "head %llu init %llu done %llu steps %llu switches %llu claims %.0f phases %.0f | wave "
-                                 "time trace %.3f shade %.3f idle %.3f (%.1f wave-s)\n",
-                                 (unsigned long long) waves, w32(HPT_MC_CHUNKS), w32(HPT_MC_RAY_TAIL), w32(HPT_MC_RAY_HEAD),
-                                 w32(HPT_MC_POSTS), w32(HPT_MC_POST_TAIL), w32(HPT_MC_POST_HEAD), w32(HPT_MC_INIT),
-                                 w32(HPT_MC_DONE), w32(HPT_MC_STEPS), w32(HPT_MC_SWITCHES), w64(HPT_MC_CLAIMS),
-                                 w64(HPT_MC_PHASES), w64(HPT_MC_T_TRACE) / tot, w64(HPT_MC_T_SHADE) / tot,
-                                 w64(HPT_MC_T_IDLE) / tot, tot * 1e-8);
-                    std::fprintf(stderr, "[paths] rounds %.4g lane use %.3f drains %.0f\n", w64(HPT_MC_ROUNDS),
-                                 w64(HPT_MC_LANES) / std::max(1.0, 64.0 * w64(HPT_MC_ROUNDS)), w64(HPT_MC_DRAINS));
-                }
-            }
-            if (hostCnt[HPT_C_OVERFLOW]) c->megaScale *= 2.0; /* the wave is rendered again below */
-            c->stats.paths_launches++;
-        } else {
         if (ahead) {
             const BounceSchedule &k = known->second;
             for (size_t i = 0; i < k.shade.size() && e == hipSuccess; ++i, ++b)
@@ -1438,7 +1317,6 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             seen.shade.push_back(n);
             e = wavefrontBounce(p, n, 0u);
         }
-        } /* usePaths */
         if (e) break;
         if (hostCnt[HPT_C_OVERFLOW] && !ahead) {
             (void) hipStreamSynchronize(s);
@@ -1453,7 +1331,7 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
             c->stats.schedule_misses++;
             for (size_t i = evMark; i < evTrace.size(); ++i) evUsed -= 2; /* events back to the pool */
             evTrace.resize(evMark);
-            for (int i = 0; i < 8; ++i) {
+            for (int i = 0; i < 7; ++i) {
                 for (size_t k = evMarkOther[i]; k < evOther[i].size(); ++k) evUsed -= 2;
                 evOther[i].resize(evMarkOther[i]);
             }
@@ -1468,9 +1346,6 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
                 for (auto &n : seen.shade) n = std::max<uint32_t>(1, n / 2);
             if (c->scheduleTest == 2 && !extended && seen.tail && !seen.shade.empty()) seen.shade.pop_back();
             if (c->schedules.size() >= 4096) c->schedules.clear(); /* e.g. a long run of -r passes */
-            uint64_t shadedAll = 0;
-            std::memcpy(&shadedAll, hostCnt + HPT_C_BOUNCES, 8);
-            seen.bounces = shadedAll + hostCnt[HPT_C_TAIL_BOUNCES];
             c->schedules[key] = seen;
         }
         if (ahead && fits) c->stats.waves_ahead++;
@@ -1517,7 +1392,6 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         c->stats.ms_tail = sumEv(evOther[5]);
         c->stats.ms_trace_packet = sumEv(evOther[6]);
         c->stats.packet_launches = evOther[6].size();
-        c->stats.ms_paths = sumEv(evOther[7]);
     }
     if (counted) {
         uint64_t hs[24];
@@ -1572,6 +1446,7 @@ int hpt_render(hpt_context *c, const hpt_render_params *prm, float *film) {
 }
 
 int hpt_context_share_scene(hpt_context *src, int device, hpt_context **out) {
+    tlsErr.clear(); /* hpt_last_error(NULL) describes this call only */
     if (!src || !out) return HPT_EINVAL;
     *out = nullptr;
     /* src is only read here (several threads may share one source at once): failures are
@@ -1597,7 +1472,6 @@ int hpt_context_share_scene(hpt_context *src, int device, hpt_context **out) {
     c->vdcInv = src->vdcInv;
     c->maxLeafRounds = src->maxLeafRounds, c->maxRestarts = src->maxRestarts, c->packetStack = src->packetStack;
     c->tailPaths = src->tailPaths, c->bounceAhead = src->bounceAhead, c->packets = src->packets;
-    c->pathsKernel = src->pathsKernel, c->pathsCap = src->pathsCap;
     /* the shard deal: hpt_render_multi gives shard g to context g, and every context must deal
        the blocks the same way or some blocks are rendered twice and others never */
     c->blockWeights = src->blockWeights;

@@ -26,7 +26,6 @@
    with whatever hit it had; the render / batch call fails instead) */
 #define HPT_FAULT_LEAVES 1u   /* more than HptScene::maxLeafRounds (2^18) leaf rounds for one ray */
 #define HPT_FAULT_RESTARTS 2u /* more than HptScene::maxRestarts (1024) kd-restarts for one ray */
-#define HPT_FAULT_PATHS 4u    /* k_paths found no work for longer than its bound while paths were still live */
 #define HPT_MAX_LEAF_ROUNDS (1u << 18)
 #define HPT_MAX_RESTARTS 1024u
 /* k_trace work cursors (persistent waves claim rays from them), one per
@@ -58,10 +57,8 @@ struct HptWave {
     const uint32_t *doneIf;
     uint32_t doneParity;
 };
-/* doneParity HPT_DONE_PATHS: the wave's bounces ran in one k_paths launch (done unless it overflowed) */
-#define HPT_DONE_PATHS 2u
 __host__ __device__ inline bool hptWaveDone(const uint32_t *c, uint32_t p) {
-    return (p == HPT_DONE_PATHS || c[HPT_C_SHADE(p)] == 0u || c[HPT_C_TAIL_PATHS] != 0u) && c[HPT_C_OVERFLOW] == 0u &&
+    return (c[HPT_C_SHADE(p)] == 0u || c[HPT_C_TAIL_PATHS] != 0u) && c[HPT_C_OVERFLOW] == 0u &&
            c[HPT_C_ERROR] == 0u;
 }
 
@@ -117,60 +114,6 @@ struct HptPaths {
 
 
 #define HPT_COST_STRIPES 64
-
-/* k_paths: every bounce of a wave of paths in ONE persistent launch (hpt_render.hip).  A wave of
-   the grid shades 64 paths at a time into a ray chunk (64 path-bounce slots) and traces rays
-   from published chunks; the last of a slot's rays to finish appends the slot to the tracing
-   wave's post chunk, and a post chunk's 64 paths are posted and shaded together.  Slot s of
-   chunk s >> 6 keeps HPT_MEGA_FIELDS float4 fields, field f at rec[(s >> 6) * 64 * F + f * 64 +
-   (s & 63)] (a wave's field store or load of one chunk is 1 KB contiguous):
-     0 continuation origin (the hit point) | Sobol index bits 0-31  (also the shadow ray's origin)
-     1 continuation direction | Sobol bits 32-63
-     2 BSDF weight rgb | pdf
-     3 throughput rgb | state
-     4 radiance rgb | path id (26 bits) | shadow ray << 30 | continuation ray << 31
-     5 shadow direction | max t
-     6 NEE contribution rgb */
-#define HPT_MEGA_FIELDS 7
-#define HPT_MEGA_PATH_MASK 0x03ffffffu
-/* control words (HptMega::ctl, one per 128-byte line, zeroed before each launch) */
-#define HPT_MC_CHUNKS 0    /* ray chunks allocated (shade steps) */
-#define HPT_MC_RAY_TAIL 1  /* ray chunks published (rayQ entries written) */
-#define HPT_MC_RAY_HEAD 2  /* rayQ tickets handed out */
-#define HPT_MC_POSTS 3     /* post chunks allocated */
-#define HPT_MC_POST_TAIL 4 /* post chunks published */
-#define HPT_MC_POST_HEAD 5 /* postQ tickets handed out */
-#define HPT_MC_INIT 6      /* initial shade items (k_primary's queue) claimed */
-#define HPT_MC_DONE 7      /* paths finished */
-#define HPT_MC_SHADERS 8   /* waves that stopped tracing to shade (backlog control) */
-#define HPT_MC_ABORT 9     /* a capacity ran out: every wave stops, the host renders the wave again */
-#define HPT_MC_STEPS 10    /* statistics: shade steps */
-#define HPT_MC_SWITCHES 11 /* statistics: trace -> shade switches by choice */
-/* statistics (64-bit words at the start of their lines, summed over the waves at exit): wave time in
-   the trace phase / the shade phase / idle (100 MHz ticks), ray chunks claimed, trace phases */
-#define HPT_MC_T_TRACE 12
-#define HPT_MC_T_SHADE 13
-#define HPT_MC_T_IDLE 14
-#define HPT_MC_CLAIMS 15
-#define HPT_MC_PHASES 16
-#define HPT_MC_ROUNDS 17   /* statistics: traversal rounds of the trace phases (main loop), and */
-#define HPT_MC_LANES 18    /*   the active lanes summed over them (lane use = lanes / 64 rounds) */
-#define HPT_MC_DRAINS 19   /* statistics: drains (trace phases ending with running rays) */
-#define HPT_MC_WORDS 20
-#define HPT_MC_STRIDE 32
-struct HptMega {
-    float4 *rec;         /* chunk fields (above) */
-    uint64_t *slotSt;    /* per slot: hit word << 32 | unoccluded shadow ray << 8 | rays still running */
-    uint64_t *desc;      /* per chunk: [2c] closest-ray lanes, [2c + 1] shadow-ray lanes */
-    uint64_t *rayQ;      /* published ray chunks, chunk + 1 (zero: not yet) */
-    uint64_t *postItems; /* per post chunk: 64 items, slot | unoccluded << 31 | hit word << 32 */
-    uint64_t *postQ;     /* published post chunks, post chunk + 1 | items << 32 */
-    uint32_t *ctl;       /* HPT_MC_* words */
-    uint32_t chunkCap, postCap;
-    /* backlog control, in published but unclaimed ray chunks: a tracing wave may stop to shade when
-       the backlog is below low (at most maxShaders such waves at once); shading stops at high */
-    uint32_t low, high, maxShaders;
-};
 /* hit record of a miss (a segment id never has all 31 bits set) */
 #define HPT_MISS 0xffffffffu
 
@@ -212,22 +155,6 @@ hipError_t hpt_launch_post(const HptScene &sc, const HptPaths &P, const uint32_t
 #define HPT_ITEMS_ON_DEVICE (~0ull)
 hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t *shadeQ, const uint32_t *nShade,
                            uint32_t *counters, uint64_t items, uint32_t tailFrom, hipStream_t s);
-/* k_paths' one kernel argument (the kernel reaches it through the kernarg segment pointer) */
-struct HptPathsArgs {
-    const HptScene *sc; /* the device copy of the scene */
-    HptPaths P;
-    HptMega M;
-    const uint32_t *shadeQ0; /* k_primary's shade queue */
-    uint32_t *counters;
-};
-/* every bounce of the wave in one persistent launch (k_paths): the shade queue shadeQ / *nShade that
-   k_primary filled (parity 1) to termination; HPT_C_BOUNCES counts the path-bounces.  M's control
-   words and queues must be zero (hpt_mega_reset); scDev is the device copy of sc */
-hipError_t hpt_launch_paths(const HptScene &sc, const HptScene *scDev, const HptPaths &P, const HptMega &M,
-                            const uint32_t *shadeQ, uint32_t *counters, hipStream_t s);
-hipError_t hpt_mega_reset(const HptMega &M, hipStream_t s);
-/* k_paths' resident waves (its persistent grid) */
-uint32_t hpt_paths_resident_waves(bool multi);
 /* dst[i] += src[i] over n RGBW pixels (hpt_render_multi's film combine) */
 hipError_t hpt_launch_film_add(float4 *dst, const float4 *src, size_t n, hipStream_t s);
 /* k_splat + k_gather; partial = (nPaths / nSpp) * 9 float4 of scratch */

@@ -38,14 +38,6 @@
 
 using namespace hk;
 
-/* hpt_paths.hip includes this file for its device functions only (HPT_DEVICE_LIB_ONLY): there the
-   kernels below are internal and unused, and the host launch wrappers are left out */
-#ifdef HPT_DEVICE_LIB_ONLY
-#define HPT_KERNEL static __global__ __attribute__((unused))
-#else
-#define HPT_KERNEL extern "C" __global__
-#endif
-
 /* block size of the queue-producing kernels (k_camera, k_primary, k_shade, k_post) */
 #ifndef HPT_SHADE_BLOCK
 #define HPT_SHADE_BLOCK 256 /* k_shade: 4 waves/SIMD of registers; 256-thread blocks overlap better than 1024 (shade 20.9 -> 18.1 ms) */
@@ -826,14 +818,10 @@ struct RaySplitter {
         return nU;
     }
     /* trace every active lane's ray to its answer, idle lanes helping (IO::finish writes it);
-       returns the unoccluded shadow rays finished.  after() runs at the end of every round
-       (wave-uniform: k_paths publishes its post items there) */
-    struct NoAfter {
-        __device__ void operator()() const {}
-    };
-    template <bool LAT, class IO, class Probe, class After = NoAfter>
+       returns the unoccluded shadow rays finished */
+    template <bool LAT, class IO, class Probe>
     __device__ __forceinline__ uint32_t drain(const HptScene &sc, IO &io, TraceRay &r, bool &active, TraceCounters &tc,
-                                              Probe &probe, After after = After{}) {
+                                              Probe &probe) {
         uint32_t nU = 0;
         while (true) {
             step(r, active);
@@ -846,7 +834,6 @@ struct RaySplitter {
                 active = false;
             }
             if (splitM) nU += decide(sc, io, r, active, __ballot(fin) & splitM);
-            after();
         }
         return nU;
     }
@@ -2393,42 +2380,6 @@ HD void qpush(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
     }
 }
 
-/* Hand-off accesses of the persistent bounce kernel (k_paths): data one wave writes and a wave on
-   another CU (another XCD's L2) reads inside the same launch.  Every such byte is stored and
-   loaded as 8-byte agent-scope relaxed atomics (global_store / global_load ... sc1: written
-   through past the writer's L2, read past the reader's L1), and a flag that publishes it is
-   stored after the writing wave's s_waitcnt vmcnt(0) -- the "8-B agent atomics both sides" form
-   of MI355X_MICROARCH.md (inter-workgroup visibility).  Plain loads and stores would leave the
-   data in one XCD's L2 or read a stale line from another. */
-#ifndef HPT_HANDOFF_PLAIN_TIMING
-HD void handoffStore(void *p, uint64_t v) {
-    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-HD uint64_t handoffLoad(const void *p) {
-    return __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-#else /* timing experiment only (make variant): plain accesses, NOT coherent between CUs */
-HD void handoffStore(void *p, uint64_t v) { *reinterpret_cast<volatile uint64_t *>(p) = v; }
-HD uint64_t handoffLoad(const void *p) { return *reinterpret_cast<const volatile uint64_t *>(p); }
-#endif
-HD void handoffStore(float4 *p, float4 v) {
-    uint64_t *q = reinterpret_cast<uint64_t *>(p);
-    handoffStore(q, ((uint64_t) __float_as_uint(v.y) << 32) | __float_as_uint(v.x));
-    handoffStore(q + 1, ((uint64_t) __float_as_uint(v.w) << 32) | __float_as_uint(v.z));
-}
-HD float4 handoffLoadF4(const float4 *p) {
-    const uint64_t *q = reinterpret_cast<const uint64_t *>(p);
-    const uint64_t a = handoffLoad(q), b = handoffLoad(q + 1);
-    return make_float4(__uint_as_float((uint32_t) a), __uint_as_float((uint32_t) (a >> 32)), __uint_as_float((uint32_t) b),
-                       __uint_as_float((uint32_t) (b >> 32)));
-}
-/* every hand-off store this wave issued has completed (written through) before what follows */
-HD void handoffDrain() {
-#ifdef __HIP_DEVICE_COMPILE__
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-}
-
 } // namespace
 
 /* ================================================================== */
@@ -2460,7 +2411,7 @@ HD bool decodePath(const HptWave &w, uint32_t id, int &px, int &py, uint32_t &j)
     return px < w.width && py < w.height;
 }
 
-HPT_KERNEL __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, HptWave w, HptPaths P,
+extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, HptWave w, HptPaths P,
                                                             uint32_t *__restrict__ traceQ,
                                                             uint32_t *__restrict__ nTrace) {
     uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2648,7 +2599,7 @@ __device__ __forceinline__ void clearNextParity(uint32_t *counters, uint32_t q) 
         counters[HPT_C_SHADE(q)] = 0;
     }
 }
-HPT_KERNEL __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ shadowQ,
     const uint32_t *__restrict__ nTrace, const uint32_t *__restrict__ nShadow, uint32_t *__restrict__ cursors,
     uint32_t *counters, uint32_t nextParity) {
@@ -2657,7 +2608,7 @@ HPT_KERNEL __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace(
     clearNextParity(counters, nextParity);
     tracePersistent<HPT_STACK, false>(sc, io, cursors, stk + threadIdx.x, nullptr);
 }
-HPT_KERNEL __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(HptScene sc, HptPaths P,
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_counted(HptScene sc, HptPaths P,
                                                                               const uint32_t *__restrict__ traceQ,
                                                                               const uint32_t *__restrict__ shadowQ,
                                                                               const uint32_t *__restrict__ nTrace,
@@ -2679,13 +2630,13 @@ __device__ __forceinline__ void traceCamera(const HptScene &sc, const HptPaths &
     PathIO io{P, traceQ, nullptr, *nTrace, 0, 0, true, nullptr, false};
     tracePersistent<HPT_STACK, STATS>(sc, io, cursors, stk, stats);
 }
-HPT_KERNEL __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace_camera(
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace_camera(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ nTrace,
     uint32_t *__restrict__ cursors) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     traceCamera<false>(sc, P, traceQ, nTrace, cursors, nullptr, stk + threadIdx.x);
 }
-HPT_KERNEL __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_camera_counted(
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_camera_counted(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ nTrace,
     uint32_t *__restrict__ cursors, uint32_t *stats) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
@@ -2699,14 +2650,14 @@ HPT_KERNEL __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_camera_counted(
 #ifndef HPT_PACKET_BLOCK
 #define HPT_PACKET_BLOCK HPT_TRACE_BLOCK
 #endif
-HPT_KERNEL __launch_bounds__(HPT_PACKET_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_PACKET_WAVES))) void
+extern "C" __global__ __launch_bounds__(HPT_PACKET_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_PACKET_WAVES))) void
 k_trace_packet(HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ nTrace,
                uint32_t *__restrict__ cursors, uint32_t *__restrict__ overflowQ, uint32_t *__restrict__ nOverflow) {
     __shared__ PacketLds lds[HPT_PACKET_BLOCK / 64];
     PathIO io{P, traceQ, nullptr, *nTrace, 0, 0, true, nullptr, false};
     tracePackets<false, false>(sc, io, cursors, lds[threadIdx.x >> 6], nullptr, overflowQ, nOverflow);
 }
-HPT_KERNEL __launch_bounds__(HPT_PACKET_BLOCK) void k_trace_packet_counted(
+extern "C" __global__ __launch_bounds__(HPT_PACKET_BLOCK) void k_trace_packet_counted(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ nTrace,
     uint32_t *__restrict__ cursors, uint32_t *stats, uint32_t *__restrict__ overflowQ, uint32_t *__restrict__ nOverflow) {
     __shared__ PacketLds lds[HPT_PACKET_BLOCK / 64];
@@ -2715,7 +2666,7 @@ HPT_KERNEL __launch_bounds__(HPT_PACKET_BLOCK) void k_trace_packet_counted(
 }
 /* the camera rays of packets whose stack overflowed, one lane per ray (k_trace's traversal;
    a separate symbol so the profiles keep k_trace's launches apart) */
-HPT_KERNEL __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace_overflow(
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) HPT_TRACE_OCCUPANCY void k_trace_overflow(
     HptScene sc, HptPaths P, const uint32_t *__restrict__ traceQ, const uint32_t *__restrict__ overflowQ,
     const uint32_t *__restrict__ nOverflow, uint32_t *__restrict__ cursors) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
@@ -2748,7 +2699,7 @@ HD void fillIts(const HptScene &sc, uint32_t seg, V3 hp, V3 rayD, V3 &p, Frame &
 }
 
 /* primary hits / misses (path.cpp:128-143) */
-HPT_KERNEL __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, HptPaths P,
+extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, HptPaths P,
                                                              const uint32_t *__restrict__ traceQ,
                                                              const uint32_t *__restrict__ nTrace,
                                                              uint32_t *__restrict__ shadeQ,
@@ -2791,18 +2742,13 @@ HPT_KERNEL __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, HptPaths P,
    MULTI: several hair shapes, the hit shape's BSDF comes from sc.bsdfs (a
    separate kernel, so the single-shape one never mixes a kernel-argument
    pointer with a global one -- that would copy the scene to scratch) */
-/* MODE 1 (REC, the wavefront k_shade): the path comes from its shade record in[0..2] and the
+/* REC (the wavefront k_shade): the path comes from its shade record in[0..2] and the
    continuation / shadow ray go to the post record cOut[0..3] / shadow record sOut[0..2]
-   (hpt_kernels.h), which the caller appends with the queues; MODE 2 (k_paths): the same, but the
-   shadow ray's direction | max t and NEE contribution are stored at once into the path-bounce
-   slot's fields 5 / 6 (mOut: the chunk, field f of this lane's slot at mOut[64 f + lane],
-   hand-off stores, see k_paths); MODE 0 (k_tail)
-   keeps everything by path */
-template <bool MULTI, int MODE = 0>
+   (hpt_kernels.h), which the caller appends with the queues; k_tail (REC false) keeps
+   everything by path */
+template <bool MULTI, bool REC = false>
 HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec, uint32_t *__restrict__ counters,
-                  bool &cont, bool &shadow, const float4 *in, float4 *cOut, float4 *sOut, float *wiL,
-                  float4 *mOut = nullptr) {
-    constexpr bool REC = MODE != 0;
+                  bool &cont, bool &shadow, const float4 *in, float4 *cOut, float4 *sOut, float *wiL) {
     {
         const int stride = REC ? HPT_SHADE_BLOCK : (int) blockDim.x; /* REC: k_shade's block, immediate LDS offsets */
         uint32_t st = REC ? __float_as_uint(in[2].w) : P.state[id];
@@ -2883,10 +2829,7 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
                         V3 c = mul(mul(T, val), bsdfVal) * weight;
                         const float4 sd = make_float4(dW.x, dW.y, dW.z, farT * (1 - kShadowEpsilon));
                         const float4 sc4 = make_float4(c.x, c.y, c.z, 0.0f);
-                        if (MODE == 2) { /* mOut: the chunk (uniform); this lane's slot is at + lane */
-                            handoffStore(mOut + 64 * 5 + __lane_id(), sd);
-                            handoffStore(mOut + 64 * 6 + __lane_id(), sc4);
-                        } else if (REC) {
+                        if (REC) {
                             stashV3(wiL, stride, kRowSd, dW);
                             wiL[(kRowSd + 3) * stride] = sd.w;
                             stashV3(wiL, stride, kRowSc, c);
@@ -2976,7 +2919,7 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
         id = shadeQ[tid];
 #pragma unroll
         for (int i = 0; i < 3; ++i) in[i] = P.shadeRec[3 * tid + i];
-        shadePath<MULTI, 1>(sc, P, id, P.hitS[tid], q.counters, cont, shadow, in, cOut, sOut, wiL);
+        shadePath<MULTI, true>(sc, P, id, P.hitS[tid], q.counters, cont, shadow, in, cOut, sOut, wiL);
     }
     qpushBlockRec<HPT_SHADE_BLOCK, 4>(cont, id, traceQ, q.nTrace, P.postRec, cOut);
     if (shadow) { /* the shadow record from its LDS rows */
@@ -2999,13 +2942,13 @@ __device__ __forceinline__ void shadeBounce(const HptScene &sc, HptPaths &P, con
 #else
 #define HPT_SHADE_OCCUPANCY
 #endif
-HPT_KERNEL __launch_bounds__(HPT_SHADE_BLOCK) HPT_SHADE_OCCUPANCY void k_shade(HptScene sc, HptPaths P,
+extern "C" __global__ __launch_bounds__(HPT_SHADE_BLOCK) HPT_SHADE_OCCUPANCY void k_shade(HptScene sc, HptPaths P,
                                                            const uint32_t *__restrict__ shadeQ,
                                                            uint32_t *__restrict__ traceQ,
                                                            uint32_t *__restrict__ shadowQ, HptShadeIO q) {
     shadeBounce<false>(sc, P, shadeQ, traceQ, shadowQ, q);
 }
-HPT_KERNEL __launch_bounds__(HPT_SHADE_BLOCK) void k_shade_multi(HptScene sc, HptPaths P,
+extern "C" __global__ __launch_bounds__(HPT_SHADE_BLOCK) void k_shade_multi(HptScene sc, HptPaths P,
                                                                  const uint32_t *__restrict__ shadeQ,
                                                                  uint32_t *__restrict__ traceQ,
                                                                  uint32_t *__restrict__ shadowQ, HptShadeIO q) {
@@ -3016,10 +2959,9 @@ HPT_KERNEL __launch_bounds__(HPT_SHADE_BLOCK) void k_shade_multi(HptScene sc, Hp
 /* REC (k_post): the path from its post record rec[0..3], and a survivor's throughput and
    state go to sOut[2] of its next shade record (sOut[0..1] = the traced ray = rec[0..1]);
    k_tail (REC false) keeps everything by path */
-/* liReg (k_paths): the path's radiance is carried in a register, not read and written at P.li[id] */
 template <bool REC = false>
 HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, bool hit, uint32_t *__restrict__ counters,
-                 const float4 *rec = nullptr, float4 *sOut = nullptr, float4 *liReg = nullptr) {
+                 const float4 *rec = nullptr, float4 *sOut = nullptr) {
     bool alive = false;
     {
         uint32_t st = REC ? __float_as_uint(rec[3].w) : P.state[id];
@@ -3050,10 +2992,8 @@ HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, bool hit, uint32_
             if (hitEmitter) {
                 float lumPdf = (!(type & HPT_EDELTA)) ? envPdf(sc.env, envToLocal(sc.env, d)) : 0.0f;
                 V3 c = mul(T, value) * miWeight(bw.w, lumPdf);
-                const float4 l = liReg ? *liReg : P.li[id];
-                const float4 ln = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
-                if (liReg) *liReg = ln;
-                else P.li[id] = ln;
+                float4 l = P.li[id];
+                P.li[id] = make_float4(l.x + c.x, l.y + c.y, l.z + c.z, l.w);
             }
             if (hit) {
                 alive = true;
@@ -3084,7 +3024,7 @@ HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, bool hit, uint32_
     return alive;
 }
 /* continuation results of a bounce (the paths of its trace queue) */
-HPT_KERNEL __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc, HptPaths P,
+extern "C" __global__ __launch_bounds__(HPT_POST_BLOCK) void k_post(HptScene sc, HptPaths P,
                                                           const uint32_t *__restrict__ traceQ,
                                                           const uint32_t *__restrict__ nTrace,
                                                           uint32_t *__restrict__ shadeQ, uint32_t *__restrict__ nShade,
@@ -3247,12 +3187,12 @@ __device__ __forceinline__ void tailPaths(const HptScene &sc, HptPaths &P, const
 #ifndef HPT_TAIL_WAVES
 #define HPT_TAIL_WAVES 2
 #endif
-HPT_KERNEL __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void
 k_tail(HptScene sc, HptPaths P, HptTail T, uint32_t *__restrict__ counters) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     tailPaths<false>(sc, P, T, counters, stk + threadIdx.x);
 }
-HPT_KERNEL __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) __attribute__((amdgpu_waves_per_eu(HPT_TAIL_WAVES))) void
 k_tail_multi(HptScene sc, HptPaths P, HptTail T, uint32_t *__restrict__ counters) {
     __shared__ uint2 stk[(HPT_STACK + HPT_RAY_ROWS) * HPT_TRACE_BLOCK];
     tailPaths<true>(sc, P, T, counters, stk + threadIdx.x);
@@ -3267,7 +3207,7 @@ k_tail_multi(HptScene sc, HptPaths P, HptTail T, uint32_t *__restrict__ counters
    (consecutive path ids: coalesced) and accumulate the tent-weighted
    contribution to each of the 3x3 neighbour pixels, reduced across the wave
    with a fixed xor tree -> partial[slot][9] (RGB, weight). */
-HPT_KERNEL __launch_bounds__(256) void k_splat(HptScene sc, HptWave w, HptPaths P,
+extern "C" __global__ __launch_bounds__(256) void k_splat(HptScene sc, HptWave w, HptPaths P,
                                                            float4 *__restrict__ partial) {
     if (w.doneIf && !hptWaveDone(w.doneIf, w.doneParity)) return; /* uniform: the host gathers later */
     const uint32_t slot = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -3323,7 +3263,7 @@ HPT_KERNEL __launch_bounds__(256) void k_splat(HptScene sc, HptWave w, HptPaths 
 
 /* k_gather: every pixel adds, in a fixed neighbour order, the partial sums
    its 3x3 neighbours (owned by this shard) addressed to it. */
-HPT_KERNEL __launch_bounds__(256) void k_gather(HptScene sc, HptWave w, const float4 *__restrict__ partial,
+extern "C" __global__ __launch_bounds__(256) void k_gather(HptScene sc, HptWave w, const float4 *__restrict__ partial,
                                                             float4 *film) {
     if (w.doneIf && !hptWaveDone(w.doneIf, w.doneParity)) return; /* uniform: the host gathers later */
     const uint32_t pix = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3357,7 +3297,7 @@ HPT_KERNEL __launch_bounds__(256) void k_gather(HptScene sc, HptWave w, const fl
 /* ------------------------------------------------------------------ */
 /* Batch entry points for unit parity tests                             */
 /* ------------------------------------------------------------------ */
-HPT_KERNEL void k_sobol_batch(HptScene sc, int m, int n, const uint32_t *frame, const uint32_t *px,
+extern "C" __global__ void k_sobol_batch(HptScene sc, int m, int n, const uint32_t *frame, const uint32_t *px,
                                          const uint32_t *py, const uint32_t *dim, uint64_t *outIdx, float *outVal) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -3367,7 +3307,7 @@ HPT_KERNEL void k_sobol_batch(HptScene sc, int m, int n, const uint32_t *frame, 
 }
 
 /* camera rays at film positions (pixels): k_camera's own ray construction */
-HPT_KERNEL void k_camera_batch(HptScene sc, int n, const float *pos, float *o, float *d, float *mint,
+extern "C" __global__ void k_camera_batch(HptScene sc, int n, const float *pos, float *o, float *d, float *mint,
                                           float *maxt) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -3417,7 +3357,7 @@ struct BatchIO {
     }
 };
 
-HPT_KERNEL __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptScene sc, int n, const float *o,
+extern "C" __global__ __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptScene sc, int n, const float *o,
                                                                             const float *d, const float *mint,
                                                                             const float *maxt, int flags,
                                                                             float *outT, int32_t *outSeg,
@@ -3436,7 +3376,7 @@ HPT_KERNEL __launch_bounds__(HPT_TRACE_BLOCK) void k_trace_batch(HptScene sc, in
         tracePersistent<HPT_STACK, false>(sc, io, cursor, stk + threadIdx.x, nullptr);
 }
 
-HPT_KERNEL void k_bsdf_batch(HptScene sc, int n, const float *wi, const float *wo, const float *u,
+extern "C" __global__ void k_bsdf_batch(HptScene sc, int n, const float *wi, const float *wo, const float *u,
                                         float *outEval, float *outPdf, float *outWo, float *outW, float *outSPdf,
                                         uint32_t *outType) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3461,7 +3401,7 @@ HPT_KERNEL void k_bsdf_batch(HptScene sc, int n, const float *wi, const float *w
     outType[i] = type;
 }
 
-HPT_KERNEL void k_env_batch(HptScene sc, int n, const float *refp, const float *u, const float *dq,
+extern "C" __global__ void k_env_batch(HptScene sc, int n, const float *refp, const float *u, const float *dq,
                                        float *outD, float *outV, float *outPdf, float *outDist, float *outEval,
                                        float *outEvalPdf) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -3490,7 +3430,7 @@ HPT_KERNEL void k_env_batch(HptScene sc, int n, const float *refp, const float *
     outEvalPdf[i] = envPdf(sc.env, envToLocal(sc.env, q));
 }
 
-HPT_KERNEL void k_env_filtered_batch(HptScene sc, int n, const float *d, const float *rx, const float *ry,
+extern "C" __global__ void k_env_filtered_batch(HptScene sc, int n, const float *d, const float *rx, const float *ry,
                                                  float *out) {
     int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -3502,7 +3442,6 @@ HPT_KERNEL void k_env_filtered_batch(HptScene sc, int n, const float *d, const f
 }
 
 
-#ifndef HPT_DEVICE_LIB_ONLY
 /* ------------------------------------------------------------------ */
 /* host-side launch wrappers (declared in hpt_kernels.h)               */
 /* ------------------------------------------------------------------ */
@@ -3644,7 +3583,7 @@ hipError_t hpt_launch_tail(const HptScene &sc, const HptPaths &P, const uint32_t
         hipLaunchKernelGGL(k_tail, dim3(blocks), dim3(HPT_TRACE_BLOCK), 0, s, sc, P, T, counters);
     return hipGetLastError();
 }
-HPT_KERNEL __launch_bounds__(256) void k_film_add(float4 *__restrict__ dst, const float4 *__restrict__ src,
+extern "C" __global__ __launch_bounds__(256) void k_film_add(float4 *__restrict__ dst, const float4 *__restrict__ src,
                                                              uint64_t n) {
     const uint64_t i = (uint64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) {
@@ -3707,4 +3646,3 @@ hipError_t hpt_launch_env_batch(const HptScene &sc, int n, const float *refp, co
                        oe, oep);
     return hipGetLastError();
 }
-#endif /* HPT_DEVICE_LIB_ONLY */

@@ -63,8 +63,7 @@ class Stats(C.Structure):
                 ("packet_exact", C.c_uint64), ("packet_node_slots", C.c_uint64), ("packet_prim_slots", C.c_uint64),
                 ("packet_fallbacks", C.c_uint64), ("max_leaf_rounds", C.c_uint64), ("max_restarts", C.c_uint64),
                 ("restarted_rays", C.c_uint64), ("binary_nodes", C.c_uint64), ("waves_ahead", C.c_uint64),
-                ("schedule_misses", C.c_uint64), ("schedule_extensions", C.c_uint64),
-                ("paths_launches", C.c_uint64), ("ms_paths", C.c_double)]
+                ("schedule_misses", C.c_uint64), ("schedule_extensions", C.c_uint64)]
 
 
 # every symbol declared in include/hairpt.h: (restype, argtypes)

@@ -20,7 +20,8 @@
  *     reads the source);
  *   - calls that fail before they have a context of their own to report on
  *     (hpt_context_create, hpt_context_share_scene) leave the message for the
- *     calling thread: hpt_last_error(NULL).
+ *     calling thread: hpt_last_error(NULL); each such call clears it first, so
+ *     after a success it is empty.
  */
 #ifndef HAIRPT_H
 #define HAIRPT_H
@@ -236,10 +237,6 @@ typedef struct hpt_stats {
     /* waves whose schedule was launched ahead but did not cover them (the tail declined, or
        bounces ran past it): finished bounce by bounce and their schedule re-recorded */
     uint64_t schedule_extensions;
-    /* waves whose bounces ran in one persistent k_paths launch (every bounce of the wave, no
-       per-bounce drain; a wave with a recorded schedule, HPT_PATHS != 0), and its HIP event time */
-    uint64_t paths_launches;
-    double ms_paths;
 } hpt_stats;
 int hpt_get_stats(hpt_context *ctx, hpt_stats *out);
 

@@ -23,7 +23,6 @@ HAIRCURL_RADII = (0.0025, 0.0025)
 
 
 def _render_twice(name, n, radii, monkeypatch, ahead, hook, tail, max_wave=0, times=2):
-    monkeypatch.setenv("HPT_PATHS", "0")  # the wavefront loop's schedules (k_paths: test_gpu_paths.py)
     monkeypatch.setenv("HPT_BOUNCE_AHEAD", ahead)
     monkeypatch.setenv("HPT_SCHEDULE_TEST", hook)
     monkeypatch.setenv("HPT_TAIL_PATHS", tail)
