@@ -50,6 +50,13 @@ def test_share_scene_needs_a_prepared_source(tmp_path):
         r.share_scene(native.HOST_ONLY)
     # the message went to the calling thread (hpt_last_error(NULL)), not to the source context
     assert r.lib.hpt_last_error(r.h).decode() == ""
+    assert "not prepared" in r.lib.hpt_last_error(None).decode()
+    # a later create/share clears the thread's message first: after a success it no longer
+    # describes the earlier failure
+    r.prepare()
+    dst = r.share_scene(native.HOST_ONLY)
+    assert "not prepared" not in r.lib.hpt_last_error(None).decode()
+    dst.close()
     r.close()
 
 
