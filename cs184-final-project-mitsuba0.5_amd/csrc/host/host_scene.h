@@ -179,7 +179,8 @@ struct KDTreeHost {
     std::vector<HptSegment> segs;         /* per segment (index = segment id) */
     std::vector<HptSegF> leafF;           /* fp32 pre-test records in leaf (prims) order */
     std::vector<HptSegQ> leafQ;           /* the same as 16-byte records (quantised axis) */
-    float preRadius = 0.0f;               /* pre-test radius bound for leafQ (HptSegQ) */
+    float preRadius[HPT_PRE_CLASSES] = {}; /* leafQ's pre-test radius per class (HptSegQ) */
+    size_t prePassRecords = 0;            /* leaf records whose bound is unbounded (class radius 1e30) */
     std::vector<HptNode4> nodes4;         /* two-level nodes for the device traversal */
     std::vector<uint32_t> leafTable;      /* (start, end) of leaves too large for an inline ref */
     std::vector<uint32_t> segFirstVertex; /* segment id -> first vertex index */

@@ -792,7 +792,7 @@ static int uploadScene(hpt_context *c) {
     sc.radius = shapes[0].radius;
     sc.maxRadius = 0.0f;
     for (const HptShape &h : shapes) sc.maxRadius = std::max(sc.maxRadius, h.radius);
-    sc.preRadius = std::max(sc.maxRadius, c->tree.preRadius);
+    for (int k = 0; k < HPT_PRE_CLASSES; ++k) sc.preRadius[k] = c->tree.preRadius[k];
     sc.bsdf = c->bsdfRec[shapes[0].bsdf];
     if (nShapes > 1) {
         r |= upload(c, shapes.data(), shapes.size() * sizeof(HptShape), (const void **) &sc.shapes);
@@ -1670,6 +1670,18 @@ int hpt_get_kdtree(hpt_context *c, uint32_t *nodes, int64_t *n_nodes, uint32_t *
             aabb[i] = c->tree.aabbMin[i];
             aabb[3 + i] = c->tree.aabbMax[i];
         }
+    return HPT_OK;
+}
+
+int hpt_get_pretest_records(hpt_context *c, uint32_t *records, int64_t *n_records, float class_radius[4],
+                            uint64_t *n_pass) {
+    if (!c || !n_records) return HPT_EINVAL;
+    static_assert(HPT_PRE_CLASSES == 4 && sizeof(HptSegQ) == 16, "hairpt.h documents 4 classes, 16-byte records");
+    *n_records = (int64_t) c->tree.leafQ.size();
+    if (records) std::memcpy(records, c->tree.leafQ.data(), c->tree.leafQ.size() * sizeof(HptSegQ));
+    if (class_radius)
+        for (int k = 0; k < HPT_PRE_CLASSES; ++k) class_radius[k] = c->tree.preRadius[k];
+    if (n_pass) *n_pass = c->tree.prePassRecords;
     return HPT_OK;
 }
 

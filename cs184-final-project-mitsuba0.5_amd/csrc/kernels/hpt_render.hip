@@ -262,19 +262,28 @@ HD bool segMayHit(const float4 a, const float4 b, V3 o, V3 d, float r) {
 /* HptSegQ: the oct-decoded axis (kdtree_build.cpp's axisOctDecode does the same fp32 operations on
    the host to bound the quantisation angle) and the pre-test on it.  The axis is not unit length
    (|axis| in [1/sqrt(3), 1]): the test is scale-invariant in the axis except for the absolute rounding
-   margin, which a shorter axis only makes looser.  preRadius covers the quantised axis's turn. */
+   margin, which a shorter axis only makes looser.  The record's radius class (its top two bits)
+   picks the radius that covers the quantised axis's turn over its reach. */
 HD V3 axisOctDecode(uint32_t q) {
-    const float u = (float) (q & 0xffffu) * (2.0f / 65535.0f) - 1.0f;
-    const float v = (float) (q >> 16) * (2.0f / 65535.0f) - 1.0f;
+    const float u = (float) (q & 0x7fffu) * (2.0f / 32767.0f) - 1.0f;
+    const float v = (float) ((q >> 15) & 0x7fffu) * (2.0f / 32767.0f) - 1.0f;
     const float z = 1.0f - fabsf(u) - fabsf(v);
     const float fx = (1.0f - fabsf(v)) * (u >= 0.0f ? 1.0f : -1.0f);
     const float fy = (1.0f - fabsf(u)) * (v >= 0.0f ? 1.0f : -1.0f);
     return v3(z < 0.0f ? fx : u, z < 0.0f ? fy : v, z);
 }
-HD bool segMayHitQ(const uint4 q, V3 o, V3 d, float preRadius) {
+HD bool segMayHitQ(const uint4 q, V3 o, V3 d, const float (&preRadius)[HPT_PRE_CLASSES]) {
     const V3 a = axisOctDecode(q.w);
+    /* the class's radius by selects on the two bits (a per-lane index into the kernel argument
+       would go through scratch) */
+#if HPT_EXP_PRE_GLOBAL
+    const float r = preRadius[HPT_PRE_CLASSES - 1]; /* experiment: every record at the largest class radius */
+#else
+    const bool hi = (int) q.w < 0, lo = (q.w & 0x40000000u) != 0;
+    const float r = hi ? (lo ? preRadius[3] : preRadius[2]) : (lo ? preRadius[1] : preRadius[0]);
+#endif
     return segMayHit(make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), a.x),
-                     make_float4(a.y, a.z, 0.0f, 0.0f), o, d, preRadius);
+                     make_float4(a.y, a.z, 0.0f, 0.0f), o, d, r);
 }
 
 /* adaptive ray epsilon: skdtree.cpp:126-129 (closest) / :213-216 (shadow) */
@@ -412,6 +421,13 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
             if (waveLeader()) tc.nodeSlots += 64;
         }
         const uint4 na = nodes4[2 * ref], nb = nodes4[2 * ref + 1];
+#if HPT_EXP_NODE_PAD
+        /* experiment (make variant): 16 more bytes per node fetch, waited on with the node */
+        {
+            const uint4 nc = nodes4[2 * ref + 2];
+            asm volatile("" ::"v"(nc.x), "v"(nc.y), "v"(nc.z), "v"(nc.w));
+        }
+#endif
         const uint32_t flags = na.w;
         /* top split */
         const uint32_t ax0 = flags & 3u;
@@ -483,6 +499,15 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
         if (waveLeader()) tc.nodeSlots += 64;
     }
     uint32_t leafFirst = ref & 0x00ffffffu, leafLast = leafFirst + ((ref >> 24) & 0x7fu);
+#if HPT_EXP_LEAF_RT
+    /* experiment (make variant): one more dependent 4-byte fetch before a leaf's records */
+    {
+        uint32_t z;
+        asm volatile("v_and_b32 %0, 0, %1" : "=v"(z) : "v"(sc.leafSeg[leafFirst]));
+        leafFirst += z;
+        leafLast += z;
+    }
+#endif
     if (((ref >> 24) & 0x7fu) == HPT_LEAF_INLINE_MAX) {
         leafLast = sc.leafTable[2 * leafFirst + 1];
         leafFirst = sc.leafTable[2 * leafFirst];
@@ -512,7 +537,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
             uint32_t mask = 0;
 #pragma unroll
             for (uint32_t k = 0; k < 8; ++k)
-                if (k < n && segMayHit(ra[k], rb[k], o, d, sc.maxRadius)) mask |= 1u << k;
+                if (k < n && segMayHit(ra[k], rb[k], o, d, rb[k].w)) mask |= 1u << k; /* its own radius */
             uint32_t segOf[8];
 #pragma unroll
             for (uint32_t k = 0; k < 8; ++k) segOf[k] = __float_as_uint(rb[k].z);
@@ -1138,7 +1163,7 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
                         tc.prims += act;
                         if (lane == 0) tc.primSlots += 64;
                     }
-                    const bool may = segMayHit(ra[k], rb[k], o, d, sc.maxRadius);
+                    const bool may = segMayHit(ra[k], rb[k], o, d, rb[k].w); /* the record's own radius */
                     mask |= (me && may) ? 1u << k : 0u;
                 }
             }

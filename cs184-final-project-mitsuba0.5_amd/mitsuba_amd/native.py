@@ -108,6 +108,7 @@ SIGNATURES = {
                                  C.c_int]),
     "hpt_get_hair": (C.c_int64, [C.c_void_p, _f, _u8]),
     "hpt_get_kdtree": (C.c_int, [C.c_void_p, _u32, _i64, _u32, _i64, _f]),
+    "hpt_get_pretest_records": (C.c_int, [C.c_void_p, _u32, _i64, _f, _u64]),
     "hpt_get_envmap": (C.c_int, [C.c_void_p, _f, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hpt_get_marschner_tables": (C.c_int, [C.c_void_p, _f, _f, _f, _f, _f, _f]),
     "hpt_get_roughplastic_params": (C.c_int, [C.c_void_p, _f, _f, C.POINTER(C.c_int)]),
@@ -393,6 +394,18 @@ class Renderer:
         self._check(self.lib.hpt_get_kdtree(self.h, _p(nodes, _u32), C.byref(nn), _p(idx, _u32), C.byref(ni),
                                             _p(aabb, _f)))
         return nodes, idx, aabb
+
+    def pretest_records(self):
+        """k_trace's 16-byte pre-test records in leaf order ((n, 4) u32: v1 bits, oct axis | class << 30),
+        the 4 class radii and the number of records whose class passes every test."""
+        n = C.c_int64()
+        self._check(self.lib.hpt_get_pretest_records(self.h, None, C.byref(n), None, None))
+        rec = np.zeros((n.value, 4), np.uint32)
+        radii = np.zeros(4, np.float32)
+        n_pass = C.c_uint64()
+        self._check(self.lib.hpt_get_pretest_records(self.h, _p(rec, _u32), C.byref(n), _p(radii, _f),
+                                                     C.byref(n_pass)))
+        return rec, radii, n_pass.value
 
     def envmap(self):
         w = C.c_int()

@@ -95,30 +95,31 @@ def oracle_shapes(name, n_strands, workdir=None, radii=None):
     return [(f, float(rad), blocks[ref]) for f, ref, rad in zip(files, cfg.get("shapes", ["hair"]), radii)]
 
 
-def make(name, n_strands, width, height, spp, max_depth=None, device=native.HOST_ONLY, radii=None):
+def make(name, n_strands, width, height, spp, max_depth=None, device=native.HOST_ONLY, radii=None, workdir=None):
     """Return (xml_path, product Renderer (prepared), Oracle (prepared, with product kd-tree))."""
     cfg, cam, _ = config_params(name)
     max_depth = cfg["max_depth"] if max_depth is None else max_depth
-    xml = scenes.make_scene(name, WORK, n_strands=n_strands, **({"radii": radii} if radii else {}))
+    xml = scenes.make_scene(name, workdir or WORK, n_strands=n_strands, **({"radii": radii} if radii else {}))
     r = native.Renderer(device=device)
     r.load_scene_xml(xml, {"width": width, "height": height, "spp": spp, "maxDepth": max_depth})
     r.prepare()
     env = oracle_envmap(name)
     nodes, idx, _ = r.kdtree()
     o = oracle_lib.Oracle()
-    o.setup(cam, 35.0, width, height, oracle_shapes(name, n_strands, radii=radii), None, None, env, max_depth,
-            spp=spp)
+    o.setup(cam, 35.0, width, height, oracle_shapes(name, n_strands, workdir, radii=radii), None, None, env,
+            max_depth, spp=spp)
     o.set_kdtree(nodes, idx)
     o.prepare()
     return xml, r, o
 
 
-def reference_flags_floor(name, n_strands, r, width, height, spp, radii=None, max_depth=None, shard=0, n_shards=1):
+def reference_flags_floor(name, n_strands, r, width, height, spp, radii=None, max_depth=None, shard=0, n_shards=1,
+                          workdir=None):
     """L2 between the strict oracle and the oracle built with the reference's
     own compiler flags (liboracle_ref.so): the float-nondeterminism floor that
     any re-implementation of the path inherits (SURVEY.md 7 'Hard parts' i)."""
     cfg, cam, _ = config_params(name)
-    shapes = oracle_shapes(name, n_strands, radii=radii)
+    shapes = oracle_shapes(name, n_strands, workdir, radii=radii)
     films = []
     nodes, idx, _ = r.kdtree()
     for variant in ("parity", "ref"):
@@ -159,3 +160,36 @@ def assert_at_floor(m, floor, same, floor_same, factor=2.0):
     assert m["max"] <= factor * floor["max"] + 1e-5, (m, floor)
     assert m["frac_gt_1e-3"] <= factor * floor["frac_gt_1e-3"] + 2e-3, (m, floor)
     assert same >= floor_same - 0.05, (same, floor_same)
+
+
+def fold_workdir(n_strands, folded=True):
+    """A work directory whose furball hair file (the name scenes.hair_files looks for) has three
+    strands folded back on themselves near the camera -- an exact hairpin (a vertex returns to the
+    one before last: opposite tangents, NaN miter normals, a segment no exact test accepts,
+    hair.cpp:521-531), a near-exact fold (one ulp off the hairpin: a miter plane almost parallel to
+    the axis, so the segment's axial reach is ~1e5 radii) and a 179.9 degree fold -- or, with
+    folded=False, the same furball unfolded (the fold-free twin).  Scenes made with
+    scenes.make_scene(..., workdir) / make(..., workdir=) read it."""
+    d = os.path.join(WORK, "folds_%d_%d" % (n_strands, int(folded)))
+    os.makedirs(d, exist_ok=True)
+    path = os.path.join(d, "furball_%d.mitshair" % n_strands)
+    if os.path.exists(path):
+        return d
+    strands = [np.asarray(x, np.float32).copy() for x in scenes.synth_hair.furball(n_strands)]
+    if folded:
+        cam = np.array([float(x) for x in scenes.FURBALL_CAM.split()]).reshape(4, 4)[:3, 3]
+        near = np.argsort([np.linalg.norm(x[0] - cam) for x in strands])
+        pick = [int(k) for k in near if len(strands[k]) >= 6][:3]
+        hp, nf, f179 = (strands[k] for k in pick)
+        hp[3] = hp[1]                                          # exact hairpin at vertex 2
+        nf[3] = nf[1]
+        nf[3, 0] = np.nextafter(nf[3, 0], np.float32(np.inf))  # one ulp off it
+        back = (f179[1] - f179[2]).astype(np.float64)          # 179.9 degrees at vertex 2
+        side = np.cross(back, [0.3, 1.0, 0.2])
+        side /= np.linalg.norm(side)
+        ang = np.radians(0.1)
+        f179[3] = (f179[2] + np.cos(ang) * back + np.sin(ang) * np.linalg.norm(back) * side).astype(np.float32)
+    tmp = path + ".tmp%d" % os.getpid()
+    scenes.synth_hair.write_binary_hair(tmp, strands)
+    os.replace(tmp, path)
+    return d

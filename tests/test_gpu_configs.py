@@ -25,7 +25,7 @@ from mitsuba_amd import native
 pytestmark = pytest.mark.gpu
 
 
-def _parity(name, n, r, o, w, h, spp, max_depth=None, factor=2.0, shard=0, n_shards=1):
+def _parity(name, n, r, o, w, h, spp, max_depth=None, factor=2.0, shard=0, n_shards=1, workdir=None):
     film = r.render(0, spp, shard=shard, n_shards=n_shards, collect_stats=2)
     s = r.stats()
     ofilm, ostats = o.render(0, spp, threads=16, shard=shard, n_shards=n_shards, width=w, height=h)
@@ -35,7 +35,7 @@ def _parity(name, n, r, o, w, h, spp, max_depth=None, factor=2.0, shard=0, n_sha
     m = scene_util.l2_metrics(b, a)
     same = np.all(np.abs(a - b) <= 1e-5 * np.abs(b) + 1e-7, axis=-1)
     floor, floor_same = scene_util.reference_flags_floor(name, n, r, w, h, spp, max_depth=max_depth, shard=shard,
-                                                         n_shards=n_shards)
+                                                         n_shards=n_shards, workdir=workdir)
     print(name, n, (w, h, spp), "gpu vs oracle", m, "identical %.4f" % same.mean(), "| floor", floor,
           "identical %.4f" % floor_same, "| longest ray: %d leaf rounds, %d restarts, %d rays restarted"
           % (s.max_leaf_rounds, s.max_restarts, s.restarted_rays))
@@ -76,6 +76,31 @@ def test_furball_1m_reduced_matches_oracle():
     si = r.info()
     assert si.segments > 900000 and si.max_depth == 64
     _parity("furball_1m", 125000, r, o, 128, 96, 8, max_depth=64)
+
+
+def test_folded_strands_match_oracle_and_keep_the_pretest(monkeypatch):
+    """A furball with an exact hairpin, a one-ulp near-hairpin and a 179.9 degree fold near the
+    camera (scene_util.fold_workdir; hair.cpp:485-548,551-596: the miter planes of a fold are
+    almost parallel to the axis, or NaN for the exact hairpin): the film matches the oracle at the
+    reference-flags floor, and -- each pre-test record carrying its own radius class -- the fp64
+    exact tests per traced ray stay within 5 % of the fold-free twin's (one global bound would
+    have tested every record of the scene at the near-hairpin's ~570 radii).  Every bounce goes
+    through k_trace (HPT_TAIL_PATHS=0: no k_tail), whose counters the ratio reads."""
+    monkeypatch.setenv("HPT_TAIL_PATHS", "0")
+    n, w, h, spp = 3000, 128, 96, 8
+    per_ray = {}
+    for folded in (False, True):
+        d = scene_util.fold_workdir(n, folded)
+        _, r, o = scene_util.make("furball_marschner", n, w, h, spp, device=0, workdir=d)
+        rec, radii, _ = r.pretest_records()
+        s = _parity("furball_marschner", n, r, o, w, h, spp, workdir=d)
+        per_ray[folded] = s.prim_exact / (s.closest_rays + s.shadow_rays)
+        print("folded" if folded else "fold-free", "class radii / r", radii / 0.00216667,
+              "records per class", np.bincount(rec[:, 3] >> 30, minlength=4),
+              "exact tests per ray %.4f" % per_ray[folded])
+        if folded:
+            assert radii[3] > 100 * 0.00216667  # the near-hairpin is in the scene
+    assert per_ray[True] <= 1.05 * per_ray[False], per_ray
 
 
 def _full_size(name, n, w, h, spp, max_depth, parity_spp=64):
