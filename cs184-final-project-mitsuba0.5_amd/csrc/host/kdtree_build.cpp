@@ -570,8 +570,8 @@ void buildNode4(const BNode *root, KDTreeHost &t) {
     if (t.leafTable.empty()) t.leafTable.push_back(0), t.leafTable.push_back(0);
 }
 
-/* HptSegQ's axis: oct encoding (15:15, the word's top two bits hold the record's radius class) of
-   the fp64 axis, and its decode with the device's fp32 operations (axisOctDecode in hpt_render.hip) */
+/* HptSegQ's axis: oct encoding (16:16) of the fp64 axis, and its decode with the device's fp32
+   operations (axisOctDecode in hpt_render.hip) */
 uint32_t axisOctEncode(const double a[3]) {
     const double l1 = std::fabs(a[0]) + std::fabs(a[1]) + std::fabs(a[2]);
     double u = a[0] / l1, v = a[1] / l1;
@@ -581,13 +581,13 @@ uint32_t axisOctEncode(const double a[3]) {
         u = fu, v = fv;
     }
     auto q = [](double x) {
-        return (uint32_t) std::min(32767.0, std::max(0.0, std::nearbyint((x * 0.5 + 0.5) * 32767.0)));
+        return (uint32_t) std::min(65535.0, std::max(0.0, std::nearbyint((x * 0.5 + 0.5) * 65535.0)));
     };
-    return q(u) | (q(v) << 15);
+    return q(u) | (q(v) << 16);
 }
 void axisOctDecode(uint32_t q, float &x, float &y, float &z) {
-    const float u = (float) (q & 0x7fffu) * (2.0f / 32767.0f) - 1.0f;
-    const float v = (float) ((q >> 15) & 0x7fffu) * (2.0f / 32767.0f) - 1.0f;
+    const float u = (float) (q & 0xffffu) * (2.0f / 65535.0f) - 1.0f;
+    const float v = (float) (q >> 16) * (2.0f / 65535.0f) - 1.0f;
     z = 1.0f - std::fabs(u) - std::fabs(v);
     x = u;
     y = v;
@@ -621,95 +621,6 @@ double quantisedReach(const HptSegment &g, double r, float ax, float ay, float a
                                  (g.v2[2] - g.v1[2]) * (g.v2[2] - g.v1[2]));
     const double reach = std::max(r * tanOf(g.n1, g.axis), len + r * tanOf(g.n2, g.axis));
     return sinTheta == 0.0 ? r : r + reach * sinTheta; /* an unturned axis: no widening, even for infinite reach */
-}
-
-/* The pre-test radius classes: every leaf record is tested at the radius of its class, the smallest
-   class radius at or above its own bound (quantisedReach).  A bound that is not finite -- a miter
-   plane parallel to the axis, a strand folding straight back -- gets a class of its own that passes
-   every test (1e30: kept finite so the device's products never form inf * 0).  The finite classes
-   are placed by an exact dynamic program over the sorted bounds (bucketed to 512 quantiles): the
-   cost of a class radius is the number of records tested at it times the radius, a pre-test's pass
-   rate for a thin cylinder growing with its radius up to a saturation -- so one widened strand (a near-fold) or a
-   thicker shape no longer widens the test of every other record.  Returns each record's class. */
-std::vector<uint8_t> pretestClasses(const std::vector<double> &bound, float cls[HPT_PRE_CLASSES], size_t &nPass) {
-    const size_t n = bound.size();
-    std::vector<uint8_t> out(n, 0);
-    std::vector<double> fin;
-    fin.reserve(n);
-    nPass = 0;
-    for (double b : bound) {
-        if (std::isnan(b)) continue; /* a NaN miter normal: the exact test never accepts (hair.cpp:521-531) */
-        if (b < 1e30) fin.push_back(b);
-        else ++nPass;
-    }
-    std::sort(fin.begin(), fin.end());
-    const int kFin = nPass ? HPT_PRE_CLASSES - 1 : HPT_PRE_CLASSES;
-    /* candidate radii: the bounds at 256 count quantiles and at 256 steps of a geometric grid from
-       the least bound to the largest (so a few far-out bounds -- a fold -- never share a bin with
-       the bulk); a record goes to the bin of the least candidate at or above its bound */
-    std::vector<double> cand;
-    std::vector<double> cnt;
-    const size_t m = fin.size();
-    if (m > 0) {
-        const size_t nq = std::min<size_t>(256, m);
-        for (size_t k = 0; k < nq; ++k) cand.push_back(fin[(k + 1) * m / nq - 1]);
-        const double lo = std::max(fin[0], 1e-30), ratio = fin[m - 1] / lo;
-        for (int k = 1; k <= 256; ++k) {
-            const double g = lo * std::pow(ratio, k / 256.0);
-            const size_t i = (size_t) (std::upper_bound(fin.begin(), fin.end(), g) - fin.begin());
-            if (i > 0) cand.push_back(fin[i - 1]);
-        }
-        cand.push_back(fin[m - 1]);
-        std::sort(cand.begin(), cand.end());
-        cand.erase(std::unique(cand.begin(), cand.end()), cand.end());
-        size_t below = 0;
-        for (double c : cand) {
-            const size_t upTo = (size_t) (std::upper_bound(fin.begin(), fin.end(), c) - fin.begin());
-            cnt.push_back((double) (upTo - below));
-            below = upTo;
-        }
-    }
-    const size_t nc = cand.size();
-    std::vector<double> radii;
-    if (nc > 0) {
-        std::vector<double> pre(nc + 1, 0.0);
-        for (size_t i = 0; i < nc; ++i) pre[i + 1] = pre[i] + cnt[i];
-        const int K = (int) std::min<size_t>(kFin, nc);
-        /* dp[k][i]: least cost of bins 0..i with k + 1 class radii, the top one at cand[i] */
-        const double inf = std::numeric_limits<double>::infinity();
-        std::vector<std::vector<double>> dp(K, std::vector<double>(nc, inf));
-        std::vector<std::vector<int>> from(K, std::vector<int>(nc, -1));
-        /* a radius many times the least bound passes about every ray that reaches the record's
-           leaf: the cost saturates there, so two far-out bounds share a class and the bulk keeps
-           the classes it can use */
-        const double sat = 16.0 * cand[0];
-        auto cost = [&](size_t i) { return std::min(cand[i], sat); };
-        for (size_t i = 0; i < nc; ++i) dp[0][i] = pre[i + 1] * cost(i);
-        for (int k = 1; k < K; ++k)
-            for (size_t i = k; i < nc; ++i)
-                for (size_t j = k - 1; j < i; ++j) {
-                    const double c = dp[k - 1][j] + (pre[i + 1] - pre[j + 1]) * cost(i);
-                    if (c < dp[k][i]) dp[k][i] = c, from[k][i] = (int) j;
-                }
-        int k = K - 1;
-        for (int i = (int) nc - 1; i >= 0 && k >= 0; i = from[k][i], --k) radii.push_back(cand[i]);
-        std::reverse(radii.begin(), radii.end());
-    }
-    /* a 1e-5 relative slack covers the fp32 rounding of the radius itself and of the device's decode */
-    int nr = 0;
-    for (double r : radii) cls[nr++] = (float) std::min(r * (1.0 + 1e-5), 1e30);
-    const int top = nr;
-    while (nr < HPT_PRE_CLASSES) cls[nr++] = nPass || top == 0 ? 1e30f : cls[top - 1];
-    for (size_t e = 0; e < n; ++e) {
-        const double b = bound[e];
-        if (std::isnan(b)) continue;
-        int c = 0;
-        if (b >= 1e30) c = HPT_PRE_CLASSES - 1;
-        else
-            while ((double) cls[c] < b) ++c; /* the class radii cover every finite bound */
-        out[e] = (uint8_t) c;
-    }
-    return out;
 }
 
 } // namespace
@@ -821,7 +732,14 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
         f.seg = s;
         f.radius = hair.radiusOf(segIv[s]);
     }
-    /* the 16-byte records, each with the radius class of its own bound (pretestClasses) */
+    /* the 16-byte records and the radius of each leaf's pre-test: the largest bound
+       (quantisedReach) of the leaf's records, so a fold -- a miter plane almost parallel to its axis,
+       a bound of hundreds of radii or none at all -- widens only the leaves that hold it, and a
+       leaf of a thinner shape is tested at that shape's radius.  A NaN bound (a NaN miter normal:
+       the exact test never accepts the segment, hair.cpp:521-531) widens nothing; an unbounded one
+       gives 1e30, which passes every test and is kept finite so the device's products never form
+       inf * 0.  A 1e-5 relative slack covers the fp32 rounding of the radius itself and of the
+       device's decode. */
     t.leafQ.resize(t.prims.size());
     {
         std::vector<double> reach(S, -1.0), bound(t.prims.size());
@@ -838,8 +756,22 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
             }
             bound[e] = reach[s];
         }
-        const std::vector<uint8_t> cls = pretestClasses(bound, t.preRadius, t.prePassRecords);
-        for (size_t e = 0; e < t.prims.size(); ++e) t.leafQ[e].axisOct |= (uint32_t) cls[e] << 30;
+        t.leafRad.assign(t.prims.size() + 1, 0.0f); /* + 1: an empty leaf at the end may read it */
+        t.preRadius = 0.0f;
+        t.preWideLeaves = 0;
+        for (const HptNode &nd : t.nodes) {
+            if (!(nd.w0 & 0x80000000u)) continue;
+            const uint32_t a = nd.w0 & 0x7fffffffu, b = nd.w1;
+            double m = 0.0, rmax = 0.0;
+            for (uint32_t e = a; e < b; ++e) {
+                if (!std::isnan(bound[e])) m = std::max(m, bound[e]);
+                rmax = std::max(rmax, (double) t.leafF[e].radius);
+            }
+            const float rad = (float) std::min(m * (1.0 + 1e-5), 1e30);
+            for (uint32_t e = a; e < b; ++e) t.leafRad[e] = rad;
+            t.preRadius = std::max(t.preRadius, rad);
+            if (b > a && rad > 1.02 * rmax) ++t.preWideLeaves;
+        }
     }
     t.buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return t;

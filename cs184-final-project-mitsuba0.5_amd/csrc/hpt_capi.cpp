@@ -306,18 +306,21 @@ int hpt_context_create(int device, hpt_context **out) {
         return HPT_OK;
     }
     int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return HPT_EDEVICE;
-    if (device < 0 || device >= n) return HPT_EINVAL;
-    if (hipSetDevice(device) != hipSuccess) return HPT_EDEVICE;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return setErr(nullptr, HPT_EDEVICE, "no HIP device");
+    if (device < 0 || device >= n)
+        return setErr(nullptr, HPT_EINVAL, "device " + std::to_string(device) + " of " + std::to_string(n));
+    if (hipSetDevice(device) != hipSuccess) return setErr(nullptr, HPT_EDEVICE, "hipSetDevice failed");
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return HPT_EDEVICE;
-    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return HPT_EDEVICE;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+        return setErr(nullptr, HPT_EDEVICE, "hipGetDeviceProperties failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return setErr(nullptr, HPT_EDEVICE, std::string("not a gfx950 device: ") + prop.gcnArchName);
     hpt_context *c = new hpt_context();
     c->device = device;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void **) &c->hostCnt, HPT_Q_COUNT * 4, hipHostMallocDefault) != hipSuccess) {
         delete c;
-        return HPT_EDEVICE;
+        return setErr(nullptr, HPT_EDEVICE, "stream / pinned counter allocation failed");
     }
     c->dataDir = defaultDataDir();
     std::memset(&c->sc, 0, sizeof(c->sc));
@@ -745,6 +748,7 @@ static int uploadScene(hpt_context *c) {
     r |= upload(c, c->tree.leafTable.data(), c->tree.leafTable.size() * 4, (const void **) &sc.leafTable);
     r |= upload(c, c->tree.leafF.data(), c->tree.leafF.size() * sizeof(HptSegF), (const void **) &sc.leafF);
     r |= upload(c, c->tree.leafQ.data(), c->tree.leafQ.size() * sizeof(HptSegQ), (const void **) &sc.leafQ);
+    r |= upload(c, c->tree.leafRad.data(), c->tree.leafRad.size() * 4, (const void **) &sc.leafRad);
     r |= upload(c, c->tree.prims.data(), c->tree.prims.size() * 4, (const void **) &sc.leafSeg);
     r |= upload(c, c->tree.segs.data(), c->tree.segs.size() * sizeof(HptSegment), (const void **) &sc.segs);
     for (int i = 0; i < 3; ++i) {
@@ -792,7 +796,6 @@ static int uploadScene(hpt_context *c) {
     sc.radius = shapes[0].radius;
     sc.maxRadius = 0.0f;
     for (const HptShape &h : shapes) sc.maxRadius = std::max(sc.maxRadius, h.radius);
-    for (int k = 0; k < HPT_PRE_CLASSES; ++k) sc.preRadius[k] = c->tree.preRadius[k];
     sc.bsdf = c->bsdfRec[shapes[0].bsdf];
     if (nShapes > 1) {
         r |= upload(c, shapes.data(), shapes.size() * sizeof(HptShape), (const void **) &sc.shapes);
@@ -1673,15 +1676,15 @@ int hpt_get_kdtree(hpt_context *c, uint32_t *nodes, int64_t *n_nodes, uint32_t *
     return HPT_OK;
 }
 
-int hpt_get_pretest_records(hpt_context *c, uint32_t *records, int64_t *n_records, float class_radius[4],
-                            uint64_t *n_pass) {
+int hpt_get_pretest_records(hpt_context *c, uint32_t *records, float *radius, int64_t *n_records,
+                            uint64_t *wide_leaves) {
     if (!c || !n_records) return HPT_EINVAL;
-    static_assert(HPT_PRE_CLASSES == 4 && sizeof(HptSegQ) == 16, "hairpt.h documents 4 classes, 16-byte records");
-    *n_records = (int64_t) c->tree.leafQ.size();
-    if (records) std::memcpy(records, c->tree.leafQ.data(), c->tree.leafQ.size() * sizeof(HptSegQ));
-    if (class_radius)
-        for (int k = 0; k < HPT_PRE_CLASSES; ++k) class_radius[k] = c->tree.preRadius[k];
-    if (n_pass) *n_pass = c->tree.prePassRecords;
+    static_assert(sizeof(HptSegQ) == 16, "hairpt.h documents 16-byte records");
+    const size_t n = c->tree.leafQ.size();
+    *n_records = (int64_t) n;
+    if (records) std::memcpy(records, c->tree.leafQ.data(), n * sizeof(HptSegQ));
+    if (radius) std::memcpy(radius, c->tree.leafRad.data(), n * 4);
+    if (wide_leaves) *wide_leaves = c->tree.preWideLeaves;
     return HPT_OK;
 }
 

@@ -56,19 +56,17 @@ struct HptSegF {
 };
 
 /* 16-byte pre-test record of the per-lane traversal (k_trace), leaf order:
- * the segment's first vertex, its axis oct-encoded in 15:15 bits (one dwordx4
- * per record instead of 24 of HptSegF's 32 bytes) and, in the top two bits,
- * the record's radius class.  The quantised axis turns the pre-test line by an
- * angle theta; the record's bound is its shape's radius widened by its axial
- * reach (up to the miter planes) times sin(theta), and it is tested at
- * HptScene::preRadius[class], the smallest class radius covering that bound
- * (kdtree_build.cpp pretestClasses), so the test stays conservative per record.
- * Decoded by axisOctDecode (hpt_render.hip) and its host twin in
- * kdtree_build.cpp, with the same fp32 operations. */
-#define HPT_PRE_CLASSES 4
+ * the segment's first vertex and its axis oct-encoded in 16:16 bits (one
+ * dwordx4 per record instead of 24 of HptSegF's 32 bytes).  The quantised
+ * axis turns the pre-test line by an angle theta; a record's bound is its
+ * shape's radius widened by its axial reach (up to the miter planes) times
+ * sin(theta), and a leaf's records are tested at the largest bound in the leaf
+ * (HptScene::leafRad, kdtree_build.cpp), so the test stays conservative and a
+ * fold widens only its own leaves.  Decoded by axisOctDecode (hpt_render.hip)
+ * and its host twin in kdtree_build.cpp, with the same fp32 operations. */
 struct HptSegQ {
     float v1[3];
-    uint32_t axisOct; /* bits 0-14 u, 15-29 v, 30-31 radius class */
+    uint32_t axisOct;
 };
 
 /* kd-tree node, 8 bytes (gkdtree.h:452-583 layout with absolute child index):
@@ -215,7 +213,7 @@ struct HptScene {
     float aabbMin[3], aabbMax[3];
     float radius;               /* shape 0's radius (every shape's when nShapes == 1) */
     float maxRadius;            /* largest shape radius: bound for the conservative fp32 pre-test */
-    float preRadius[HPT_PRE_CLASSES]; /* the HptSegQ pre-test's radius per class (see HptSegQ) */
+    const float *leafRad;       /* the HptSegQ pre-test's radius per leaf entry (its leaf's, see HptSegQ) */
     HptBsdf bsdf;               /* shape 0's BSDF */
     /* several hair shapes (hair-curl): HptSegment::shape indexes shapes[],
        which gives the radius and the entry of bsdfs[] (both in HBM: a kernel

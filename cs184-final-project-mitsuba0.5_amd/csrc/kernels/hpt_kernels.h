@@ -76,7 +76,7 @@ __host__ __device__ inline uint32_t hptState(uint32_t st, uint32_t depth, uint32
 /* path state, structure of arrays in HBM (16-byte rows where possible) */
 struct HptPaths {
     float4 *ro;        /* ray origin xyz, mint                       */
-    float4 *rd;        /* ray direction xyz, maxt                    */
+    float4 *rd;        /* ray direction xyz, maxt (k_camera: direction xyz, 1 / d.z in camera space) */
     float2 *pos;       /* film sample position (pixels)              */
     uint64_t *sobol;   /* Sobol index of the sample (look_up)        */
     uint32_t *state;   /* dim[0:11) | depth[11:24) | sampledType[24:31) | scattered[31] */

@@ -262,28 +262,24 @@ HD bool segMayHit(const float4 a, const float4 b, V3 o, V3 d, float r) {
 /* HptSegQ: the oct-decoded axis (kdtree_build.cpp's axisOctDecode does the same fp32 operations on
    the host to bound the quantisation angle) and the pre-test on it.  The axis is not unit length
    (|axis| in [1/sqrt(3), 1]): the test is scale-invariant in the axis except for the absolute rounding
-   margin, which a shorter axis only makes looser.  The record's radius class (its top two bits)
-   picks the radius that covers the quantised axis's turn over its reach. */
+   margin, which a shorter axis only makes looser.  The leaf's radius covers the quantised axis's
+   turn over the reach of each of its records.  rr = radius * 1.000001 is formed once per leaf and
+   stands in for both of segMayHit's radius terms (the margin 3e-6 rr is the larger). */
 HD V3 axisOctDecode(uint32_t q) {
-    const float u = (float) (q & 0x7fffu) * (2.0f / 32767.0f) - 1.0f;
-    const float v = (float) ((q >> 15) & 0x7fffu) * (2.0f / 32767.0f) - 1.0f;
+    const float u = (float) (q & 0xffffu) * (2.0f / 65535.0f) - 1.0f;
+    const float v = (float) (q >> 16) * (2.0f / 65535.0f) - 1.0f;
     const float z = 1.0f - fabsf(u) - fabsf(v);
     const float fx = (1.0f - fabsf(v)) * (u >= 0.0f ? 1.0f : -1.0f);
     const float fy = (1.0f - fabsf(u)) * (v >= 0.0f ? 1.0f : -1.0f);
     return v3(z < 0.0f ? fx : u, z < 0.0f ? fy : v, z);
 }
-HD bool segMayHitQ(const uint4 q, V3 o, V3 d, const float (&preRadius)[HPT_PRE_CLASSES]) {
+HD bool segMayHitQ(const uint4 q, V3 o, V3 d, float rr) {
     const V3 a = axisOctDecode(q.w);
-    /* the class's radius by selects on the two bits (a per-lane index into the kernel argument
-       would go through scratch) */
-#if HPT_EXP_PRE_GLOBAL
-    const float r = preRadius[HPT_PRE_CLASSES - 1]; /* experiment: every record at the largest class radius */
-#else
-    const bool hi = (int) q.w < 0, lo = (q.w & 0x40000000u) != 0;
-    const float r = hi ? (lo ? preRadius[3] : preRadius[2]) : (lo ? preRadius[1] : preRadius[0]);
-#endif
-    return segMayHit(make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), a.x),
-                     make_float4(a.y, a.z, 0.0f, 0.0f), o, d, r);
+    const float wx = o.x - __uint_as_float(q.x), wy = o.y - __uint_as_float(q.y), wz = o.z - __uint_as_float(q.z);
+    const float nx = d.y * a.z - d.z * a.y, ny = d.z * a.x - d.x * a.z, nz = d.x * a.y - d.y * a.x;
+    const float nn = nx * nx + ny * ny + nz * nz;
+    const float wn = fabsf(wx * nx + wy * ny + wz * nz);
+    return wn <= rr * __builtin_amdgcn_sqrtf(nn) + 3e-6f * (rr + fabsf(wx) + fabsf(wy) + fabsf(wz));
 }
 
 /* adaptive ray epsilon: skdtree.cpp:126-129 (closest) / :213-216 (shadow) */
@@ -520,6 +516,9 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
        16-byte HptSegQ records (one dwordx4 per record: the kernel's vector
        memory path is busy ~3/4 of its cycles) */
     const uint32_t first = leafFirst, last = leafLast;
+    /* the leaf's pre-test radius (HptScene::leafRad), fetched with its first record */
+    float rr = 0.0f;
+    if (!LAT && first < last) rr = sc.leafRad[first] * 1.000001f;
     if (LAT) {
         /* latency mode (k_tail: few waves, registers to spare): every record of a
            chunk of 8 is requested at once and each candidate's whole fp64 record in
@@ -577,7 +576,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
                 tc.shadowPrims += r.shadow ? 1u : 0u;
                 if (waveLeader()) tc.primSlots += 64;
             }
-            if (segMayHitQ(fq, o, d, sc.preRadius)) mask |= 1u << (e - c0);
+            if (segMayHitQ(fq, o, d, rr)) mask |= 1u << (e - c0);
         }
         while (mask) {
             const uint32_t e = c0 + (uint32_t) (__ffs(mask) - 1);
@@ -2411,17 +2410,32 @@ HD void qpush(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
 /* Kernels                                                             */
 /* ================================================================== */
 
-/* PerspectiveCameraImpl::sampleRayDifferential, the ray itself (perspective.cpp:271-290) */
-HD void cameraRay(const HptCamera &c, float posx, float posy, V3 &o, V3 &dw, float &mint, float &maxt) {
+/* PerspectiveCameraImpl::sampleRayDifferential, the ray itself (perspective.cpp:271-290).  The
+   origin is the same for every ray (cameraOrigin), and mint / maxt are the clip distances times
+   1 / d.z: k_camera stores the world direction and that factor, and the trace launch and
+   k_primary rebuild the ray from them bit for bit (cameraRayFrom). */
+HD V3 cameraOrigin(const HptCamera &c) {
+    const float *T = c.toWorld;
+    return v3(T[0] * 0.0f + T[1] * 0.0f + T[2] * 0.0f + T[3], T[4] * 0.0f + T[5] * 0.0f + T[6] * 0.0f + T[7],
+              T[8] * 0.0f + T[9] * 0.0f + T[10] * 0.0f + T[11]);
+}
+HD void cameraRay(const HptCamera &c, float posx, float posy, V3 &o, V3 &dw, float &mint, float &maxt,
+                  float *invZOut = nullptr) {
     const V3 nearP = xformPoint(c.s2c, v3(posx * c.invResX, posy * c.invResY, 0.0f));
     const V3 d = normalize(nearP);
     const float invZ = 1.0f / d.z;
-    const float *T = c.toWorld;
-    o = v3(T[0] * 0.0f + T[1] * 0.0f + T[2] * 0.0f + T[3], T[4] * 0.0f + T[5] * 0.0f + T[6] * 0.0f + T[7],
-           T[8] * 0.0f + T[9] * 0.0f + T[10] * 0.0f + T[11]);
-    dw = xformVector(T, d);
+    o = cameraOrigin(c);
+    dw = xformVector(c.toWorld, d);
     mint = c.nearClip * invZ;
     maxt = c.farClip * invZ;
+    if (invZOut) *invZOut = invZ;
+}
+/* the camera ray from k_camera's record {world direction, 1 / d.z} */
+HD void cameraRayFrom(const HptCamera &c, float4 rec, V3 &o, V3 &dw, float &mint, float &maxt) {
+    o = cameraOrigin(c);
+    dw = v3(rec.x, rec.y, rec.z);
+    mint = c.nearClip * rec.w;
+    maxt = c.farClip * rec.w;
 }
 
 /* Decode a path id of the current wave: id = slot * nSpp + (j - sppBegin),
@@ -2459,19 +2473,16 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
         }
         float posx = px + ox, posy = py + oy;
         if (wps > 1) quad = (posx - px >= 0.5f ? 1u : 0u) | (posy - py >= 0.5f ? 2u : 0u);
+        /* the ray as its world direction and 1 / d.z (cameraRayFrom rebuilds the common origin
+           and the clip distances): 16 bytes instead of 32.  A camera path's throughput (1), state
+           (dim 2, depth 1) and radiance (0, or the environment on a miss) are k_primary's to
+           write, so none of them goes through HBM here */
         V3 o, dw;
-        float mint, maxt;
-        cameraRay(c, posx, posy, o, dw, mint, maxt);
-        P.ro[id] = make_float4(o.x, o.y, o.z, mint);
-        P.rd[id] = make_float4(dw.x, dw.y, dw.z, maxt);
+        float mint, maxt, invZ;
+        cameraRay(c, posx, posy, o, dw, mint, maxt, &invZ);
+        P.rd[id] = make_float4(dw.x, dw.y, dw.z, invZ);
         P.pos[id] = make_float2(posx, posy);
         P.sobol[id] = sidx;
-        /* a camera path's throughput (1) and state (dim 2, depth 1) are the same for every path:
-           k_primary writes them into its shade record, none goes through HBM here */
-        P.li[id] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    } else if (id < w.nPaths) {
-        P.state[id] = 0xffffffffu; /* outside the image */
-        P.li[id] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     qpushCamera<HPT_QBLOCK>(valid, quad, wps, id, traceQ, nTrace);
 }
@@ -2512,6 +2523,12 @@ struct PathIO {
             const uint32_t q = posQ ? posQ[k] : k;
             const uint32_t path = traceQ[q];
             id = byQueue ? q : path; /* the key: where finish() writes the record */
+            if (byQueue) { /* the camera pass: k_camera's record {direction, 1 / d.z} */
+                V3 o, dw;
+                float mint, maxt;
+                cameraRayFrom(sc.cam, P.rd[path], o, dw, mint, maxt);
+                return beginRay(sc, r, o, dw, mint, maxt, false);
+            }
             const float4 ro = P.ro[path], rd = P.rd[path];
             return beginRay(sc, r, v3(ro.x, ro.y, ro.z), v3(rd.x, rd.y, rd.z), ro.w, rd.w, false);
         }
@@ -2738,27 +2755,29 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_primary(HptScene sc, 
     if (tid < n) {
         id = traceQ[tid];
         seg = P.hitQ[tid];
+        V3 o, d;
+        float mint, maxt;
+        cameraRayFrom(sc.cam, P.rd[id], o, d, mint, maxt);
+        float4 li = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         if (seg != HPT_MISS) {
             alive = true;
             /* the shade record (hpt_kernels.h): the camera ray, its Sobol index, throughput 1 and
                the camera state (dim = 2, depth = 1) */
-            const float4 ro = P.ro[id], rd = P.rd[id];
             const uint64_t sidx = P.sobol[id];
-            sOut[0] = make_float4(ro.x, ro.y, ro.z, __uint_as_float((uint32_t) sidx));
-            sOut[1] = make_float4(rd.x, rd.y, rd.z, __uint_as_float((uint32_t) (sidx >> 32)));
+            sOut[0] = make_float4(o.x, o.y, o.z, __uint_as_float((uint32_t) sidx));
+            sOut[1] = make_float4(d.x, d.y, d.z, __uint_as_float((uint32_t) (sidx >> 32)));
             sOut[2] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(hptState(0u, 1u, 2u)));
         } else if (!sc.hideEmitters) {
             /* a camera ray keeps its differentials: EWA-filtered lookup (envmap.cpp:394-406) */
-            const float4 rd = P.rd[id];
             const float2 pos = P.pos[id];
-            const V3 d = v3(rd.x, rd.y, rd.z);
             V3 rx, ry;
             cameraDifferentials(sc.cam, pos.x, pos.y, d, rx, ry);
             V3 L = envEvalFiltered(sc.env, d, rx, ry); /* throughput == 1 */
             V3 T = v3(1.0f, 1.0f, 1.0f);
             V3 c = mul(T, L);
-            P.li[id] = make_float4(0.0f + c.x, 0.0f + c.y, 0.0f + c.z, 0.0f);
+            li = make_float4(0.0f + c.x, 0.0f + c.y, 0.0f + c.z, 0.0f);
         }
+        P.li[id] = li; /* every camera path's radiance starts here */
     }
     qpushBlockRec<HPT_QBLOCK, 3>(alive, id, shadeQ, nShade, P.shadeRec, sOut, P.hitS, seg);
 }

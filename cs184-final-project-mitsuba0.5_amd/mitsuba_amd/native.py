@@ -108,7 +108,7 @@ SIGNATURES = {
                                  C.c_int]),
     "hpt_get_hair": (C.c_int64, [C.c_void_p, _f, _u8]),
     "hpt_get_kdtree": (C.c_int, [C.c_void_p, _u32, _i64, _u32, _i64, _f]),
-    "hpt_get_pretest_records": (C.c_int, [C.c_void_p, _u32, _i64, _f, _u64]),
+    "hpt_get_pretest_records": (C.c_int, [C.c_void_p, _u32, _f, _i64, _u64]),
     "hpt_get_envmap": (C.c_int, [C.c_void_p, _f, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hpt_get_marschner_tables": (C.c_int, [C.c_void_p, _f, _f, _f, _f, _f, _f]),
     "hpt_get_roughplastic_params": (C.c_int, [C.c_void_p, _f, _f, C.POINTER(C.c_int)]),
@@ -135,7 +135,10 @@ def load_library(path: str = None):
         if not os.path.exists(path):
             raise OSError("libhairpt.so not built at %s (run __graft_entry__.build())" % path)
         lib = C.CDLL(path)
+        experiment = path != LIB_PATH
         for name, (res, args) in SIGNATURES.items():
+            if experiment and not hasattr(lib, name):
+                continue  # an older experiment build: exports added since then stay unbound
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
@@ -396,16 +399,16 @@ class Renderer:
         return nodes, idx, aabb
 
     def pretest_records(self):
-        """k_trace's 16-byte pre-test records in leaf order ((n, 4) u32: v1 bits, oct axis | class << 30),
-        the 4 class radii and the number of records whose class passes every test."""
+        """k_trace's 16-byte pre-test records in leaf order ((n, 4) u32: v1 bits, oct axis), the radius
+        each is tested at (its leaf's) and the number of leaves tested 2 % above their shape's radius."""
         n = C.c_int64()
-        self._check(self.lib.hpt_get_pretest_records(self.h, None, C.byref(n), None, None))
+        self._check(self.lib.hpt_get_pretest_records(self.h, None, None, C.byref(n), None))
         rec = np.zeros((n.value, 4), np.uint32)
-        radii = np.zeros(4, np.float32)
-        n_pass = C.c_uint64()
-        self._check(self.lib.hpt_get_pretest_records(self.h, _p(rec, _u32), C.byref(n), _p(radii, _f),
-                                                     C.byref(n_pass)))
-        return rec, radii, n_pass.value
+        radius = np.zeros(n.value, np.float32)
+        wide = C.c_uint64()
+        self._check(self.lib.hpt_get_pretest_records(self.h, _p(rec, _u32), _p(radius, _f), C.byref(n),
+                                                     C.byref(wide)))
+        return rec, radius, wide.value
 
     def envmap(self):
         w = C.c_int()

@@ -1,14 +1,13 @@
 """The 16-byte pre-test record (HptSegQ, hpt_device.h) stays conservative, per record.
 
 k_trace's leaf pass rejects a segment when the ray line passes farther than its
-record's class radius from the line through v1 along the *oct-quantised* axis
+leaf's pre-test radius from the line through v1 along the *oct-quantised* axis
 (segMayHitQ, hpt_render.hip).  A point the exact test accepts (hair.cpp:
 485-548: inside the cylinder and between the two miter planes) lies at an
 axial offset s in [-r tan(phi1), len + r tan(phi2)] from v1, so within
 r + |s| sin(theta) of the quantised line: that is the record's bound
-(kdtree_build.cpp quantisedReach), and kdtree_build.cpp pretestClasses gives
-each record the smallest of four class radii covering it (a bound that is not
-finite gets a class that passes every test).  This test restates the encode /
+(kdtree_build.cpp quantisedReach), and a leaf is tested at the largest bound
+of its records (HptScene::leafRad), so a fold widens only its own leaves.  This test restates the encode /
 decode and the bound in numpy (fp32 where the device computes in fp32) and
 checks, on rays aimed at points just inside random mitered cylinders (grazing
 and head-on), that every ray the fp64 exact test accepts passes the quantised
@@ -29,22 +28,22 @@ F = np.float32
 
 
 def oct_encode(a):
-    """kdtree_build.cpp axisOctEncode: fp64 axis -> 15:15 bits (bits 30-31: the radius class)."""
+    """kdtree_build.cpp axisOctEncode: fp64 axis -> 16:16 bits."""
     l1 = np.abs(a).sum(axis=1)
     u, v = a[:, 0] / l1, a[:, 1] / l1
     neg = a[:, 2] < 0
     fu = (1.0 - np.abs(v)) * np.where(u >= 0, 1.0, -1.0)
     fv = (1.0 - np.abs(u)) * np.where(v >= 0, 1.0, -1.0)
     u, v = np.where(neg, fu, u), np.where(neg, fv, v)
-    q = lambda x: np.clip(np.rint((x * 0.5 + 0.5) * 32767.0), 0, 32767).astype(np.uint32)  # noqa: E731
-    return q(u) | (q(v) << 15)
+    q = lambda x: np.clip(np.rint((x * 0.5 + 0.5) * 65535.0), 0, 65535).astype(np.uint32)  # noqa: E731
+    return q(u) | (q(v) << 16)
 
 
 def oct_decode(q):
     """axisOctDecode (device and host): fp32 operations."""
-    k = F(2.0) / F(32767.0)
-    u = (q & 0x7FFF).astype(F) * k - F(1)
-    v = ((q >> 15) & 0x7FFF).astype(F) * k - F(1)
+    k = F(2.0) / F(65535.0)
+    u = (q & 0xFFFF).astype(F) * k - F(1)
+    v = (q >> 16).astype(F) * k - F(1)
     z = F(1) - np.abs(u) - np.abs(v)
     fx = (F(1) - np.abs(v)) * np.where(u >= 0, F(1), F(-1))
     fy = (F(1) - np.abs(u)) * np.where(v >= 0, F(1), F(-1))
@@ -62,7 +61,7 @@ def test_oct_roundtrip_angle_small():
     a[:6] = [[1, 0, 0], [0, 1, 0], [0, 0, 1], [-1, 0, 0], [0, -1, 0], [0, 0, -1]]
     q = oct_decode(oct_encode(a)).astype(np.float64)
     sin_t = np.linalg.norm(np.cross(a, q), axis=1) / np.linalg.norm(q, axis=1)
-    assert sin_t.max() < 2e-4  # 15-bit oct cells: a few 1e-5 rad
+    assert sin_t.max() < 1e-4  # 16-bit oct cells: a few 1e-5 rad
     assert np.all(np.linalg.norm(q, axis=1) >= 1 / np.sqrt(3) - 1e-6)
 
 
@@ -155,7 +154,8 @@ def exact_hits(o, d, v1, v2, a, n1, n2, r):
 
 
 def pretest(o, d, v1f, qa, rad):
-    """segMayHit on the decoded axis at radius rad (per record), fp32 without contraction."""
+    """segMayHitQ on the decoded axis at its leaf's radius rad (per record), fp32 without contraction:
+    rr = rad * 1.000001 stands in for both radius terms."""
     w = o - v1f
     ax, ay, az = qa[:, 0], qa[:, 1], qa[:, 2]
     nx = d[:, 1] * az - d[:, 2] * ay
@@ -163,8 +163,9 @@ def pretest(o, d, v1f, qa, rad):
     nz = d[:, 0] * ay - d[:, 1] * ax
     nn = nx * nx + ny * ny + nz * nz
     wn = np.abs(w[:, 0] * nx + w[:, 1] * ny + w[:, 2] * nz)
-    margin = F(3e-6) * (rad + np.abs(w[:, 0]) + np.abs(w[:, 1]) + np.abs(w[:, 2]))
-    return wn <= rad * np.sqrt(nn) * F(1.000001) + margin
+    rr = (rad * F(1.000001)).astype(F)
+    margin = F(3e-6) * (rr + np.abs(w[:, 0]) + np.abs(w[:, 1]) + np.abs(w[:, 2]))
+    return wn <= rr * np.sqrt(nn) + margin
 
 
 def _segments(r):
@@ -173,8 +174,8 @@ def _segments(r):
     xyz, starts = r.hair()
     _, iv, _ = r.kdtree()
     iv = iv.astype(np.int64)
-    rec, radii, n_pass = r.pretest_records()
-    assert rec.shape == (len(iv), 4)
+    rec, radius, wide = r.pretest_records()
+    assert rec.shape == (len(iv), 4) and radius.shape == (len(iv),)
     X = xyz.astype(np.float64)
 
     def nrm(x):
@@ -186,7 +187,7 @@ def _segments(r):
     has_prev, has_next = starts[iv] == 0, starts[iv + 2] == 0
     n1 = np.where(has_prev[:, None], nrm(nrm(v1 - X[np.maximum(iv - 1, 0)]) + a), a)
     n2 = np.where(has_next[:, None], nrm(a + nrm(X[np.minimum(iv + 2, len(X) - 1)] - v2)), a)
-    return v1, v2, a, n1, n2, rec, radii, n_pass
+    return v1, v2, a, n1, n2, rec, radius, wide
 
 
 def _fold_renderer(folded):
@@ -208,38 +209,39 @@ def fold_scene():
 def test_library_records_match_the_restatement(fold_scene):
     # the library's axis bits are numpy's oct_encode of the fp64 axis, v1 its fp32 first vertex
     v1, _, a, _, _, rec, _, _ = _segments(fold_scene)
-    np.testing.assert_array_equal(rec[:, 3] & 0x3FFFFFFF, oct_encode(a))
+    np.testing.assert_array_equal(rec[:, 3], oct_encode(a))
     np.testing.assert_array_equal(rec[:, :3].view(np.float32), v1.astype(np.float32))
 
 
-def test_fold_gets_a_class_of_its_own(fold_scene):
-    v1, v2, a, n1, n2, rec, radii, n_pass = _segments(fold_scene)
+def test_fold_widens_only_its_leaves(fold_scene):
+    v1, v2, a, n1, n2, rec, radius, wide = _segments(fold_scene)
     rad = F(0.00216667)
-    cls = rec[:, 3] >> 30
-    assert np.all(np.diff(radii) >= 0) and radii[0] >= rad
-    # the near-exact fold's bound is many radii (its miter plane is almost parallel to its axis) ...
-    assert radii[3] > 5 * rad, radii
-    # ... but only its own records are tested at it: the others keep radii within a few % of r
     with np.errstate(invalid="ignore"):
         folded = (np.abs(np.sum(n1 * a, 1)) < 0.01) | (np.abs(np.sum(n2 * a, 1)) < 0.01)
-    far = radii[cls] > 1.5 * rad
-    assert 0 < far.sum() <= 8 and np.all(folded[far]), (far.sum(), radii)
-    assert radii[cls][~folded].mean() < 1.02 * rad and radii[cls][~folded].max() < 1.1 * rad, radii
-    assert n_pass == 0  # a one-ulp fold is wide but finite; the exact hairpin's NaN normals never hit
     nan_normal = np.isnan(n1).any(1) | np.isnan(n2).any(1)
-    assert nan_normal.sum() >= 2  # both segments at the hairpin
+    near = folded & ~nan_normal
+    # the near-hairpin's bound is hundreds of radii: its leaves are tested that wide ...
+    assert near.sum() >= 2 and radius[near].max() > 5 * rad, radius[near]
+    # ... and only they: every other record keeps a radius within 2 % of the shape's
+    widened = radius > 1.02 * rad
+    assert 0 < wide <= 16 and widened.sum() < 0.01 * len(rec), (wide, widened.sum())
+    assert np.all(radius >= rad)
+    # the exact hairpin's NaN miter normals (no exact test accepts the segment) widen nothing
+    assert nan_normal.sum() >= 2
 
 
-def test_per_record_class_radius_is_conservative(fold_scene):
-    """Rays aimed just inside each record's mitered cylinder -- every fold record and a sample of
-    the rest -- pass the pre-test at the record's class radius whenever the exact test hits."""
-    v1, v2, a, n1, n2, rec, radii, _ = _segments(fold_scene)
+def test_per_record_pretest_is_conservative(fold_scene):
+    """Rays aimed just inside each record's mitered cylinder -- every record of a widened leaf and a
+    sample of the rest -- pass the pre-test at the record's leaf radius whenever the exact test
+    hits; at the shape's radius the fold records' exact hits would be rejected."""
+    v1, v2, a, n1, n2, rec, radius, _ = _segments(fold_scene)
     rng = np.random.default_rng(11)
-    cls = rec[:, 3] >> 30
     qa = oct_decode(rec[:, 3])
     rad = 0.00216667
     ok = ~(np.isnan(n1).any(1) | np.isnan(n2).any(1))
-    wide = np.nonzero(ok & (radii[cls] > 1.02 * rad))[0]
+    with np.errstate(invalid="ignore"):
+        folded = (np.abs(np.sum(n1 * a, 1)) < 0.01) | (np.abs(np.sum(n2 * a, 1)) < 0.01)
+    wide = np.nonzero(ok & folded)[0]
     rest = rng.choice(np.nonzero(ok)[0], 4000, replace=False)
     e = np.concatenate([np.repeat(wide, 4000), np.repeat(rest, 20)])
     n = len(e)
@@ -261,12 +263,14 @@ def test_per_record_class_radius_is_conservative(fold_scene):
     o = (p - d.astype(np.float64) * rng.uniform(0.01, 0.2, size=n)[:, None]).astype(F)
     hit = exact_hits(o, d, V1, V2, A, N1, N2, r)
     assert hit[: len(wide) * 4000].sum() > 1000 and hit.sum() > n // 5
-    may = pretest(o, d, V1.astype(F), qa[e], radii[cls[e]])
-    assert not np.any(hit & ~may), "class radius rejected %d exact hits" % np.sum(hit & ~may)
+    may = pretest(o, d, V1.astype(F), qa[e], radius[e])
+    assert not np.any(hit & ~may), "pre-test rejected %d exact hits" % np.sum(hit & ~may)
+    narrow = pretest(o, d, V1.astype(F), qa[e], np.full(n, F(1.02 * rad)))
+    assert np.any(hit & ~narrow), "no fold record needed its widened leaf"
 
 
-def test_fold_free_twin_has_no_wide_class():
+def test_fold_free_twin_radius():
     r = _fold_renderer(False)
-    _, _, _, _, _, rec, radii, n_pass = _segments(r)
-    assert n_pass == 0 and radii[3] < 1.02 * 0.00216667, radii
+    _, _, _, _, _, rec, radius, wide = _segments(r)
+    assert radius.max() < 1.02 * 0.00216667 and wide == 0, (radius.max(), wide)
     r.close()
