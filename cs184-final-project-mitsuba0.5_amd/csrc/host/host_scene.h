@@ -179,9 +179,8 @@ struct KDTreeHost {
     std::vector<HptSegment> segs;         /* per segment (index = segment id) */
     std::vector<HptSegF> leafF;           /* fp32 pre-test records in leaf (prims) order */
     std::vector<HptSegQ> leafQ;           /* the same as 16-byte records (quantised axis) */
-    std::vector<float> leafRad;           /* leafQ's pre-test radius per leaf entry (its leaf's, HptSegQ) */
-    float preRadius = 0.0f;               /* the largest of them */
-    size_t preWideLeaves = 0;             /* leaves tested 2 % or more above their thickest shape's radius */
+    float preRadius = 0.0f;               /* leafQ's pre-test radius (HptSegQ), flagged records aside */
+    size_t prePassRecords = 0;            /* records flagged to pass every pre-test (HPT_PRE_PASS) */
     std::vector<HptNode4> nodes4;         /* two-level nodes for the device traversal */
     std::vector<uint32_t> leafTable;      /* (start, end) of leaves too large for an inline ref */
     std::vector<uint32_t> segFirstVertex; /* segment id -> first vertex index */

@@ -570,8 +570,8 @@ void buildNode4(const BNode *root, KDTreeHost &t) {
     if (t.leafTable.empty()) t.leafTable.push_back(0), t.leafTable.push_back(0);
 }
 
-/* HptSegQ's axis: oct encoding (16:16) of the fp64 axis, and its decode with the device's fp32
-   operations (axisOctDecode in hpt_render.hip) */
+/* HptSegQ's axis: oct encoding (u 16 bits, v 15 bits; bit 31 is the record's pass flag) of the
+   fp64 axis, and its decode with the device's fp32 operations (axisOctDecode in hpt_render.hip) */
 uint32_t axisOctEncode(const double a[3]) {
     const double l1 = std::fabs(a[0]) + std::fabs(a[1]) + std::fabs(a[2]);
     double u = a[0] / l1, v = a[1] / l1;
@@ -580,14 +580,12 @@ uint32_t axisOctEncode(const double a[3]) {
         const double fv = (1.0 - std::fabs(u)) * (v >= 0.0 ? 1.0 : -1.0);
         u = fu, v = fv;
     }
-    auto q = [](double x) {
-        return (uint32_t) std::min(65535.0, std::max(0.0, std::nearbyint((x * 0.5 + 0.5) * 65535.0)));
-    };
-    return q(u) | (q(v) << 16);
+    auto q = [](double x, double m) { return (uint32_t) std::min(m, std::max(0.0, std::nearbyint((x * 0.5 + 0.5) * m))); };
+    return q(u, 65535.0) | (q(v, 32767.0) << 16);
 }
 void axisOctDecode(uint32_t q, float &x, float &y, float &z) {
     const float u = (float) (q & 0xffffu) * (2.0f / 65535.0f) - 1.0f;
-    const float v = (float) (q >> 16) * (2.0f / 65535.0f) - 1.0f;
+    const float v = (float) ((q >> 16) & 0x7fffu) * (2.0f / 32767.0f) - 1.0f;
     z = 1.0f - std::fabs(u) - std::fabs(v);
     x = u;
     y = v;
@@ -602,6 +600,7 @@ void axisOctDecode(uint32_t q, float &x, float &y, float &z) {
    len + r tan(phi2)] (phi = the angle between the axis and a miter plane's normal, hair.cpp:
    537-541), so it lies within r + |s| sin(theta) of the quantised line through v1 (theta = the
    angle between the two axes).  Returns r + max|s| sin(theta) for one segment. */
+#define HPT_PASS_REACH 1.05
 double quantisedReach(const HptSegment &g, double r, float ax, float ay, float az) {
     /* a NaN miter normal (a strand folding exactly back: the bisector of opposite tangents) fails
        both plane tests of hair.cpp:521-531, so the exact test never accepts the segment: NaN */
@@ -715,6 +714,15 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
     auto tl = std::chrono::steady_clock::now();
     t.nodes.reserve(2 * S);
     layoutTreelets(tree.get(), t);
+    /* each segment's pre-test bound on its 16-byte record (quantisedReach) */
+    std::vector<double> segBound(S);
+    std::vector<float> segRad(S);
+    for (size_t s = 0; s < S; ++s) {
+        float x, y, z;
+        axisOctDecode(axisOctEncode(t.segs[s].axis), x, y, z);
+        segRad[s] = hair.radiusOf(segIv[s]);
+        segBound[s] = quantisedReach(t.segs[s], (double) segRad[s], x, y, z);
+    }
     buildNode4(tree.get(), t);
     if (std::getenv("HPT_KD_TIMING"))
         std::fprintf(stderr, "kd: bounds %.3f s, build %.3f s, layout %.3f s\n",
@@ -732,47 +740,31 @@ KDTreeHost buildHairKDTree(const HairData &hair, const KDBuildParams &params) {
         f.seg = s;
         f.radius = hair.radiusOf(segIv[s]);
     }
-    /* the 16-byte records and the radius of each leaf's pre-test: the largest bound
-       (quantisedReach) of the leaf's records, so a fold -- a miter plane almost parallel to its axis,
-       a bound of hundreds of radii or none at all -- widens only the leaves that hold it, and a
-       leaf of a thinner shape is tested at that shape's radius.  A NaN bound (a NaN miter normal:
-       the exact test never accepts the segment, hair.cpp:521-531) widens nothing; an unbounded one
-       gives 1e30, which passes every test and is kept finite so the device's products never form
-       inf * 0.  A 1e-5 relative slack covers the fp32 rounding of the radius itself and of the
-       device's decode. */
+    /* the 16-byte records.  A record whose bound exceeds its shape's radius by more than
+       HPT_PASS_REACH -- a fold: a miter plane almost parallel to the axis, a bound of hundreds of
+       radii or none at all -- is flagged to pass every pre-test (its exact test decides), and the
+       scene's pre-test radius is the largest bound of the others: a fold no longer widens the
+       test of every record.  (A NaN bound -- a NaN miter normal, which no exact test accepts,
+       hair.cpp:521-531 -- needs neither.)  A 1e-5 relative slack covers the fp32 rounding of the
+       radius itself and of the device's decode. */
     t.leafQ.resize(t.prims.size());
-    {
-        std::vector<double> reach(S, -1.0), bound(t.prims.size());
-        for (size_t e = 0; e < t.prims.size(); ++e) {
-            const uint32_t s = t.prims[e];
-            HptSegQ &q = t.leafQ[e];
-            for (int k = 0; k < 3; ++k) q.v1[k] = t.leafF[e].v1[k];
-            q.axisOct = axisOctEncode(t.segs[s].axis);
-            if (reach[s] < 0.0) {
-                float x, y, z;
-                axisOctDecode(q.axisOct, x, y, z);
-                reach[s] = quantisedReach(t.segs[s], (double) t.leafF[e].radius, x, y, z);
-                if (reach[s] < 0.0) reach[s] = 1e30; /* not reached: the bound is never negative */
-            }
-            bound[e] = reach[s];
-        }
-        t.leafRad.assign(t.prims.size() + 1, 0.0f); /* + 1: an empty leaf at the end may read it */
-        t.preRadius = 0.0f;
-        t.preWideLeaves = 0;
-        for (const HptNode &nd : t.nodes) {
-            if (!(nd.w0 & 0x80000000u)) continue;
-            const uint32_t a = nd.w0 & 0x7fffffffu, b = nd.w1;
-            double m = 0.0, rmax = 0.0;
-            for (uint32_t e = a; e < b; ++e) {
-                if (!std::isnan(bound[e])) m = std::max(m, bound[e]);
-                rmax = std::max(rmax, (double) t.leafF[e].radius);
-            }
-            const float rad = (float) std::min(m * (1.0 + 1e-5), 1e30);
-            for (uint32_t e = a; e < b; ++e) t.leafRad[e] = rad;
-            t.preRadius = std::max(t.preRadius, rad);
-            if (b > a && rad > 1.02 * rmax) ++t.preWideLeaves;
+    double preBound = 0.0;
+    t.prePassRecords = 0;
+    for (size_t e = 0; e < t.prims.size(); ++e) {
+        const uint32_t s = t.prims[e];
+        HptSegQ &q = t.leafQ[e];
+        for (int k = 0; k < 3; ++k) q.v1[k] = t.leafF[e].v1[k];
+        q.axisOct = axisOctEncode(t.segs[s].axis);
+        const double b = segBound[s];
+        if (std::isnan(b)) continue;
+        if (b > HPT_PASS_REACH * segRad[s]) {
+            q.axisOct |= HPT_PRE_PASS;
+            ++t.prePassRecords;
+        } else {
+            preBound = std::max(preBound, b);
         }
     }
+    t.preRadius = (float) (preBound * (1.0 + 1e-5));
     t.buildSeconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     return t;
 }

@@ -748,7 +748,6 @@ static int uploadScene(hpt_context *c) {
     r |= upload(c, c->tree.leafTable.data(), c->tree.leafTable.size() * 4, (const void **) &sc.leafTable);
     r |= upload(c, c->tree.leafF.data(), c->tree.leafF.size() * sizeof(HptSegF), (const void **) &sc.leafF);
     r |= upload(c, c->tree.leafQ.data(), c->tree.leafQ.size() * sizeof(HptSegQ), (const void **) &sc.leafQ);
-    r |= upload(c, c->tree.leafRad.data(), c->tree.leafRad.size() * 4, (const void **) &sc.leafRad);
     r |= upload(c, c->tree.prims.data(), c->tree.prims.size() * 4, (const void **) &sc.leafSeg);
     r |= upload(c, c->tree.segs.data(), c->tree.segs.size() * sizeof(HptSegment), (const void **) &sc.segs);
     for (int i = 0; i < 3; ++i) {
@@ -796,6 +795,7 @@ static int uploadScene(hpt_context *c) {
     sc.radius = shapes[0].radius;
     sc.maxRadius = 0.0f;
     for (const HptShape &h : shapes) sc.maxRadius = std::max(sc.maxRadius, h.radius);
+    sc.preRadius = c->tree.preRadius;
     sc.bsdf = c->bsdfRec[shapes[0].bsdf];
     if (nShapes > 1) {
         r |= upload(c, shapes.data(), shapes.size() * sizeof(HptShape), (const void **) &sc.shapes);
@@ -1676,15 +1676,15 @@ int hpt_get_kdtree(hpt_context *c, uint32_t *nodes, int64_t *n_nodes, uint32_t *
     return HPT_OK;
 }
 
-int hpt_get_pretest_records(hpt_context *c, uint32_t *records, float *radius, int64_t *n_records,
-                            uint64_t *wide_leaves) {
+int hpt_get_pretest_records(hpt_context *c, uint32_t *records, int64_t *n_records, float *radius,
+                            uint64_t *n_pass) {
     if (!c || !n_records) return HPT_EINVAL;
     static_assert(sizeof(HptSegQ) == 16, "hairpt.h documents 16-byte records");
     const size_t n = c->tree.leafQ.size();
     *n_records = (int64_t) n;
     if (records) std::memcpy(records, c->tree.leafQ.data(), n * sizeof(HptSegQ));
-    if (radius) std::memcpy(radius, c->tree.leafRad.data(), n * 4);
-    if (wide_leaves) *wide_leaves = c->tree.preWideLeaves;
+    if (radius) *radius = c->tree.preRadius;
+    if (n_pass) *n_pass = c->tree.prePassRecords;
     return HPT_OK;
 }
 

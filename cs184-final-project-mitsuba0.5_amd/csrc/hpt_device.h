@@ -56,17 +56,20 @@ struct HptSegF {
 };
 
 /* 16-byte pre-test record of the per-lane traversal (k_trace), leaf order:
- * the segment's first vertex and its axis oct-encoded in 16:16 bits (one
- * dwordx4 per record instead of 24 of HptSegF's 32 bytes).  The quantised
- * axis turns the pre-test line by an angle theta; a record's bound is its
- * shape's radius widened by its axial reach (up to the miter planes) times
- * sin(theta), and a leaf's records are tested at the largest bound in the leaf
- * (HptScene::leafRad, kdtree_build.cpp), so the test stays conservative and a
- * fold widens only its own leaves.  Decoded by axisOctDecode (hpt_render.hip)
- * and its host twin in kdtree_build.cpp, with the same fp32 operations. */
+ * the segment's first vertex and its axis oct-encoded (u 16 bits, v 15 bits:
+ * one dwordx4 per record instead of 24 of HptSegF's 32 bytes), bit 31 a pass
+ * flag.  The quantised axis turns the pre-test line by an angle theta; a
+ * record's bound is its shape's radius widened by its axial reach (up to the
+ * miter planes) times sin(theta).  HptScene::preRadius covers every bound but
+ * those of the flagged records, whose bound exceeds their shape's radius by
+ * more than 5 % (a fold: a miter plane almost parallel to the axis) and which
+ * pass every pre-test (kdtree_build.cpp), so a fold no longer widens the test
+ * of every record.  Decoded by axisOctDecode (hpt_render.hip) and its host
+ * twin in kdtree_build.cpp, with the same fp32 operations. */
+#define HPT_PRE_PASS 0x80000000u
 struct HptSegQ {
     float v1[3];
-    uint32_t axisOct;
+    uint32_t axisOct; /* bits 0-15 u, 16-30 v, 31 pass flag */
 };
 
 /* kd-tree node, 8 bytes (gkdtree.h:452-583 layout with absolute child index):
@@ -213,7 +216,7 @@ struct HptScene {
     float aabbMin[3], aabbMax[3];
     float radius;               /* shape 0's radius (every shape's when nShapes == 1) */
     float maxRadius;            /* largest shape radius: bound for the conservative fp32 pre-test */
-    const float *leafRad;       /* the HptSegQ pre-test's radius per leaf entry (its leaf's, see HptSegQ) */
+    float preRadius;            /* the HptSegQ pre-test's radius (flagged records pass, see HptSegQ) */
     HptBsdf bsdf;               /* shape 0's BSDF */
     /* several hair shapes (hair-curl): HptSegment::shape indexes shapes[],
        which gives the radius and the entry of bsdfs[] (both in HBM: a kernel

@@ -262,24 +262,21 @@ HD bool segMayHit(const float4 a, const float4 b, V3 o, V3 d, float r) {
 /* HptSegQ: the oct-decoded axis (kdtree_build.cpp's axisOctDecode does the same fp32 operations on
    the host to bound the quantisation angle) and the pre-test on it.  The axis is not unit length
    (|axis| in [1/sqrt(3), 1]): the test is scale-invariant in the axis except for the absolute rounding
-   margin, which a shorter axis only makes looser.  The leaf's radius covers the quantised axis's
-   turn over the reach of each of its records.  rr = radius * 1.000001 is formed once per leaf and
-   stands in for both of segMayHit's radius terms (the margin 3e-6 rr is the larger). */
+   margin, which a shorter axis only makes looser.  preRadius covers the quantised axis's turn over
+   the reach of every record but the flagged ones, which pass (HptSegQ). */
 HD V3 axisOctDecode(uint32_t q) {
     const float u = (float) (q & 0xffffu) * (2.0f / 65535.0f) - 1.0f;
-    const float v = (float) (q >> 16) * (2.0f / 65535.0f) - 1.0f;
+    const float v = (float) ((q >> 16) & 0x7fffu) * (2.0f / 32767.0f) - 1.0f;
     const float z = 1.0f - fabsf(u) - fabsf(v);
     const float fx = (1.0f - fabsf(v)) * (u >= 0.0f ? 1.0f : -1.0f);
     const float fy = (1.0f - fabsf(u)) * (v >= 0.0f ? 1.0f : -1.0f);
     return v3(z < 0.0f ? fx : u, z < 0.0f ? fy : v, z);
 }
-HD bool segMayHitQ(const uint4 q, V3 o, V3 d, float rr) {
+HD bool segMayHitQ(const uint4 q, V3 o, V3 d, float preRadius) {
     const V3 a = axisOctDecode(q.w);
-    const float wx = o.x - __uint_as_float(q.x), wy = o.y - __uint_as_float(q.y), wz = o.z - __uint_as_float(q.z);
-    const float nx = d.y * a.z - d.z * a.y, ny = d.z * a.x - d.x * a.z, nz = d.x * a.y - d.y * a.x;
-    const float nn = nx * nx + ny * ny + nz * nz;
-    const float wn = fabsf(wx * nx + wy * ny + wz * nz);
-    return wn <= rr * __builtin_amdgcn_sqrtf(nn) + 3e-6f * (rr + fabsf(wx) + fabsf(wy) + fabsf(wz));
+    return segMayHit(make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), a.x),
+                     make_float4(a.y, a.z, 0.0f, 0.0f), o, d, preRadius) |
+           ((int) q.w < 0); /* HPT_PRE_PASS */
 }
 
 /* adaptive ray epsilon: skdtree.cpp:126-129 (closest) / :213-216 (shadow) */
@@ -516,9 +513,6 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
        16-byte HptSegQ records (one dwordx4 per record: the kernel's vector
        memory path is busy ~3/4 of its cycles) */
     const uint32_t first = leafFirst, last = leafLast;
-    /* the leaf's pre-test radius (HptScene::leafRad), fetched with its first record */
-    float rr = 0.0f;
-    if (!LAT && first < last) rr = sc.leafRad[first] * 1.000001f;
     if (LAT) {
         /* latency mode (k_tail: few waves, registers to spare): every record of a
            chunk of 8 is requested at once and each candidate's whole fp64 record in
@@ -576,7 +570,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
                 tc.shadowPrims += r.shadow ? 1u : 0u;
                 if (waveLeader()) tc.primSlots += 64;
             }
-            if (segMayHitQ(fq, o, d, rr)) mask |= 1u << (e - c0);
+            if (segMayHitQ(fq, o, d, sc.preRadius)) mask |= 1u << (e - c0);
         }
         while (mask) {
             const uint32_t e = c0 + (uint32_t) (__ffs(mask) - 1);

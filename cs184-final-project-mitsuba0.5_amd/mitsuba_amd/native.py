@@ -108,7 +108,7 @@ SIGNATURES = {
                                  C.c_int]),
     "hpt_get_hair": (C.c_int64, [C.c_void_p, _f, _u8]),
     "hpt_get_kdtree": (C.c_int, [C.c_void_p, _u32, _i64, _u32, _i64, _f]),
-    "hpt_get_pretest_records": (C.c_int, [C.c_void_p, _u32, _f, _i64, _u64]),
+    "hpt_get_pretest_records": (C.c_int, [C.c_void_p, _u32, _i64, _f, _u64]),
     "hpt_get_envmap": (C.c_int, [C.c_void_p, _f, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
     "hpt_get_marschner_tables": (C.c_int, [C.c_void_p, _f, _f, _f, _f, _f, _f]),
     "hpt_get_roughplastic_params": (C.c_int, [C.c_void_p, _f, _f, C.POINTER(C.c_int)]),
@@ -399,16 +399,16 @@ class Renderer:
         return nodes, idx, aabb
 
     def pretest_records(self):
-        """k_trace's 16-byte pre-test records in leaf order ((n, 4) u32: v1 bits, oct axis), the radius
-        each is tested at (its leaf's) and the number of leaves tested 2 % above their shape's radius."""
+        """k_trace's 16-byte pre-test records in leaf order ((n, 4) u32: v1 bits, oct axis | pass << 31),
+        the radius the unflagged records are tested at and the number of flagged records."""
         n = C.c_int64()
-        self._check(self.lib.hpt_get_pretest_records(self.h, None, None, C.byref(n), None))
+        self._check(self.lib.hpt_get_pretest_records(self.h, None, C.byref(n), None, None))
         rec = np.zeros((n.value, 4), np.uint32)
-        radius = np.zeros(n.value, np.float32)
-        wide = C.c_uint64()
-        self._check(self.lib.hpt_get_pretest_records(self.h, _p(rec, _u32), _p(radius, _f), C.byref(n),
-                                                     C.byref(wide)))
-        return rec, radius, wide.value
+        radius = C.c_float()
+        n_pass = C.c_uint64()
+        self._check(self.lib.hpt_get_pretest_records(self.h, _p(rec, _u32), C.byref(n), C.byref(radius),
+                                                     C.byref(n_pass)))
+        return rec, radius.value, n_pass.value
 
     def envmap(self):
         w = C.c_int()

@@ -276,12 +276,11 @@ int64_t hpt_get_hair(hpt_context *ctx, float *xyz, uint8_t *starts_fiber /* n+1 
 int hpt_get_kdtree(hpt_context *ctx, uint32_t *nodes, int64_t *n_nodes, uint32_t *indices, int64_t *n_indices,
                    float aabb[6]);
 /* k_trace's 16-byte pre-test records in leaf order (the order of hpt_get_kdtree's indices): 4 u32
-   each -- the first vertex as 3 floats, then the axis oct-encoded 16:16 -- and the radius each is
-   tested at (its leaf's: the largest bound of the leaf's records), n_records of each; wide_leaves:
-   the leaves tested 2 % or more above their thickest shape's radius (folds).  NULL records / radius /
-   wide_leaves are skipped (query n_records first). */
-int hpt_get_pretest_records(hpt_context *ctx, uint32_t *records, float *radius, int64_t *n_records,
-                            uint64_t *wide_leaves);
+   each -- the first vertex as 3 floats, then the axis oct-encoded (u bits 0-15, v bits 16-30) with
+   bit 31 set on a record that passes every pre-test (a fold: its bound exceeds its shape's radius
+   by more than 5 %) -- the radius the other records are tested at, and how many are flagged.
+   NULL records / radius / n_pass are skipped (query n_records first). */
+int hpt_get_pretest_records(hpt_context *ctx, uint32_t *records, int64_t *n_records, float *radius, uint64_t *n_pass);
 int hpt_get_envmap(hpt_context *ctx, float *rgb, int *w, int *h);
 /* the perspective camera's m_sampleToCamera (row-major 4x4) and near-plane position
    differentials m_dx / m_dy (src/sensors/perspective.cpp:150-163), built in float

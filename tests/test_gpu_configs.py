@@ -82,9 +82,10 @@ def test_folded_strands_match_oracle_and_keep_the_pretest(monkeypatch):
     """A furball with an exact hairpin, a one-ulp near-hairpin and a 179.9 degree fold near the
     camera (scene_util.fold_workdir; hair.cpp:485-548,551-596: the miter planes of a fold are
     almost parallel to the axis, or NaN for the exact hairpin): the film matches the oracle at the
-    reference-flags floor, and -- each leaf tested at its own records' largest bound -- the fp64
-    exact tests per traced ray stay within 5 % of the fold-free twin's (one global bound would have
-    tested every record of the scene at the near-hairpin's ~570 radii).  Every bounce goes
+    reference-flags floor, and -- the near-hairpin's records flagged to pass instead of widening
+    the scene's pre-test radius -- the fp64 exact tests per traced ray stay within 5 % of the
+    fold-free twin's (one global bound would have tested every record of the scene at the
+    near-hairpin's ~150 radii).  Every bounce goes
     through k_trace (HPT_TAIL_PATHS=0: no k_tail), whose counters the ratio reads."""
     monkeypatch.setenv("HPT_TAIL_PATHS", "0")
     n, w, h, spp = 3000, 128, 96, 8
@@ -92,14 +93,13 @@ def test_folded_strands_match_oracle_and_keep_the_pretest(monkeypatch):
     for folded in (False, True):
         d = scene_util.fold_workdir(n, folded)
         _, r, o = scene_util.make("furball_marschner", n, w, h, spp, device=0, workdir=d)
-        rec, radius, wide = r.pretest_records()
+        rec, radius, n_pass = r.pretest_records()
         s = _parity("furball_marschner", n, r, o, w, h, spp, workdir=d)
         per_ray[folded] = s.prim_exact / (s.closest_rays + s.shadow_rays)
-        print("folded" if folded else "fold-free", "leaf radius / r: max %.3f, mean %.5f" %
-              (radius.max() / 0.00216667, radius.mean() / 0.00216667), "widened leaves %d" % wide,
-              "exact tests per ray %.4f" % per_ray[folded])
+        print("folded" if folded else "fold-free", "pre-test radius / r %.5f" % (radius / 0.00216667),
+              "records flagged to pass %d of %d" % (n_pass, len(rec)), "exact tests per ray %.4f" % per_ray[folded])
         if folded:
-            assert wide > 0 and radius.max() > 100 * 0.00216667
+            assert n_pass > 0 and radius < 1.05 * 0.00216667
     assert per_ray[True] <= 1.05 * per_ray[False], per_ray
 
 

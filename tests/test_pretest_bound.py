@@ -1,13 +1,15 @@
 """The 16-byte pre-test record (HptSegQ, hpt_device.h) stays conservative, per record.
 
-k_trace's leaf pass rejects a segment when the ray line passes farther than its
-leaf's pre-test radius from the line through v1 along the *oct-quantised* axis
-(segMayHitQ, hpt_render.hip).  A point the exact test accepts (hair.cpp:
+k_trace's leaf pass rejects a segment when the ray line passes farther than the
+scene's pre-test radius from the line through v1 along the *oct-quantised* axis
+(segMayHitQ, hpt_render.hip), unless the record is flagged to pass.  A point the exact test accepts (hair.cpp:
 485-548: inside the cylinder and between the two miter planes) lies at an
 axial offset s in [-r tan(phi1), len + r tan(phi2)] from v1, so within
 r + |s| sin(theta) of the quantised line: that is the record's bound
-(kdtree_build.cpp quantisedReach), and a leaf is tested at the largest bound
-of its records (HptScene::leafRad), so a fold widens only its own leaves.  This test restates the encode /
+(kdtree_build.cpp quantisedReach).  A record whose bound exceeds its shape's
+radius by more than 5 % (a fold) is flagged to pass every pre-test, and the
+scene's radius is the largest bound of the others, so a fold no longer widens
+the test of every record.  This test restates the encode /
 decode and the bound in numpy (fp32 where the device computes in fp32) and
 checks, on rays aimed at points just inside random mitered cylinders (grazing
 and head-on), that every ray the fp64 exact test accepts passes the quantised
@@ -28,22 +30,21 @@ F = np.float32
 
 
 def oct_encode(a):
-    """kdtree_build.cpp axisOctEncode: fp64 axis -> 16:16 bits."""
+    """kdtree_build.cpp axisOctEncode: fp64 axis -> u 16 bits, v 15 bits (bit 31: the pass flag)."""
     l1 = np.abs(a).sum(axis=1)
     u, v = a[:, 0] / l1, a[:, 1] / l1
     neg = a[:, 2] < 0
     fu = (1.0 - np.abs(v)) * np.where(u >= 0, 1.0, -1.0)
     fv = (1.0 - np.abs(u)) * np.where(v >= 0, 1.0, -1.0)
     u, v = np.where(neg, fu, u), np.where(neg, fv, v)
-    q = lambda x: np.clip(np.rint((x * 0.5 + 0.5) * 65535.0), 0, 65535).astype(np.uint32)  # noqa: E731
-    return q(u) | (q(v) << 16)
+    q = lambda x, m: np.clip(np.rint((x * 0.5 + 0.5) * m), 0, m).astype(np.uint32)  # noqa: E731
+    return q(u, 65535.0) | (q(v, 32767.0) << 16)
 
 
 def oct_decode(q):
     """axisOctDecode (device and host): fp32 operations."""
-    k = F(2.0) / F(65535.0)
-    u = (q & 0xFFFF).astype(F) * k - F(1)
-    v = (q >> 16).astype(F) * k - F(1)
+    u = (q & 0xFFFF).astype(F) * (F(2.0) / F(65535.0)) - F(1)
+    v = ((q >> 16) & 0x7FFF).astype(F) * (F(2.0) / F(32767.0)) - F(1)
     z = F(1) - np.abs(u) - np.abs(v)
     fx = (F(1) - np.abs(v)) * np.where(u >= 0, F(1), F(-1))
     fy = (F(1) - np.abs(u)) * np.where(v >= 0, F(1), F(-1))
@@ -154,8 +155,7 @@ def exact_hits(o, d, v1, v2, a, n1, n2, r):
 
 
 def pretest(o, d, v1f, qa, rad):
-    """segMayHitQ on the decoded axis at its leaf's radius rad (per record), fp32 without contraction:
-    rr = rad * 1.000001 stands in for both radius terms."""
+    """segMayHit on the decoded axis qa at radius rad (per record), fp32 without contraction."""
     w = o - v1f
     ax, ay, az = qa[:, 0], qa[:, 1], qa[:, 2]
     nx = d[:, 1] * az - d[:, 2] * ay
@@ -163,9 +163,8 @@ def pretest(o, d, v1f, qa, rad):
     nz = d[:, 0] * ay - d[:, 1] * ax
     nn = nx * nx + ny * ny + nz * nz
     wn = np.abs(w[:, 0] * nx + w[:, 1] * ny + w[:, 2] * nz)
-    rr = (rad * F(1.000001)).astype(F)
-    margin = F(3e-6) * (rr + np.abs(w[:, 0]) + np.abs(w[:, 1]) + np.abs(w[:, 2]))
-    return wn <= rr * np.sqrt(nn) + margin
+    margin = F(3e-6) * (rad + np.abs(w[:, 0]) + np.abs(w[:, 1]) + np.abs(w[:, 2]))
+    return wn <= rad * np.sqrt(nn) * F(1.000001) + margin
 
 
 def _segments(r):
@@ -174,8 +173,8 @@ def _segments(r):
     xyz, starts = r.hair()
     _, iv, _ = r.kdtree()
     iv = iv.astype(np.int64)
-    rec, radius, wide = r.pretest_records()
-    assert rec.shape == (len(iv), 4) and radius.shape == (len(iv),)
+    rec, radius, n_pass = r.pretest_records()
+    assert rec.shape == (len(iv), 4)
     X = xyz.astype(np.float64)
 
     def nrm(x):
@@ -187,7 +186,7 @@ def _segments(r):
     has_prev, has_next = starts[iv] == 0, starts[iv + 2] == 0
     n1 = np.where(has_prev[:, None], nrm(nrm(v1 - X[np.maximum(iv - 1, 0)]) + a), a)
     n2 = np.where(has_next[:, None], nrm(a + nrm(X[np.minimum(iv + 2, len(X) - 1)] - v2)), a)
-    return v1, v2, a, n1, n2, rec, radius, wide
+    return v1, v2, a, n1, n2, rec, radius, n_pass
 
 
 def _fold_renderer(folded):
@@ -209,32 +208,32 @@ def fold_scene():
 def test_library_records_match_the_restatement(fold_scene):
     # the library's axis bits are numpy's oct_encode of the fp64 axis, v1 its fp32 first vertex
     v1, _, a, _, _, rec, _, _ = _segments(fold_scene)
-    np.testing.assert_array_equal(rec[:, 3], oct_encode(a))
+    np.testing.assert_array_equal(rec[:, 3] & 0x7FFFFFFF, oct_encode(a))
     np.testing.assert_array_equal(rec[:, :3].view(np.float32), v1.astype(np.float32))
 
 
-def test_fold_widens_only_its_leaves(fold_scene):
-    v1, v2, a, n1, n2, rec, radius, wide = _segments(fold_scene)
+def test_fold_records_pass_without_widening(fold_scene):
+    v1, v2, a, n1, n2, rec, radius, n_pass = _segments(fold_scene)
     rad = F(0.00216667)
+    flag = (rec[:, 3] >> 31).astype(bool)
     with np.errstate(invalid="ignore"):
         folded = (np.abs(np.sum(n1 * a, 1)) < 0.01) | (np.abs(np.sum(n2 * a, 1)) < 0.01)
     nan_normal = np.isnan(n1).any(1) | np.isnan(n2).any(1)
-    near = folded & ~nan_normal
-    # the near-hairpin's bound is hundreds of radii: its leaves are tested that wide ...
-    assert near.sum() >= 2 and radius[near].max() > 5 * rad, radius[near]
-    # ... and only they: every other record keeps a radius within 2 % of the shape's
-    widened = radius > 1.02 * rad
-    assert 0 < wide <= 16 and widened.sum() < 0.01 * len(rec), (wide, widened.sum())
-    assert np.all(radius >= rad)
-    # the exact hairpin's NaN miter normals (no exact test accepts the segment) widen nothing
-    assert nan_normal.sum() >= 2
+    # the near-hairpin (a bound of ~150 radii) is flagged, and only a fold is: the radius every
+    # other record is tested at stays within 5 % of the shape's (the 179.9 degree fold's bound)
+    assert n_pass == flag.sum() and 0 < n_pass <= 8, n_pass
+    assert np.all(folded[flag]), "an unfolded record is flagged"
+    assert rad <= radius < 1.05 * rad, radius
+    # the exact hairpin's NaN miter normals: no exact test accepts the segment, it needs no flag
+    assert nan_normal.sum() >= 2 and not np.any(flag[nan_normal])
 
 
 def test_per_record_pretest_is_conservative(fold_scene):
-    """Rays aimed just inside each record's mitered cylinder -- every record of a widened leaf and a
-    sample of the rest -- pass the pre-test at the record's leaf radius whenever the exact test
-    hits; at the shape's radius the fold records' exact hits would be rejected."""
+    """Rays aimed just inside each record's mitered cylinder -- every fold record and a sample of
+    the rest -- pass k_trace's pre-test (the scene's radius, or the flag) whenever the exact test
+    hits; without its flag the near-hairpin's exact hits would be rejected."""
     v1, v2, a, n1, n2, rec, radius, _ = _segments(fold_scene)
+    flag = (rec[:, 3] >> 31).astype(bool)
     rng = np.random.default_rng(11)
     qa = oct_decode(rec[:, 3])
     rad = 0.00216667
@@ -263,14 +262,14 @@ def test_per_record_pretest_is_conservative(fold_scene):
     o = (p - d.astype(np.float64) * rng.uniform(0.01, 0.2, size=n)[:, None]).astype(F)
     hit = exact_hits(o, d, V1, V2, A, N1, N2, r)
     assert hit[: len(wide) * 4000].sum() > 1000 and hit.sum() > n // 5
-    may = pretest(o, d, V1.astype(F), qa[e], radius[e])
+    test = pretest(o, d, V1.astype(F), qa[e], np.full(n, F(radius)))
+    may = test | flag[e]
     assert not np.any(hit & ~may), "pre-test rejected %d exact hits" % np.sum(hit & ~may)
-    narrow = pretest(o, d, V1.astype(F), qa[e], np.full(n, F(1.02 * rad)))
-    assert np.any(hit & ~narrow), "no fold record needed its widened leaf"
+    assert np.any(hit & ~test), "no flagged record needed its flag"
 
 
 def test_fold_free_twin_radius():
     r = _fold_renderer(False)
-    _, _, _, _, _, rec, radius, wide = _segments(r)
-    assert radius.max() < 1.02 * 0.00216667 and wide == 0, (radius.max(), wide)
+    _, _, _, _, _, rec, radius, n_pass = _segments(r)
+    assert radius < 1.02 * 0.00216667 and n_pass == 0, (radius, n_pass)
     r.close()

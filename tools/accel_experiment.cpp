@@ -585,8 +585,8 @@ int main(int argc, char **argv) {
     float radius = hair.radius;
     printf("segments %zu, kd nodes %zu, kd refs %zu (%.2f per segment), build %.2f s\n", nseg, kd.nodes.size(),
            kd.prims.size(), (double) kd.prims.size() / nseg, kd.buildSeconds);
-    printf("radius %.6g, 16-byte pre-test: largest leaf radius %.6g (x%.5f), %zu leaves 2%% wider than their shape\n",
-           hair.radius, kd.preRadius, kd.preRadius / hair.radius, kd.preWideLeaves);
+    printf("radius %.6g, 16-byte pre-test radius %.6g (x%.5f), %zu records flagged to pass\n", hair.radius,
+           kd.preRadius, kd.preRadius / hair.radius, kd.prePassRecords);
     if (argc > 5) return 0;
 
     /* segment solids: axis segment extended by the miter overhang, radius + slack */
