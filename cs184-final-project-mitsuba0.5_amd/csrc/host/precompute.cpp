@@ -907,6 +907,12 @@ void setupCamera(const SceneDesc &d, HptCamera &cam) {
     if (!cameraSampleToCamera(d, cam.s2c))
         throw std::runtime_error("Unable to invert singular matrix (perspective camera)");
     std::memcpy(cam.toWorld, d.toWorld, sizeof(cam.toWorld));
+    /* the origin of every camera ray: toWorld applied to (0, 0, 0) in the order the reference's
+       Transform::operator()(Point) evaluates it (transform.h:108-121, fp32, no contraction) */
+    for (int k = 0; k < 3; ++k) {
+        const float *T = cam.toWorld + 4 * k;
+        cam.origin[k] = T[0] * 0.0f + T[1] * 0.0f + T[2] * 0.0f + T[3];
+    }
     cam.invResX = 1.0f / (float) d.width;
     cam.invResY = 1.0f / (float) d.height;
     /* position differentials on the near plane (perspective.cpp:160-163) */

@@ -97,6 +97,7 @@ struct HptCamera {
     float dx[3], dy[3]; /* near-plane position differentials (perspective.cpp:160-163) */
     float diffScale;    /* 1/sqrt(sampleCount): scaleDifferential (integrator.cpp:143-144) */
     float toWorld[16];  /* camera-to-world, row-major */
+    float origin[3];    /* toWorld * (0, 0, 0): every camera ray's origin (setupCamera) */
     float invResX, invResY, nearClip, farClip;
     float resolution;   /* Sobol pixel resolution (sobol.cpp:147-158) */
     int width, height;

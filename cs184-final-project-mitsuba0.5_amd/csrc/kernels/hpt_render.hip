@@ -2408,11 +2408,7 @@ HD void qpush(bool pred, uint32_t value, uint32_t *queue, uint32_t *counter) {
    origin is the same for every ray (cameraOrigin), and mint / maxt are the clip distances times
    1 / d.z: k_camera stores the world direction and that factor, and the trace launch and
    k_primary rebuild the ray from them bit for bit (cameraRayFrom). */
-HD V3 cameraOrigin(const HptCamera &c) {
-    const float *T = c.toWorld;
-    return v3(T[0] * 0.0f + T[1] * 0.0f + T[2] * 0.0f + T[3], T[4] * 0.0f + T[5] * 0.0f + T[6] * 0.0f + T[7],
-              T[8] * 0.0f + T[9] * 0.0f + T[10] * 0.0f + T[11]);
-}
+HD V3 cameraOrigin(const HptCamera &c) { return v3(c.origin[0], c.origin[1], c.origin[2]); }
 HD void cameraRay(const HptCamera &c, float posx, float posy, V3 &o, V3 &dw, float &mint, float &maxt,
                   float *invZOut = nullptr) {
     const V3 nearP = xformPoint(c.s2c, v3(posx * c.invResX, posy * c.invResY, 0.0f));

@@ -22,5 +22,5 @@ print(v, d["value"], d["ms_per_step"], d["stats"]["exact_tests_per_ray"], d["sta
       {x: k.get(x) for x in ("camera", "trace_packet", "primary", "trace")})
 PY
 }
-timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py::test_folded_strands_match_oracle_and_keep_the_pretest -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/lr_tests.log 2>&1; rc=$?; grep -E "passed|failed|Error|folded|fold-free" $O/lr_tests.log | tail -5; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_camera.py -m gpu -x -v -s --timeout 300 --timeout-method thread > $O/lr_tests.log 2>&1; rc=$?; grep -E "passed|failed|Error|folded|fold-free" $O/lr_tests.log | tail -5; [ $rc -eq 0 ] || exit $rc
 run main $L/lib/libhairpt.so && run base $L/libv_base/libhairpt.so && run main2 $L/lib/libhairpt.so && run base2 $L/libv_base/libhairpt.so
