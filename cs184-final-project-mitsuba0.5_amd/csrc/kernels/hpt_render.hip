@@ -278,6 +278,15 @@ HD bool segMayHitQ(const uint4 q, V3 o, V3 d, float preRadius) {
                      make_float4(a.y, a.z, 0.0f, 0.0f), o, d, preRadius) |
            ((int) q.w < 0); /* HPT_PRE_PASS */
 }
+/* the same as a 0 / 1 word: the test's select falls back to the record's pass bit (one v_cndmask
+   where a bool OR of the two costs a compare and a mask merge more) */
+HD uint32_t segMayHitQBit(const uint4 q, V3 o, V3 d, float preRadius) {
+    const V3 a = axisOctDecode(q.w);
+    return segMayHit(make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), a.x),
+                     make_float4(a.y, a.z, 0.0f, 0.0f), o, d, preRadius)
+               ? 1u
+               : q.w >> 31; /* HPT_PRE_PASS */
+}
 
 /* adaptive ray epsilon: skdtree.cpp:126-129 (closest) / :213-216 (shadow) */
 HD float adaptiveMint(V3 o, float mint, bool shadow) {
@@ -570,7 +579,7 @@ HD bool traceRound(const HptScene &sc, TraceRay &r, uint2 *stk, int stride, Trac
                 tc.shadowPrims += r.shadow ? 1u : 0u;
                 if (waveLeader()) tc.primSlots += 64;
             }
-            if (segMayHitQ(fq, o, d, sc.preRadius)) mask |= 1u << (e - c0);
+            mask |= segMayHitQBit(fq, o, d, sc.preRadius) << (e - c0);
         }
         while (mask) {
             const uint32_t e = c0 + (uint32_t) (__ffs(mask) - 1);
