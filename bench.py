@@ -287,11 +287,14 @@ def main():
         acc["p_launches"] += s.packet_launches
 
     dt = timed_steps(lambda: step(3), args.steps, world, dist, torch.cuda.synchronize, "cuda:%d" % local, collect)
-    # the per-kernel split of one more (untimed) frame, with an event around every kernel
-    step(1)
-    s1 = r.stats()
-    for k in ("camera", "trace_packet", "trace", "primary", "shade", "post", "tail", "gather"):
-        acc["kernels"][k] = getattr(s1, "ms_" + k)
+    # the per-kernel split, averaged over three more (untimed) frames with an event around every
+    # kernel (the timed steps carry events around the traversal launches only: collect_stats 3)
+    split_frames = 3
+    for _ in range(split_frames):
+        step(1)
+        s1 = r.stats()
+        for k in ("camera", "trace_packet", "trace", "primary", "shade", "post", "tail", "gather"):
+            acc["kernels"][k] = acc["kernels"].get(k, 0.0) + getattr(s1, "ms_" + k) / split_frames
     # the same frame once more with no recorded bounce schedule (what a render of a new spp range
     # or the CLI's first pass does: every bounce's queue length read back); not
     # part of `value`, which times repeated frames of the same spp range
@@ -419,7 +422,7 @@ def main():
             "first_render_ms": round(first_ms, 3),
             "kernel_ms_per_step": {k: round(v, 3) for k, v in ms_kernels.items()},
             "timing": "timed steps: HIP events around the traversal launches only (collect_stats 3); "
-                      "kernel_ms_per_step: one more frame with an event around every kernel",
+                      "kernel_ms_per_step: the mean of three more frames with an event around every kernel",
             "cpu_baseline": cpu,
             "stats": {"bounces_per_path": round(tot["bounces"] / max(1, paths_total / world), 4),
                       "nodes_per_ray": round(tot["nodes"] / max(1, tot["closest"] + tot["shadow"]), 2),
