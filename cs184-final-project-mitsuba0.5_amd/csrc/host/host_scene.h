@@ -262,6 +262,31 @@ bool cameraSampleToCamera(const SceneDesc &d, float s2c[16]);
 float cameraXFov(const SceneDesc &d);                       /* sensor.cpp:237-305 */
 void setupTent(float *lut, float &scale);                 /* rfilter.cpp:38-56 */
 
+/* Matrix4x4::invert (matrix.inl:138-190): float Gauss-Jordan with full pivoting, row-major */
+bool invertMatrix4(const float src[16], float out[16]);
+
+/* ---- triangle-mesh scenes (mesh.cpp): the C1 shapes and BSDFs, flattened for the device
+   (HptMeshScene) ---- */
+struct MeshSceneHost {
+    std::vector<float> p, n, uv;         /* per vertex, world space */
+    std::vector<float> dpdu;             /* per triangle */
+    std::vector<HptTri> tris;
+    std::vector<HptMeshInfo> meshes;
+    std::vector<HptRect> rects;
+    std::vector<HptBvhNode> nodes;
+    std::vector<uint32_t> prims;
+    std::vector<HptMeshBsdf> bsdfs;      /* desc.bsdfs first (same indices), nested records after */
+    float aabbMin[3] = {0, 0, 0}, aabbMax[3] = {0, 0, 0};
+    uint32_t depth = 0;                  /* BVH depth (levels) */
+    size_t vertexCount() const { return p.size() / 3; }
+};
+/* obj.cpp / trimesh.cpp / rectangle.cpp loading of SceneDesc::meshes, the BSDF records of
+   SceneDesc::bsdfs (diffuse, plastic, twosided), the BVH and the enlarged scene bounds.
+   Throws std::runtime_error with the reference's message on failure. */
+MeshSceneHost buildMeshScene(const SceneDesc &d);
+/* fresnelDiffuseReflectance(eta, fast = false) (util.cpp:808-859): adaptive Gauss-Lobatto */
+float fresnelDiffuseReflectance(float eta);
+
 /* float <-> IEEE half (round to nearest even) */
 uint16_t floatToHalf(float f);
 float halfToFloat(uint16_t h);

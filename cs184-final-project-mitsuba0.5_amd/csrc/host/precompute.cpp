@@ -863,6 +863,14 @@ float degToRad(float v) { return v * (kPi / 180.0f); }
 float radToDeg(float v) { return v * (180.0f / kPi); }
 } // namespace
 
+bool invertMatrix4(const float src[16], float out[16]) {
+    M44 s, t;
+    std::copy(src, src + 16, s.begin());
+    if (!gaussJordanInvert(s, t)) return false;
+    std::copy(t.begin(), t.end(), out);
+    return true;
+}
+
 /* the horizontal field of view after PerspectiveCamera::configure (sensor.cpp:237-305) */
 float cameraXFov(const SceneDesc &d) {
     const float aspect = (float) d.width / (float) d.height; /* sensor.cpp:101-102 */

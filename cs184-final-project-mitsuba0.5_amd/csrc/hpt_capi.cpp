@@ -98,6 +98,11 @@ struct hpt_context {
     bool hairFromFile = false;     /* desc.shapes are loaded from files at prepare */
     HairData hair;                 /* every hair shape, merged */
     KDTreeHost tree;
+    /* a triangle-mesh scene (C1: obj / rectangle shapes, no hair): mesh.cpp's arrays and their
+       device view; k_mesh_paths renders it */
+    bool meshScene = false;
+    MeshSceneHost mesh;
+    HptMeshScene ms{};
     /* per BSDF of desc.bsdfs: host tables and the device record */
     std::vector<MarschnerHost> mar;
     std::vector<RoughPlasticHost> rp;
@@ -648,11 +653,53 @@ int hpt_prepare(hpt_context *c) {
     if (!c) return HPT_EINVAL;
     if (!c->haveCamera || !c->haveHair || !c->haveBSDF || !c->haveEnv)
         return setErr(c, HPT_ESTATE, "scene incomplete: need camera, hair, bsdf and emitter");
-    if (!c->desc.meshes.empty())
-        return setErr(c, HPT_EINVAL, "scene has obj/rectangle shapes: the device path renders hair only; "
-                                     "triangle scenes (C1) render on the CPU path from hpt_export_scene_json");
+    if (!c->desc.meshes.empty() && !c->desc.shapes.empty())
+        return setErr(c, HPT_EINVAL, "scene mixes hair with obj/rectangle shapes: the device path renders a hair "
+                                     "scene or a triangle-mesh scene (C1), not both");
     c->prepared = false;
+    c->meshScene = !c->desc.meshes.empty();
     const SceneDesc &d = c->desc;
+    if (c->meshScene) {
+        /* C1: the meshes, their BSDFs (diffuse / plastic / twosided) and the environment; the
+           camera, sampler and film are the hair path's */
+        try {
+            if (c->sobol32.empty()) {
+                std::string dir = c->dataDir + "/sobol/";
+                if (!readFile(dir + "matrices32.u32", c->sobol32) || c->sobol32.size() != HPT_SOBOL_DIMS * HPT_SOBOL_BITS ||
+                    !readFile(dir + "vdc.u64", c->vdc) || !readFile(dir + "vdc_inv.u64", c->vdcInv))
+                    return setErr(c, HPT_EIO, "cannot read Sobol tables from " + dir);
+            }
+            if (d.emitter != "envmap" && d.emitter != "sunsky")
+                return setErr(c, HPT_EINVAL, "mesh scene without an envmap / sunsky emitter");
+            c->mesh = buildMeshScene(d);
+            if (c->mesh.depth + 1 > HPT_MESH_STACK)
+                return setErr(c, HPT_EINVAL, "mesh BVH deeper than the traversal stack");
+            c->hair = HairData();
+            c->tree = KDTreeHost();
+            c->mar.clear();
+            c->rp.clear();
+            c->bsdfRec.clear();
+            if (c->envFromSunsky) {
+                if (c->sunsky.hosek.empty()) {
+                    std::string err;
+                    if (!loadSunSkyTables(c->dataDir, c->sunsky, err)) return setErr(c, HPT_EIO, err);
+                }
+                c->env = EnvHost();
+                rasterizeSunSky(d, c->sunsky, c->env);
+            }
+            buildEnvMap(c->env);
+            buildEnvMipmap(c->env);
+        } catch (const std::exception &e) {
+            return setErr(c, HPT_EINVAL, e.what());
+        }
+        c->sceneId = 0;
+        const int rc = uploadScene(c);
+        if (rc == HPT_OK) {
+            static std::atomic<uint64_t> meshCounter{1ull << 62};
+            c->sceneId = ++meshCounter;
+        }
+        return rc;
+    }
     try {
         /* Sobol tables (data/sobol, extracted from src/samplers/sobolseq.cpp) */
         if (c->sobol32.empty()) {
@@ -750,9 +797,9 @@ static int uploadScene(hpt_context *c) {
     r |= upload(c, c->tree.leafQ.data(), c->tree.leafQ.size() * sizeof(HptSegQ), (const void **) &sc.leafQ);
     r |= upload(c, c->tree.prims.data(), c->tree.prims.size() * 4, (const void **) &sc.leafSeg);
     r |= upload(c, c->tree.segs.data(), c->tree.segs.size() * sizeof(HptSegment), (const void **) &sc.segs);
-    for (int i = 0; i < 3; ++i) {
-        sc.aabbMin[i] = c->tree.aabbMin[i];
-        sc.aabbMax[i] = c->tree.aabbMax[i];
+    for (int i = 0; i < 3; ++i) { /* the scene bounds: the hair kd-tree's, or the mesh scene's */
+        sc.aabbMin[i] = c->meshScene ? c->mesh.aabbMin[i] : c->tree.aabbMin[i];
+        sc.aabbMax[i] = c->meshScene ? c->mesh.aabbMax[i] : c->tree.aabbMax[i];
     }
     /* BSDF records: device tables first, then the records themselves */
     for (size_t i = 0; i < c->bsdfRec.size(); ++i) {
@@ -796,7 +843,7 @@ static int uploadScene(hpt_context *c) {
     sc.maxRadius = 0.0f;
     for (const HptShape &h : shapes) sc.maxRadius = std::max(sc.maxRadius, h.radius);
     sc.preRadius = c->tree.preRadius;
-    sc.bsdf = c->bsdfRec[shapes[0].bsdf];
+    if (!c->bsdfRec.empty()) sc.bsdf = c->bsdfRec[shapes[0].bsdf];
     if (nShapes > 1) {
         r |= upload(c, shapes.data(), shapes.size() * sizeof(HptShape), (const void **) &sc.shapes);
         r |= upload(c, c->bsdfRec.data(), c->bsdfRec.size() * sizeof(HptBsdf), (const void **) &sc.bsdfs);
@@ -866,6 +913,24 @@ static int uploadScene(hpt_context *c) {
         float radius = std::sqrt(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]);
         for (int i = 0; i < 3; ++i) E.bsCenter[i] = ctr[i];
         E.bsRadius = std::max(1e-4f, radius * 1.5f);
+    }
+    if (c->meshScene) { /* the mesh scene's arrays (HptMeshScene) */
+        const MeshSceneHost &M = c->mesh;
+        HptMeshScene &ms = c->ms;
+        std::memset(&ms, 0, sizeof(ms));
+        r |= upload(c, M.nodes.data(), M.nodes.size() * sizeof(HptBvhNode), (const void **) &ms.nodes);
+        r |= upload(c, M.prims.data(), M.prims.size() * 4, (const void **) &ms.prims);
+        r |= upload(c, M.tris.data(), M.tris.size() * sizeof(HptTri), (const void **) &ms.tris);
+        r |= upload(c, M.rects.data(), M.rects.size() * sizeof(HptRect), (const void **) &ms.rects);
+        r |= upload(c, M.meshes.data(), M.meshes.size() * sizeof(HptMeshInfo), (const void **) &ms.meshes);
+        r |= upload(c, M.p.data(), M.p.size() * 4, (const void **) &ms.p);
+        r |= upload(c, M.n.data(), M.n.size() * 4, (const void **) &ms.n);
+        r |= upload(c, M.uv.data(), M.uv.size() * 4, (const void **) &ms.uv);
+        r |= upload(c, M.dpdu.data(), M.dpdu.size() * 4, (const void **) &ms.dpdu);
+        r |= upload(c, M.bsdfs.data(), M.bsdfs.size() * sizeof(HptMeshBsdf), (const void **) &ms.bsdfs);
+        for (int i = 0; i < 3; ++i) ms.aabbMin[i] = M.aabbMin[i], ms.aabbMax[i] = M.aabbMax[i];
+        ms.nNodes = (uint32_t) M.nodes.size();
+        ms.stackDepth = M.depth + 1;
     }
     r |= upload(c, c->sobol32.data(), c->sobol32.size() * 4, (const void **) &sc.sobol);
     sc.scramble = 0;
@@ -976,6 +1041,13 @@ int hpt_get_scene_info(hpt_context *c, hpt_scene_info *o) {
         o->bsphere_center[i] = c->sc.env.bsCenter[i];
     }
     o->bsphere_radius = c->sc.env.bsRadius;
+    if (c->meshScene) { /* a mesh scene: its BVH in the kd fields, its bounds */
+        o->kd_nodes = c->mesh.nodes.size();
+        o->kd_indices = c->mesh.prims.size();
+        o->kd_depth = (int) c->mesh.depth;
+        o->vertices = c->mesh.vertexCount();
+        for (int i = 0; i < 3; ++i) o->aabb_min[i] = c->mesh.aabbMin[i], o->aabb_max[i] = c->mesh.aabbMax[i];
+    }
     return HPT_OK;
 }
 
@@ -1199,6 +1271,25 @@ static int renderImpl(hpt_context *c, const hpt_render_params *prm, float4 *dFil
         HIPCHK(c, hipMemcpyAsync(c->dBlockCost + costWords, c->dBlockCost, costWords * 4, hipMemcpyDeviceToDevice, s));
         HIPCHK(c, hipMemsetAsync(c->counters, 0, HPT_COUNTER_WORDS * 4, s));
         uint32_t *C = c->counters, *dst = counted ? (uint32_t *) c->dstats : nullptr;
+        if (c->meshScene) {
+            /* C1: every camera sample of the wave to termination in one launch (k_mesh_paths),
+               then the film splat; its time is reported as ms_shade */
+            e = timed(2, [&] { return hpt_launch_mesh_paths(sc, c->ms, w, c->P, C, s); });
+            if (e) break;
+            e = timed(4, [&] { return hpt_launch_gather(sc, w, c->P, c->partial, dFilm, s); });
+            if (e) break;
+            e = hipMemcpyAsync(hostCnt, C, HPT_Q_COUNT * 4, hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            if (e) break;
+            if (hostCnt[HPT_C_ERROR])
+                return setErr(c, HPT_EINVAL, "Lookup dimension exceeds the direction number table size! You may have "
+                                             "to reduce the 'maxDepth' parameter of your integrator.");
+            uint64_t shaded = 0;
+            std::memcpy(&shaded, hostCnt + HPT_C_BOUNCES, 8);
+            bounces += shaded;
+            c->stats.paths += w.nPaths;
+            continue;
+        }
         uint32_t *curPacket = C + HPT_CURSOR_SET(2), *curOverflow = C + HPT_CURSOR_SET(3);
         /* the camera pass is bounce 0 (parity 0) */
         e = timed(0, [&] { return hpt_launch_camera(sc, w, c->P, c->qTrace, C + HPT_C_TRACE(0), s); });
@@ -1466,6 +1557,8 @@ int hpt_context_share_scene(hpt_context *src, int device, hpt_context **out) {
     c->haveEnv = src->haveEnv, c->hairFromFile = src->hairFromFile, c->envFromSunsky = src->envFromSunsky;
     c->hair = src->hair;
     c->tree = src->tree;
+    c->meshScene = src->meshScene;
+    c->mesh = src->mesh;
     c->mar = src->mar;
     c->rp = src->rp;
     c->bsdfRec = src->bsdfRec;

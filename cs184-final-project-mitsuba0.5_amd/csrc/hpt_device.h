@@ -239,4 +239,78 @@ struct HptScene {
     uint32_t packetStack;       /* camera packets' stack entries (0 = the build's; hpt_set_packet_stack, a test hook) */
 };
 
+/* ---- triangle-mesh scenes (C1, models/teapot: obj.cpp / rectangle.cpp shapes, diffuse /
+ * plastic / twosided BSDFs, checkerboard texture), rendered by k_mesh_paths (hpt_mesh.h).
+ * Geometry lives in world space; the camera, sampler, environment and film come from the
+ * HptScene of the same context. */
+
+/* one triangle: Wald's projection record (triaccel.h:37-158; k = 3 marks a degenerate
+ * triangle, which never hits) and the vertex indices of the hit-record fill.  64 bytes. */
+struct HptTri {
+    uint32_t k;
+    float n_u, n_v, n_d, a_u, a_v, b_nu, b_nv, c_nu, c_nv;
+    uint32_t i0, i1, i2; /* into HptMeshScene::p / n / uv */
+    uint32_t mesh;       /* into HptMeshScene::meshes */
+    uint32_t pad[2];
+};
+
+/* per TriMesh (trimesh.cpp): its BSDF and which vertex attributes it has */
+struct HptMeshInfo {
+    int bsdf, hasNormals, hasUV, pad;
+};
+
+/* rectangle.cpp:80-168: the world-to-object affine rows, the geometric frame, dpdu */
+struct HptRect {
+    float w2o[12];
+    float s[3], t[3], n[3];
+    float dpdu[3];
+    int bsdf;
+    int pad[3];
+};
+
+/* BVH node (32 bytes) over triangles and rectangles: count == 0 is an inner node whose
+ * left child is the next node and whose right child is node a; a leaf holds the
+ * primitive references prims[a, a + count) */
+struct HptBvhNode {
+    float mn[3];
+    uint32_t a;
+    float mx[3];
+    uint32_t count;
+};
+#define HPT_PRIM_RECT 0x80000000u /* a primitive reference to rectangle (ref & ~HPT_PRIM_RECT) */
+
+/* mesh-scene BSDF instance (diffuse.cpp:60-140 with a constant or checkerboard reflectance,
+ * plastic.cpp:143-440, twosided.cpp:84-183 over the records nested[0..1]) */
+#define HPT_MBSDF_DIFFUSE 0
+#define HPT_MBSDF_PLASTIC 1
+#define HPT_MBSDF_TWOSIDED 2
+struct HptMeshBsdf {
+    int kind, smooth;
+    /* diffuse */
+    int textured;
+    float refl[3], color0[3], color1[3];
+    float uoffset, voffset, uscale, vscale;
+    /* plastic */
+    int nonlinear;
+    float eta, invEta2, fdrInt, specularSamplingWeight;
+    float diffuse[3], specular[3];
+    /* twosided */
+    int nested[2];
+};
+
+/* k_mesh_paths' per-lane BVH stack entries: hpt_prepare refuses a BVH deeper than this - 1 levels */
+#define HPT_MESH_STACK 64
+struct HptMeshScene {
+    const HptBvhNode *nodes;
+    const uint32_t *prims;     /* leaf primitive references */
+    const HptTri *tris;
+    const HptRect *rects;
+    const HptMeshInfo *meshes;
+    const float *p, *n, *uv;   /* per vertex: 3, 3 (meshes with normals), 2 (meshes with uv) floats */
+    const float *dpdu;         /* per triangle, 3 floats: computeUVTangents, or p1 - p0 without uv */
+    const HptMeshBsdf *bsdfs;
+    float aabbMin[3], aabbMax[3]; /* the scene bounds, enlarged as gkdtree.h:1213-1220 does */
+    uint32_t nNodes, stackDepth; /* the BVH's depth bounds the traversal stack (HPT_MESH_STACK) */
+};
+
 #endif

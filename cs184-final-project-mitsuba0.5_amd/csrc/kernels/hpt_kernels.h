@@ -160,6 +160,10 @@ hipError_t hpt_launch_film_add(float4 *dst, const float4 *src, size_t n, hipStre
 /* k_splat + k_gather; partial = (nPaths / nSpp) * 9 float4 of scratch */
 hipError_t hpt_launch_gather(const HptScene &sc, const HptWave &w, const HptPaths &P, float4 *partial, float4 *film,
                              hipStream_t s);
+/* triangle-mesh scenes (C1, hpt_mesh.h): every camera sample of the wave to termination, one lane
+   each; P.pos / P.li for hpt_launch_gather, path-bounces and the Sobol error to counters */
+hipError_t hpt_launch_mesh_paths(const HptScene &sc, const HptMeshScene &ms, const HptWave &w, const HptPaths &P,
+                                 uint32_t *counters, hipStream_t s);
 hipError_t hpt_launch_sobol_batch(const HptScene &sc, int m, int n, const uint32_t *frame, const uint32_t *px,
                                   const uint32_t *py, const uint32_t *dim, uint64_t *oi, float *ov, hipStream_t s);
 hipError_t hpt_launch_camera_batch(const HptScene &sc, int n, const float *pos, float *o, float *d, float *mint,

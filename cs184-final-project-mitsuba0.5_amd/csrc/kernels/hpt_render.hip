@@ -3689,3 +3689,6 @@ hipError_t hpt_launch_env_batch(const HptScene &sc, int n, const float *refp, co
                        oe, oep);
     return hipGetLastError();
 }
+
+/* triangle-mesh scenes (C1): k_mesh_paths over this file's sampler, camera, environment and film */
+#include "hpt_mesh.h"

@@ -57,8 +57,9 @@ int hpt_set_data_dir(hpt_context *ctx, const char *dir);
 /* Parse a Mitsuba scene XML (src/librender/scenehandler.cpp) with -D style
    defines: integrator "path", sensor "perspective" + sampler "sobol" + film,
    shape "hair", bsdf "marschner"/"kajiyakay"/"roughplastic"/"marschnerdielectric"/"thindielectric"/"diffuse"
-   (parsed too, CPU path only: shape "obj"/"rectangle", bsdf "plastic"/"twosided", texture "checkerboard")
-   (one per hair shape; several shapes per scene), emitter "sunsky"/"envmap". */
+   (one per hair shape; several shapes per scene), emitter "sunsky"/"envmap"; or, for a
+   triangle-mesh scene (C1, models/teapot), shape "obj"/"rectangle" with bsdf "diffuse" (constant
+   or "checkerboard" texture) / "plastic" / "twosided" over those two. */
 int hpt_load_scene_xml(hpt_context *ctx, const char *path, int n_defines, const char *const *keys,
                        const char *const *values);
 /* Process-wide -D defines, merged under the explicit ones by every later
@@ -74,8 +75,7 @@ int hpt_set_default_defines(int n_defines, const char *const *keys, const char *
    (plastic, twosided, diffuse with a checkerboard texture ...).  Replaces
    reading the SceneHandler's object graph (src/librender/scenehandler.cpp:
    endElement) from C.  With buf == NULL only *needed (bytes incl. the NUL) is
-   set.  hpt_prepare refuses scenes with mesh shapes: triangles render on the
-   CPU path only (BASELINE.json configs[0]). */
+   set. */
 int hpt_export_scene_json(hpt_context *ctx, char *buf, size_t capacity, size_t *needed);
 
 /* ---- low-level scene setters (what a Mitsuba plugin shim would call) ---- */
@@ -141,7 +141,11 @@ int hpt_set_sunsky(hpt_context *ctx, const float sun_direction[3], float turbidi
                    float sun_scale, float sun_radius_scale, int resolution);
 
 /* Build the hair kd-tree (HairKDTree ctor, hair.cpp:108-159), precompute the
-   BSDF / envmap tables and upload the scene to HBM (Scene::preprocess). */
+   BSDF / envmap tables and upload the scene to HBM (Scene::preprocess).  A scene whose
+   shapes are obj / rectangle meshes (C1) is loaded instead (WavefrontOBJ, obj.cpp:199-349;
+   TriMesh::configure, trimesh.cpp:362-386; Rectangle, rectangle.cpp:80-122) into a BVH, and
+   hpt_render traces its paths with the mesh kernel (k_mesh_paths); hpt_get_scene_info then
+   reports the BVH in its kd_* fields.  A scene mixing hair and meshes is refused (HPT_EINVAL). */
 int hpt_prepare(hpt_context *ctx);
 
 typedef struct hpt_scene_info {

@@ -1,0 +1,91 @@
+"""C1's mesh path on the host (CPU, no device): the product's own OBJ / rectangle loading, BSDF
+records and BVH (csrc/host/mesh.cpp) through hpt_prepare on a host-only context, checked against
+the oracle's mesh restatement (oracle/mesh_geom.h), and the scenes the mesh path refuses.
+The device render of the same scene is tests/test_gpu_c1.py."""
+import os
+
+import numpy as np
+import pytest
+
+import c1_scene
+import oracle_lib
+from mitsuba_amd import native, synth_hair
+
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "oracle"))
+import film as ref  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def host(tmp_path_factory):
+    d = tmp_path_factory.mktemp("c1host")
+    xml = c1_scene.write(d)
+    r = native.Renderer(device=native.HOST_ONLY)
+    r.load_scene_xml(xml, {"w": 64, "h": 64, "spp": 4})
+    r.prepare()
+    return {"dir": d, "r": r, "js": r.scene_json(), "env": ref.read_pfm(str(d / "env.pfm"))}
+
+
+def test_mesh_scene_loads_like_the_oracle(host):
+    info = host["r"].info()
+    o = oracle_lib.MeshOracle()
+    o.setup_scene(host["js"], host["env"], 64, 64, 4)
+    mi = o.mesh_info()
+    assert mi["meshes"] == 3 and mi["rectangles"] == 1
+    # obj.cpp's vertex merge and fan triangulation: the same vertex and primitive counts
+    assert info.vertices == mi["vertices"]
+    assert info.kd_indices == mi["triangles"] + mi["rectangles"]
+    # a BVH over ~11 k primitives: median splits, leaves of <= 4
+    assert info.kd_nodes == 2 * ((info.kd_indices + 3) // 4) - 1 or info.kd_nodes < 2 * info.kd_indices
+    assert 12 <= info.kd_depth < 64
+    # the bounds enclose the floor rectangle (|x|, |z| up to 56.5) and the body (height ~6.6),
+    # enlarged as gkdtree.h:1213-1220
+    lo, hi = np.array(info.aabb_min), np.array(info.aabb_max)
+    assert lo[0] < -56 and hi[0] > 56 and lo[2] < -56 and hi[2] > 56
+    assert lo[1] < 0 < 6 < hi[1]
+    np.testing.assert_array_equal(host["r"].envmap(), host["env"])
+
+
+def test_host_only_context_cannot_render_mesh_scene(host):
+    with pytest.raises(native.HairPTError, match="host-only"):
+        host["r"].render(0, 1)
+
+
+def _write_scene(d, shapes):
+    body = c1_scene.SCENE
+    cut = body.index("  <shape type=\"rectangle\">")
+    end = body.index("  <emitter")
+    return body[:cut] + shapes + body[end:]
+
+
+def test_mixed_hair_and_mesh_scene_is_refused(tmp_path):
+    c1_scene.write(tmp_path)
+    synth_hair.write_binary_hair(str(tmp_path / "h.mitshair"),
+                                 [np.array([[0, 0, 0], [0, 1, 0], [0, 2, 0.1]], np.float32)])
+    shapes = ('  <shape type="hair"><string name="filename" value="h.mitshair"/><ref id="Floor"/></shape>\n'
+              '  <shape type="obj"><string name="filename" value="models/Mesh000.obj"/><ref id="Material"/></shape>\n')
+    (tmp_path / "mixed.xml").write_text(_write_scene(tmp_path, shapes))
+    r = native.Renderer(device=native.HOST_ONLY)
+    r.load_scene_xml(str(tmp_path / "mixed.xml"))
+    with pytest.raises(native.HairPTError, match="mixes hair"):
+        r.prepare()
+
+
+def test_mesh_path_refuses_what_it_does_not_render(tmp_path):
+    c1_scene.write(tmp_path)
+    # a BSDF the mesh path has no kernel for
+    shapes = ('  <shape type="obj"><string name="filename" value="models/Mesh000.obj"/>\n'
+              '    <bsdf type="roughplastic"/></shape>\n')
+    (tmp_path / "rp.xml").write_text(_write_scene(tmp_path, shapes))
+    r = native.Renderer(device=native.HOST_ONLY)
+    r.load_scene_xml(str(tmp_path / "rp.xml"))
+    with pytest.raises(native.HairPTError, match="outside this path"):
+        r.prepare()
+    # a missing mesh file: obj.cpp's message
+    shapes = '  <shape type="obj"><string name="filename" value="models/none.obj"/><ref id="Material"/></shape>\n'
+    (tmp_path / "missing.xml").write_text(_write_scene(tmp_path, shapes))
+    r = native.Renderer(device=native.HOST_ONLY)
+    r.load_scene_xml(str(tmp_path / "missing.xml"))
+    with pytest.raises(native.HairPTError, match="not found"):
+        r.prepare()

@@ -6,8 +6,9 @@ floor; two `obj` meshes; an RGBE `envmap`) is loaded through the product's
 C ABI (hpt_load_scene_xml, host-only context) and exported as JSON
 (hpt_export_scene_json); the CPU path (the oracle's restatement of obj.cpp /
 trimesh.cpp / TriAccel / rectangle.cpp / plastic.cpp / twosided.cpp /
-checkerboard.cpp, oracle/mesh_*.h) renders it at 64 x 64 @ 16 spp.  The device
-path renders hair only and refuses the scene at hpt_prepare, loudly.
+checkerboard.cpp, oracle/mesh_*.h) renders it at 64 x 64 @ 16 spp.  The product
+prepares the same scene with its own loader (csrc/host/mesh.cpp); its device render
+(k_mesh_paths) is checked against the oracle in tests/test_gpu_c1.py.
 
 The reference does not ship models/Mesh00{0,1}.obj: tests/teapot_meshes.py
 writes seeded stand-ins.  The scene file and its envmap are read from
@@ -88,9 +89,16 @@ def test_scene_parses_through_the_c_abi(teapot):
     np.testing.assert_allclose(em["toWorld"][:4], [-0.922278, 0, 0.386527, 0], rtol=1e-6)
 
 
-def test_device_path_refuses_mesh_scene_loudly(teapot):
-    with pytest.raises(native.HairPTError, match="CPU path"):
-        teapot["r"].prepare()
+def test_product_prepares_the_teapot_like_the_oracle(teapot):
+    # the product's own loader (csrc/host/mesh.cpp) behind hpt_prepare: the device path renders the
+    # scene (k_mesh_paths; tests/test_gpu_c1.py checks that render against the oracle)
+    r = teapot["r"]
+    r.prepare()
+    info, mi = r.info(), teapot["o"].mesh_info()
+    assert info.vertices == mi["vertices"]
+    assert info.kd_indices == mi["triangles"] + mi["rectangles"]
+    with pytest.raises(native.HairPTError, match="host-only"):
+        r.render(0, 1)
 
 
 def test_substitute_meshes_load(teapot):
