@@ -100,3 +100,16 @@ def test_c1_render_is_deterministic_and_shards_add_up(c1):
     # a sample range in two calls (the -r partial flushes) accumulates to the whole
     half = r.render(0, SPP // 2) + r.render(SPP // 2, SPP)
     np.testing.assert_allclose(half, f1, rtol=1e-5, atol=1e-6)
+
+
+def test_cli_renders_the_mesh_scene(c1, tmp_path):
+    """bin/mitsuba on the C1 scene (the drop-in: the reference's own command line, mitsuba.cpp:52-400)
+    writes the ldrfilm PNG a library render of the same scene develops to."""
+    import subprocess
+    cli = os.path.join(os.path.dirname(native.__file__), "..", "bin", "mitsuba")
+    cmd = [cli, "-D", "w=%d" % W, "-D", "h=%d" % H, "-D", "spp=%d" % SPP, "-o", str(tmp_path / "teapot.png"), c1["xml"]]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr
+    r = c1["r"]
+    out = r.write_film(tmp_path / "lib.png", r.render(0, SPP))
+    np.testing.assert_array_equal(ref.read_png(str(tmp_path / "teapot.png")), ref.read_png(out))
