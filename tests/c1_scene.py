@@ -97,12 +97,46 @@ def write_pfm(path, img):
 
 
 
-def write(d):
-    """Write the scene, its meshes and its sky under directory d; returns the scene path."""
+def variant_scene():
+    """The other branches of the mesh path in the same scene: face normals on Mesh001
+    (trimesh.cpp:608-616: no vertex normals, the geometric frame shades), flipped normals on the
+    floor (rectangle.cpp:96-99) and on Mesh000 (vertex normals negated, trimesh.cpp:617-622), a
+    one-sided linear plastic with a coloured specular on Mesh000 (no twosided wrapper: its back
+    faces reflect nothing), a constant-reflectance diffuse floor, no strictNormals."""
+    s = SCENE.replace('<boolean name="strictNormals" value="true"/>', '<boolean name="strictNormals" value="false"/>')
+    s = s.replace("""  <bsdf type="twosided" id="Floor">""", """  <bsdf type="plastic" id="Knob">
+    <float name="intIOR" value="1.33"/>
+    <rgb name="diffuseReflectance" value="0.2, 0.5, 0.7"/>
+    <rgb name="specularReflectance" value="0.8, 0.7, 0.6"/>
+  </bsdf>
+  <bsdf type="twosided" id="Floor">""")
+    s = s.replace("""      <texture name="reflectance" type="checkerboard">
+        <rgb name="color1" value="0.325, 0.31, 0.25"/>
+        <rgb name="color0" value="0.725, 0.71, 0.68"/>
+        <float name="uoffset" value="0"/>
+        <float name="voffset" value="0"/>
+        <float name="uscale" value="10"/>
+        <float name="vscale" value="10"/>
+      </texture>""", """      <rgb name="reflectance" value="0.6, 0.55, 0.5"/>""")
+    s = s.replace("""    <ref id="Floor"/>""", """    <boolean name="flipNormals" value="true"/>
+    <ref id="Floor"/>""")
+    s = s.replace("""    <string name="filename" value="models/Mesh001.obj"/>""", """    <string name="filename" value="models/Mesh001.obj"/>
+    <boolean name="faceNormals" value="true"/>""")
+    s = s.replace("""    <string name="filename" value="models/Mesh000.obj"/>
+    <ref id="Material"/>""", """    <string name="filename" value="models/Mesh000.obj"/>
+    <boolean name="flipNormals" value="true"/>
+    <ref id="Knob"/>""")
+    assert s.count("flipNormals") == 2 and "faceNormals" in s and 'ref id="Knob"' in s
+    return s
+
+
+def write(d, variant=False):
+    """Write the scene (or its variant_scene), its meshes and its sky under directory d; returns
+    the scene path."""
     d = str(d)
     teapot_meshes.write_all(os.path.join(d, "models"))
     write_pfm(os.path.join(d, "env.pfm"), synthetic_sky())
-    path = os.path.join(d, "scene.xml")
+    path = os.path.join(d, "scene_variant.xml" if variant else "scene.xml")
     with open(path, "w") as f:
-        f.write(SCENE)
+        f.write(variant_scene() if variant else SCENE)
     return path

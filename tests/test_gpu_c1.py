@@ -69,6 +69,23 @@ def test_mesh_scene_prepares_on_device(c1):
 
 
 def test_c1_render_matches_oracle(c1, oracle_render):
+    _check_against_oracle(c1, oracle_render)
+
+
+def test_c1_variant_matches_oracle(tmp_path):
+    """face normals, flipped normals, a one-sided plastic, a constant diffuse, strictNormals off"""
+    xml = c1_scene.write(tmp_path, variant=True)
+    r = native.Renderer(device=0)
+    r.load_scene_xml(xml, {"w": W, "h": H, "spp": SPP})
+    r.prepare()
+    js = r.scene_json()
+    assert [m["flipNormals"] for m in js["meshes"]] == [True, False, True]
+    assert [m["faceNormals"] for m in js["meshes"]][1] is True
+    v = {"r": r, "js": js, "env": ref.read_pfm(str(tmp_path / "env.pfm"))}
+    _check_against_oracle(v, oracle_film(v))
+
+
+def _check_against_oracle(c1, oracle_render):
     r = c1["r"]
     film = r.render(0, SPP, collect_stats=True)
     ofilm, ostats = oracle_render
