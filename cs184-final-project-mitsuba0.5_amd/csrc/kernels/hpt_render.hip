@@ -3266,29 +3266,46 @@ extern "C" __global__ __launch_bounds__(256) void k_splat(HptScene sc, HptWave w
     float acc[9][4];
 #pragma unroll
     for (int k = 0; k < 9; ++k) acc[k][0] = acc[k][1] = acc[k][2] = acc[k][3] = 0.0f;
-    for (uint32_t jj = lane; jj < w.nSpp; jj += 64) {
-        const uint32_t id = slot * w.nSpp + jj;
-        const float4 l = P.li[id];
-        if (!(isfinite(l.x) && isfinite(l.y) && isfinite(l.z)) || l.x < 0 || l.y < 0 || l.z < 0) continue;
-        const float2 ps = P.pos[id];
-        const float rx = ps.x - 0.5f - ox, ry = ps.y - 0.5f - oy;
-        const float x0 = ceilf(rx - 1.0f), x1 = floorf(rx + 1.0f), y0 = ceilf(ry - 1.0f), y1 = floorf(ry + 1.0f);
+    /* the lane's samples lane, lane + 64, ... in that order (the film's summation order); their
+       records are loaded four at a time ahead of the accumulation, so a wave waits on one round
+       trip per four samples instead of one per sample */
+    for (uint32_t j0 = lane; j0 < w.nSpp; j0 += 4 * 64) {
+        float4 lk[4];
+        float2 pk[4];
 #pragma unroll
-        for (int dy = -1; dy <= 1; ++dy) {
-            const float yr = (float) (py + dy) - oy;
-            if (yr < y0 || yr > y1) continue;
-            const float wy = sc.tent[imin((int) fabsf((yr - ry) * sc.tentScale), HPT_FILTER_RES)];
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t jj = j0 + 64u * k;
+            lk[k] = make_float4(-1.0f, 0.0f, 0.0f, 0.0f); /* past the wave's samples: rejected below */
+            pk[k] = make_float2(0.0f, 0.0f);
+            if (jj < w.nSpp) {
+                lk[k] = P.li[slot * w.nSpp + jj];
+                pk[k] = P.pos[slot * w.nSpp + jj];
+            }
+        }
 #pragma unroll
-            for (int dx = -1; dx <= 1; ++dx) {
-                const float xr = (float) (px + dx) - ox;
-                if (xr < x0 || xr > x1) continue;
-                const float wx = sc.tent[imin((int) fabsf((xr - rx) * sc.tentScale), HPT_FILTER_RES)];
-                const float wgt = wx * wy;
-                float *a = acc[(dy + 1) * 3 + (dx + 1)];
-                a[0] += wgt * l.x;
-                a[1] += wgt * l.y;
-                a[2] += wgt * l.z;
-                a[3] += wgt * 1.0f;
+        for (int k = 0; k < 4; ++k) {
+            const float4 l = lk[k];
+            if (!(isfinite(l.x) && isfinite(l.y) && isfinite(l.z)) || l.x < 0 || l.y < 0 || l.z < 0) continue;
+            const float2 ps = pk[k];
+            const float rx = ps.x - 0.5f - ox, ry = ps.y - 0.5f - oy;
+            const float x0 = ceilf(rx - 1.0f), x1 = floorf(rx + 1.0f), y0 = ceilf(ry - 1.0f), y1 = floorf(ry + 1.0f);
+#pragma unroll
+            for (int dy = -1; dy <= 1; ++dy) {
+                const float yr = (float) (py + dy) - oy;
+                if (yr < y0 || yr > y1) continue;
+                const float wy = sc.tent[imin((int) fabsf((yr - ry) * sc.tentScale), HPT_FILTER_RES)];
+#pragma unroll
+                for (int dx = -1; dx <= 1; ++dx) {
+                    const float xr = (float) (px + dx) - ox;
+                    if (xr < x0 || xr > x1) continue;
+                    const float wx = sc.tent[imin((int) fabsf((xr - rx) * sc.tentScale), HPT_FILTER_RES)];
+                    const float wgt = wx * wy;
+                    float *a = acc[(dy + 1) * 3 + (dx + 1)];
+                    a[0] += wgt * l.x;
+                    a[1] += wgt * l.y;
+                    a[2] += wgt * l.z;
+                    a[3] += wgt * 1.0f;
+                }
             }
         }
     }
