@@ -1169,13 +1169,20 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
                     mask |= (me && may) ? 1u << k : 0u;
                 }
             }
+#ifdef HPT_PK_EXACT_STEPS /* probe variant: count the wave's exact-test steps instead of its lanes' tests */
+            if (STATS)
+                for (uint32_t k = 0; k < HPT_PACKET_LEAF_BATCH; ++k)
+                    if (__ballot((mask >> k) & 1u) != 0 && lane == 0) ++tc.exact;
+#endif
 #pragma unroll
             for (uint32_t k = 0; k < HPT_PACKET_LEAF_BATCH; ++k) {
                 if (mask & (1u << k)) {
                     const uint32_t sg = __float_as_uint(rb[k].z);
                     const float rad = segRadius(sc, sg);
                     const double r2 = (double) (rad * rad); /* Float product (hair.cpp:500) */
+#ifndef HPT_PK_EXACT_STEPS
                     if (STATS) ++tc.exact;
+#endif
                     float t;
                     uint32_t far;
                     if (segIntersect(sc.segs, sg, o, d, r2, r.mint, r.tHit, t, far)) {
