@@ -130,3 +130,19 @@ def test_cli_renders_the_mesh_scene(c1, tmp_path):
     r = c1["r"]
     out = r.write_film(tmp_path / "lib.png", r.render(0, SPP))
     np.testing.assert_array_equal(ref.read_png(str(tmp_path / "teapot.png")), ref.read_png(out))
+
+
+def test_mesh_scene_shares_and_renders_on_several_contexts(c1):
+    """hpt_context_share_scene / hpt_render_multi on a mesh scene (two contexts on the box's one
+    device): the meshes are loaded once, uploaded per context, and the combined film is the
+    host sum of the two shard films, and the one-context film up to the per-pixel sum order."""
+    r0 = c1["r"]
+    r1 = r0.share_scene(0)
+    assert r1.info().vertices == r0.info().vertices and r1.info().kd_nodes == r0.info().kd_nodes
+    single = r0.render(0, SPP)
+    multi = native.Renderer.render_multi([r0, r1], 0, SPP)
+    f0 = r0.render(0, SPP, shard=0, n_shards=2)
+    f1 = r1.render(0, SPP, shard=1, n_shards=2)
+    np.testing.assert_array_equal(multi, f0 + f1)
+    np.testing.assert_allclose(multi, single, rtol=1e-5, atol=1e-6)
+    r1.close()
