@@ -73,9 +73,42 @@ HD float sobolSample(const HptScene &sc, uint64_t index, uint32_t dim) {
    with a select, instead of a per-lane loop of dependent table loads.  Falls
    back to sobolSample when the wave disagrees.  Same XOR of the same
    matrix rows as sobolseq.h:43-58. */
+/* sobolSample for a per-lane dimension in a latency-bound kernel (k_tail: the lanes of a wave are
+   at different bounces, so their dimensions differ): the dimension's 52 direction numbers are read
+   as 16-byte loads issued together, and every index bit is applied with a select -- one round trip
+   where sobolSample's loop waits on one table load per set bit.  Same XOR of the same rows. */
+HD float sobolSampleRow(const HptScene &sc, uint64_t index, uint32_t dim) {
+    const uint4 *__restrict__ row = reinterpret_cast<const uint4 *>(sc.sobol + dim * HPT_SOBOL_BITS); /* 208-B rows */
+    const uint32_t lo = (uint32_t) index, hi = (uint32_t) (index >> 32);
+    uint32_t result = sc.scramble;
+    uint4 q[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) q[k] = row[k];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        result ^= ((lo >> (4 * k)) & 1u) ? q[k].x : 0u;
+        result ^= ((lo >> (4 * k + 1)) & 1u) ? q[k].y : 0u;
+        result ^= ((lo >> (4 * k + 2)) & 1u) ? q[k].z : 0u;
+        result ^= ((lo >> (4 * k + 3)) & 1u) ? q[k].w : 0u;
+    }
+    if (hi) { /* index bits 32-51: words 32-51 of the row */
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const uint4 r = row[8 + k];
+            result ^= ((hi >> (4 * k)) & 1u) ? r.x : 0u;
+            result ^= ((hi >> (4 * k + 1)) & 1u) ? r.y : 0u;
+            result ^= ((hi >> (4 * k + 2)) & 1u) ? r.z : 0u;
+            result ^= ((hi >> (4 * k + 3)) & 1u) ? r.w : 0u;
+        }
+    }
+    return fminr((float) result * (1.0f / 4294967296.0f), kOneMinusEps);
+}
+
+/* LAT: a wave that disagrees on the dimension takes sobolSampleRow (k_tail) instead of sobolSample */
+template <bool LAT = false>
 HD float sobolSampleUniform(const HptScene &sc, uint64_t index, uint32_t dim) {
     const uint32_t d0 = __builtin_amdgcn_readfirstlane(dim);
-    if (__ballot(dim != d0) != 0) return sobolSample(sc, index, dim);
+    if (__ballot(dim != d0) != 0) return LAT ? sobolSampleRow(sc, index, dim) : sobolSample(sc, index, dim);
     const uint32_t *__restrict__ m = sc.sobol + d0 * HPT_SOBOL_BITS;
     const uint32_t lo = (uint32_t) index, hi = (uint32_t) (index >> 32);
     uint32_t result = sc.scramble;
@@ -2861,7 +2894,7 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
             };
             /* ---- direct illumination (path.cpp:175, scene.cpp:828-852, envmap.cpp:516-543) ---- */
             if (B.smooth) {
-                float nx = sobolSampleUniform(sc, sidx, dim), ny = sobolSampleUniform(sc, sidx, dim + 1);
+                float nx = sobolSampleUniform<!REC>(sc, sidx, dim), ny = sobolSampleUniform<!REC>(sc, sidx, dim + 1);
                 dim += 2;
                 V3 dl, value;
                 float pdf;
@@ -2893,7 +2926,7 @@ HD void shadePath(const HptScene &sc, HptPaths &P, uint32_t id, uint32_t hitRec,
                 }
             }
             /* ---- BSDF sampling ---- */
-            float bx = sobolSampleUniform(sc, sidx, dim), by = sobolSampleUniform(sc, sidx, dim + 1);
+            float bx = sobolSampleUniform<!REC>(sc, sidx, dim), by = sobolSampleUniform<!REC>(sc, sidx, dim + 1);
             dim += 2;
             V3 woL;
             float bpdf = 0.0f;
@@ -3054,7 +3087,7 @@ HD bool postPath(const HptScene &sc, HptPaths &P, uint32_t id, bool hit, uint32_
                     float q = fminr(maxc(T) * 1.0f * 1.0f, 0.95f);
                     const uint64_t sidx =
                         REC ? ((uint64_t) __float_as_uint(rec[1].w) << 32) | __float_as_uint(rec[0].w) : P.sobol[id];
-                    float u = sobolSampleUniform(sc, sidx, dim);
+                    float u = sobolSampleUniform<!REC>(sc, sidx, dim);
                     dim += 1;
                     if (u >= q) alive = false;
                     else T = divs(T, q);
