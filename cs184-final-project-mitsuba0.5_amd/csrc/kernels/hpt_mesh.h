@@ -314,7 +314,10 @@ extern "C" __global__ __launch_bounds__(256) void k_mesh_paths(HptScene sc, HptM
     if (valid) {
         const HptCamera &c = sc.cam;
         /* k_camera's sample (sampler->generate + next2D, integrator.cpp:165-178) */
-        const uint64_t sidx = (c.logRes > 1) ? sobolLookUp(sc, c.logRes, j, (uint32_t) px, (uint32_t) py) : (uint64_t) j;
+        const uint32_t lastFrame = w.sppBegin + w.nSpp - 1u;
+        const uint32_t frameBits = lastFrame ? 32u - (uint32_t) __builtin_clz(lastFrame) : 0u;
+        const uint64_t sidx = (c.logRes > 1) ? sobolLookUpWave(sc, c.logRes, j, (uint32_t) px, (uint32_t) py, frameBits)
+                                             : (uint64_t) j;
         float ox, oy;
         if (sidx != (uint64_t) j) {
             ox = sobolSample(sc, sidx, 0) * c.resolution - px;

@@ -135,6 +135,36 @@ HD uint64_t sobolLookUp(const HptScene &sc, uint32_t m, uint32_t frame, uint32_t
     return index;
 }
 
+/* sobolLookUp for a wave whose m (the resolution's log2) is uniform and whose frames are below
+   2^frameBits (frameBits uniform, <= 32): the same XOR of the same table columns, as selects over a
+   uniform run of columns read eight at a time by the scalar unit, instead of per-lane loops that
+   wait on one table load per set bit.  vdc_sobol_matrices[m - 1][c] < 2^m, so delta < 2^m and
+   b < 2^(2m): columns from 2m on are never read (sobolseq.h:98-131) */
+HD uint64_t sobolLookUpWave(const HptScene &sc, uint32_t m, uint32_t frame, uint32_t px, uint32_t py,
+                            uint32_t frameBits) {
+    const uint64_t *vdc = sc.vdc + (m - 1) * HPT_SOBOL_BITS;
+    const uint64_t *inv = sc.vdcInv + (m - 1) * HPT_SOBOL_BITS;
+    uint32_t delta = 0;
+    for (uint32_t c0 = 0; c0 < frameBits; c0 += 8) { /* uniform bound; c0 + 7 < 52 */
+        uint64_t col[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) col[k] = vdc[c0 + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) delta ^= ((frame >> (c0 + k)) & 1u) ? (uint32_t) col[k] : 0u;
+    }
+    const uint32_t sm = sc.scramble >> (32 - m);
+    const uint64_t b = (((uint64_t) (px ^ sm) << m) | (py ^ sm)) ^ delta;
+    uint64_t index = (uint64_t) frame << (m << 1);
+    for (uint32_t c0 = 0; c0 < 2 * m; c0 += 8) { /* columns past the row's 52 read as 0 (b has no such bits) */
+        uint64_t col[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) col[k] = (c0 + k < HPT_SOBOL_BITS) ? inv[c0 + k] : 0ull;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) index ^= ((b >> (c0 + k)) & 1ull) ? col[k] : 0ull;
+    }
+    return index;
+}
+
 /* ------------------------------------------------------------------ */
 /* Camera (perspective.cpp:271-298)                                     */
 /* ------------------------------------------------------------------ */
@@ -2501,7 +2531,11 @@ extern "C" __global__ __launch_bounds__(HPT_QBLOCK) void k_camera(HptScene sc, H
     const uint32_t wps = (w.nSpp % 64u == 0 && w.nSpp >= 128u && HPT_QBLOCK % w.nSpp == 0) ? w.nSpp / 64u : 1u;
     if (valid) {
         const HptCamera &c = sc.cam;
-        uint64_t sidx = (c.logRes > 1) ? sobolLookUp(sc, c.logRes, j, (uint32_t) px, (uint32_t) py) : (uint64_t) j;
+        /* the wave's frames are below sppBegin + nSpp: a uniform bound on their bits */
+        const uint32_t lastFrame = w.sppBegin + w.nSpp - 1u;
+        const uint32_t frameBits = lastFrame ? 32u - (uint32_t) __builtin_clz(lastFrame) : 0u;
+        uint64_t sidx = (c.logRes > 1) ? sobolLookUpWave(sc, c.logRes, j, (uint32_t) px, (uint32_t) py, frameBits)
+                                       : (uint64_t) j;
         float ox, oy;
         if (sidx != (uint64_t) j) {
             ox = sobolSample(sc, sidx, 0) * c.resolution - px;
