@@ -89,3 +89,35 @@ def test_mesh_path_refuses_what_it_does_not_render(tmp_path):
     r.load_scene_xml(str(tmp_path / "missing.xml"))
     with pytest.raises(native.HairPTError, match="not found"):
         r.prepare()
+
+
+def _obj_scene(tmp_path, obj_text, name="m.obj"):
+    c1_scene.write(tmp_path)
+    (tmp_path / name).write_text(obj_text)
+    shapes = '  <shape type="obj"><string name="filename" value="%s"/><ref id="Material"/></shape>\n' % name
+    path = tmp_path / ("s_%s.xml" % name.replace(".", "_"))
+    path.write_text(_write_scene(tmp_path, shapes))
+    r = native.Renderer(device=native.HOST_ONLY)
+    r.load_scene_xml(str(path))
+    return r
+
+
+def test_obj_edge_cases(tmp_path):
+    # obj.cpp:371-390 / 608-715: a quad as a fan, negative (relative) indices, `v//vn` and `v/vt`
+    # faces, a degenerate triangle (TriAccel k = 3: loaded, never hit), a trailing '\' continuation
+    obj = ("v 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nvn 0 0 1\nvt 0 0\nvt 1 0\nvt 1 1\n"
+           "f 1//1 2//1 3//1 4//1\n"
+           "f -4/1 -3/2 \\\n -2/3\n"
+           "f 1 1 2\n")
+    r = _obj_scene(tmp_path, obj)
+    r.prepare()
+    info = r.info()
+    assert info.kd_indices == 2 + 1 + 1  # the fan's two triangles, the relative-index one, the degenerate one
+    o = oracle_lib.MeshOracle()
+    o.setup_scene(r.scene_json(), c1_scene.synthetic_sky(), 16, 16, 1)
+    assert info.vertices == o.mesh_info()["vertices"]
+    # out-of-range indices and material libraries fail loudly, as obj.cpp does
+    with pytest.raises(native.HairPTError, match="vertex"):
+        _obj_scene(tmp_path, "v 0 0 0\nv 1 0 0\nf 1 2 7\n", "bad.obj").prepare()
+    with pytest.raises(native.HairPTError, match="mtllib"):
+        _obj_scene(tmp_path, "mtllib x.mtl\nv 0 0 0\n", "mtl.obj").prepare()
