@@ -83,8 +83,8 @@ struct BsdfDesc {
     std::vector<BsdfDesc> nested;                  /* twosided: the one or two nested BSDFs */
 };
 
-/* ---- a triangle-mesh shape (obj.cpp / rectangle.cpp).  The GPU path renders hair;
-   scenes with these shapes are parsed, exported and rendered by the CPU path (C1) ---- */
+/* ---- a triangle-mesh shape (obj.cpp / rectangle.cpp): loaded by mesh.cpp, rendered by the mesh
+   kernel (k_mesh_paths) -- a scene has hair shapes or mesh shapes, not both (hpt_prepare) ---- */
 struct MeshShapeDesc {
     std::string type;                              /* obj | rectangle */
     std::string file;                              /* obj: resolved against the scene directory */
