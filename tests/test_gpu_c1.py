@@ -117,6 +117,10 @@ def test_c1_render_is_deterministic_and_shards_add_up(c1):
     # a sample range in two calls (the -r partial flushes) accumulates to the whole
     half = r.render(0, SPP // 2) + r.render(SPP // 2, SPP)
     np.testing.assert_allclose(half, f1, rtol=1e-5, atol=1e-6)
+    # several waves per call (a frame larger than one wave of paths): the same film
+    waves = r.render(0, SPP, max_wave_paths=W * H * 2, collect_stats=True)
+    assert r.stats().waves == SPP // 2
+    np.testing.assert_allclose(waves, f1, rtol=1e-5, atol=1e-6)
 
 
 def test_cli_renders_the_mesh_scene(c1, tmp_path):
