@@ -1232,10 +1232,13 @@ HD bool tracePacket(const HptScene &sc, TraceRay &r, bool valid, PacketLds &L, T
                     mask |= (me && may) ? 1u << k : 0u;
                 }
             }
-#ifdef HPT_PK_EXACT_STEPS /* probe variant: count the wave's exact-test steps instead of its lanes' tests */
-            if (STATS)
-                for (uint32_t k = 0; k < HPT_PACKET_LEAF_BATCH; ++k)
-                    if (__ballot((mask >> k) & 1u) != 0 && lane == 0) ++tc.exact;
+#ifdef HPT_PK_EXACT_STEPS /* probe variant: count the wave's exact-test steps (1) or the leaf batches
+                             with any exact test (2) instead of its lanes' tests */
+            if (STATS) {
+                uint32_t steps = 0;
+                for (uint32_t k = 0; k < HPT_PACKET_LEAF_BATCH; ++k) steps += __ballot((mask >> k) & 1u) != 0 ? 1u : 0u;
+                if (lane == 0) tc.exact += HPT_PK_EXACT_STEPS == 2 ? (steps ? 1u : 0u) : steps;
+            }
 #endif
 #pragma unroll
             for (uint32_t k = 0; k < HPT_PACKET_LEAF_BATCH; ++k) {
