@@ -298,8 +298,9 @@ struct HptMeshBsdf {
     int nested[2];
 };
 
-/* k_mesh_paths' per-lane BVH stack entries: hpt_prepare refuses a BVH deeper than this - 1 levels */
-#define HPT_MESH_STACK 64
+/* k_mesh_paths' per-lane BVH stack entries (LDS): hpt_prepare refuses a BVH deeper than this - 1
+   levels -- the median-split build is ~log2(primitives / 4) + 1 deep, 14 for the teapot */
+#define HPT_MESH_STACK 32
 struct HptMeshScene {
     const HptBvhNode *nodes;
     const uint32_t *prims;     /* leaf primitive references */

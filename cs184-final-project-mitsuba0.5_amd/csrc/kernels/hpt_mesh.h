@@ -17,7 +17,7 @@
  *              TwoSidedBRDF (twosided.cpp:108-183)
  *
  * C1 is 64x64 @ 16 spp (65,536 paths): the configuration is plumbing, not throughput, so the
- * kernel is a plain per-lane megakernel (the BVH stack in scratch).  Every float operation
+ * kernel is a plain per-lane megakernel (the BVH stack in LDS).  Every float operation
  * follows the oracle's restatement (oracle/mesh_geom.h, mesh_bsdf.h, oracle.cpp Li) in the
  * same order, built with -ffp-contract=off like the rest of the device code.
  */
@@ -95,22 +95,24 @@ struct MeshHit {
     uint32_t prim; /* triangle index, or HPT_PRIM_RECT | rectangle */
 };
 
-/* closest hit (or, SHADOW, any hit) in [mint, maxt], maxt shrinking to each hit in test order */
+/* closest hit (or, SHADOW, any hit) in [mint, maxt], maxt shrinking to each hit in test order.
+   stk: the lane's column of the block's LDS stack (entry e at stk[e * HPT_MESH_BLOCK]) */
+#define HPT_MESH_BLOCK 256
 template <bool SHADOW>
-HD bool meshTraverse(const HptMeshScene &ms, V3 o, V3 d, float mint, float maxt, MeshHit &hit) {
+HD bool meshTraverse(const HptMeshScene &ms, V3 o, V3 d, float mint, float maxt, MeshHit &hit, uint32_t *stk) {
     const V3 rcp = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    uint32_t stack[HPT_MESH_STACK];
+    auto stack = [&](int e) -> uint32_t & { return stk[e * HPT_MESH_BLOCK]; };
     int sp = 0;
-    stack[sp++] = 0;
+    stack(sp++) = 0;
     bool found = false;
     while (sp > 0) {
-        const uint32_t ni = stack[--sp];
+        const uint32_t ni = stack(--sp);
         const HptBvhNode nd = ms.nodes[ni];
         float nearT, farT;
         if (!nodeHit(nd, o, d, rcp, nearT, farT) || farT < mint || nearT > maxt) continue;
         if (nd.count == 0) {
-            stack[sp++] = nd.a;
-            stack[sp++] = ni + 1;
+            stack(sp++) = nd.a;
+            stack(sp++) = ni + 1;
             continue;
         }
         for (uint32_t k = nd.a; k < nd.a + nd.count; ++k) {
@@ -132,7 +134,7 @@ HD bool meshTraverse(const HptMeshScene &ms, V3 o, V3 d, float mint, float maxt,
 }
 
 /* ShapeKDTree::rayIntersect (skdtree.cpp:112-141): scene-AABB clip + adaptive epsilon */
-HD bool meshIntersect(const HptMeshScene &ms, V3 o, V3 d, float rmint, float rmaxt, MeshHit &hit) {
+HD bool meshIntersect(const HptMeshScene &ms, V3 o, V3 d, float rmint, float rmaxt, MeshHit &hit, uint32_t *stk) {
     const V3 rcp = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     float mint, maxt;
     if (!sceneBoxHit(ms, o, d, rcp, mint, maxt)) return false;
@@ -140,10 +142,10 @@ HD bool meshIntersect(const HptMeshScene &ms, V3 o, V3 d, float rmint, float rma
     if (rayMinT > mint) mint = rayMinT;
     if (rmaxt < maxt) maxt = rmaxt;
     if (!(maxt > mint)) return false;
-    return meshTraverse<false>(ms, o, d, mint, maxt, hit);
+    return meshTraverse<false>(ms, o, d, mint, maxt, hit, stk);
 }
 /* ShapeKDTree::rayIntersect(shadow) (skdtree.cpp:207-226) */
-HD bool meshOccluded(const HptMeshScene &ms, V3 o, V3 d, float rmint, float rmaxt) {
+HD bool meshOccluded(const HptMeshScene &ms, V3 o, V3 d, float rmint, float rmaxt, uint32_t *stk) {
     const V3 rcp = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     float mint, maxt;
     if (!sceneBoxHit(ms, o, d, rcp, mint, maxt)) return false;
@@ -152,7 +154,7 @@ HD bool meshOccluded(const HptMeshScene &ms, V3 o, V3 d, float rmint, float rmax
     if (rmaxt < maxt) maxt = rmaxt;
     if (!(maxt > mint)) return false;
     MeshHit unused;
-    return meshTraverse<true>(ms, o, d, mint, maxt, unused);
+    return meshTraverse<true>(ms, o, d, mint, maxt, unused, stk);
 }
 
 struct MeshIts {
@@ -303,8 +305,12 @@ HD V3 meshBsdfSample(const HptMeshScene &ms, int bi, V3 wi, float sx, float sy, 
    then path.cpp:119-294 to termination; the sample's film position and radiance go to
    P.pos / P.li for k_splat.  counters: HPT_C_BOUNCES (path-bounces), HPT_C_ERROR (Sobol
    dimensions exhausted) */
-extern "C" __global__ __launch_bounds__(256) void k_mesh_paths(HptScene sc, HptMeshScene ms, HptWave w, HptPaths P,
-                                                               uint32_t *__restrict__ counters) {
+extern "C" __global__ __launch_bounds__(HPT_MESH_BLOCK) void k_mesh_paths(HptScene sc, HptMeshScene ms, HptWave w,
+                                                                          HptPaths P, uint32_t *__restrict__ counters) {
+    /* the BVH stacks in LDS (a lane's column, conflict-free), shared by the lane's closest and shadow
+       queries: 32 entries x 256 lanes = 32 KB per block */
+    __shared__ uint32_t stackLds[HPT_MESH_STACK * HPT_MESH_BLOCK];
+    uint32_t *const stk = stackLds + threadIdx.x;
     const uint32_t id = blockIdx.x * blockDim.x + threadIdx.x;
     int px = 0, py = 0;
     uint32_t j = 0;
@@ -336,7 +342,7 @@ extern "C" __global__ __launch_bounds__(256) void k_mesh_paths(HptScene sc, HptM
         int depth = 1;
         MeshHit h;
         MeshIts its;
-        bool hitValid = meshIntersect(ms, ro, rd, mint, maxt, h);
+        bool hitValid = meshIntersect(ms, ro, rd, mint, maxt, h, stk);
         if (hitValid) meshFill(ms, ro, rd, h, its);
         while (depth <= sc.maxDepth || sc.maxDepth < 0) {
             if (!hitValid) {
@@ -371,7 +377,7 @@ extern "C" __global__ __launch_bounds__(256) void k_mesh_paths(HptScene sc, HptM
                 float nearT, farT;
                 if (!(isZero(value) || pdf == 0 || !bsphereIntersect(sc.env, its.p, dW, nearT, farT) || nearT >= 0 ||
                       farT <= 0) &&
-                    !meshOccluded(ms, its.p, dW, kEpsilon, farT * (1 - kShadowEpsilon))) {
+                    !meshOccluded(ms, its.p, dW, kEpsilon, farT * (1 - kShadowEpsilon), stk)) {
                     const V3 val = divs(value, pdf);
                     const V3 wo = its.sh.toLocal(dW);
                     const V3 bsdfVal = meshBsdfEval(ms, bi, its.wi, wo, its.u, its.v);
@@ -398,7 +404,7 @@ extern "C" __global__ __launch_bounds__(256) void k_mesh_paths(HptScene sc, HptM
             primary = false;
             bool hitEmitter = false;
             V3 value = v3(0, 0, 0);
-            hitValid = meshIntersect(ms, ro, rd, kEpsilon, finf(), h);
+            hitValid = meshIntersect(ms, ro, rd, kEpsilon, finf(), h, stk);
             if (hitValid) {
                 meshFill(ms, ro, rd, h, its);
             } else {
@@ -438,6 +444,7 @@ extern "C" __global__ __launch_bounds__(256) void k_mesh_paths(HptScene sc, HptM
 hipError_t hpt_launch_mesh_paths(const HptScene &sc, const HptMeshScene &ms, const HptWave &w, const HptPaths &P,
                                  uint32_t *counters, hipStream_t s) {
     if (w.nPaths == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_mesh_paths, dim3((w.nPaths + 255u) / 256u), dim3(256), 0, s, sc, ms, w, P, counters);
+    hipLaunchKernelGGL(k_mesh_paths, dim3((w.nPaths + HPT_MESH_BLOCK - 1) / HPT_MESH_BLOCK), dim3(HPT_MESH_BLOCK), 0, s,
+                       sc, ms, w, P, counters);
     return hipGetLastError();
 }
