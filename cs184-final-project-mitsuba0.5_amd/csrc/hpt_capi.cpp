@@ -467,6 +467,12 @@ int hpt_debug_sfmt(uint64_t seed, uint64_t n, uint64_t *out) {
     return HPT_OK;
 }
 
+int hpt_debug_fresnel_diffuse(int n, const float *eta, float *out) {
+    if (n < 0 || (n > 0 && (!eta || !out))) return HPT_EINVAL;
+    for (int i = 0; i < n; ++i) out[i] = fresnelDiffuseReflectance(eta[i]);
+    return HPT_OK;
+}
+
 int hpt_set_traversal_bounds(hpt_context *c, uint32_t max_leaf_rounds, uint32_t max_restarts) {
     if (!c || max_leaf_rounds == 0) return HPT_EINVAL;
     c->maxLeafRounds = std::min<uint32_t>(max_leaf_rounds, HPT_MAX_LEAF_ROUNDS);

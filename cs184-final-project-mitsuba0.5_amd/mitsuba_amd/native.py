@@ -85,6 +85,7 @@ SIGNATURES = {
     "hpt_set_block_weights": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.c_int]),
     "hpt_block_deal": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int32)]),
     "hpt_debug_sfmt": (C.c_int, [C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
+    "hpt_debug_fresnel_diffuse": (C.c_int, [C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
     "hpt_set_integrator": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int]),
     "hpt_set_hair_file": (C.c_int, [C.c_void_p, C.c_char_p, C.c_float, C.c_float, _f]),
     "hpt_set_hair_reduction": (C.c_int, [C.c_void_p, C.c_float]),

@@ -90,6 +90,10 @@ int hpt_set_sampler_scramble(hpt_context *ctx, uint64_t scramble);
    Random(seed) (src/libcore/random.cpp:497-526), n outputs of Random::nextULong (:551-553);
    pinned by the reference's known answers for Random(4321) (src/tests/test_random.cpp:434-507) */
 int hpt_debug_sfmt(uint64_t seed, uint64_t n, uint64_t *out);
+/* Test hook: fresnelDiffuseReflectance(eta, fast = false) (src/libcore/util.cpp:808-859, the
+   adaptive Gauss-Lobatto of quad.cpp:287-409) as the mesh path's plastic BSDF configures it
+   (plastic.cpp:186-217), n values */
+int hpt_debug_fresnel_diffuse(int n, const float *eta, float *out);
 /* Test hook (no reference counterpart): lower the per-ray traversal bounds (leaf rounds, kd-restarts;
    defaults and maxima 2^18 and 1024) past which a render or trace call fails with HPT_ETRAVERSAL */
 int hpt_set_traversal_bounds(hpt_context *ctx, uint32_t max_leaf_rounds, uint32_t max_restarts);

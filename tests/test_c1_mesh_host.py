@@ -121,3 +121,18 @@ def test_obj_edge_cases(tmp_path):
         _obj_scene(tmp_path, "v 0 0 0\nv 1 0 0\nf 1 2 7\n", "bad.obj").prepare()
     with pytest.raises(native.HairPTError, match="mtllib"):
         _obj_scene(tmp_path, "mtllib x.mtl\nv 0 0 0\n", "mtl.obj").prepare()
+
+
+def test_fresnel_diffuse_reflectance_equals_the_oracle():
+    """The product's adaptive Gauss-Lobatto (mesh.cpp, util.cpp:808-859 over quad.cpp:287-409) that
+    configures plastic's diffuse term gives the oracle's value bit for bit (oracle/lobatto.h,
+    itself within 2e-5 of scipy's float64 quadrature, tests/test_c1_mesh_pins.py)."""
+    import ctypes as C
+    lib = native.load_library()
+    eta = np.array([1.5, 1 / 1.5, 1.33, 1 / 1.33, 1.000277, 2.4, 1.0], np.float32)
+    out = np.zeros_like(eta)
+    assert lib.hpt_debug_fresnel_diffuse(len(eta), eta.ctypes.data_as(C.POINTER(C.c_float)),
+                                         out.ctypes.data_as(C.POINTER(C.c_float))) == 0
+    ref = np.array([oracle_lib.fresnel_diffuse_reflectance(float(e)) for e in eta], np.float32)
+    np.testing.assert_array_equal(out, ref)
+    assert out[-1] == 0.0 and 0.05 < out[0] < 0.15  # eta = 1 reflects nothing; glass ~0.09
